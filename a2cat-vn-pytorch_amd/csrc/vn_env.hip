@@ -1,0 +1,682 @@
+// vn_env.hip — batched cached-scene env.step for gfx950 (CDNA4).
+//
+// Semantics restate THORDiscreteCachedEnv (environments/gym_ai2thor/envs/cached.py):
+//   transition  nxt = graph[s][a]; -1 = blocked                     (cached.py:74-79)
+//   terminal    goal == state                                        (cached.py:83)
+//   reward      -reward_configuration[1], goal -> [0], blocked -> [2] (cached.py:84-88)
+//   obs         (frame[s], frame[g]), or the previous obs on terminal (cached.py:90-98)
+//   reset       goal ~ U[0,N), start ~ U[0,N) until spd[start][goal] > 0 (cached.py:38-45)
+// batched the way deep_rl's SubprocVecEnv drives it (auto-reset on done, the reset
+// observation replaces the terminal one) under gym's TimeLimit(900).
+//
+// Design (DESIGN.md "vn_step"): one wave64 per env, 4 envs per 256-thread workgroup.
+// The per-env state is wave-uniform (scalar loads); a reset runs 64 Philox start
+// candidates in parallel, one per lane, and a wave ballot picks the first valid one —
+// the same result as the sequential rejection loop over the same counter stream.
+// The two frames are then streamed with 16-B lanes, 8 loads in flight per lane.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "vn_common.h"
+
+namespace vn {
+
+static thread_local std::string g_last_error;
+void set_error(const std::string& msg) { g_last_error = msg; }
+int fail(int code, const std::string& msg) {
+  set_error(msg);
+  return code;
+}
+int hip_fail(hipError_t e, const char* what) {
+  set_error(std::string(what) + ": " + hipGetErrorString(e));
+  return VN_EHIP;
+}
+const std::string& last_error() { return g_last_error; }
+
+struct SceneDev {
+  int64_t row_base;  // first arena row (frame) of the scene
+  int64_t spd_off;   // element offset of the scene's [N][N] spd block
+  int32_t graph_off; // first row of the scene's [N][4] adjacency block
+  int32_t n;         // states
+  float r_goal, r_step, r_coll;
+  int32_t terminal_obs;
+};
+
+enum { ST_SCENE = 0, ST_STATE, ST_GOAL, ST_OBS, ST_ELAPSED, ST_EPISODE, ST_SCHED, ST_COUNT };
+
+struct EnvArgs {
+  const SceneDev* scenes;
+  const int32_t* graph;
+  const int32_t* spd;
+  const uint8_t* arena;
+  int64_t frame_bytes;
+  int32_t* st;  // [ST_COUNT][n_envs]
+  float* ep_ret;
+  const int32_t* env_scene;
+  const int32_t* tasks;
+  const int32_t* sched;
+  uint32_t* flags;
+  int n_tasks, sched_len, max_steps, autoreset, n_envs;
+  uint32_t k0, k1;
+  // per call
+  const int32_t* actions;
+  const int32_t* mask;
+  uint8_t* obs;
+  uint8_t* goal_out;
+  float* reward;
+  uint8_t* done;
+  int32_t* state_out;
+  float* info_ret;
+  int32_t* info_len;
+  int32_t* info_term;
+  uint8_t* info_trunc;
+  int32_t* info_img_row;
+  int32_t* info_goal_row;
+};
+
+enum { MODE_STEP = 0, MODE_RESET = 1, MODE_OBSERVE = 2 };
+constexpr int kEnvsPerBlock = 4;
+constexpr int kStartRounds = 16;  // 1024 rejection attempts before flagging
+
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// Wave-cooperative reset of env e (all 64 lanes call with uniform arguments).
+__device__ void reset_env(const EnvArgs& a, int e, int lane, int& sc, int& s, int& g) {
+  const int n_envs = a.n_envs;
+  const int k = a.st[ST_EPISODE * n_envs + e];
+  const int sp = a.st[ST_SCHED * n_envs + e];
+  if (a.sched_len > 0 && sp < a.sched_len) {
+    sc = a.env_scene[e];
+    const int n = a.scenes[sc].n;
+    s = a.sched[((int64_t)e * a.sched_len + sp) * 2 + 0];
+    g = a.sched[((int64_t)e * a.sched_len + sp) * 2 + 1];
+    if ((unsigned)s >= (unsigned)n || (unsigned)g >= (unsigned)n) {
+      if (lane == 0) atomicOr(a.flags, (uint32_t)VN_FLAG_BAD_SCHEDULE);
+      s = min(max(s, 0), n - 1);
+      g = min(max(g, 0), n - 1);
+    }
+    if (lane == 0) a.st[ST_SCHED * n_envs + e] = sp + 1;
+    return;
+  }
+  const u32x4 rg = philox4x32_10(u32x4{(uint32_t)e, (uint32_t)k, 0u, STREAM_GOAL}, a.k0, a.k1);
+  if (a.n_tasks > 0) {
+    const int t = (int)uniform_below(rg.x, (uint32_t)a.n_tasks);
+    sc = a.tasks[2 * t];
+    g = a.tasks[2 * t + 1];
+    if (g < 0) g = (int)uniform_below(rg.y, (uint32_t)a.scenes[sc].n);
+  } else {
+    sc = a.env_scene[e];
+    g = (int)uniform_below(rg.x, (uint32_t)a.scenes[sc].n);
+  }
+  const SceneDev S = a.scenes[sc];
+  const int32_t* spd = a.spd + S.spd_off;
+  s = -1;
+  for (int round = 0; round < kStartRounds; ++round) {
+    const uint32_t att = (uint32_t)(round * 64 + lane);
+    const u32x4 r = philox4x32_10(u32x4{(uint32_t)e, (uint32_t)k, att, STREAM_START}, a.k0, a.k1);
+    const int cand = (int)uniform_below(r.x, (uint32_t)S.n);
+    const bool ok = spd[(int64_t)cand * S.n + g] > 0;
+    const unsigned long long m = __ballot(ok);
+    if (m) {
+      s = __shfl(cand, __ffsll((long long)m) - 1);
+      break;
+    }
+  }
+  if (s < 0) {  // bounded search exhausted: flag and take attempt 0
+    if (lane == 0) atomicOr(a.flags, (uint32_t)VN_FLAG_RESET_EXHAUSTED);
+    const u32x4 r = philox4x32_10(u32x4{(uint32_t)e, (uint32_t)k, 0u, STREAM_START}, a.k0, a.k1);
+    s = (int)uniform_below(r.x, (uint32_t)S.n);
+  }
+  s = uni(s);
+}
+
+// Copy the image frame and goal frame of one env: 16-B lanes, 8 loads in flight.
+template <int VEC>
+__device__ __forceinline__ void copy_two_frames(uint8_t* __restrict__ d1, const uint8_t* __restrict__ s1,
+                                                uint8_t* __restrict__ d2, const uint8_t* __restrict__ s2,
+                                                int64_t bytes, int lane) {
+  if constexpr (VEC == 16) {
+    const int n = (int)(bytes >> 4);
+    const uint4* a = reinterpret_cast<const uint4*>(s1);
+    const uint4* b = reinterpret_cast<const uint4*>(s2);
+    uint4* x = reinterpret_cast<uint4*>(d1);
+    uint4* y = reinterpret_cast<uint4*>(d2);
+    int i = lane;
+    for (; i + 192 < n; i += 256) {
+      const uint4 a0 = a[i], a1 = a[i + 64], a2 = a[i + 128], a3 = a[i + 192];
+      const uint4 b0 = b[i], b1 = b[i + 64], b2 = b[i + 128], b3 = b[i + 192];
+      x[i] = a0; x[i + 64] = a1; x[i + 128] = a2; x[i + 192] = a3;
+      y[i] = b0; y[i + 64] = b1; y[i + 128] = b2; y[i + 192] = b3;
+    }
+    for (; i < n; i += 64) {
+      const uint4 a0 = a[i], b0 = b[i];
+      x[i] = a0;
+      y[i] = b0;
+    }
+  } else if constexpr (VEC == 4) {
+    const int n = (int)(bytes >> 2);
+    const uint32_t* a = reinterpret_cast<const uint32_t*>(s1);
+    const uint32_t* b = reinterpret_cast<const uint32_t*>(s2);
+    uint32_t* x = reinterpret_cast<uint32_t*>(d1);
+    uint32_t* y = reinterpret_cast<uint32_t*>(d2);
+    for (int i = lane; i < n; i += 64) {
+      const uint32_t a0 = a[i], b0 = b[i];
+      x[i] = a0;
+      y[i] = b0;
+    }
+  } else {
+    for (int64_t i = lane; i < bytes; i += 64) {
+      d1[i] = s1[i];
+      d2[i] = s2[i];
+    }
+  }
+}
+
+template <int MODE, int VEC>
+__global__ __launch_bounds__(256) void env_kernel(EnvArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int e = uni(blockIdx.x * kEnvsPerBlock + (threadIdx.x >> 6));
+  if (e >= a.n_envs) return;
+  const int n_envs = a.n_envs;
+  int32_t* st = a.st;
+
+  int sc = st[ST_SCENE * n_envs + e];
+  int s = st[ST_STATE * n_envs + e];
+  int g = st[ST_GOAL * n_envs + e];
+  int os = st[ST_OBS * n_envs + e];
+
+  if constexpr (MODE == MODE_STEP) {
+    int t = st[ST_ELAPSED * n_envs + e];
+    const SceneDev S = a.scenes[sc];
+    const int act = a.actions[e];
+    const bool bad = (unsigned)act > 3u;
+    int nxt = -1;
+    if (!bad) nxt = a.graph[((int64_t)S.graph_off + s) * 4 + act];
+    const bool collided = nxt == -1;
+    if (!collided) s = nxt;
+    const bool terminal = (s == g);
+    float r = S.r_step;
+    if (terminal) r = S.r_goal;
+    if (collided) r = S.r_coll;
+    if (!terminal || S.terminal_obs) os = s;
+    t += 1;
+    const bool limit = a.max_steps > 0 && t >= a.max_steps;
+    const bool done = terminal || limit;
+    const float ret = a.ep_ret[e] + r;
+    const int term_state = os;
+    const int ep_len = t;
+    float new_ret = ret;
+    if (done && a.autoreset) {
+      reset_env(a, e, lane, sc, s, g);
+      os = s;
+      t = 0;
+      new_ret = 0.0f;
+    }
+    if (lane == 0) {
+      st[ST_SCENE * n_envs + e] = sc;
+      st[ST_STATE * n_envs + e] = s;
+      st[ST_GOAL * n_envs + e] = g;
+      st[ST_OBS * n_envs + e] = os;
+      st[ST_ELAPSED * n_envs + e] = t;
+      if (done && a.autoreset) st[ST_EPISODE * n_envs + e] += 1;
+      a.ep_ret[e] = new_ret;
+      if (bad) atomicOr(a.flags, (uint32_t)VN_FLAG_BAD_ACTION);
+      if (a.reward) a.reward[e] = r;
+      if (a.done) a.done[e] = done ? 1 : 0;
+      if (a.state_out) a.state_out[e] = s;
+      if (a.info_ret) a.info_ret[e] = ret;
+      if (a.info_len) a.info_len[e] = ep_len;
+      if (a.info_term) a.info_term[e] = term_state;
+      if (a.info_trunc) a.info_trunc[e] = (limit && !terminal) ? 1 : 0;
+    }
+  } else if constexpr (MODE == MODE_RESET) {
+    if (a.mask == nullptr || a.mask[e] != 0) {
+      reset_env(a, e, lane, sc, s, g);
+      os = s;
+      if (lane == 0) {
+        st[ST_SCENE * n_envs + e] = sc;
+        st[ST_STATE * n_envs + e] = s;
+        st[ST_GOAL * n_envs + e] = g;
+        st[ST_OBS * n_envs + e] = os;
+        st[ST_ELAPSED * n_envs + e] = 0;
+        st[ST_EPISODE * n_envs + e] += 1;
+        a.ep_ret[e] = 0.0f;
+      }
+    }
+    return;
+  } else {
+    if (lane == 0 && a.state_out) a.state_out[e] = s;
+  }
+
+  const int64_t base = a.scenes[sc].row_base;
+  const int64_t img_row = base + os, goal_row = base + g;
+  if (lane == 0) {
+    if (a.info_img_row) a.info_img_row[e] = (int32_t)img_row;
+    if (a.info_goal_row) a.info_goal_row[e] = (int32_t)goal_row;
+  }
+  if (a.obs != nullptr && a.goal_out != nullptr) {
+    const int64_t F = a.frame_bytes;
+    copy_two_frames<VEC>(a.obs + (int64_t)e * F, a.arena + img_row * F, a.goal_out + (int64_t)e * F,
+                         a.arena + goal_row * F, F, lane);
+  } else if (a.obs != nullptr || a.goal_out != nullptr) {
+    const int64_t F = a.frame_bytes;
+    uint8_t* d = a.obs ? a.obs + (int64_t)e * F : a.goal_out + (int64_t)e * F;
+    const uint8_t* src = a.arena + (a.obs ? img_row : goal_row) * F;
+    for (int64_t i = lane; i < F; i += 64) d[i] = src[i];
+  }
+}
+
+__global__ void synth_frames_kernel(uint8_t* arena, int64_t row_base, int n_rows, int64_t frame_bytes,
+                                    uint32_t scene_id) {
+  const int64_t words = frame_bytes >> 2;
+  const int64_t total = words * n_rows;
+  uint32_t* dst = reinterpret_cast<uint32_t*>(arena + row_base * frame_bytes);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = i / words, w = i - row * words;
+    dst[i] = frame_hash(scene_id, (uint32_t)row, (uint32_t)w);
+  }
+}
+
+__global__ void random_actions_kernel(int32_t* actions, int n, uint32_t k0, uint32_t k1, uint64_t step) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const u32x4 r = philox4x32_10(u32x4{(uint32_t)e, (uint32_t)step, (uint32_t)(step >> 32), STREAM_ACTION}, k0, k1);
+  actions[e] = (int32_t)(r.x >> 30);
+}
+
+}  // namespace vn
+
+using namespace vn;
+
+struct vn_ctx {
+  int device = 0;
+  int n_envs = 0, n_scenes = 0;
+  uint64_t seed = 0;
+  int64_t frame_bytes = 0, n_rows = 0;
+  uint8_t* arena = nullptr;
+  int32_t* graph = nullptr;
+  int32_t* spd = nullptr;
+  SceneDev* scenes = nullptr;
+  std::vector<SceneDev> scenes_host;
+  int32_t* st = nullptr;
+  float* ep_ret = nullptr;
+  int32_t* env_scene = nullptr;
+  int32_t* tasks = nullptr;
+  int n_tasks = 0;
+  int32_t* sched = nullptr;
+  int sched_len = 0;
+  uint32_t* flags = nullptr;
+  int max_steps = 900, autoreset = 1;
+  float* info_ret = nullptr;
+  int32_t* info_len = nullptr;
+  int32_t* info_term = nullptr;
+  uint8_t* info_trunc = nullptr;
+  int32_t* info_img_row = nullptr;
+  int32_t* info_goal_row = nullptr;
+};
+
+namespace {
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int d) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    (void)hipSetDevice(d);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+EnvArgs make_args(vn_ctx* c) {
+  EnvArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.scenes = c->scenes;
+  a.graph = c->graph;
+  a.spd = c->spd;
+  a.arena = c->arena;
+  a.frame_bytes = c->frame_bytes;
+  a.st = c->st;
+  a.ep_ret = c->ep_ret;
+  a.env_scene = c->env_scene;
+  a.tasks = c->tasks;
+  a.sched = c->sched;
+  a.flags = c->flags;
+  a.n_tasks = c->n_tasks;
+  a.sched_len = c->sched_len;
+  a.max_steps = c->max_steps;
+  a.autoreset = c->autoreset;
+  a.n_envs = c->n_envs;
+  a.k0 = (uint32_t)c->seed;
+  a.k1 = (uint32_t)(c->seed >> 32);
+  a.info_ret = c->info_ret;
+  a.info_len = c->info_len;
+  a.info_term = c->info_term;
+  a.info_trunc = c->info_trunc;
+  a.info_img_row = c->info_img_row;
+  a.info_goal_row = c->info_goal_row;
+  return a;
+}
+
+template <int MODE>
+int launch_env(vn_ctx* c, const EnvArgs& a, hipStream_t stream) {
+  const dim3 grid((c->n_envs + kEnvsPerBlock - 1) / kEnvsPerBlock), block(64 * kEnvsPerBlock);
+  const int64_t F = c->frame_bytes;
+  const bool al16 = (F % 16 == 0) && ((uintptr_t)a.obs % 16 == 0) && ((uintptr_t)a.goal_out % 16 == 0);
+  const bool al4 = (F % 4 == 0) && ((uintptr_t)a.obs % 4 == 0) && ((uintptr_t)a.goal_out % 4 == 0);
+  if (al16)
+    hipLaunchKernelGGL((env_kernel<MODE, 16>), grid, block, 0, stream, a);
+  else if (al4)
+    hipLaunchKernelGGL((env_kernel<MODE, 4>), grid, block, 0, stream, a);
+  else
+    hipLaunchKernelGGL((env_kernel<MODE, 1>), grid, block, 0, stream, a);
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
+
+void free_ctx(vn_ctx* c) {
+  if (!c) return;
+  void* ptrs[] = {c->arena, c->graph, c->spd, c->scenes, c->st, c->ep_ret, c->env_scene,
+                  c->tasks, c->sched, c->flags};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  delete c;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* vn_version(void) { return "vnav 0.1.0 gfx950"; }
+
+int vn_last_error(char* buf, size_t len) {
+  if (!buf || len == 0) return VN_EINVAL;
+  const std::string& m = vn::last_error();
+  const size_t n = std::min(len - 1, m.size());
+  std::memcpy(buf, m.data(), n);
+  buf[n] = 0;
+  return VN_OK;
+}
+
+int vn_create(const vn_scene_desc* scenes, int n_scenes, int n_envs, uint64_t seed, int device,
+              vn_ctx** out) {
+  if (!out) return fail(VN_EINVAL, "vn_create: out is NULL");
+  *out = nullptr;
+  if (!scenes || n_scenes <= 0) return fail(VN_EINVAL, "vn_create: need at least one scene");
+  if (n_envs <= 0) return fail(VN_EINVAL, "vn_create: n_envs must be > 0");
+  const int H = scenes[0].height, W = scenes[0].width, C = scenes[0].channels;
+  if (H <= 0 || W <= 0 || C <= 0) return fail(VN_EINVAL, "vn_create: bad frame shape");
+  const int64_t F = (int64_t)H * W * C;
+  int64_t rows = 0, graph_rows = 0, spd_elems = 0;
+  std::vector<SceneDev> sh(n_scenes);
+  for (int k = 0; k < n_scenes; ++k) {
+    const vn_scene_desc& d = scenes[k];
+    if (d.height != H || d.width != W || d.channels != C)
+      return fail(VN_EINVAL, "vn_create: all scenes must share one frame shape");
+    if (d.n_states <= 0 || !d.graph || !d.spd) return fail(VN_EINVAL, "vn_create: scene missing graph/spd");
+    if (!d.observations && (F % 4) != 0)
+      return fail(VN_EINVAL, "vn_create: synthetic frames need frame bytes % 4 == 0");
+    sh[k].row_base = rows;
+    sh[k].graph_off = (int32_t)graph_rows;
+    sh[k].spd_off = spd_elems;
+    sh[k].n = d.n_states;
+    sh[k].r_goal = d.reward_goal;
+    sh[k].r_step = d.reward_step;
+    sh[k].r_coll = d.reward_collision;
+    sh[k].terminal_obs = d.terminal_obs;
+    rows += d.n_states;
+    graph_rows += d.n_states;
+    spd_elems += (int64_t)d.n_states * d.n_states;
+  }
+  if (rows >= (1ll << 31)) return fail(VN_EINVAL, "vn_create: more than 2^31 frames");
+  // Host-side conversion int64 -> int32 with range checks (the h5 datasets are int64).
+  std::vector<int32_t> g32(graph_rows * 4);
+  std::vector<int32_t> spd32(spd_elems);
+  for (int k = 0; k < n_scenes; ++k) {
+    const vn_scene_desc& d = scenes[k];
+    const int64_t n = d.n_states;
+    for (int64_t i = 0; i < n * 4; ++i) {
+      const int64_t v = d.graph[i];
+      if (v < -1 || v >= n) return fail(VN_EINVAL, "vn_create: graph entry out of range");
+      g32[(int64_t)sh[k].graph_off * 4 + i] = (int32_t)v;
+    }
+    for (int64_t i = 0; i < n * n; ++i) {
+      const int64_t v = d.spd[i];
+      spd32[sh[k].spd_off + i] = (int32_t)std::max<int64_t>(std::min<int64_t>(v, INT32_MAX), INT32_MIN);
+    }
+  }
+  DeviceGuard guard(device);
+  vn_ctx* c = new (std::nothrow) vn_ctx();
+  if (!c) return fail(VN_ENOMEM, "vn_create: host allocation failed");
+  c->device = device;
+  c->n_envs = n_envs;
+  c->n_scenes = n_scenes;
+  c->seed = seed;
+  c->frame_bytes = F;
+  c->n_rows = rows;
+  c->scenes_host = sh;
+  auto alloc = [&](void** p, size_t bytes) -> bool {
+    return hipMalloc(p, std::max<size_t>(bytes, 16)) == hipSuccess;
+  };
+  bool ok = alloc((void**)&c->arena, (size_t)(rows * F)) && alloc((void**)&c->graph, g32.size() * 4) &&
+            alloc((void**)&c->spd, spd32.size() * 4) && alloc((void**)&c->scenes, sh.size() * sizeof(SceneDev)) &&
+            alloc((void**)&c->st, (size_t)ST_COUNT * n_envs * 4) && alloc((void**)&c->ep_ret, (size_t)n_envs * 4) &&
+            alloc((void**)&c->env_scene, (size_t)n_envs * 4) && alloc((void**)&c->flags, 4);
+  if (!ok) {
+    free_ctx(c);
+    return fail(VN_ENOMEM, "vn_create: device allocation failed");
+  }
+  hipError_t e = hipSuccess;
+  std::vector<int32_t> es(n_envs);
+  for (int i = 0; i < n_envs; ++i) es[i] = i % n_scenes;
+  if (e == hipSuccess) e = hipMemcpy(c->graph, g32.data(), g32.size() * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(c->spd, spd32.data(), spd32.size() * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(c->scenes, sh.data(), sh.size() * sizeof(SceneDev), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(c->env_scene, es.data(), es.size() * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemset(c->st, 0, (size_t)ST_COUNT * n_envs * 4);
+  if (e == hipSuccess) e = hipMemset(c->ep_ret, 0, (size_t)n_envs * 4);
+  if (e == hipSuccess) e = hipMemset(c->flags, 0, 4);
+  for (int k = 0; k < n_scenes && e == hipSuccess; ++k) {
+    const vn_scene_desc& d = scenes[k];
+    if (d.observations) {
+      e = hipMemcpy(c->arena + sh[k].row_base * F, d.observations, (size_t)d.n_states * F, hipMemcpyHostToDevice);
+    } else {
+      hipLaunchKernelGGL(synth_frames_kernel, dim3(2048), dim3(256), 0, 0, c->arena, sh[k].row_base, d.n_states, F,
+                         d.synth_id);
+      e = hipGetLastError();
+    }
+  }
+  if (e != hipSuccess) {
+    free_ctx(c);
+    return hip_fail(e, "vn_create: upload");
+  }
+  // The constructor's reset (cached.py:36): every env starts from a sampled (start, goal).
+  EnvArgs a = make_args(c);
+  int rc = launch_env<MODE_RESET>(c, a, 0);
+  if (rc == VN_OK) {
+    e = hipDeviceSynchronize();
+    if (e != hipSuccess) rc = hip_fail(e, "vn_create: initial reset");
+  }
+  if (rc != VN_OK) {
+    free_ctx(c);
+    return rc;
+  }
+  *out = c;
+  return VN_OK;
+}
+
+int vn_destroy(vn_ctx* c) {
+  if (!c) return VN_OK;
+  DeviceGuard guard(c->device);
+  (void)hipDeviceSynchronize();
+  free_ctx(c);
+  return VN_OK;
+}
+
+int vn_num_envs(vn_ctx* c) { return c ? c->n_envs : VN_EINVAL; }
+
+int vn_reset(vn_ctx* c, const int32_t* env_mask_dev, vn_stream_t stream) {
+  if (!c) return fail(VN_EINVAL, "vn_reset: NULL ctx");
+  DeviceGuard guard(c->device);
+  EnvArgs a = make_args(c);
+  a.mask = env_mask_dev;
+  return launch_env<MODE_RESET>(c, a, (hipStream_t)stream);
+}
+
+int vn_observe(vn_ctx* c, uint8_t* obs_dev, uint8_t* goal_dev, int32_t* state_dev, vn_stream_t stream) {
+  if (!c) return fail(VN_EINVAL, "vn_observe: NULL ctx");
+  DeviceGuard guard(c->device);
+  EnvArgs a = make_args(c);
+  a.obs = obs_dev;
+  a.goal_out = goal_dev;
+  a.state_out = state_dev;
+  a.info_img_row = nullptr;
+  a.info_goal_row = nullptr;
+  return launch_env<MODE_OBSERVE>(c, a, (hipStream_t)stream);
+}
+
+int vn_step(vn_ctx* c, const int32_t* actions_dev, uint8_t* obs_dev, uint8_t* goal_dev, float* reward_dev,
+            uint8_t* done_dev, int32_t* state_dev, vn_stream_t stream) {
+  if (!c) return fail(VN_EINVAL, "vn_step: NULL ctx");
+  if (!actions_dev) return fail(VN_EINVAL, "vn_step: actions is NULL");
+  DeviceGuard guard(c->device);
+  EnvArgs a = make_args(c);
+  a.actions = actions_dev;
+  a.obs = obs_dev;
+  a.goal_out = goal_dev;
+  a.reward = reward_dev;
+  a.done = done_dev;
+  a.state_out = state_dev;
+  return launch_env<MODE_STEP>(c, a, (hipStream_t)stream);
+}
+
+int vn_set_info_buffers(vn_ctx* c, float* ep_return, int32_t* ep_length, int32_t* terminal_state,
+                        uint8_t* truncated, int32_t* img_row, int32_t* goal_row) {
+  if (!c) return fail(VN_EINVAL, "vn_set_info_buffers: NULL ctx");
+  c->info_ret = ep_return;
+  c->info_len = ep_length;
+  c->info_term = terminal_state;
+  c->info_trunc = truncated;
+  c->info_img_row = img_row;
+  c->info_goal_row = goal_row;
+  return VN_OK;
+}
+
+int vn_set_schedule(vn_ctx* c, const int32_t* start_goal_dev, int len) {
+  if (!c) return fail(VN_EINVAL, "vn_set_schedule: NULL ctx");
+  if (len < 0 || (len > 0 && !start_goal_dev)) return fail(VN_EINVAL, "vn_set_schedule: bad schedule");
+  DeviceGuard guard(c->device);
+  if (c->sched) {
+    VN_HIP(hipDeviceSynchronize());
+    VN_HIP(hipFree(c->sched));
+    c->sched = nullptr;
+  }
+  c->sched_len = 0;
+  if (len > 0) {
+    const size_t bytes = (size_t)c->n_envs * len * 2 * 4;
+    if (hipMalloc((void**)&c->sched, bytes) != hipSuccess) return fail(VN_ENOMEM, "vn_set_schedule: alloc");
+    VN_HIP(hipMemcpy(c->sched, start_goal_dev, bytes, hipMemcpyDefault));
+    c->sched_len = len;
+  }
+  VN_HIP(hipMemset(c->st + (size_t)ST_SCHED * c->n_envs, 0, (size_t)c->n_envs * 4));
+  return VN_OK;
+}
+
+int vn_set_tasks(vn_ctx* c, const int32_t* tasks_host, int n_tasks) {
+  if (!c) return fail(VN_EINVAL, "vn_set_tasks: NULL ctx");
+  if (n_tasks < 0 || (n_tasks > 0 && !tasks_host)) return fail(VN_EINVAL, "vn_set_tasks: bad tasks");
+  for (int t = 0; t < n_tasks; ++t) {
+    const int sc = tasks_host[2 * t], g = tasks_host[2 * t + 1];
+    if (sc < 0 || sc >= c->n_scenes) return fail(VN_EINVAL, "vn_set_tasks: scene out of range");
+    if (g < -1 || g >= c->scenes_host[sc].n) return fail(VN_EINVAL, "vn_set_tasks: goal out of range");
+  }
+  DeviceGuard guard(c->device);
+  if (c->tasks) {
+    VN_HIP(hipDeviceSynchronize());
+    VN_HIP(hipFree(c->tasks));
+    c->tasks = nullptr;
+  }
+  c->n_tasks = 0;
+  if (n_tasks > 0) {
+    if (hipMalloc((void**)&c->tasks, (size_t)n_tasks * 8) != hipSuccess) return fail(VN_ENOMEM, "vn_set_tasks: alloc");
+    VN_HIP(hipMemcpy(c->tasks, tasks_host, (size_t)n_tasks * 8, hipMemcpyHostToDevice));
+    c->n_tasks = n_tasks;
+  }
+  return VN_OK;
+}
+
+int vn_set_env_scenes(vn_ctx* c, const int32_t* env_scene_host) {
+  if (!c || !env_scene_host) return fail(VN_EINVAL, "vn_set_env_scenes: NULL argument");
+  for (int e = 0; e < c->n_envs; ++e)
+    if (env_scene_host[e] < 0 || env_scene_host[e] >= c->n_scenes)
+      return fail(VN_EINVAL, "vn_set_env_scenes: scene out of range");
+  DeviceGuard guard(c->device);
+  VN_HIP(hipMemcpy(c->env_scene, env_scene_host, (size_t)c->n_envs * 4, hipMemcpyHostToDevice));
+  return VN_OK;
+}
+
+int vn_set_max_episode_steps(vn_ctx* c, int max_steps) {
+  if (!c) return fail(VN_EINVAL, "vn_set_max_episode_steps: NULL ctx");
+  c->max_steps = max_steps;
+  return VN_OK;
+}
+
+int vn_set_autoreset(vn_ctx* c, int on) {
+  if (!c) return fail(VN_EINVAL, "vn_set_autoreset: NULL ctx");
+  c->autoreset = on ? 1 : 0;
+  return VN_OK;
+}
+
+int vn_random_actions(vn_ctx* c, int32_t* actions_dev, uint64_t step, vn_stream_t stream) {
+  if (!c || !actions_dev) return fail(VN_EINVAL, "vn_random_actions: NULL argument");
+  DeviceGuard guard(c->device);
+  hipLaunchKernelGGL(random_actions_kernel, dim3((c->n_envs + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     actions_dev, c->n_envs, (uint32_t)c->seed ^ 0xA5A5A5A5u, (uint32_t)(c->seed >> 32), step);
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
+
+int vn_get_state(vn_ctx* c, int32_t* dst, vn_stream_t stream) {
+  if (!c || !dst) return fail(VN_EINVAL, "vn_get_state: NULL argument");
+  DeviceGuard guard(c->device);
+  VN_HIP(hipMemcpyAsync(dst, c->st, (size_t)ST_COUNT * c->n_envs * 4, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return VN_OK;
+}
+
+int vn_set_state(vn_ctx* c, const int32_t* src, vn_stream_t stream) {
+  if (!c || !src) return fail(VN_EINVAL, "vn_set_state: NULL argument");
+  DeviceGuard guard(c->device);
+  VN_HIP(hipMemcpyAsync(c->st, src, (size_t)ST_COUNT * c->n_envs * 4, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return VN_OK;
+}
+
+int vn_frame_arena(vn_ctx* c, const uint8_t** arena, int64_t* frame_bytes, int64_t* n_rows) {
+  if (!c) return fail(VN_EINVAL, "vn_frame_arena: NULL ctx");
+  if (arena) *arena = c->arena;
+  if (frame_bytes) *frame_bytes = c->frame_bytes;
+  if (n_rows) *n_rows = c->n_rows;
+  return VN_OK;
+}
+
+int vn_scene_row_base(vn_ctx* c, int scene, int64_t* row_base) {
+  if (!c || !row_base || scene < 0 || scene >= c->n_scenes) return fail(VN_EINVAL, "vn_scene_row_base: bad args");
+  *row_base = c->scenes_host[scene].row_base;
+  return VN_OK;
+}
+
+int vn_error_flags_sync(vn_ctx* c, uint32_t* flags, int clear) {
+  if (!c || !flags) return fail(VN_EINVAL, "vn_error_flags_sync: NULL argument");
+  DeviceGuard guard(c->device);
+  VN_HIP(hipDeviceSynchronize());
+  VN_HIP(hipMemcpy(flags, c->flags, 4, hipMemcpyDeviceToHost));
+  if (clear) VN_HIP(hipMemset(c->flags, 0, 4));
+  return VN_OK;
+}
+
+}  // extern "C"

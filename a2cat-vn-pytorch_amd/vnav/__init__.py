@@ -1,0 +1,10 @@
+"""vnav — MI355X-native batched cached-scene visual-navigation rollout engine.
+
+Hot path of felipefelixarias/a2cat-vn-pytorch rebuilt for gfx950: the cached-scene
+env.step (VectorEnv, libvnav.so) and the A2C rollout/update of the goal-conditioned
+CNN policy. See DESIGN.md at the repository root.
+"""
+from .scenes import Scene, grid_tables, maze_scene, synthetic_scene, scene_from_arrays  # noqa: F401
+from .envs import VectorEnv, make, to_float_chw  # noqa: F401
+
+__version__ = "0.1.0"

@@ -1,0 +1,239 @@
+"""VectorEnv — the batched cached-scene environment on one GPU.
+
+Drop-in for the deep_rl ``SubprocVecEnv`` of THORDiscreteCachedEnv / THORCachedEnv
+processes (experiments/thor_cached_auxiliary.py:58-71): ``reset()``, ``step(actions)``
+with baselines-style auto-reset, ``call_unwrapped('set_complexity', x)`` and
+``set_hardness``. Every env lives on the device; a step is one HIP launch
+(``vn_step`` in libvnav.so) — there is no per-env process, pipe or host copy.
+
+Observations are the tuple ``(image, goal)`` of uint8 ``[E,H,W,C]`` device tensors (the
+raw cached frames, cached.py:59-60 / gym_thor_cached.py:52-53). The reference
+wrapper chain TransposeImage + ScaledFloatFrame is ``to_float_chw`` below; the policy
+kernels consume the uint8 frames directly and fuse that conversion.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from .scenes import Scene
+
+ST_FIELDS = ("scene", "state", "goal", "obs_state", "elapsed", "episode", "sched_pos")
+
+
+def to_float_chw(frames):
+    """TransposeImage + ScaledFloatFrame: uint8 [...,H,W,C] -> float32 [...,C,H,W] / 255."""
+    return frames.permute(*range(frames.dim() - 3), -1, -3, -2).to(torch.float32) / 255.0
+
+
+class VectorEnv:
+    num_actions = 4  # THORDiscreteCachedEnv.get_action_size (cached.py:66-68)
+
+    def __init__(self, scenes, num_envs, seed=0, device=None, max_episode_steps=900, tasks=None,
+                 env_scenes=None, autoreset=True):
+        if isinstance(scenes, Scene):
+            scenes = [scenes]
+        if not scenes:
+            raise ValueError("VectorEnv needs at least one scene")
+        if not torch.cuda.is_available():
+            raise _lib.VnavError("VectorEnv requires a ROCm GPU (no CPU fallback)")
+        self.lib = _lib.load()
+        self.device = torch.device("cuda", torch.cuda.current_device() if device is None else
+                                   torch.device(device).index or 0)
+        self.scenes = list(scenes)
+        self.num_envs = int(num_envs)
+        self.seed = int(seed)
+        self.frame_shape = tuple(self.scenes[0].frame_shape)
+        descs = (_lib.SceneDesc * len(self.scenes))()
+        self._keep = []
+        for i, s in enumerate(self.scenes):
+            d = descs[i]
+            d.n_states = s.n_states
+            d.height, d.width, d.channels = s.frame_shape
+            d.graph = s.graph.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))
+            d.spd = s.spd.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))
+            if s.observations is not None:
+                d.observations = s.observations.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+            d.reward_goal, d.reward_step, d.reward_collision = s.rewards
+            d.terminal_obs = s.terminal_obs
+            d.synth_id = s.synth_id
+            self._keep.append(s)
+        handle = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.vn_create(descs, len(self.scenes), self.num_envs,
+                                          ctypes.c_uint64(self.seed & (2**64 - 1)),
+                                          self.device.index, ctypes.byref(handle)), "vn_create")
+        self._ctx = handle
+        E = self.num_envs
+        kw = dict(device=self.device)
+        self._info = dict(
+            ep_return=torch.zeros(E, dtype=torch.float32, **kw),
+            ep_length=torch.zeros(E, dtype=torch.int32, **kw),
+            terminal_state=torch.zeros(E, dtype=torch.int32, **kw),
+            truncated=torch.zeros(E, dtype=torch.uint8, **kw),
+            img_row=torch.zeros(E, dtype=torch.int32, **kw),
+            goal_row=torch.zeros(E, dtype=torch.int32, **kw),
+        )
+        i = self._info
+        _lib.check(self.lib.vn_set_info_buffers(self._ctx, _lib.ptr(i["ep_return"]), _lib.ptr(i["ep_length"]),
+                                                _lib.ptr(i["terminal_state"]), _lib.ptr(i["truncated"]),
+                                                _lib.ptr(i["img_row"]), _lib.ptr(i["goal_row"])),
+                   "vn_set_info_buffers")
+        self.set_max_episode_steps(max_episode_steps)
+        if not autoreset:
+            _lib.check(self.lib.vn_set_autoreset(self._ctx, 0), "vn_set_autoreset")
+        if env_scenes is not None:
+            self.set_env_scenes(env_scenes)
+        if tasks:
+            self.set_tasks(tasks)
+        self.complexity = None
+        self._schedule = None
+
+    # -- configuration -------------------------------------------------------
+    def set_max_episode_steps(self, n):
+        _lib.check(self.lib.vn_set_max_episode_steps(self._ctx, int(n or 0)), "vn_set_max_episode_steps")
+
+    def set_tasks(self, tasks):
+        """tasks: [(scene_index, goal_state or -1)] sampled uniformly at each reset."""
+        arr = np.ascontiguousarray(np.asarray(tasks, dtype=np.int32).reshape(-1, 2))
+        _lib.check(self.lib.vn_set_tasks(self._ctx, arr.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), len(arr)),
+                   "vn_set_tasks")
+
+    def set_env_scenes(self, env_scenes):
+        arr = np.ascontiguousarray(np.asarray(env_scenes, dtype=np.int32))
+        if arr.shape != (self.num_envs,):
+            raise ValueError("env_scenes must have one entry per env")
+        _lib.check(self.lib.vn_set_env_scenes(self._ctx, arr.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))),
+                   "vn_set_env_scenes")
+
+    def set_schedule(self, schedule):
+        """Exact-replay test mode: schedule [E, L, 2] int32 (start, goal) per reset."""
+        if schedule is None:
+            _lib.check(self.lib.vn_set_schedule(self._ctx, None, 0), "vn_set_schedule")
+            self._schedule = None
+            return
+        sched = torch.as_tensor(schedule, dtype=torch.int32).to(self.device).contiguous()
+        if sched.dim() != 3 or sched.shape[0] != self.num_envs or sched.shape[2] != 2:
+            raise ValueError("schedule must be [num_envs, L, 2]")
+        torch.cuda.synchronize(self.device)
+        _lib.check(self.lib.vn_set_schedule(self._ctx, _lib.ptr(sched), sched.shape[1]), "vn_set_schedule")
+        self._schedule = sched
+
+    def set_complexity(self, complexity=None):
+        """Curriculum hook (graph/env.py:98-99, experiments/thor_cached_auxiliary.py:68-70).
+        Recorded only: on-device curriculum sampling is a SURVEY §8f 'next' item."""
+        self.complexity = complexity
+
+    set_hardness = set_complexity
+
+    def call_unwrapped(self, name, *args, **kwargs):
+        return getattr(self, name)(*args, **kwargs)
+
+    # -- gym VecEnv API -------------------------------------------------------
+    def _stream(self):
+        return _lib.stream_ptr(self.device)
+
+    def _frames(self):
+        shape = (self.num_envs,) + self.frame_shape
+        return (torch.empty(shape, dtype=torch.uint8, device=self.device),
+                torch.empty(shape, dtype=torch.uint8, device=self.device))
+
+    def reset(self, mask=None):
+        m = None
+        if mask is not None:
+            m = torch.as_tensor(mask, device=self.device).to(torch.int32).contiguous()
+        _lib.check(self.lib.vn_reset(self._ctx, _lib.ptr(m), self._stream()), "vn_reset")
+        return self.observe()
+
+    def observe(self, out=None):
+        img, goal = out if out is not None else self._frames()
+        _lib.check(self.lib.vn_observe(self._ctx, _lib.ptr(img), _lib.ptr(goal), None, self._stream()), "vn_observe")
+        return img, goal
+
+    def step(self, actions, out=None, gather=True):
+        """actions: int32 [E] device tensor (other integer dtypes are converted).
+        Returns ((image, goal), reward f32 [E], done bool [E], info dict of [E] tensors).
+        ``out`` = dict of preallocated outputs (image, goal, reward, done, state) to write
+        in place; ``gather=False`` skips the frame copy (index-only step: info img_row /
+        goal_row address the frames in the scene cache)."""
+        a = torch.as_tensor(actions, device=self.device)
+        if a.dtype != torch.int32:
+            a = a.to(torch.int32)
+        a = a.contiguous()
+        if a.shape != (self.num_envs,):
+            raise ValueError("actions must have shape [num_envs]")
+        if out is None:
+            img, goal = self._frames() if gather else (None, None)
+            reward = torch.empty(self.num_envs, dtype=torch.float32, device=self.device)
+            done = torch.empty(self.num_envs, dtype=torch.bool, device=self.device)
+            state = torch.empty(self.num_envs, dtype=torch.int32, device=self.device)
+        else:
+            img, goal = (out["image"], out["goal"]) if gather else (None, None)
+            reward, done, state = out["reward"], out["done"], out["state"]
+        _lib.check(self.lib.vn_step(self._ctx, _lib.ptr(a), _lib.ptr(img), _lib.ptr(goal), _lib.ptr(reward),
+                                    _lib.ptr(done), _lib.ptr(state), self._stream()), "vn_step")
+        info = dict(self._info)
+        info["state"] = state
+        return (img, goal), reward, done, info
+
+    def random_actions(self, step, out=None):
+        out = torch.empty(self.num_envs, dtype=torch.int32, device=self.device) if out is None else out
+        _lib.check(self.lib.vn_random_actions(self._ctx, _lib.ptr(out), ctypes.c_uint64(int(step)), self._stream()),
+                   "vn_random_actions")
+        return out
+
+    # -- state / checkpoint ----------------------------------------------------
+    def get_state(self):
+        buf = torch.empty((len(ST_FIELDS), self.num_envs), dtype=torch.int32, device=self.device)
+        _lib.check(self.lib.vn_get_state(self._ctx, _lib.ptr(buf), self._stream()), "vn_get_state")
+        return buf
+
+    def set_state(self, buf):
+        buf = buf.to(device=self.device, dtype=torch.int32).contiguous()
+        _lib.check(self.lib.vn_set_state(self._ctx, _lib.ptr(buf), self._stream()), "vn_set_state")
+
+    def frame_arena(self):
+        """(arena uint8 tensor view [rows, H, W, C] over the scene cache, row bases per scene)."""
+        p, fb, rows = ctypes.c_void_p(), ctypes.c_int64(), ctypes.c_int64()
+        _lib.check(self.lib.vn_frame_arena(self._ctx, ctypes.byref(p), ctypes.byref(fb), ctypes.byref(rows)),
+                   "vn_frame_arena")
+        bases = []
+        for k in range(len(self.scenes)):
+            b = ctypes.c_int64()
+            _lib.check(self.lib.vn_scene_row_base(self._ctx, k, ctypes.byref(b)), "vn_scene_row_base")
+            bases.append(b.value)
+        return p.value, fb.value, rows.value, bases
+
+    def error_flags(self, clear=True):
+        f = ctypes.c_uint32()
+        _lib.check(self.lib.vn_error_flags_sync(self._ctx, ctypes.byref(f), int(clear)), "vn_error_flags_sync")
+        return f.value
+
+    def close(self):
+        if getattr(self, "_ctx", None):
+            self.lib.vn_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+# gym-style registry mirroring environments.make ids (environments/__init__.py:2,
+# environments/gym_ai2thor/__init__.py:45-49, environments/gym_graph/__init__.py:18-27)
+REGISTRY = {
+    "CachedThor-v0": dict(max_episode_steps=900),
+    "AuxiliaryGraph-v0": dict(max_episode_steps=900),
+    "OrientedGraph-v0": dict(max_episode_steps=900),
+}
+
+
+def make(id, scenes, num_envs, **kwargs):
+    if id not in REGISTRY:
+        raise KeyError("unknown env id %r (known: %s)" % (id, sorted(REGISTRY)))
+    opts = dict(REGISTRY[id])
+    opts.update(kwargs)
+    return VectorEnv(scenes, num_envs, **opts)

@@ -1,0 +1,150 @@
+/*
+ * vnav.h — C ABI of libvnav.so, the MI355X-native batched cached-scene
+ * visual-navigation engine (env.step hot path + A2C policy kernels).
+ *
+ * Every entry point returns 0 on success or a negative VN_E* code; the text of
+ * the last error of the calling thread is available from vn_last_error().
+ * Device buffers are caller-owned (e.g. torch tensors) and passed as raw
+ * pointers; the library owns only the scene cache, per-env state and RNG keys.
+ * All launches are stream-ordered and asynchronous; nothing here synchronises
+ * the device except the explicitly named *_sync getters. A context is bound to
+ * one GPU and is not thread-safe.
+ *
+ * Reference interfaces each group replaces (paths inside the reference repo
+ * felipefelixarias/a2cat-vn-pytorch):
+ *   vn_create/vn_destroy  <- THORDiscreteCachedEnv.__init__ loading the h5
+ *                            datasets (environments/gym_ai2thor/envs/cached.py:19-36)
+ *                            and THORCachedEnv.ensure_scene_loaded
+ *                            (environments/gym_thor_cached.py:25-35)
+ *   vn_reset              <- THORDiscreteCachedEnv.reset / _get_random_start_goal_tuple
+ *                            (cached.py:38-57), THORCachedEnv.reset (gym_thor_cached.py:45-50)
+ *   vn_observe            <- _render_observation / observe (cached.py:59-60,
+ *                            gym_thor_cached.py:52-53)
+ *   vn_step               <- THORDiscreteCachedEnv.step (cached.py:74-99) batched as the
+ *                            deep_rl SubprocVecEnv.step with auto-reset
+ *                            (experiments/thor_cached_auxiliary.py:66-67) and gym's
+ *                            TimeLimit(max_episode_steps=900)
+ *                            (environments/gym_ai2thor/__init__.py:45-49)
+ *   vn_policy_*           <- BigGoalHouseModel trunk + heads (models/goal.py:36-59,77-92)
+ *   vn_a2c_*              <- the deep_rl A2C update used by the Trainer
+ *                            (experiments/thor_cached_auxiliary.py:26-42)
+ */
+#ifndef VNAV_H
+#define VNAV_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct vn_ctx vn_ctx;
+typedef void* vn_stream_t; /* a hipStream_t; NULL = the null stream */
+
+enum {
+  VN_OK = 0,
+  VN_EINVAL = -1,   /* bad argument */
+  VN_EHIP = -2,     /* HIP runtime error */
+  VN_ENOMEM = -3,   /* device allocation failed */
+  VN_ESTATE = -4,   /* call not valid in the context's current state */
+};
+
+/* Device-side error flags (sticky; read with vn_error_flags_sync). */
+enum {
+  VN_FLAG_BAD_ACTION = 1u << 0,     /* an action outside [0,4) was treated as a blocked move */
+  VN_FLAG_RESET_EXHAUSTED = 1u << 1,/* no start with spd[s][g] > 0 found within the bounded search */
+  VN_FLAG_BAD_SCHEDULE = 1u << 2,   /* a schedule entry was out of range */
+};
+
+/* One cached scene (the h5 layout written by graph/util.py:202-247):
+ *   graph        [N][4] int64, -1 = blocked (row convention util.py:212-218,231-232)
+ *   spd          [N][N] int64 shortest_path_distance (used by reset, cached.py:43)
+ *   observations [N][H][W][C] uint8, or NULL to synthesise frames on the device
+ *                from the counter hash (scene_id, state, word) documented in DESIGN.md
+ * Rewards follow reward_configuration (cached.py:70-72, 84-88): a plain move
+ * returns reward_step (cached.py uses -0.0), reaching the goal reward_goal, a
+ * blocked move reward_collision. terminal_obs = 0 re-emits the previous
+ * observation on a terminal step (cached.py:90-96); 1 emits the goal-state frame
+ * (graph/env.py:130-133). */
+typedef struct vn_scene_desc {
+  int32_t n_states;
+  int32_t height, width, channels;
+  const int64_t* graph;
+  const int64_t* spd;
+  const uint8_t* observations;
+  float reward_goal;
+  float reward_step;
+  float reward_collision;
+  int32_t terminal_obs;
+  uint32_t synth_id; /* scene id fed to the frame hash when observations == NULL */
+} vn_scene_desc;
+
+/* ---- environment ------------------------------------------------------- */
+
+int vn_create(const vn_scene_desc* scenes, int n_scenes, int n_envs, uint64_t seed,
+              int device, vn_ctx** out);
+int vn_destroy(vn_ctx* ctx);
+
+/* Re-sample (scene, start, goal) for every env whose env_mask_dev[e] != 0
+ * (NULL = all envs). */
+int vn_reset(vn_ctx* ctx, const int32_t* env_mask_dev, vn_stream_t stream);
+
+/* Write the current (image, goal) frames, [n_envs][H][W][C] uint8 each, and the
+ * current state index per env; any output may be NULL. */
+int vn_observe(vn_ctx* ctx, uint8_t* obs_dev, uint8_t* goal_dev, int32_t* state_dev,
+               vn_stream_t stream);
+
+/* One batched env.step. actions_dev: [n_envs] int32. Outputs per env: the
+ * (image, goal) frames (NULL skips the gather: index-only step), reward f32,
+ * done u8, state int32 (after any auto-reset). */
+int vn_step(vn_ctx* ctx, const int32_t* actions_dev, uint8_t* obs_dev, uint8_t* goal_dev,
+            float* reward_dev, uint8_t* done_dev, int32_t* state_dev, vn_stream_t stream);
+
+/* Optional persistent per-env info outputs written by every vn_step (any may be NULL):
+ *   ep_return/ep_length: the finished episode's sum of rewards / length where done
+ *     (RewardCollector statistics, experiments/thor_cached_auxiliary.py:60);
+ *   terminal_state: the state index the single env returned as its terminal state;
+ *   truncated: 1 where done came from the TimeLimit only;
+ *   img_row/goal_row: global frame rows (arena rows, see vn_frame_arena) of the
+ *     emitted frames — the zero-copy handle the fused policy input gather uses. */
+int vn_set_info_buffers(vn_ctx* ctx, float* ep_return, int32_t* ep_length,
+                        int32_t* terminal_state, uint8_t* truncated, int32_t* img_row,
+                        int32_t* goal_row);
+
+/* Test-mode exact replay: schedule_dev [n_envs][len][2] = (start, goal) consumed in
+ * order by each env's subsequent resets (then back to the RNG). len = 0 clears. */
+int vn_set_schedule(vn_ctx* ctx, const int32_t* start_goal_dev, int len);
+
+/* Multi-scene tasks (gym_thor_cached.py:45-50): tasks_host [n][2] = (scene, goal);
+ * goal = -1 draws a uniform goal. n = 0 restores fixed env->scene assignment. */
+int vn_set_tasks(vn_ctx* ctx, const int32_t* tasks_host, int n_tasks);
+/* Fixed env -> scene assignment (default e mod n_scenes). */
+int vn_set_env_scenes(vn_ctx* ctx, const int32_t* env_scene_host);
+int vn_set_max_episode_steps(vn_ctx* ctx, int max_steps); /* <= 0: no limit */
+int vn_set_autoreset(vn_ctx* ctx, int on);                /* default on */
+
+/* Synthetic uniform actions in [0,4) from Philox(seed, env, step). */
+int vn_random_actions(vn_ctx* ctx, int32_t* actions_dev, uint64_t step, vn_stream_t stream);
+
+/* Per-env state tensors (device, [n_envs] int32 each): for checkpoint/resume and tests.
+ * Order: scene, state, goal, obs_state, elapsed, episode(reset count), sched_pos. */
+int vn_get_state(vn_ctx* ctx, int32_t* dst_dev_7xE, vn_stream_t stream);
+int vn_set_state(vn_ctx* ctx, const int32_t* src_dev_7xE, vn_stream_t stream);
+
+/* Scene-cache arena: all scenes' frames back to back, row = frame. */
+int vn_frame_arena(vn_ctx* ctx, const uint8_t** arena_dev, int64_t* frame_bytes,
+                   int64_t* n_rows);
+int vn_scene_row_base(vn_ctx* ctx, int scene, int64_t* row_base);
+
+int vn_error_flags_sync(vn_ctx* ctx, uint32_t* flags, int clear);
+int vn_num_envs(vn_ctx* ctx);
+
+/* Copy the message of the calling thread's last error (NUL-terminated). */
+int vn_last_error(char* buf, size_t len);
+const char* vn_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VNAV_H */

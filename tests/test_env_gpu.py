@@ -1,0 +1,262 @@
+"""VectorEnv (libvnav.so vn_step) on the GPU vs the reference goldens and the oracle.
+
+Bit-exact: states, done, reward bits, emitted frame indices and the gathered bytes.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import envs as oe
+from oracle import graph as og
+from oracle.frames import synth_frames
+
+pytestmark = pytest.mark.gpu
+
+FRAME = (84, 84, 3)
+
+
+def _vnav():
+    import vnav
+    return vnav
+
+
+def golden_scenes(golden):
+    vnav = _vnav()
+    h = golden("h5_scenes.npz")
+    out = []
+    for k in range(3):
+        frames = synth_frames(100 + k, np.arange(len(h["graph%d" % k])), FRAME)
+        out.append(vnav.scene_from_arrays(h["graph%d" % k], h["spd%d" % k], frames))
+    return out
+
+
+def test_golden_replay_autoreset(golden):
+    vnav = _vnav()
+    d = golden("cached_env.npz")
+    sc = golden_scenes(golden)
+    cases = [0, 1, 2]
+    metas = [d["c%d_meta" % c] for c in cases]
+    n_steps = int(metas[0][3])
+    L = max(len(d["c%d_resets" % c]) for c in cases) - 1
+    sched = np.zeros((len(cases), L, 2), dtype=np.int32)
+    for i, c in enumerate(cases):
+        r = d["c%d_resets" % c][1:]
+        sched[i, : len(r)] = r
+        sched[i, len(r):] = r[-1]
+    env = vnav.VectorEnv(sc, len(cases), seed=1, env_scenes=[int(m[0]) for m in metas], max_episode_steps=0)
+    env.set_schedule(sched)
+    img, goal = env.reset()
+    for i, c in enumerate(cases):
+        frames = sc[int(metas[i][0])].observations
+        assert np.array_equal(img[i].cpu().numpy(), frames[d["c%d_first_img_idx" % c][0]])
+    k = [1] * len(cases)
+    acts = np.stack([d["c%d_actions" % c] for c in cases], 1)
+    for t in range(n_steps):
+        (img, goal), reward, done, info = env.step(torch.as_tensor(acts[t], device="cuda"))
+        img, goal = img.cpu().numpy(), goal.cpu().numpy()
+        rb = reward.cpu().numpy().view(np.uint32)
+        dn = done.cpu().numpy()
+        st = info["state"].cpu().numpy()
+        ts = info["terminal_state"].cpu().numpy()
+        for i, c in enumerate(cases):
+            p = "c%d_" % c
+            frames = sc[int(metas[i][0])].observations
+            assert rb[i] == d[p + "reward_bits"][t], (c, t)
+            assert bool(dn[i]) == bool(d[p + "dones"][t]), (c, t)
+            assert ts[i] == d[p + "img_idx"][t], (c, t)
+            if dn[i]:
+                s0, g0 = d[p + "resets"][k[i] + 1]
+                k[i] += 1
+                assert st[i] == s0
+                assert np.array_equal(img[i], frames[s0]) and np.array_equal(goal[i], frames[g0])
+            else:
+                assert st[i] == d[p + "states"][t], (c, t)
+                assert np.array_equal(img[i], frames[d[p + "img_idx"][t]]), (c, t)
+                assert np.array_equal(goal[i], frames[d[p + "goal_idx"][t]]), (c, t)
+    assert env.error_flags() == 0
+
+
+def test_golden_no_reset_last_state_quirk(golden):
+    vnav = _vnav()
+    d = golden("cached_env.npz")
+    sc = golden_scenes(golden)
+    p = "c3_"
+    scene = int(d[p + "meta"][0])
+    env = vnav.VectorEnv(sc, 1, seed=2, env_scenes=[scene], max_episode_steps=0, autoreset=False)
+    env.set_schedule(d[p + "resets"][1:][None].astype(np.int32))
+    env.reset()
+    frames = sc[scene].observations
+    for t, a in enumerate(d[p + "actions"]):
+        (img, goal), reward, done, info = env.step(torch.tensor([int(a)], device="cuda"))
+        assert info["state"].item() == d[p + "states"][t]
+        assert reward.cpu().numpy().view(np.uint32)[0] == d[p + "reward_bits"][t]
+        assert bool(done.item()) == bool(d[p + "dones"][t])
+        assert np.array_equal(img[0].cpu().numpy(), frames[d[p + "img_idx"][t]])
+        assert np.array_equal(goal[0].cpu().numpy(), frames[d[p + "goal_idx"][t]])
+
+
+def small_scenes(shape=(6, 10, 3)):
+    vnav = _vnav()
+    out = []
+    for k, (X, Y, p) in enumerate([(6, 8, 0.3), (5, 5, 0.0), (7, 4, 0.25)]):
+        maze = np.random.RandomState(40 + k).rand(X, Y) >= p
+        graph, spd, _ = og.h5_tables(maze)
+        frames = synth_frames(7 + k, np.arange(len(graph)), shape)
+        out.append(vnav.scene_from_arrays(graph, spd, frames))
+    return out
+
+
+def oracle_of(scenes, n, seed, **kw):
+    sd = [dict(graph=s.graph, spd=s.spd, rewards=s.rewards, terminal_obs=s.terminal_obs) for s in scenes]
+    return oe.VectorEnvOracle(sd, n, seed, **kw)
+
+
+def compare_step(env_out, o, arena, tag):
+    (img, goal), reward, done, info = env_out
+    assert np.array_equal(reward.cpu().numpy().view(np.uint32), o["reward"].view(np.uint32)), tag
+    assert np.array_equal(done.cpu().numpy(), o["done"]), tag
+    assert np.array_equal(info["state"].cpu().numpy(), o["state"]), tag
+    assert np.array_equal(info["img_row"].cpu().numpy(), o["img_row"]), tag
+    assert np.array_equal(info["goal_row"].cpu().numpy(), o["goal_row"]), tag
+    assert np.array_equal(info["ep_length"].cpu().numpy(), o["ep_length"]), tag
+    assert np.array_equal(info["terminal_state"].cpu().numpy(), o["terminal_state"]), tag
+    assert np.array_equal(info["truncated"].cpu().numpy().astype(bool), o["truncated"]), tag
+    assert np.array_equal(info["ep_return"].cpu().numpy().view(np.uint32), o["ep_return"].view(np.uint32)), tag
+    if img is not None:
+        assert np.array_equal(img.cpu().numpy(), arena[o["img_row"]]), tag
+        assert np.array_equal(goal.cpu().numpy(), arena[o["goal_row"]]), tag
+
+
+@pytest.mark.parametrize("mode", ["env_scene", "tasks"])
+def test_vector_env_matches_oracle(mode):
+    vnav = _vnav()
+    sc = small_scenes()
+    arena = np.concatenate([s.observations for s in sc])
+    n = 1000
+    kw = dict(max_episode_steps=25)
+    tasks = None
+    if mode == "tasks":
+        tasks = [(0, 3), (2, -1), (1, 9), (0, -1)]
+    env = vnav.VectorEnv(sc, n, seed=12345, tasks=tasks, **kw)
+    o = oracle_of(sc, n, 12345, max_steps=25, tasks=tasks)
+    if tasks:  # the constructor reset ran before the tasks were set: re-draw both sides
+        env.reset()
+        o.reset()
+    obs = env.observe()
+    ob = o.observe()
+    assert np.array_equal(obs[0].cpu().numpy(), arena[ob["img_row"]])
+    rng = np.random.RandomState(0)
+    for t in range(120):
+        a = rng.randint(0, 4, size=n).astype(np.int32)
+        if t % 37 == 5:
+            a[::97] = -1
+            a[1::101] = 4
+        out = env.step(torch.as_tensor(a, device="cuda"))
+        compare_step(out, o.step(a), arena, (mode, t))
+    assert env.error_flags() == o.flags == oe.FLAG_BAD_ACTION
+
+
+def test_index_only_step_and_masked_reset():
+    vnav = _vnav()
+    sc = small_scenes()
+    n = 300
+    env = vnav.VectorEnv(sc, n, seed=9, max_episode_steps=40)
+    o = oracle_of(sc, n, 9, max_steps=40)
+    arena = np.concatenate([s.observations for s in sc])
+    rng = np.random.RandomState(1)
+    for t in range(60):
+        a = rng.randint(0, 4, size=n).astype(np.int32)
+        out = env.step(torch.as_tensor(a, device="cuda"), gather=(t % 2 == 0))
+        compare_step(out, o.step(a), arena, t)
+        if t == 30:
+            mask = np.zeros(n, dtype=bool)
+            mask[::3] = True
+            env.reset(torch.as_tensor(mask, device="cuda"))
+            o.reset(mask)
+
+
+def test_full_size_synthetic_scenes():
+    """4096 envs, 4 synthetic 24x24 scenes, 84x84 frames synthesised on the device."""
+    vnav = _vnav()
+    sc = [vnav.synthetic_scene(k) for k in range(4)]
+    n = 4096
+    env = vnav.VectorEnv(sc, n, seed=77)
+    o = oracle_of(sc, n, 77, max_steps=900)
+    bases = np.concatenate([[0], np.cumsum([s.n_states for s in sc])[:-1]])
+    rng = np.random.RandomState(3)
+    sample = rng.choice(n, 64, replace=False)
+    for t in range(40):
+        a = rng.randint(0, 4, size=n).astype(np.int32)
+        (img, goal), reward, done, info = env.step(torch.as_tensor(a, device="cuda"))
+        ob = o.step(a)
+        assert np.array_equal(info["state"].cpu().numpy(), ob["state"])
+        assert np.array_equal(done.cpu().numpy(), ob["done"])
+        assert np.array_equal(reward.cpu().numpy().view(np.uint32), ob["reward"].view(np.uint32))
+        assert np.array_equal(info["img_row"].cpu().numpy(), ob["img_row"])
+        if t % 10 == 0:
+            im = img[torch.as_tensor(sample, device="cuda")].cpu().numpy()
+            gl = goal[torch.as_tensor(sample, device="cuda")].cpu().numpy()
+            for j, e in enumerate(sample):
+                k = int(o.scene[e])
+                row_i, row_g = ob["img_row"][e] - bases[k], ob["goal_row"][e] - bases[k]
+                assert np.array_equal(im[j], synth_frames(k, [row_i], FRAME)[0])
+                assert np.array_equal(gl[j], synth_frames(k, [row_g], FRAME)[0])
+
+
+def test_maze_config_c1(golden):
+    """SimpleGraphEnv maze (graph/env.py) through the engine, replaying the golden starts."""
+    vnav = _vnav()
+    m = golden("maze.npz")
+    maze, goal = m["maze"], tuple(m["goal"].tolist())
+    scene = vnav.maze_scene(maze, goal)
+    lookup = {p: i for i, p in enumerate(scene.locations)}
+    g = scene.goals[0]
+    starts = [lookup[tuple(s)] for s in m["m_starts"].tolist()]
+    env = vnav.VectorEnv([scene], 1, seed=0, tasks=[(0, g)], max_episode_steps=0)
+    env.set_schedule(np.array([[(s, g) for s in starts]], dtype=np.int32))
+    img, _ = env.reset()
+    assert np.array_equal(img[0].cpu().numpy().astype(np.float32) / 255.0, m["m_obs0"])
+    k = 0
+    for t, a in enumerate(m["m_actions"]):
+        (img, _), reward, done, info = env.step(torch.tensor([int(a)], device="cuda"))
+        assert reward.cpu().numpy().view(np.uint32)[0] == m["m_reward_bits"][t]
+        assert bool(done.item()) == bool(m["m_dones"][t])
+        ts = int(info["terminal_state"].item())
+        assert scene.locations[ts] == tuple(m["m_states"][t])
+        frame = scene.observations[ts].astype(np.float32) / 255.0
+        assert np.array_equal(frame, m["m_obs"][t])
+        if done.item():
+            k += 1
+            assert info["state"].item() == starts[k]
+
+
+def test_reset_exhausted_flag():
+    vnav = _vnav()
+    # state 2 is unreachable from everything: spd[:, 2] <= 0
+    graph = np.array([[1, -1, -1, -1], [0, -1, -1, -1], [-1, -1, -1, -1]], dtype=np.int64)
+    spd = np.array([[0, 1, -1], [1, 0, -1], [-1, -1, 0]], dtype=np.int64)
+    frames = synth_frames(1, np.arange(3), (4, 4, 4))
+    scene = vnav.scene_from_arrays(graph, spd, frames)
+    env = vnav.VectorEnv([scene], 64, seed=5, tasks=[(0, 2)])
+    env.reset()
+    torch.cuda.synchronize()
+    assert env.error_flags() & oe.FLAG_RESET_EXHAUSTED
+
+
+def test_state_checkpoint_roundtrip():
+    vnav = _vnav()
+    sc = small_scenes()
+    env = vnav.VectorEnv(sc, 257, seed=31, max_episode_steps=15)
+    acts = [env.random_actions(t).clone() for t in range(40)]
+    for t in range(10):
+        env.step(acts[t])
+    saved = env.get_state().clone()
+    ret = env._info["ep_return"].clone()
+    first = [env.step(acts[t], gather=False) for t in range(10, 40)]
+    first = [(r.clone(), d.clone(), i["state"].clone()) for (_, r, d, i) in first]
+    env.set_state(saved)
+    for t in range(10, 40):
+        _, r, d, i = env.step(acts[t], gather=False)
+        r0, d0, s0 = first[t - 10]
+        assert torch.equal(r, r0) and torch.equal(d, d0) and torch.equal(i["state"], s0)
+    assert ret.shape[0] == 257
