@@ -1,0 +1,244 @@
+// vn_a2c.hip — the A2C pieces around the policy on gfx950: categorical sampling,
+// n-step returns, the loss gradient w.r.t. the head outputs, the global gradient norm
+// and the fused clip + RMSprop step.
+//
+// Contract (DESIGN.md "A2C contract"; parity unpinned at this level because the
+// reference's trainer is the absent deep-rl==0.2.9, experiments/thor_cached_auxiliary.py:26-42):
+//   R_T = V(s_T); R_t = r_t + gamma R_{t+1} (1 - done_t); A_t = R_t - V(s_t)
+//   L = vc mean(A^2) - mean(A.detach() log pi(a_t)) - ec mean(H(pi))
+//   clip_grad_norm_(max_norm) then RMSprop(lr, alpha, eps) with torch's update rule.
+#include <hip/hip_runtime.h>
+
+#include "vn_common.h"
+
+namespace vn {
+
+constexpr int OUT_LD_A2C = 8;
+
+__device__ __forceinline__ void softmax_stats(const float* lg, int A, float* p, float* logp, float& H) {
+  float mx = lg[0];
+  for (int j = 1; j < A; ++j) mx = fmaxf(mx, lg[j]);
+  float s = 0.0f;
+  for (int j = 0; j < A; ++j) s += expf(lg[j] - mx);
+  const float ls = logf(s);
+  H = 0.0f;
+  for (int j = 0; j < A; ++j) {
+    logp[j] = lg[j] - mx - ls;
+    p[j] = expf(logp[j]);
+    H -= p[j] * logp[j];
+  }
+}
+
+__global__ void sample_kernel(const float* __restrict__ out, int n, int A, uint32_t k0, uint32_t k1, uint64_t ctr,
+                              int32_t* actions, float* logp_out, float* ent_out, float* value_out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float lg[7], p[7], lp[7], H;
+  for (int j = 0; j < A; ++j) lg[j] = out[(int64_t)i * OUT_LD_A2C + j];
+  softmax_stats(lg, A, p, lp, H);
+  const u32x4 r = philox4x32_10(u32x4{(uint32_t)i, (uint32_t)ctr, (uint32_t)(ctr >> 32), STREAM_POLICY}, k0, k1);
+  const float u = (float)(r.x >> 8) * (1.0f / 16777216.0f);
+  int a = A - 1;
+  float c = 0.0f;
+  for (int j = 0; j < A - 1; ++j) {
+    c += p[j];
+    if (u < c) {
+      a = j;
+      break;
+    }
+  }
+  actions[i] = a;
+  if (logp_out) logp_out[i] = lp[a];
+  if (ent_out) ent_out[i] = H;
+  if (value_out) value_out[i] = out[(int64_t)i * OUT_LD_A2C + A];
+}
+
+__global__ void greedy_kernel(const float* __restrict__ out, int n, int A, int32_t* actions) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int a = 0;
+  float best = out[(int64_t)i * OUT_LD_A2C];
+  for (int j = 1; j < A; ++j) {
+    const float v = out[(int64_t)i * OUT_LD_A2C + j];
+    if (v > best) {
+      best = v;
+      a = j;
+    }
+  }
+  actions[i] = a;
+}
+
+__global__ void returns_kernel(const float* __restrict__ rewards, const uint8_t* __restrict__ dones,
+                               const float* __restrict__ boot_out, int T, int E, int A, float gamma, float* returns) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  float R = boot_out[(int64_t)e * OUT_LD_A2C + A];
+  for (int t = T - 1; t >= 0; --t) {
+    const int64_t i = (int64_t)t * E + e;
+    R = rewards[i] + gamma * R * (1.0f - (float)dones[i]);
+    returns[i] = R;
+  }
+}
+
+// dL/d(head outputs) for L = vc mean(A^2) - mean(A logp_a) - ec mean(H); stats += block sums of
+// (A^2, -A logp_a, H, R).
+__global__ __launch_bounds__(256) void loss_grad_kernel(const float* __restrict__ out, const int32_t* __restrict__ actions,
+                                                        const float* __restrict__ returns, int n, int A, float vc,
+                                                        float ec, float inv_n, float* dout, float* stats) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (i < n) {
+    float lg[7], p[7], lp[7], H;
+    for (int j = 0; j < A; ++j) lg[j] = out[(int64_t)i * OUT_LD_A2C + j];
+    softmax_stats(lg, A, p, lp, H);
+    const int a = actions[i];
+    const float R = returns[i];
+    const float V = out[(int64_t)i * OUT_LD_A2C + A];
+    const float adv = R - V;
+    for (int j = 0; j < A; ++j) {
+      const float ind = (j == a) ? 1.0f : 0.0f;
+      dout[(int64_t)i * OUT_LD_A2C + j] = (-adv * (ind - p[j]) + ec * p[j] * (lp[j] + H)) * inv_n;
+    }
+    dout[(int64_t)i * OUT_LD_A2C + A] = vc * (-2.0f * adv) * inv_n;
+    for (int j = A + 1; j < OUT_LD_A2C; ++j) dout[(int64_t)i * OUT_LD_A2C + j] = 0.0f;
+    s0 = adv * adv;
+    s1 = -adv * lp[a];
+    s2 = H;
+    s3 = R;
+  }
+  __shared__ float red[4][4];
+  for (int off = 32; off > 0; off >>= 1) {
+    s0 += __shfl_down(s0, off);
+    s1 += __shfl_down(s1, off);
+    s2 += __shfl_down(s2, off);
+    s3 += __shfl_down(s3, off);
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[w][0] = s0;
+    red[w][1] = s1;
+    red[w][2] = s2;
+    red[w][3] = s3;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    const float v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    atomicAdd(&stats[threadIdx.x], v);
+  }
+}
+
+constexpr int kNormBlocks = 512;
+
+__global__ __launch_bounds__(256) void sumsq_partial_kernel(const float* __restrict__ g, int64_t n, float scale,
+                                                            double* partial) {
+  double s = 0.0;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float v = g[i] * scale;
+    s += (double)v * (double)v;
+  }
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off);
+  __shared__ double red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+// scalars[0] = total norm, scalars[1] = clip coefficient (torch clip_grad_norm_: max_norm / (norm + 1e-6), <= 1)
+__global__ void norm_final_kernel(const double* partial, int nb, float max_norm, float* scalars) {
+  __shared__ double red[256];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < nb; i += 256) s += partial[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float norm = (float)sqrt(red[0]);
+    scalars[0] = norm;
+    scalars[1] = max_norm > 0.0f ? fminf(max_norm / (norm + 1e-6f), 1.0f) : 1.0f;
+  }
+}
+
+__global__ __launch_bounds__(256) void rmsprop_kernel(float* __restrict__ params, const float* __restrict__ grads,
+                                                      float* __restrict__ sq, int64_t n, float scale,
+                                                      const float* __restrict__ scalars, float lr, float alpha,
+                                                      float eps) {
+  const float coef = scalars[1] * scale;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float g = grads[i] * coef;
+    const float s = sq[i] * alpha + (1.0f - alpha) * g * g;
+    sq[i] = s;
+    params[i] += -lr * (g / (sqrtf(s) + eps));
+  }
+}
+
+}  // namespace vn
+
+using namespace vn;
+
+extern "C" {
+
+int vn_policy_sample(const float* out, int n, int num_actions, uint64_t seed, uint64_t counter, int32_t* actions,
+                     float* logp, float* entropy, float* value, vn_stream_t stream) {
+  if (!out || !actions || n <= 0 || num_actions < 1 || num_actions > 7)
+    return fail(VN_EINVAL, "vn_policy_sample: bad args");
+  hipLaunchKernelGGL(sample_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, out, n, num_actions,
+                     (uint32_t)seed, (uint32_t)(seed >> 32), counter, actions, logp, entropy, value);
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
+
+int vn_policy_greedy(const float* out, int n, int num_actions, int32_t* actions, vn_stream_t stream) {
+  if (!out || !actions || n <= 0 || num_actions < 1 || num_actions > 7)
+    return fail(VN_EINVAL, "vn_policy_greedy: bad args");
+  hipLaunchKernelGGL(greedy_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, out, n, num_actions,
+                     actions);
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
+
+int vn_a2c_returns(const float* rewards, const uint8_t* dones, const float* bootstrap_out, int T, int E,
+                   int num_actions, float gamma, float* returns, vn_stream_t stream) {
+  if (!rewards || !dones || !bootstrap_out || !returns || T <= 0 || E <= 0)
+    return fail(VN_EINVAL, "vn_a2c_returns: bad args");
+  hipLaunchKernelGGL(returns_kernel, dim3((E + 255) / 256), dim3(256), 0, (hipStream_t)stream, rewards, dones,
+                     bootstrap_out, T, E, num_actions, gamma, returns);
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
+
+int vn_a2c_loss_grad(const float* out, const int32_t* actions, const float* returns, int n, int num_actions,
+                     float value_coef, float entropy_coef, float* dout, float* stats4, vn_stream_t stream) {
+  if (!out || !actions || !returns || !dout || !stats4 || n <= 0 || num_actions < 1 || num_actions > 7)
+    return fail(VN_EINVAL, "vn_a2c_loss_grad: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  VN_HIP(hipMemsetAsync(stats4, 0, 4 * sizeof(float), st));
+  hipLaunchKernelGGL(loss_grad_kernel, dim3((n + 255) / 256), dim3(256), 0, st, out, actions, returns, n,
+                     num_actions, value_coef, entropy_coef, 1.0f / (float)n, dout, stats4);
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
+
+int vn_grad_norm(const float* grads, int64_t n, float scale, float max_norm, double* partial_512, float* scalars2,
+                 vn_stream_t stream) {
+  if (!grads || !partial_512 || !scalars2 || n <= 0) return fail(VN_EINVAL, "vn_grad_norm: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(sumsq_partial_kernel, dim3(kNormBlocks), dim3(256), 0, st, grads, n, scale, partial_512);
+  hipLaunchKernelGGL(norm_final_kernel, dim3(1), dim3(256), 0, st, partial_512, kNormBlocks, max_norm, scalars2);
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
+
+int vn_rmsprop_step(float* params, const float* grads, float* square_avg, int64_t n, float scale,
+                    const float* scalars2, float lr, float alpha, float eps, vn_stream_t stream) {
+  if (!params || !grads || !square_avg || !scalars2 || n <= 0) return fail(VN_EINVAL, "vn_rmsprop_step: bad args");
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 2048);
+  hipLaunchKernelGGL(rmsprop_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, params, grads, square_avg, n,
+                     scale, scalars2, lr, alpha, eps);
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
+
+}  // extern "C"

@@ -536,8 +536,6 @@ int vn_observe(vn_ctx* c, uint8_t* obs_dev, uint8_t* goal_dev, int32_t* state_de
   a.obs = obs_dev;
   a.goal_out = goal_dev;
   a.state_out = state_dev;
-  a.info_img_row = nullptr;
-  a.info_goal_row = nullptr;
   return launch_env<MODE_OBSERVE>(c, a, (hipStream_t)stream);
 }
 

@@ -1,0 +1,632 @@
+// vn_policy.hip — goal-conditioned CNN policy (BigGoalHouseModel trunk + heads) forward
+// and backward in fp32 on MFMA, gfx950.
+//
+// Reference topology (models/goal.py:36-59, 77-92):
+//   shared_base: Conv(3->32, k7 s4) ReLU, Conv(32->32, k4 s2) ReLU   — image and goal, shared weights
+//   concat(image, goal) on channels                                   — goal.py:88
+//   conv_base:  Conv(64->64, k4 s2) ReLU, Conv(64->32, k1) ReLU
+//   conv_merge: Flatten, Linear(32*h3*w3 -> 512), ReLU                — in_features derived from the frame
+//   heads:      policy_logits Linear(512->A), critic Linear(512->1)   — fused into one [A+1 x 512] head
+// Layout: activations NHWC fp32, samples contiguous, frame f = 2*sample + {0: image, 1: goal};
+// weights [Cout][ky][kx][Cin] (K padded to a multiple of 4) + bias. conv_merge runs as a
+// 3x3 "conv" over the 3x3x32 map (its torch weight [512][c*9+y*3+x] is permuted on load).
+// Inputs: uint8 HWC frames gathered straight from the scene cache by row index (the
+// env never has to materialise the batch), converted x = u8/255 as ScaledFloatFrame does.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <new>
+
+#include "vn_common.h"
+#include "vn_gemm.h"
+
+namespace vn {
+
+struct FrameSrc {
+  const uint8_t* base[2];
+  const int32_t* rows[2];
+  int64_t stride;
+  const float* f32[2];  // optional dense float NCHW frames (TransposeImage+ScaledFloatFrame output)
+};
+
+// ---- operand loaders ---------------------------------------------------------
+// conv1 im2col over 3-channel frames; k = (ky*7 + kx)*3 + c, K = 147 (padded 148).
+template <int H, int W, int OH, int OW>
+struct FramesIm2col {
+  FrameSrc src;
+  int M;  // 2 * samples * OH * OW
+  __device__ __forceinline__ f4 load4(int m, int k, int kend) const {
+    f4 v = f4zero();
+    if (m >= M) return v;
+    const int f = m / (OH * OW);
+    const int r = m - f * (OH * OW);
+    const int oy = r / OW, ox = r - (r / OW) * OW;
+    const int smp = f >> 1, h = f & 1;
+    const int lim = min(kend, 147);
+    if (src.f32[h]) {
+      const float* fr = src.f32[h] + (int64_t)smp * 3 * H * W;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int kk = k + j;
+        if (kk < lim) {
+          const int ky = kk / 21, kx = (kk / 3) % 7, c = kk % 3;
+          v[j] = fr[((int64_t)c * H + oy * 4 + ky) * W + ox * 4 + kx];
+        }
+      }
+    } else {
+      const int64_t row = src.rows[h] ? (int64_t)src.rows[h][smp] : (int64_t)smp;
+      const uint8_t* fr = src.base[h] + row * src.stride;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int kk = k + j;
+        if (kk < lim) {
+          const int ky = kk / 21, kx = (kk / 3) % 7, c = kk % 3;
+          v[j] = (float)fr[((oy * 4 + ky) * W + ox * 4 + kx) * 3 + c] / 255.0f;
+        }
+      }
+    }
+    return v;
+  }
+  template <int ROWS, int BK>
+  __device__ __forceinline__ void fill(float* s, int r0, int k0, int ke, int tid) const {
+    fill_rows<ROWS, BK>(*this, s, r0, k0, ke, tid);
+  }
+};
+
+// im2col over NHWC fp32 with G channel-concatenated input groups (C % 4 == 0).
+template <int C, int KH, int KW, int S, int H, int W, int OH, int OW, int G>
+struct NhwcIm2col {
+  const float* X;
+  int M;  // samples * OH * OW
+  __device__ __forceinline__ f4 load4(int m, int k, int kend) const {
+    if (m >= M || k >= kend) return f4zero();
+    const int n = m / (OH * OW);
+    const int r = m - n * (OH * OW);
+    const int oy = r / OW, ox = r - (r / OW) * OW;
+    const int c = k % C;
+    int t = k / C;
+    const int g = t % G;
+    t /= G;
+    const int ky = t / KW, kx = t % KW;
+    return *reinterpret_cast<const f4*>(X + ((((int64_t)n * G + g) * H + oy * S + ky) * W + ox * S + kx) * C + c);
+  }
+  template <int ROWS, int BK>
+  __device__ __forceinline__ void fill(float* s, int r0, int k0, int ke, int tid) const {
+    fill_rows<ROWS, BK>(*this, s, r0, k0, ke, tid);
+  }
+};
+
+// Dense row-major matrix [rows][ld] (ld % 4 == 0, 16-B aligned).
+struct DenseRows {
+  const float* A;
+  int64_t ld;
+  int M;
+  __device__ __forceinline__ f4 load4(int m, int k, int kend) const {
+    if (m >= M || k >= kend) return f4zero();
+    const float* p = A + (int64_t)m * ld + k;
+    if (k + 3 < kend) return *reinterpret_cast<const f4*>(p);
+    f4 v = f4zero();
+    for (int j = 0; j < 4 && k + j < kend; ++j) v[j] = p[j];
+    return v;
+  }
+  template <int ROWS, int BK>
+  __device__ __forceinline__ void fill(float* s, int r0, int k0, int ke, int tid) const {
+    fill_rows<ROWS, BK>(*this, s, r0, k0, ke, tid);
+  }
+};
+
+// wgrad A operand: dZ [P][ld] read as rows r..r+3 (output channels) at pixel p.
+struct DenseT {
+  const float* A;
+  int64_t ld;
+  int ncols;
+  __device__ __forceinline__ f4 load4t(int p, int r) const {
+    const float* q = A + (int64_t)p * ld + r;
+    if (r + 3 < ncols) return *reinterpret_cast<const f4*>(q);
+    f4 v = f4zero();
+    for (int j = 0; j < 4 && r + j < ncols; ++j) v[j] = q[j];
+    return v;
+  }
+  template <int ROWS, int BK>
+  __device__ __forceinline__ void fill(float* s, int r0, int k0, int ke, int tid) const {
+    fill_trans<ROWS, BK>(*this, s, r0, k0, ke, tid);
+  }
+};
+
+// wgrad B operand: an im2col loader read transposed, plus a ones column at k == KP
+// (that column of the product is the bias gradient).
+template <class L>
+struct Im2colT {
+  L l;
+  int KP;
+  __device__ __forceinline__ f4 load4t(int p, int r) const {
+    f4 v = l.load4(p, r, KP);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (r + j == KP) v[j] = 1.0f;
+    return v;
+  }
+  template <int ROWS, int BK>
+  __device__ __forceinline__ void fill(float* s, int r0, int k0, int ke, int tid) const {
+    fill_trans<ROWS, BK>(*this, s, r0, k0, ke, tid);
+  }
+};
+
+// dgrad of a strided conv, one (group g, parity py, px) class per launch: rows are the
+// input pixels y = yy*S + py, x = xx*S + px; k = (tky, tkx, co) over the KH/S x KW/S taps
+// that reach them (ky = py + tky*S, oy = yy - tky).
+template <int COUT, int KW, int S, int OH, int OW>
+struct DgradA {
+  const float* dZ;
+  int M, HYc, WXc;
+  __device__ __forceinline__ f4 load4(int m, int k, int kend) const {
+    if (m >= M || k >= kend) return f4zero();
+    const int per = HYc * WXc;
+    const int n = m / per;
+    const int r = m - n * per;
+    const int yy = r / WXc, xx = r - (r / WXc) * WXc;
+    const int co = k % COUT;
+    const int t = k / COUT;
+    const int tky = t / (KW / S), tkx = t % (KW / S);
+    const int oy = yy - tky, ox = xx - tkx;
+    if (oy < 0 || oy >= OH || ox < 0 || ox >= OW) return f4zero();
+    return *reinterpret_cast<const f4*>(dZ + (((int64_t)n * OH + oy) * OW + ox) * COUT + co);
+  }
+  template <int ROWS, int BK>
+  __device__ __forceinline__ void fill(float* s, int r0, int k0, int ke, int tid) const {
+    fill_rows<ROWS, BK>(*this, s, r0, k0, ke, tid);
+  }
+};
+
+template <int COUT, int KW, int S, int CINF>
+struct DgradB {
+  const float* WT;  // [KH*KW*CINF][COUT]
+  int cin, g_off, py, px;
+  __device__ __forceinline__ f4 load4(int j, int k, int kend) const {
+    if (j >= cin || k >= kend) return f4zero();
+    const int co = k % COUT;
+    const int t = k / COUT;
+    const int ky = py + (t / (KW / S)) * S, kx = px + (t % (KW / S)) * S;
+    return *reinterpret_cast<const f4*>(WT + ((int64_t)(ky * KW + kx) * CINF + g_off + j) * COUT + co);
+  }
+  template <int ROWS, int BK>
+  __device__ __forceinline__ void fill(float* s, int r0, int k0, int ke, int tid) const {
+    fill_rows<ROWS, BK>(*this, s, r0, k0, ke, tid);
+  }
+};
+
+// ---- epilogues ----------------------------------------------------------------
+struct EpiBiasAct {
+  float* Y;
+  int64_t ld;
+  const float* bias;
+  int relu;
+  __device__ __forceinline__ void operator()(int row, int col, float v, int) const {
+    v += bias[col];
+    Y[(int64_t)row * ld + col] = relu ? fmaxf(v, 0.0f) : v;
+  }
+};
+
+// dX masked by the ReLU that produced X (X = relu(z) -> dz = dX * [X > 0]); may alias X.
+struct EpiMask {
+  float* out;
+  const float* X;
+  int64_t ld;
+  __device__ __forceinline__ void operator()(int row, int col, float v, int) const {
+    const int64_t i = (int64_t)row * ld + col;
+    out[i] = X[i] > 0.0f ? v : 0.0f;
+  }
+};
+
+template <int H, int W, int S>
+struct EpiMaskParity {
+  float* out;
+  const float* X;
+  int WXc, HYc, py, px, g, G, cin;
+  __device__ __forceinline__ void operator()(int row, int col, float v, int) const {
+    const int per = HYc * WXc;
+    const int n = row / per;
+    const int r = row - n * per;
+    const int y = (r / WXc) * S + py, x = (r % WXc) * S + px;
+    const int64_t i = ((((int64_t)n * G + g) * H + y) * W + x) * cin + col;
+    out[i] = X[i] > 0.0f ? v : 0.0f;
+  }
+};
+
+struct EpiSlab {
+  float* slab;
+  int M, N;
+  __device__ __forceinline__ void operator()(int row, int col, float v, int z) const {
+    slab[((int64_t)z * M + row) * N + col] = v;
+  }
+};
+
+__global__ void wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int M, int N, float* dW, float* db) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= M * N) return;
+  const int row = idx / N, col = idx - (idx / N) * N;
+  float s = 0.0f;
+  for (int z = 0; z < splits; ++z) s += slab[((int64_t)z * M + row) * N + col];
+  if (col < N - 1)
+    dW[(int64_t)row * (N - 1) + col] = s;
+  else
+    db[row] = s;
+}
+
+__global__ void transpose_kernel(const float* __restrict__ W, int rows, int cols, float* __restrict__ WT) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= rows * cols) return;
+  const int r = idx / cols, c = idx - (idx / cols) * cols;
+  WT[(int64_t)c * rows + r] = W[idx];
+}
+
+// ---- geometry & layout ------------------------------------------------------------
+struct LayerOff {
+  int64_t w, b;
+  int cout, kp;
+};
+
+struct PolicyLayout {
+  int H, W, A, OH1, OW1, OH2, OW2, OH3, OW3, FCIN;
+  LayerOff l[6];  // conv1, conv2, conv3, conv4, fc, head
+  int64_t n_params;
+  int64_t sz[5];  // per-sample floats of X1..X5
+  int64_t wt_off[6], wt_total;
+};
+
+inline PolicyLayout make_layout(int H, int W, int A) {
+  PolicyLayout L{};
+  L.H = H;
+  L.W = W;
+  L.A = A;
+  L.OH1 = (H - 7) / 4 + 1;
+  L.OW1 = (W - 7) / 4 + 1;
+  L.OH2 = (L.OH1 - 4) / 2 + 1;
+  L.OW2 = (L.OW1 - 4) / 2 + 1;
+  L.OH3 = (L.OH2 - 4) / 2 + 1;
+  L.OW3 = (L.OW2 - 4) / 2 + 1;
+  L.FCIN = 32 * L.OH3 * L.OW3;
+  const int couts[6] = {32, 32, 64, 32, 512, A + 1};
+  const int ks[6] = {148, 16 * 32, 16 * 64, 64, L.FCIN, 512};
+  int64_t off = 0, wt = 0;
+  for (int i = 0; i < 6; ++i) {
+    L.l[i].cout = couts[i];
+    L.l[i].kp = ks[i];
+    L.l[i].w = off;
+    off += (int64_t)couts[i] * ks[i];
+    L.l[i].b = off;
+    off += couts[i];
+    L.wt_off[i] = wt;
+    if (i > 0) wt += (int64_t)couts[i] * ks[i];
+  }
+  L.n_params = off;
+  L.wt_total = wt;
+  L.sz[0] = 2ll * L.OH1 * L.OW1 * 32;
+  L.sz[1] = 2ll * L.OH2 * L.OW2 * 32;
+  L.sz[2] = (int64_t)L.OH3 * L.OW3 * 64;
+  L.sz[3] = (int64_t)L.OH3 * L.OW3 * 32;
+  L.sz[4] = 512;
+  return L;
+}
+
+constexpr int OUT_LD = 8;  // [n][8]: logits 0..A-1, value at A
+
+inline dim3 grid_for(int M, int N, int BM, int BN, int splits = 1) {
+  return dim3((M + BM - 1) / BM, (N + BN - 1) / BN, splits);
+}
+
+template <int BM, int BN, int BK, int WM, int WN, class FA, class FB, class EP>
+inline void launch_gemm(FA fa, FB fb, EP ep, int M, int N, int K, hipStream_t st, int splits = 1, int kchunk = 0) {
+  if (M <= 0 || N <= 0) return;
+  if (kchunk <= 0) kchunk = K;
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, FA, FB, EP>), grid_for(M, N, BM, BN, splits), dim3(256), 0,
+                     st, fa, fb, ep, M, N, K, kchunk);
+}
+
+// Split-K wgrad: dW [M][KP] and db [M] of a layer from A^T (dZ [P][M]) x B (im2col [P][KP]).
+template <int BM, int BN, int WM, int WN, class FB>
+inline void launch_wgrad(const float* dZ, int64_t ldz, int M, FB fb, int KP, int P, float* slab, int64_t slab_cap,
+                         float* dW, float* db, hipStream_t st) {
+  constexpr int BK = 32;
+  const int N = KP + 1;
+  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  int splits = std::max(1, std::min((2048 + tiles - 1) / tiles, (P + 255) / 256));
+  while ((int64_t)splits * M * N > slab_cap && splits > 1) splits /= 2;
+  int kchunk = (P + splits - 1) / splits;
+  kchunk = (kchunk + BK - 1) / BK * BK;
+  splits = (P + kchunk - 1) / kchunk;
+  DenseT fa{dZ, ldz, M};
+  EpiSlab ep{slab, M, N};
+  launch_gemm<BM, BN, BK, WM, WN>(fa, fb, ep, M, N, P, st, splits, kchunk);
+  const int total = M * N;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, slab, splits, M, N, dW, db);
+}
+
+template <int H0, int W0>
+struct Geo {
+  static constexpr int OH1 = (H0 - 7) / 4 + 1, OW1 = (W0 - 7) / 4 + 1;
+  static constexpr int OH2 = (OH1 - 4) / 2 + 1, OW2 = (OW1 - 4) / 2 + 1;
+  static constexpr int OH3 = (OH2 - 4) / 2 + 1, OW3 = (OW2 - 4) / 2 + 1;
+  static constexpr int FCIN = 32 * OH3 * OW3;
+};
+
+struct Acts {
+  float* X[5];
+};
+
+inline Acts acts_at(const PolicyLayout& L, float* base, int64_t cap, int64_t off) {
+  Acts a;
+  float* p = base;
+  for (int i = 0; i < 5; ++i) {
+    a.X[i] = p + off * L.sz[i];
+    p += cap * L.sz[i];
+  }
+  return a;
+}
+
+template <int H0, int W0>
+int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int n, const Acts& a, float* out,
+                 hipStream_t st) {
+  using G = Geo<H0, W0>;
+  const int A1 = L.A + 1;
+  // conv1 (frames -> X1), 2n frames
+  {
+    FramesIm2col<H0, W0, G::OH1, G::OW1> fa{src, 2 * n * G::OH1 * G::OW1};
+    DenseRows fb{P + L.l[0].w, 148, 32};
+    EpiBiasAct ep{a.X[0], 32, P + L.l[0].b, 1};
+    launch_gemm<64, 32, 32, 4, 1>(fa, fb, ep, fa.M, 32, 148, st);
+  }
+  // conv2 (X1 -> X2)
+  {
+    NhwcIm2col<32, 4, 4, 2, G::OH1, G::OW1, G::OH2, G::OW2, 1> fa{a.X[0], 2 * n * G::OH2 * G::OW2};
+    DenseRows fb{P + L.l[1].w, 512, 32};
+    EpiBiasAct ep{a.X[1], 32, P + L.l[1].b, 1};
+    launch_gemm<64, 32, 32, 4, 1>(fa, fb, ep, fa.M, 32, 512, st);
+  }
+  // conv3 over concat(image, goal) (X2 -> X3)
+  {
+    NhwcIm2col<32, 4, 4, 2, G::OH2, G::OW2, G::OH3, G::OW3, 2> fa{a.X[1], n * G::OH3 * G::OW3};
+    DenseRows fb{P + L.l[2].w, 1024, 64};
+    EpiBiasAct ep{a.X[2], 64, P + L.l[2].b, 1};
+    launch_gemm<64, 64, 32, 2, 2>(fa, fb, ep, fa.M, 64, 1024, st);
+  }
+  // conv4 1x1 (X3 -> X4)
+  {
+    DenseRows fa{a.X[2], 64, n * G::OH3 * G::OW3};
+    DenseRows fb{P + L.l[3].w, 64, 32};
+    EpiBiasAct ep{a.X[3], 32, P + L.l[3].b, 1};
+    launch_gemm<64, 32, 32, 4, 1>(fa, fb, ep, fa.M, 32, 64, st);
+  }
+  // conv_merge Linear (X4 flattened NHWC -> X5)
+  {
+    DenseRows fa{a.X[3], G::FCIN, n};
+    DenseRows fb{P + L.l[4].w, G::FCIN, 512};
+    EpiBiasAct ep{a.X[4], 512, P + L.l[4].b, 1};
+    launch_gemm<64, 64, 32, 2, 2>(fa, fb, ep, n, 512, G::FCIN, st);
+  }
+  // heads (X5 -> out[n][8]: logits, value)
+  {
+    DenseRows fa{a.X[4], 512, n};
+    DenseRows fb{P + L.l[5].w, 512, A1};
+    EpiBiasAct ep{out, OUT_LD, P + L.l[5].b, 0};
+    launch_gemm<64, 16, 32, 4, 1>(fa, fb, ep, n, A1, 512, st);
+  }
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
+
+struct BwdWork {
+  float* wt;
+  float* dz5;
+  float* dz4;
+  float* dz3;
+  float* dz2;
+  float* slab;
+  int64_t slab_cap;
+};
+
+inline int64_t slab_floats(const PolicyLayout& L) {
+  return 8ll << 20;  // split-K slab capacity (launch_wgrad halves the split count to fit)
+}
+
+inline int64_t workspace_floats(const PolicyLayout& L, int64_t n) {
+  return L.wt_total + n * 512 + n * L.FCIN + n * L.sz[2] + n * L.sz[1] + slab_floats(L) + 64;
+}
+
+inline BwdWork carve(const PolicyLayout& L, float* ws, int64_t n) {
+  BwdWork w;
+  float* p = ws;
+  w.wt = p;
+  p += L.wt_total;
+  w.dz5 = p;
+  p += n * 512;
+  w.dz4 = p;
+  p += n * L.FCIN;
+  w.dz3 = p;
+  p += n * L.sz[2];
+  w.dz2 = p;
+  p += n * L.sz[1];
+  w.slab = p;
+  w.slab_cap = slab_floats(L);
+  return w;
+}
+
+template <int H0, int W0>
+int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int n, const Acts& a,
+                  const float* dout, float* Gr, const BwdWork& w, hipStream_t st) {
+  using G = Geo<H0, W0>;
+  const int A1 = L.A + 1;
+  auto T = [&](int i) { return w.wt + L.wt_off[i]; };
+  // transposed weights for the dgrad products
+  for (int i = 1; i < 6; ++i) {
+    const int rows = L.l[i].cout, cols = L.l[i].kp;
+    hipLaunchKernelGGL(transpose_kernel, dim3((rows * cols + 255) / 256), dim3(256), 0, st, P + L.l[i].w, rows, cols,
+                       T(i));
+  }
+  const int n9 = n * G::OH3 * G::OW3;
+  // ---- head: dX5 = dout x Whead, masked by X5 ; dWhead = dout^T x X5
+  {
+    DenseRows fa{dout, OUT_LD, n};
+    DenseRows fb{T(5), A1, 512};  // WT [512][A1]
+    EpiMask ep{w.dz5, a.X[4], 512};
+    launch_gemm<64, 64, 32, 2, 2>(fa, fb, ep, n, 512, A1, st);
+    Im2colT<DenseRows> fbw{DenseRows{a.X[4], 512, n}, 512};
+    launch_wgrad<32, 64, 2, 2>(dout, OUT_LD, A1, fbw, 512, n, w.slab, w.slab_cap, Gr + L.l[5].w, Gr + L.l[5].b, st);
+  }
+  // ---- conv_merge Linear: dX4 = dz5 x Wfc masked by X4 ; dWfc = dz5^T x X4
+  {
+    DenseRows fa{w.dz5, 512, n};
+    DenseRows fb{T(4), 512, G::FCIN};  // WT [FCIN][512]
+    EpiMask ep{w.dz4, a.X[3], G::FCIN};
+    launch_gemm<64, 64, 32, 2, 2>(fa, fb, ep, n, G::FCIN, 512, st);
+    Im2colT<DenseRows> fbw{DenseRows{a.X[3], G::FCIN, n}, G::FCIN};
+    launch_wgrad<64, 64, 2, 2>(w.dz5, 512, 512, fbw, G::FCIN, n, w.slab, w.slab_cap, Gr + L.l[4].w, Gr + L.l[4].b,
+                               st);
+  }
+  // ---- conv4 (1x1): dX3 = dz4 x W4 masked by X3 ; dW4 = dz4^T x X3
+  {
+    DenseRows fa{w.dz4, 32, n9};
+    DenseRows fb{T(3), 32, 64};  // WT [64][32]
+    EpiMask ep{w.dz3, a.X[2], 64};
+    launch_gemm<64, 64, 32, 2, 2>(fa, fb, ep, n9, 64, 32, st);
+    Im2colT<DenseRows> fbw{DenseRows{a.X[2], 64, n9}, 64};
+    launch_wgrad<32, 64, 2, 2>(w.dz4, 32, 32, fbw, 64, n9, w.slab, w.slab_cap, Gr + L.l[3].w, Gr + L.l[3].b, st);
+  }
+  // ---- conv3 (k4 s2, 2 input groups): wgrad, then dgrad into dz2 masked by X2
+  {
+    using Im = NhwcIm2col<32, 4, 4, 2, G::OH2, G::OW2, G::OH3, G::OW3, 2>;
+    Im2colT<Im> fbw{Im{a.X[1], n9}, 1024};
+    launch_wgrad<64, 64, 2, 2>(w.dz3, 64, 64, fbw, 1024, n9, w.slab, w.slab_cap, Gr + L.l[2].w, Gr + L.l[2].b, st);
+    for (int g = 0; g < 2; ++g)
+      for (int py = 0; py < 2; ++py)
+        for (int px = 0; px < 2; ++px) {
+          const int HYc = (G::OH2 - py + 1) / 2, WXc = (G::OW2 - px + 1) / 2;
+          const int M = n * HYc * WXc;
+          DgradA<64, 4, 2, G::OH3, G::OW3> fa{w.dz3, M, HYc, WXc};
+          DgradB<64, 4, 2, 64> fb{T(2), 32, g * 32, py, px};
+          EpiMaskParity<G::OH2, G::OW2, 2> ep{w.dz2, a.X[1], WXc, HYc, py, px, g, 2, 32};
+          launch_gemm<64, 32, 32, 4, 1>(fa, fb, ep, M, 32, 4 * 64, st);
+        }
+  }
+  // ---- conv2 (k4 s2): wgrad (needs X1), then dgrad into dz1 written over X1
+  {
+    using Im = NhwcIm2col<32, 4, 4, 2, G::OH1, G::OW1, G::OH2, G::OW2, 1>;
+    const int P2 = 2 * n * G::OH2 * G::OW2;
+    Im2colT<Im> fbw{Im{a.X[0], P2}, 512};
+    launch_wgrad<32, 64, 2, 2>(w.dz2, 32, 32, fbw, 512, P2, w.slab, w.slab_cap, Gr + L.l[1].w, Gr + L.l[1].b, st);
+    for (int py = 0; py < 2; ++py)
+      for (int px = 0; px < 2; ++px) {
+        const int HYc = (G::OH1 - py + 1) / 2, WXc = (G::OW1 - px + 1) / 2;
+        const int M = 2 * n * HYc * WXc;
+        DgradA<32, 4, 2, G::OH2, G::OW2> fa{w.dz2, M, HYc, WXc};
+        DgradB<32, 4, 2, 32> fb{T(1), 32, 0, py, px};
+        EpiMaskParity<G::OH1, G::OW1, 2> ep{a.X[0], a.X[0], WXc, HYc, py, px, 0, 1, 32};
+        launch_gemm<64, 32, 32, 4, 1>(fa, fb, ep, M, 32, 4 * 32, st);
+      }
+  }
+  // ---- conv1: wgrad from dz1 (in X1's storage) and the frames
+  {
+    using Im = FramesIm2col<H0, W0, G::OH1, G::OW1>;
+    const int P1 = 2 * n * G::OH1 * G::OW1;
+    Im2colT<Im> fbw{Im{src, P1}, 148};
+    launch_wgrad<32, 64, 2, 2>(a.X[0], 32, 32, fbw, 148, P1, w.slab, w.slab_cap, Gr + L.l[0].w, Gr + L.l[0].b, st);
+  }
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
+
+}  // namespace vn
+
+using namespace vn;
+
+struct vn_policy {
+  PolicyLayout L;
+};
+
+namespace {
+bool supported(int H, int W) { return (H == 84 && W == 84) || (H == 174 && W == 174); }
+
+FrameSrc to_src(const vn_frames* f) {
+  FrameSrc s{};
+  s.base[0] = f->image;
+  s.base[1] = f->goal;
+  s.rows[0] = f->image_rows;
+  s.rows[1] = f->goal_rows;
+  s.stride = f->frame_bytes;
+  s.f32[0] = f->image_f32;
+  s.f32[1] = f->goal_f32;
+  return s;
+}
+}  // namespace
+
+extern "C" {
+
+int vn_policy_create(int frame_h, int frame_w, int num_actions, vn_policy** out) {
+  if (!out) return fail(VN_EINVAL, "vn_policy_create: out is NULL");
+  *out = nullptr;
+  if (!supported(frame_h, frame_w))
+    return fail(VN_EINVAL, "vn_policy_create: frame size must be 84x84 or 174x174");
+  if (num_actions < 1 || num_actions + 1 > OUT_LD) return fail(VN_EINVAL, "vn_policy_create: 1..7 actions");
+  vn_policy* p = new (std::nothrow) vn_policy();
+  if (!p) return fail(VN_ENOMEM, "vn_policy_create: host allocation");
+  p->L = make_layout(frame_h, frame_w, num_actions);
+  *out = p;
+  return VN_OK;
+}
+
+int vn_policy_destroy(vn_policy* p) {
+  delete p;
+  return VN_OK;
+}
+
+int vn_policy_info(vn_policy* p, int64_t* n_params, int64_t* act_floats_per_sample, int64_t* layout12) {
+  if (!p) return fail(VN_EINVAL, "vn_policy_info: NULL policy");
+  if (n_params) *n_params = p->L.n_params;
+  if (act_floats_per_sample) {
+    int64_t s = 0;
+    for (int i = 0; i < 5; ++i) s += p->L.sz[i];
+    *act_floats_per_sample = s;
+  }
+  if (layout12)
+    for (int i = 0; i < 6; ++i) {
+      layout12[2 * i] = p->L.l[i].w;
+      layout12[2 * i + 1] = p->L.l[i].b;
+    }
+  return VN_OK;
+}
+
+int vn_policy_workspace_floats(vn_policy* p, int64_t n, int64_t* floats) {
+  if (!p || !floats || n <= 0) return fail(VN_EINVAL, "vn_policy_workspace_floats: bad args");
+  *floats = workspace_floats(p->L, n);
+  return VN_OK;
+}
+
+int vn_policy_forward(vn_policy* p, const float* params, const vn_frames* frames, int n, float* acts,
+                      int64_t act_capacity, int64_t act_offset, float* out, vn_stream_t stream) {
+  if (!p || !params || !frames || !acts || !out || n <= 0) return fail(VN_EINVAL, "vn_policy_forward: bad args");
+  if (act_offset < 0 || act_offset + n > act_capacity)
+    return fail(VN_EINVAL, "vn_policy_forward: samples exceed the activation capacity");
+  const FrameSrc src = to_src(frames);
+  if ((!src.base[0] && !src.f32[0]) || (!src.base[1] && !src.f32[1]))
+    return fail(VN_EINVAL, "vn_policy_forward: missing frames");
+  const Acts a = acts_at(p->L, acts, act_capacity, act_offset);
+  hipStream_t st = (hipStream_t)stream;
+  if (p->L.H == 84) return forward_impl<84, 84>(p->L, params, src, n, a, out, st);
+  return forward_impl<174, 174>(p->L, params, src, n, a, out, st);
+}
+
+int vn_policy_backward(vn_policy* p, const float* params, const vn_frames* frames, int n, float* acts,
+                       int64_t act_capacity, const float* dout, float* grads, float* workspace,
+                       vn_stream_t stream) {
+  if (!p || !params || !frames || !acts || !dout || !grads || !workspace || n <= 0)
+    return fail(VN_EINVAL, "vn_policy_backward: bad args");
+  if (n > act_capacity) return fail(VN_EINVAL, "vn_policy_backward: n exceeds the activation capacity");
+  const FrameSrc src = to_src(frames);
+  const Acts a = acts_at(p->L, acts, act_capacity, 0);
+  const BwdWork w = carve(p->L, workspace, n);
+  hipStream_t st = (hipStream_t)stream;
+  if (p->L.H == 84) return backward_impl<84, 84>(p->L, params, src, n, a, dout, grads, w, st);
+  return backward_impl<174, 174>(p->L, params, src, n, a, dout, grads, w, st);
+}
+
+}  // extern "C"

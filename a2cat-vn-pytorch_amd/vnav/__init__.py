@@ -6,5 +6,7 @@ CNN policy. See DESIGN.md at the repository root.
 """
 from .scenes import Scene, grid_tables, maze_scene, synthetic_scene, scene_from_arrays  # noqa: F401
 from .envs import VectorEnv, make, to_float_chw  # noqa: F401
+from .policy import GoalNavPolicy, PolicyNet  # noqa: F401
+from .a2c import A2CTrainer  # noqa: F401
 
 __version__ = "0.1.0"

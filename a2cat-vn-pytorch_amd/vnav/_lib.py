@@ -65,6 +65,35 @@ SIGNATURES = {
     "vn_num_envs": (c_int, [c_void_p]),
 }
 
+SIGNATURES.update({
+    "vn_policy_create": (c_int, [c_int, c_int, c_int, P(c_void_p)]),
+    "vn_policy_destroy": (c_int, [c_void_p]),
+    "vn_policy_info": (c_int, [c_void_p, P(c_int64), P(c_int64),
+                                      P(c_int64)]),
+    "vn_policy_workspace_floats": (c_int, [c_void_p, c_int64, P(c_int64)]),
+    "vn_policy_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_int,
+                                         c_void_p, c_int64, c_int64, c_void_p,
+                                         c_void_p]),
+    "vn_policy_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_int,
+                                          c_void_p, c_int64, c_void_p, c_void_p,
+                                          c_void_p, c_void_p]),
+    "vn_policy_sample": (c_int, [c_void_p, c_int, c_int, c_uint64, c_uint64,
+                                        c_void_p, c_void_p, c_void_p, c_void_p,
+                                        c_void_p]),
+    "vn_policy_greedy": (c_int, [c_void_p, c_int, c_int, c_void_p,
+                                        c_void_p]),
+    "vn_a2c_returns": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int,
+                                      c_int, c_float, c_void_p, c_void_p]),
+    "vn_a2c_loss_grad": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int,
+                                        c_float, c_float, c_void_p, c_void_p,
+                                        c_void_p]),
+    "vn_grad_norm": (c_int, [c_void_p, c_int64, c_float, c_float, c_void_p,
+                                    c_void_p, c_void_p]),
+    "vn_rmsprop_step": (c_int, [c_void_p, c_void_p, c_void_p, c_int64,
+                                       c_float, c_void_p, c_float, c_float,
+                                       c_float, c_void_p]),
+})
+
 _lib = None
 
 

@@ -1,0 +1,199 @@
+"""A2C rollout/update loop on one GPU per process (RCCL all-reduce across processes).
+
+Mirrors the deep_rl Trainer surface the reference drives (train.py:24-25,
+experiments/thor_cached_auxiliary.py:26-56): hyper-parameters as attributes with the
+reference's values (num_steps 20, gamma .99, RMSprop alpha .99 / eps 1e-5, grad-norm
+clip 0.5, lr 7e-4 -> 0 linearly over max_time_steps), ``step()`` = one rollout of
+num_steps on every local env + one update, ``run()`` loops to max_time_steps,
+``create_env`` / ``create_model`` hooks. The loss is the standard A2C stated in
+DESIGN.md ("A2C contract"; value/entropy coefficients are not visible in the
+reference — deep-rl 0.2.9 is absent — so parity is unpinned at this level).
+
+Everything per step is a device launch: policy forward on frames gathered zero-copy
+from the scene cache by row index, categorical sampling, env step (index-only), then
+returns, loss gradient, backward, one flat-buffer all-reduce, norm, clip + RMSprop. No
+host synchronisation inside ``step(sync=False)``.
+"""
+import ctypes
+import time
+
+import torch
+
+from . import _lib
+from .policy import OUT_LD, PolicyNet, frames_from_rows
+
+
+class A2CTrainer:
+    def __init__(self, env, net=None, params=None, num_steps=20, gamma=0.99, learning_rate=7e-4,
+                 max_time_steps=2e6, rms_alpha=0.99, rms_epsilon=1e-5, max_gradient_norm=0.5,
+                 value_coefficient=0.5, entropy_coefficient=0.01, seed=0, process_group=None):
+        self.env = env
+        self.lib = _lib.load()
+        self.device = env.device
+        self.num_steps = int(num_steps)
+        self.gamma = float(gamma)
+        self.learning_rate = float(learning_rate)
+        self.max_time_steps = float(max_time_steps)
+        self.rms_alpha = float(rms_alpha)
+        self.rms_epsilon = float(rms_epsilon)
+        self.max_gradient_norm = float(max_gradient_norm)
+        self.value_coefficient = float(value_coefficient)
+        self.entropy_coefficient = float(entropy_coefficient)
+        self.seed = int(seed)
+        self.group = process_group
+        self.world = 1
+        self.rank = 0
+        if torch.distributed.is_available() and torch.distributed.is_initialized():
+            self.world = torch.distributed.get_world_size(process_group)
+            self.rank = torch.distributed.get_rank(process_group)
+        self.net = net if net is not None else PolicyNet(env.frame_shape[:2], env.num_actions, self.device)
+        self.A = self.net.num_actions
+        self.params = params if params is not None else self.net.init_params(self.seed)
+        if self.world > 1:
+            torch.distributed.broadcast(self.params, src=0, group=self.group)
+        P = self.net.n_params
+        E, T = env.num_envs, self.num_steps
+        N = T * E
+        kw = dict(device=self.device)
+        self.grads = torch.zeros(P, dtype=torch.float32, **kw)
+        self.square_avg = torch.zeros(P, dtype=torch.float32, **kw)
+        self.acts = self.net.new_acts(N)
+        self.boot_acts = self.net.new_acts(E)
+        self.out = torch.zeros((N, OUT_LD), dtype=torch.float32, **kw)
+        self.boot_out = torch.zeros((E, OUT_LD), dtype=torch.float32, **kw)
+        self.rows_img = torch.zeros(N, dtype=torch.int32, **kw)
+        self.rows_goal = torch.zeros(N, dtype=torch.int32, **kw)
+        self.actions = torch.zeros(N, dtype=torch.int32, **kw)
+        self.rewards = torch.zeros((T, E), dtype=torch.float32, **kw)
+        self.dones = torch.zeros((T, E), dtype=torch.bool, **kw)
+        self.states = torch.zeros(E, dtype=torch.int32, **kw)
+        self.returns = torch.zeros(N, dtype=torch.float32, **kw)
+        self.dout = torch.zeros((N, OUT_LD), dtype=torch.float32, **kw)
+        self.stats = torch.zeros(4, dtype=torch.float32, **kw)
+        self.norm_partial = torch.zeros(512, dtype=torch.float64, **kw)
+        self.scalars = torch.zeros(2, dtype=torch.float32, **kw)
+        self.episode_stats = torch.zeros(3, dtype=torch.float32, **kw)  # count, return sum, length sum
+        self.workspace = torch.empty(self.net.workspace_floats(N), dtype=torch.float32, **kw)
+        arena, fb, _, _ = env.frame_arena()
+        self._arena, self._fb = arena, fb
+        env.observe(gather=False)  # refresh the obs row buffers for the first forward
+        self.num_updates = 0
+        self.total_steps = 0
+
+    # deep_rl hook names (experiments/thor_cached_auxiliary.py:50-56)
+    def create_env(self, kwargs):
+        return self.env
+
+    def create_model(self):
+        return self.net
+
+    def _stream(self):
+        return _lib.stream_ptr(self.device)
+
+    def _frames(self, img_rows, goal_rows):
+        return frames_from_rows(self._arena, self._fb, img_rows, goal_rows)
+
+    def current_lr(self):
+        """LinearSchedule(7e-4, 0, max_time_steps) (experiments/thor_cached_auxiliary.py:37)."""
+        frac = min(self.total_steps / self.max_time_steps, 1.0) if self.max_time_steps > 0 else 0.0
+        return self.learning_rate * (1.0 - frac)
+
+    def rollout(self):
+        env, net, lib = self.env, self.net, self.lib
+        E, T, A = env.num_envs, self.num_steps, self.A
+        N = T * E
+        info = env._info
+        self.episode_stats.zero_()
+        for t in range(T):
+            sl = slice(t * E, (t + 1) * E)
+            self.rows_img[sl].copy_(info["img_row"])
+            self.rows_goal[sl].copy_(info["goal_row"])
+            net.forward(self.params, self._frames(self.rows_img[sl], self.rows_goal[sl]), E, self.acts, N, t * E,
+                        self.out[sl])
+            counter = (self.num_updates * T + t) & (2 ** 64 - 1)
+            _lib.check(lib.vn_policy_sample(_lib.ptr(self.out[sl]), E, A, ctypes.c_uint64(self.seed * 7919 + self.rank),
+                                            ctypes.c_uint64(counter), _lib.ptr(self.actions[sl]), None, None, None,
+                                            self._stream()), "vn_policy_sample")
+            env.step(self.actions[sl], out=dict(reward=self.rewards[t], done=self.dones[t], state=self.states),
+                     gather=False)
+            d = self.dones[t].to(torch.float32)
+            self.episode_stats[0] += d.sum()
+            self.episode_stats[1] += (info["ep_return"] * d).sum()
+            self.episode_stats[2] += (info["ep_length"].to(torch.float32) * d).sum()
+        # bootstrap value of the final observation
+        net.forward(self.params, self._frames(info["img_row"], info["goal_row"]), E, self.boot_acts, E, 0,
+                    self.boot_out)
+
+    def update(self):
+        lib, net = self.lib, self.net
+        E, T, A = self.env.num_envs, self.num_steps, self.A
+        N = T * E
+        st = self._stream()
+        _lib.check(lib.vn_a2c_returns(_lib.ptr(self.rewards), _lib.ptr(self.dones), _lib.ptr(self.boot_out), T, E, A,
+                                      ctypes.c_float(self.gamma), _lib.ptr(self.returns), st), "vn_a2c_returns")
+        _lib.check(lib.vn_a2c_loss_grad(_lib.ptr(self.out), _lib.ptr(self.actions), _lib.ptr(self.returns), N, A,
+                                        ctypes.c_float(self.value_coefficient),
+                                        ctypes.c_float(self.entropy_coefficient), _lib.ptr(self.dout),
+                                        _lib.ptr(self.stats), st), "vn_a2c_loss_grad")
+        net.backward(self.params, self._frames(self.rows_img, self.rows_goal), N, self.acts, N, self.dout, self.grads,
+                     self.workspace)
+        scale = 1.0
+        if self.world > 1:
+            torch.distributed.all_reduce(self.grads, group=self.group)  # RCCL, one flat bucket
+            scale = 1.0 / self.world
+        P = net.n_params
+        _lib.check(lib.vn_grad_norm(_lib.ptr(self.grads), P, ctypes.c_float(scale),
+                                    ctypes.c_float(self.max_gradient_norm), _lib.ptr(self.norm_partial),
+                                    _lib.ptr(self.scalars), st), "vn_grad_norm")
+        _lib.check(lib.vn_rmsprop_step(_lib.ptr(self.params), _lib.ptr(self.grads), _lib.ptr(self.square_avg), P,
+                                       ctypes.c_float(scale), _lib.ptr(self.scalars),
+                                       ctypes.c_float(self.current_lr()), ctypes.c_float(self.rms_alpha),
+                                       ctypes.c_float(self.rms_epsilon), st), "vn_rmsprop_step")
+
+    def step(self, sync=True):
+        """One rollout (num_steps x num_envs) + one update. Returns the metric dict
+        (deep_rl log keys) as floats when sync, else as device tensors."""
+        t0 = time.perf_counter()
+        self.rollout()
+        self.update()
+        N = self.num_steps * self.env.num_envs
+        self.total_steps += N * self.world
+        self.num_updates += 1
+        m = torch.cat([self.stats / N, self.episode_stats, self.scalars[:1]])
+        if self.world > 1:
+            torch.distributed.all_reduce(m, group=self.group)
+            m[:4] /= self.world
+            m[7] /= self.world
+        if not sync:
+            return {"raw": m}
+        vals = m.tolist()
+        vl, al, ent, ret_mean, eps, rsum, lsum, gnorm = vals
+        dt = time.perf_counter() - t0
+        return {
+            "step": self.total_steps, "updates": self.num_updates,
+            "value_loss": vl, "action_loss": al, "entropy": ent,
+            "loss": self.value_coefficient * vl + al - self.entropy_coefficient * ent,
+            "episodes": eps, "reward": rsum / eps if eps else float("nan"),
+            "episode_length": lsum / eps if eps else float("nan"),
+            "grad_norm": gnorm, "return_mean": ret_mean, "fps": N * self.world / dt,
+        }
+
+    def run(self, log_every=10, logger=print):
+        while self.total_steps < self.max_time_steps:
+            metrics = self.step(sync=(self.num_updates % log_every == 0))
+            if "raw" not in metrics and self.rank == 0 and logger:
+                logger(metrics)
+        return self
+
+    def state_dict(self):
+        return {"params": self.params.detach().cpu(), "square_avg": self.square_avg.cpu(),
+                "env_state": self.env.get_state().cpu(), "num_updates": self.num_updates,
+                "total_steps": self.total_steps, "seed": self.seed}
+
+    def load_state_dict(self, sd):
+        self.params.copy_(sd["params"].to(self.device))
+        self.square_avg.copy_(sd["square_avg"].to(self.device))
+        self.env.set_state(sd["env_state"])
+        self.num_updates = int(sd["num_updates"])
+        self.total_steps = int(sd["total_steps"])
+        self.env.observe(gather=False)

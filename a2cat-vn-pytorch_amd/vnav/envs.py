@@ -146,7 +146,11 @@ class VectorEnv:
         _lib.check(self.lib.vn_reset(self._ctx, _lib.ptr(m), self._stream()), "vn_reset")
         return self.observe()
 
-    def observe(self, out=None):
+    def observe(self, out=None, gather=True):
+        """Current (image, goal) frames; gather=False only refreshes info img_row/goal_row."""
+        if not gather:
+            _lib.check(self.lib.vn_observe(self._ctx, None, None, None, self._stream()), "vn_observe")
+            return None, None
         img, goal = out if out is not None else self._frames()
         _lib.check(self.lib.vn_observe(self._ctx, _lib.ptr(img), _lib.ptr(goal), None, self._stream()), "vn_observe")
         return img, goal

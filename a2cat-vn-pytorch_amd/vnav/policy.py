@@ -1,0 +1,278 @@
+"""The goal-conditioned CNN policy on libvnav.so's MFMA kernels.
+
+GoalNavPolicy mirrors BigGoalHouseModel's interface (models/goal.py:15-92):
+``forward(inputs, masks, states) -> [policy_logits, critic, states]`` and
+``initial_states(batch)``, with the trunk + heads (goal.py:36-59) computed by the HIP
+kernels. The recurrent core (MaskedRNN/LSTM, goal.py:61-67) is outside this slice
+("next"): features feed the heads directly and ``states`` pass through.
+
+All parameters live in ONE flat fp32 device buffer (layout in include/vnav.h), so the
+optimizer, the gradient norm and the RCCL all-reduce each touch one contiguous tensor.
+"""
+import ctypes
+import math
+import re
+
+import numpy as np
+import torch
+
+from . import _lib
+
+LAYERS = ("conv1", "conv2", "conv3", "conv4", "fc", "head")
+OUT_LD = 8
+
+
+
+class Frames(ctypes.Structure):
+    """vn_frames (include/vnav.h)."""
+    _fields_ = [("image", ctypes.c_void_p), ("goal", ctypes.c_void_p), ("image_rows", ctypes.c_void_p),
+                ("goal_rows", ctypes.c_void_p), ("frame_bytes", ctypes.c_int64), ("image_f32", ctypes.c_void_p),
+                ("goal_f32", ctypes.c_void_p)]
+
+
+def frames_from_batch(image, goal):
+    """Dense frames: uint8 [n,H,W,3] (env output) or float [n,3,H,W] (reference wrappers)."""
+    f = Frames()
+    if image.dtype == torch.uint8:
+        f.image, f.goal = image.data_ptr(), goal.data_ptr()
+        f.frame_bytes = int(np.prod(image.shape[1:]))
+    else:
+        f.image_f32, f.goal_f32 = image.data_ptr(), goal.data_ptr()
+    return f
+
+
+def frames_from_rows(arena_ptr, frame_bytes, img_rows, goal_rows):
+    """Zero-copy frames: rows of the VectorEnv scene-cache arena."""
+    f = Frames()
+    f.image = f.goal = arena_ptr
+    f.image_rows, f.goal_rows = img_rows.data_ptr(), goal_rows.data_ptr()
+    f.frame_bytes = frame_bytes
+    return f
+
+
+def trunk_sizes(h, w):
+    o1 = ((h - 7) // 4 + 1, (w - 7) // 4 + 1)
+    o2 = ((o1[0] - 4) // 2 + 1, (o1[1] - 4) // 2 + 1)
+    o3 = ((o2[0] - 4) // 2 + 1, (o2[1] - 4) // 2 + 1)
+    return o1, o2, o3
+
+
+class PolicyNet:
+    """Handle on a vn_policy: flat parameter layout, forward/backward launches."""
+
+    def __init__(self, frame_hw=(84, 84), num_actions=4, device=None):
+        self.lib = _lib.load()
+        self.frame_hw = tuple(frame_hw)
+        self.num_actions = int(num_actions)
+        self.device = torch.device("cuda", torch.cuda.current_device() if device is None else
+                                   torch.device(device).index or 0)
+        h = ctypes.c_void_p()
+        _lib.check(self.lib.vn_policy_create(frame_hw[0], frame_hw[1], num_actions, ctypes.byref(h)),
+                   "vn_policy_create")
+        self._h = h
+        n, a = ctypes.c_int64(), ctypes.c_int64()
+        lay = (ctypes.c_int64 * 12)()
+        _lib.check(self.lib.vn_policy_info(h, ctypes.byref(n), ctypes.byref(a), lay), "vn_policy_info")
+        self.n_params = n.value
+        self.act_floats = a.value
+        self.offsets = {name: (lay[2 * i], lay[2 * i + 1]) for i, name in enumerate(LAYERS)}
+        _, _, o3 = trunk_sizes(*frame_hw)
+        self.fc_in = 32 * o3[0] * o3[1]
+        self.shapes = {"conv1": (32, 148), "conv2": (32, 512), "conv3": (64, 1024), "conv4": (32, 64),
+                       "fc": (512, self.fc_in), "head": (num_actions + 1, 512)}
+
+    def __del__(self):
+        try:
+            if getattr(self, "_h", None):
+                self.lib.vn_policy_destroy(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+    # -- parameter layout -----------------------------------------------------------
+    def views(self, flat):
+        """{layer: (W [Cout][K], b [Cout])} views into a flat buffer."""
+        out = {}
+        for name in LAYERS:
+            w, b = self.offsets[name]
+            co, k = self.shapes[name]
+            out[name] = (flat[w:w + co * k].view(co, k), flat[b:b + co])
+        return out
+
+    def new_params(self):
+        return torch.zeros(self.n_params, dtype=torch.float32, device=self.device)
+
+    def init_params(self, seed=0):
+        """BigGoalHouseModel.init_weights (goal.py:26-30): bias 0, W ~ U(+-1/sqrt(fan_in))."""
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        flat = torch.zeros(self.n_params, dtype=torch.float32)
+        fan_in = {"conv1": 147, "conv2": 512, "conv3": 1024, "conv4": 64, "fc": self.fc_in, "head": 512}
+        v = self.views(flat)
+        for name in LAYERS:
+            w, _ = v[name]
+            d = 1.0 / math.sqrt(fan_in[name])
+            k = 147 if name == "conv1" else w.shape[1]
+            w[:, :k].uniform_(-d, d, generator=g)
+        return flat.to(self.device)
+
+    def from_reference(self, sd):
+        """Reference state dict (BigGoalHouseModel names, any prefix) -> flat params."""
+        flat = torch.zeros(self.n_params, dtype=torch.float32)
+        v = self.views(flat)
+        pick = _ReferenceNames(sd)
+        t = lambda x: torch.as_tensor(np.asarray(x), dtype=torch.float32)  # noqa: E731
+        w, b = v["conv1"]
+        w[:, :147] = t(pick("shared_base", 0, "weight")).permute(0, 2, 3, 1).reshape(32, 147)
+        b[:] = t(pick("shared_base", 0, "bias"))
+        w, b = v["conv2"]
+        w[:] = t(pick("shared_base", 1, "weight")).permute(0, 2, 3, 1).reshape(32, 512)
+        b[:] = t(pick("shared_base", 1, "bias"))
+        w, b = v["conv3"]
+        w[:] = t(pick("conv_base", 0, "weight")).permute(0, 2, 3, 1).reshape(64, 1024)
+        b[:] = t(pick("conv_base", 0, "bias"))
+        w, b = v["conv4"]
+        w[:] = t(pick("conv_base", 1, "weight")).reshape(32, 64)
+        b[:] = t(pick("conv_base", 1, "bias"))
+        _, _, o3 = trunk_sizes(*self.frame_hw)
+        w, b = v["fc"]
+        w[:] = t(pick("conv_merge", 0, "weight")).view(512, 32, o3[0], o3[1]).permute(0, 2, 3, 1).reshape(512, -1)
+        b[:] = t(pick("conv_merge", 0, "bias"))
+        w, b = v["head"]
+        A = self.num_actions
+        w[:A] = t(pick("policy_logits", 0, "weight"))
+        b[:A] = t(pick("policy_logits", 0, "bias"))
+        w[A] = t(pick("critic", 0, "weight")).view(-1)
+        b[A] = t(pick("critic", 0, "bias")).view(())
+        return flat.to(self.device)
+
+    def to_reference(self, flat):
+        """Flat params (or grads) -> dict in the reference's tensor shapes."""
+        v = self.views(flat.detach().float().cpu())
+        _, _, o3 = trunk_sizes(*self.frame_hw)
+        A = self.num_actions
+        out = {}
+        w, b = v["conv1"]
+        out["shared_base.0.0.weight"] = w[:, :147].reshape(32, 7, 7, 3).permute(0, 3, 1, 2).contiguous()
+        out["shared_base.0.0.bias"] = b.clone()
+        w, b = v["conv2"]
+        out["shared_base.0.2.weight"] = w.reshape(32, 4, 4, 32).permute(0, 3, 1, 2).contiguous()
+        out["shared_base.0.2.bias"] = b.clone()
+        w, b = v["conv3"]
+        out["conv_base.0.0.weight"] = w.reshape(64, 4, 4, 64).permute(0, 3, 1, 2).contiguous()
+        out["conv_base.0.0.bias"] = b.clone()
+        w, b = v["conv4"]
+        out["conv_base.0.2.weight"] = w.reshape(32, 64, 1, 1).clone()
+        out["conv_base.0.2.bias"] = b.clone()
+        w, b = v["fc"]
+        out["conv_merge.0.1.weight"] = w.reshape(512, o3[0], o3[1], 32).permute(0, 3, 1, 2).reshape(512, -1).contiguous()
+        out["conv_merge.0.1.bias"] = b.clone()
+        w, b = v["head"]
+        out["policy_logits.0.weight"] = w[:A].clone()
+        out["policy_logits.0.bias"] = b[:A].clone()
+        out["critic.0.weight"] = w[A:A + 1].clone()
+        out["critic.0.bias"] = b[A:A + 1].clone()
+        return out
+
+    # -- launches -------------------------------------------------------------------
+    def workspace_floats(self, n):
+        f = ctypes.c_int64()
+        _lib.check(self.lib.vn_policy_workspace_floats(self._h, int(n), ctypes.byref(f)), "vn_policy_workspace_floats")
+        return f.value
+
+    def new_acts(self, capacity):
+        return torch.empty(int(capacity) * self.act_floats, dtype=torch.float32, device=self.device)
+
+    def forward(self, params, frames, n, acts, capacity, offset, out):
+        _lib.check(self.lib.vn_policy_forward(self._h, _lib.ptr(params), ctypes.byref(frames), int(n), _lib.ptr(acts),
+                                              int(capacity), int(offset), _lib.ptr(out),
+                                              _lib.stream_ptr(self.device)), "vn_policy_forward")
+
+    def backward(self, params, frames, n, acts, capacity, dout, grads, workspace):
+        _lib.check(self.lib.vn_policy_backward(self._h, _lib.ptr(params), ctypes.byref(frames), int(n), _lib.ptr(acts),
+                                               int(capacity), _lib.ptr(dout), _lib.ptr(grads), _lib.ptr(workspace),
+                                               _lib.stream_ptr(self.device)), "vn_policy_backward")
+
+
+class _ReferenceNames:
+    """Resolve reference parameter names with or without the TimeDistributed/Sequential
+    nesting (e.g. 'shared_base.0.0.weight' or 'shared_base.module.0.weight')."""
+
+    def __init__(self, sd):
+        self.sd = {k: v for k, v in sd.items()}
+
+    def __call__(self, module, index, kind):
+        cands = []
+        for k in self.sd:
+            parts = k.split(".")
+            if parts[0] != module or parts[-1] != kind:
+                continue
+            nums = [int(p) for p in parts[1:-1] if re.fullmatch(r"\d+", p)]
+            cands.append((nums, k))
+        cands.sort()
+        if index >= len(cands):
+            raise KeyError("no %s[%d].%s in the state dict" % (module, index, kind))
+        return self.sd[cands[index][1]]
+
+
+class _GoalNavFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, params, image, goal, net):
+        n = image.shape[0]
+        acts = net.new_acts(n)
+        out = torch.empty((n, OUT_LD), dtype=torch.float32, device=params.device)
+        frames = frames_from_batch(image, goal)
+        net.forward(params, frames, n, acts, n, 0, out)
+        ctx.save_for_backward(params, image, goal, acts)
+        ctx.net = net
+        return out[:, : net.num_actions + 1]
+
+    @staticmethod
+    def backward(ctx, dout):
+        params, image, goal, acts = ctx.saved_tensors
+        net = ctx.net
+        n = image.shape[0]
+        d = torch.zeros((n, OUT_LD), dtype=torch.float32, device=params.device)
+        d[:, : net.num_actions + 1] = dout
+        grads = torch.empty_like(params)
+        ws = torch.empty(net.workspace_floats(n), dtype=torch.float32, device=params.device)
+        net.backward(params, frames_from_batch(image, goal), n, acts, n, d, grads, ws)
+        return grads, None, None, None
+
+
+class GoalNavPolicy(torch.nn.Module):
+    """Drop-in for BigGoalHouseModel's trunk + heads (see module docstring)."""
+
+    def __init__(self, num_inputs=3, num_outputs=4, frame_hw=(84, 84), device=None, seed=0):
+        super().__init__()
+        if num_inputs != 3:
+            raise ValueError("frames are RGB (num_inputs=3)")
+        self.net = PolicyNet(frame_hw, num_outputs, device)
+        self.params = torch.nn.Parameter(self.net.init_params(seed))
+        self.lstm_layers, self.lstm_hidden_size = 1, 512  # goal.py:61-62 (state shape contract)
+
+    def initial_states(self, batch_size):
+        return tuple(torch.zeros([batch_size, self.lstm_layers, self.lstm_hidden_size], dtype=torch.float32)
+                     for _ in range(2))
+
+    def load_reference_state_dict(self, sd):
+        with torch.no_grad():
+            self.params.copy_(self.net.from_reference(sd))
+        return self
+
+    def reference_state_dict(self):
+        return self.net.to_reference(self.params)
+
+    def forward(self, inputs, masks=None, states=None):
+        observations, _last_reward_action = inputs if isinstance(inputs, tuple) and len(inputs) == 2 and \
+            isinstance(inputs[0], (tuple, list)) else (inputs, None)
+        image, goal = observations[0], observations[1]
+        lead = image.shape[:2]
+        if image.dtype == torch.uint8:   # env frames [B,T,H,W,3]
+            img = image.reshape(-1, *image.shape[2:]).contiguous()
+            gl = goal.reshape(-1, *goal.shape[2:]).contiguous()
+        else:                            # reference wrapper output [B,T,3,H,W] float
+            img = image.reshape(-1, *image.shape[2:]).float().contiguous()
+            gl = goal.reshape(-1, *goal.shape[2:]).float().contiguous()
+        out = _GoalNavFunction.apply(self.params, img, gl, self.net)
+        A = self.net.num_actions
+        return [out[:, :A].reshape(*lead, A), out[:, A:A + 1].reshape(*lead, 1), states]

@@ -91,7 +91,8 @@ int vn_destroy(vn_ctx* ctx);
 int vn_reset(vn_ctx* ctx, const int32_t* env_mask_dev, vn_stream_t stream);
 
 /* Write the current (image, goal) frames, [n_envs][H][W][C] uint8 each, and the
- * current state index per env; any output may be NULL. */
+ * current state index per env; any output may be NULL. Also refreshes the img_row /
+ * goal_row info buffers (vn_set_info_buffers). */
 int vn_observe(vn_ctx* ctx, uint8_t* obs_dev, uint8_t* goal_dev, int32_t* state_dev,
                vn_stream_t stream);
 
@@ -139,6 +140,60 @@ int vn_scene_row_base(vn_ctx* ctx, int scene, int64_t* row_base);
 
 int vn_error_flags_sync(vn_ctx* ctx, uint32_t* flags, int clear);
 int vn_num_envs(vn_ctx* ctx);
+
+
+/* ---- policy: BigGoalHouseModel trunk + heads (models/goal.py:36-59,77-92) ---- */
+
+typedef struct vn_policy vn_policy;
+
+/* Frames for a batch of n samples (uint8 HWC, as the env emits them): sample i uses
+ * image + image_rows[i]*frame_bytes and goal + goal_rows[i]*frame_bytes (rows NULL =
+ * i). Passing the scene-cache arena (vn_frame_arena) with the env's img_row/goal_row
+ * info makes the policy input a zero-copy gather. image_f32/goal_f32, when set, are
+ * dense float [n][3][H][W] frames (the reference's TransposeImage + ScaledFloatFrame
+ * output) used instead. */
+typedef struct vn_frames {
+  const uint8_t* image;
+  const uint8_t* goal;
+  const int32_t* image_rows;
+  const int32_t* goal_rows;
+  int64_t frame_bytes;
+  const float* image_f32;
+  const float* goal_f32;
+} vn_frames;
+
+/* frame 84x84 or 174x174; num_actions 1..7. Parameters live in one flat fp32 buffer:
+ * per layer (conv1, conv2, conv3, conv4, conv_merge, head) W [Cout][ky][kx][Cin] (K padded
+ * to a multiple of 4) then b [Cout]; the head stacks policy_logits (rows 0..A-1) and critic
+ * (row A). layout12 = (w, b) float offsets per layer. */
+int vn_policy_create(int frame_h, int frame_w, int num_actions, vn_policy** out);
+int vn_policy_destroy(vn_policy* p);
+int vn_policy_info(vn_policy* p, int64_t* n_params, int64_t* act_floats_per_sample, int64_t* layout12);
+int vn_policy_workspace_floats(vn_policy* p, int64_t n_samples, int64_t* floats);
+/* out [n][8]: logits in 0..A-1, value at A. Activations of the n samples are kept at
+ * sample offset act_offset of an activation store holding act_capacity samples. */
+int vn_policy_forward(vn_policy* p, const float* params, const vn_frames* frames, int n, float* acts,
+                      int64_t act_capacity, int64_t act_offset, float* out, vn_stream_t stream);
+/* Gradients of the n samples stored from offset 0 given dL/d(out) [n][8]; overwrites grads
+ * (flat, same layout as params). Consumes the stored activations (conv1's are overwritten). */
+int vn_policy_backward(vn_policy* p, const float* params, const vn_frames* frames, int n, float* acts,
+                       int64_t act_capacity, const float* dout, float* grads, float* workspace,
+                       vn_stream_t stream);
+
+/* ---- A2C (the deep_rl trainer contract; DESIGN.md "A2C contract") ---- */
+int vn_policy_sample(const float* out, int n, int num_actions, uint64_t seed, uint64_t counter,
+                     int32_t* actions, float* logp, float* entropy, float* value, vn_stream_t stream);
+int vn_policy_greedy(const float* out, int n, int num_actions, int32_t* actions, vn_stream_t stream);
+int vn_a2c_returns(const float* rewards, const uint8_t* dones, const float* bootstrap_out, int T, int E,
+                   int num_actions, float gamma, float* returns, vn_stream_t stream);
+int vn_a2c_loss_grad(const float* out, const int32_t* actions, const float* returns, int n,
+                     int num_actions, float value_coef, float entropy_coef, float* dout,
+                     float* stats4, vn_stream_t stream);
+/* scalars2 = (total norm of scale*grads, clip coefficient) computed on the device. */
+int vn_grad_norm(const float* grads, int64_t n, float scale, float max_norm, double* partial_512,
+                 float* scalars2, vn_stream_t stream);
+int vn_rmsprop_step(float* params, const float* grads, float* square_avg, int64_t n, float scale,
+                    const float* scalars2, float lr, float alpha, float eps, vn_stream_t stream);
 
 /* Copy the message of the calling thread's last error (NUL-terminated). */
 int vn_last_error(char* buf, size_t len);

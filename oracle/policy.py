@@ -1,0 +1,99 @@
+"""BigGoalHouseModel trunk + heads in torch fp32 on the CPU (TEST INFRASTRUCTURE ONLY).
+
+Restates models/goal.py:36-59 and 77-92 of the reference (shared_base applied to image
+and goal with shared weights, channel concat, conv_base, conv_merge Linear -> 512, ReLU,
+then the policy_logits / critic Linear heads). The LSTM (goal.py:61-67) is out of the
+slice: the heads read the 512-d features directly. in_features
+of conv_merge is derived from the frame size (the reference hard-codes 9*9*32, valid
+only for 171-178 px inputs: documented deviation). Pinned against the reference modules
+by tests/golden/gen_model_goldens.py.
+"""
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+def trunk_sizes(h, w):
+    o1 = ((h - 7) // 4 + 1, (w - 7) // 4 + 1)
+    o2 = ((o1[0] - 4) // 2 + 1, (o1[1] - 4) // 2 + 1)
+    o3 = ((o2[0] - 4) // 2 + 1, (o2[1] - 4) // 2 + 1)
+    return o1, o2, o3
+
+
+class GoalNetOracle(nn.Module):
+    def __init__(self, frame_hw=(84, 84), num_inputs=3, num_outputs=4):
+        super().__init__()
+        _, _, o3 = trunk_sizes(*frame_hw)
+        self.conv1 = nn.Conv2d(num_inputs, 32, 7, stride=4)
+        self.conv2 = nn.Conv2d(32, 32, 4, stride=2)
+        self.conv3 = nn.Conv2d(64, 64, 4, stride=2)
+        self.conv4 = nn.Conv2d(64, 32, 1)
+        self.fc = nn.Linear(32 * o3[0] * o3[1], 512)
+        self.policy_logits = nn.Linear(512, num_outputs)
+        self.critic = nn.Linear(512, 1)
+
+    def features(self, image, goal):
+        """image, goal: float [N,3,H,W] (TransposeImage + ScaledFloatFrame output)."""
+        def base(x):
+            return F.relu(self.conv2(F.relu(self.conv1(x))))
+        x = torch.cat((base(image), base(goal)), 1)
+        x = F.relu(self.conv4(F.relu(self.conv3(x))))
+        return F.relu(self.fc(x.flatten(1)))
+
+    def forward(self, image, goal):
+        f = self.features(image, goal)
+        return self.policy_logits(f), self.critic(f)
+
+    def load_reference(self, sd):
+        """Reference state-dict names (deep_rl TimeDistributed wrapping an nn.Sequential)."""
+        m = {"shared_base.0.0": self.conv1, "shared_base.0.2": self.conv2,
+             "conv_base.0.0": self.conv3, "conv_base.0.2": self.conv4,
+             "conv_merge.0.1": self.fc, "policy_logits.0": self.policy_logits, "critic.0": self.critic}
+        for k, mod in m.items():
+            mod.weight.data.copy_(torch.as_tensor(sd[k + ".weight"]))
+            mod.bias.data.copy_(torch.as_tensor(sd[k + ".bias"]))
+        return self
+
+
+def frames_to_float(u8):
+    """uint8 [...,H,W,C] -> float32 [...,C,H,W] / 255 (TransposeImage + ScaledFloatFrame)."""
+    x = torch.as_tensor(u8)
+    return x.permute(*range(x.dim() - 3), -1, -3, -2).to(torch.float32) / 255.0
+
+
+REFERENCE_PARAM_ORDER = (  # BigGoalHouseModel.named_parameters() order for the used modules
+    "shared_base.0.0.weight", "shared_base.0.0.bias", "shared_base.0.2.weight", "shared_base.0.2.bias",
+    "conv_base.0.0.weight", "conv_base.0.0.bias", "conv_base.0.2.weight", "conv_base.0.2.bias",
+    "conv_merge.0.1.weight", "conv_merge.0.1.bias", "critic.0.weight", "critic.0.bias",
+    "policy_logits.0.weight", "policy_logits.0.bias",
+)
+
+
+def reference_shapes(frame_hw=(84, 84), num_outputs=4):
+    _, _, o3 = trunk_sizes(*frame_hw)
+    return {
+        "shared_base.0.0.weight": (32, 3, 7, 7), "shared_base.0.0.bias": (32,),
+        "shared_base.0.2.weight": (32, 32, 4, 4), "shared_base.0.2.bias": (32,),
+        "conv_base.0.0.weight": (64, 64, 4, 4), "conv_base.0.0.bias": (64,),
+        "conv_base.0.2.weight": (32, 64, 1, 1), "conv_base.0.2.bias": (32,),
+        "conv_merge.0.1.weight": (512, 32 * o3[0] * o3[1]), "conv_merge.0.1.bias": (512,),
+        "critic.0.weight": (1, 512), "critic.0.bias": (1,),
+        "policy_logits.0.weight": (num_outputs, 512), "policy_logits.0.bias": (num_outputs,),
+    }
+
+
+def seeded_reference_state(frame_hw, seed):
+    """The weights tests/golden/gen_model_goldens.py:seeded_weights draws (PCG64)."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    shapes = reference_shapes(frame_hw)
+    out = {}
+    for name in REFERENCE_PARAM_ORDER:
+        shape = shapes[name]
+        if name.endswith("bias"):
+            v = rng.uniform(-0.05, 0.05, size=shape)
+        else:
+            d = 1.0 / np.sqrt(int(np.prod(shape[1:])))
+            v = rng.uniform(-d, d, size=shape)
+        out[name] = v.astype(np.float32)
+    return out

@@ -1,0 +1,115 @@
+"""Generate policy golden vectors by running the REFERENCE model modules (models/goal.py).
+
+Run ONLY in the build container:  python tests/golden/gen_model_goldens.py
+(python3.10 + torch; deep_rl.model is replaced by the stand-ins under
+tests/golden/stubs/deep_rl because deep-rl==0.2.9 is absent from the image).
+
+Cases
+  84x84  BigGoalHouseModel(3, 4) with conv_merge's Linear(9*9*32, 512) rebuilt as
+         Linear(288, 512) (the 84x84 trunk ends at 3x3x32) and re-initialised with the
+         reference's own init_weights; biases then perturbed so bias paths are exercised.
+  174x174 the unmodified reference topology (Linear(2592, 512)).
+For each: weights (reference state-dict names), uint8 frame inputs, trunk features,
+logits and value from the reference modules, and the gradients of the engine's A2C
+loss (oracle/a2c.py, parity unpinned at the trainer level) through the reference
+modules by torch autograd.
+"""
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path[:0] = [os.path.join(HERE, "stubs"), "/root/reference", REPO]
+
+from models.goal import BigGoalHouseModel  # noqa: E402  (the reference module)
+
+from oracle import a2c  # noqa: E402
+
+
+def build(frame, seed):
+    torch.manual_seed(seed)
+    model = BigGoalHouseModel(3, 4)
+    if frame != 174:
+        o = (frame - 7) // 4 + 1
+        o = (o - 4) // 2 + 1
+        o = (o - 4) // 2 + 1
+        lin = nn.Linear(32 * o * o, 512)
+        model.init_weights(lin)
+        model.conv_merge[0][1] = lin
+    g = torch.Generator().manual_seed(seed + 1)
+    for name, p in model.named_parameters():
+        if name.endswith("bias"):
+            p.data.uniform_(-0.05, 0.05, generator=g)
+    return model
+
+
+def reference_forward(model, image_u8, goal_u8):
+    """models/goal.py:83-90 up to conv_merge, then the two heads (goal.py:79-80) on the
+    pre-LSTM features. Inputs uint8 [B,T,H,W,3] -> float [B,T,3,H,W] / 255."""
+    img = image_u8.permute(0, 1, 4, 2, 3).float() / 255.0
+    gl = goal_u8.permute(0, 1, 4, 2, 3).float() / 255.0
+    a, b = model.shared_base(img), model.shared_base(gl)
+    feats = model.conv_merge(model.conv_base(torch.cat((a, b), 2)))
+    return feats, model.policy_logits(feats), model.critic(feats)
+
+
+USED = ("shared_base", "conv_base", "conv_merge", "policy_logits", "critic")
+
+
+def seeded_weights(model, seed):
+    """Deterministic weights from numpy's PCG64 (stable across versions) in the reference's
+    init distribution U(-1/sqrt(fan_in), 1/sqrt(fan_in)); lets a large case be regenerated
+    from its seed instead of being stored."""
+    rng = np.random.default_rng(seed)
+    for name, p in model.named_parameters():
+        if name.split(".")[0] not in USED:
+            continue
+        if name.endswith("bias"):
+            v = rng.uniform(-0.05, 0.05, size=p.shape)
+        else:
+            fan_in = int(np.prod(p.shape[1:]))
+            d = 1.0 / np.sqrt(fan_in)
+            v = rng.uniform(-d, d, size=p.shape)
+        p.data.copy_(torch.as_tensor(v.astype(np.float32)))
+
+
+def case(frame, B, T, seed, store_weights=True):
+    model = build(frame, seed)
+    if not store_weights:
+        seeded_weights(model, seed)
+    rng = np.random.RandomState(seed)
+    image = torch.as_tensor(rng.randint(0, 256, size=(B, T, frame, frame, 3)).astype(np.uint8))
+    goal = torch.as_tensor(rng.randint(0, 256, size=(B, T, frame, frame, 3)).astype(np.uint8))
+    feats, logits, value = reference_forward(model, image, goal)
+    N = B * T
+    actions = torch.as_tensor(rng.randint(0, 4, size=N))
+    rets = torch.as_tensor(rng.randn(N).astype(np.float32))
+    loss, _ = a2c.loss(logits.reshape(N, 4), value.reshape(N), actions, rets)
+    model.zero_grad()
+    loss.backward()
+    out = {"image": image.numpy(), "goal": goal.numpy(), "features": feats.detach().numpy(),
+           "logits": logits.detach().numpy(), "value": value.detach().numpy(),
+           "actions": actions.numpy().astype(np.int32), "returns": rets.numpy(),
+           "loss": np.array([loss.item()], dtype=np.float32)}
+    out["seed"] = np.array([seed])
+    if store_weights:
+        for name, p in model.named_parameters():
+            if name.split(".")[0] in USED:
+                out["w:" + name] = p.detach().numpy()
+                out["g:" + name] = p.grad.numpy()
+    return out
+
+
+def main():
+    np.savez_compressed(os.path.join(HERE, "policy84.npz"), **case(84, 3, 2, 11))
+    np.savez_compressed(os.path.join(HERE, "policy174.npz"), **case(174, 2, 1, 12, store_weights=False))
+    n_params = sum(p.numel() for n, p in build(84, 0).named_parameters() if n.split(".")[0] in USED)
+    print("84x84 trunk+heads parameters:", n_params)
+
+
+if __name__ == "__main__":
+    main()

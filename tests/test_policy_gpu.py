@@ -1,0 +1,238 @@
+"""Policy forward/backward HIP kernels vs the reference modules' goldens and the torch
+fp32 CPU oracle. Tolerances: logits/values/features rtol 1e-5 (north-star bar);
+parameter gradients rtol 1e-4 of each tensor's scale (long fp32 reductions summed in a
+different order)."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import a2c as oa2c
+from oracle.policy import GoalNetOracle, frames_to_float, seeded_reference_state
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref_state(d):
+    return {k[2:]: d[k] for k in d.files if k.startswith("w:")}
+
+
+def _close(a, b, rtol, what):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    scale = max(np.abs(b).max(), 1e-30)
+    err = np.abs(a - b).max() / scale
+    assert err <= rtol, "%s: max err %.3g of scale %.3g" % (what, err, scale)
+
+
+def run_forward(net, params, image, goal):
+    from vnav.policy import frames_from_batch
+    n = image.shape[0]
+    acts = net.new_acts(n)
+    out = torch.zeros((n, 8), dtype=torch.float32, device="cuda")
+    net.forward(params, frames_from_batch(image, goal), n, acts, n, 0, out)
+    return out, acts
+
+
+def x5_of(net, acts, n):
+    off = sum(n * s for s in _act_sizes(net)[:4])
+    return acts[off:off + n * 512].view(n, 512)
+
+
+def _act_sizes(net):
+    h, w = net.frame_hw
+    o1 = ((h - 7) // 4 + 1, (w - 7) // 4 + 1)
+    o2 = ((o1[0] - 4) // 2 + 1, (o1[1] - 4) // 2 + 1)
+    o3 = ((o2[0] - 4) // 2 + 1, (o2[1] - 4) // 2 + 1)
+    return [2 * o1[0] * o1[1] * 32, 2 * o2[0] * o2[1] * 32, o3[0] * o3[1] * 64, o3[0] * o3[1] * 32, 512]
+
+
+def test_forward_matches_reference_84(golden):
+    from vnav.policy import PolicyNet
+    d = golden("policy84.npz")
+    net = PolicyNet((84, 84), 4)
+    params = net.from_reference(_ref_state(d))
+    img = torch.as_tensor(d["image"].reshape(-1, 84, 84, 3)).cuda()
+    gl = torch.as_tensor(d["goal"].reshape(-1, 84, 84, 3)).cuda()
+    out, acts = run_forward(net, params, img, gl)
+    out = out.cpu().numpy()
+    _close(out[:, :4], d["logits"].reshape(-1, 4), 1e-5, "logits")
+    _close(out[:, 4:5], d["value"].reshape(-1, 1), 1e-5, "value")
+    _close(x5_of(net, acts, img.shape[0]).cpu().numpy(), d["features"].reshape(-1, 512), 1e-5, "features")
+
+
+def test_forward_matches_reference_174(golden):
+    from vnav.policy import PolicyNet
+    d = golden("policy174.npz")
+    net = PolicyNet((174, 174), 4)
+    params = net.from_reference(seeded_reference_state((174, 174), int(d["seed"][0])))
+    img = torch.as_tensor(d["image"].reshape(-1, 174, 174, 3)).cuda()
+    gl = torch.as_tensor(d["goal"].reshape(-1, 174, 174, 3)).cuda()
+    out, acts = run_forward(net, params, img, gl)
+    out = out.cpu().numpy()
+    _close(out[:, :4], d["logits"].reshape(-1, 4), 1e-5, "logits")
+    _close(out[:, 4:5], d["value"].reshape(-1, 1), 1e-5, "value")
+
+
+def loss_grad_dev(out, actions, rets, vc=0.5, ec=0.01):
+    from vnav import _lib
+    lib = _lib.load()
+    n = out.shape[0]
+    dout = torch.zeros_like(out)
+    stats = torch.zeros(4, dtype=torch.float32, device="cuda")
+    _lib.check(lib.vn_a2c_loss_grad(_lib.ptr(out), _lib.ptr(actions), _lib.ptr(rets), n, 4, ctypes.c_float(vc),
+                                    ctypes.c_float(ec), _lib.ptr(dout), _lib.ptr(stats),
+                                    _lib.stream_ptr(out.device)), "loss_grad")
+    return dout, stats
+
+
+def test_backward_matches_reference_84(golden):
+    from vnav.policy import PolicyNet, frames_from_batch
+    d = golden("policy84.npz")
+    net = PolicyNet((84, 84), 4)
+    params = net.from_reference(_ref_state(d))
+    img = torch.as_tensor(d["image"].reshape(-1, 84, 84, 3)).cuda()
+    gl = torch.as_tensor(d["goal"].reshape(-1, 84, 84, 3)).cuda()
+    n = img.shape[0]
+    out, acts = run_forward(net, params, img, gl)
+    actions = torch.as_tensor(d["actions"]).cuda()
+    rets = torch.as_tensor(d["returns"]).cuda()
+    dout, stats = loss_grad_dev(out, actions, rets)
+    grads = torch.empty_like(params)
+    ws = torch.empty(net.workspace_floats(n), dtype=torch.float32, device="cuda")
+    net.backward(params, frames_from_batch(img, gl), n, acts, n, dout, grads, ws)
+    g = net.to_reference(grads)
+    for k, v in g.items():
+        _close(v.numpy(), d["g:" + k], 1e-4, k)
+    s = stats.cpu().numpy() / n
+    loss = 0.5 * s[0] + s[1] - 0.01 * s[2]
+    np.testing.assert_allclose(loss, d["loss"][0], rtol=1e-5)
+
+
+def test_autograd_policy_vs_torch_oracle():
+    """GoalNavPolicy through torch.autograd (custom Function over the HIP kernels) vs the
+    CPU oracle at a larger batch, random weights/biases, both input formats."""
+    from vnav.policy import GoalNavPolicy
+    torch.manual_seed(0)
+    pol = GoalNavPolicy(3, 4, (84, 84))
+    with torch.no_grad():
+        pol.params.add_(torch.randn_like(pol.params) * 0.01)
+    ref = GoalNetOracle((84, 84)).load_reference(pol.reference_state_dict())
+    B, T = 4, 5
+    rng = np.random.RandomState(1)
+    img = torch.as_tensor(rng.randint(0, 256, size=(B, T, 84, 84, 3)).astype(np.uint8))
+    gl = torch.as_tensor(rng.randint(0, 256, size=(B, T, 84, 84, 3)).astype(np.uint8))
+    logits, value, _ = pol(((img.cuda(), gl.cuda()), None), None, None)
+    actions = torch.as_tensor(rng.randint(0, 4, size=B * T))
+    rets = torch.as_tensor(rng.randn(B * T).astype(np.float32))
+    loss, _ = oa2c.loss(logits.reshape(-1, 4), value.reshape(-1), actions.cuda(), rets.cuda())
+    loss.backward()
+    rl, rv = ref(frames_to_float(img.reshape(-1, 84, 84, 3)), frames_to_float(gl.reshape(-1, 84, 84, 3)))
+    _close(logits.detach().cpu().reshape(-1, 4), rl.detach(), 1e-5, "logits")
+    _close(value.detach().cpu().reshape(-1, 1), rv.detach(), 1e-5, "value")
+    rloss, _ = oa2c.loss(rl, rv.view(-1), actions, rets)
+    rloss.backward()
+    mine = pol.net.to_reference(pol.params.grad)
+    names = {"shared_base.0.0": ref.conv1, "shared_base.0.2": ref.conv2, "conv_base.0.0": ref.conv3,
+             "conv_base.0.2": ref.conv4, "conv_merge.0.1": ref.fc, "policy_logits.0": ref.policy_logits,
+             "critic.0": ref.critic}
+    for k, mod in names.items():
+        _close(mine[k + ".weight"].numpy(), mod.weight.grad.numpy(), 1e-4, k + ".weight")
+        _close(mine[k + ".bias"].numpy(), mod.bias.grad.numpy(), 1e-4, k + ".bias")
+    # float CHW input (the reference wrapper format) gives the same outputs
+    lf, vf, _ = pol(((frames_to_float(img).cuda(), frames_to_float(gl).cuda()), None), None, None)
+    _close(lf.detach().cpu(), logits.detach().cpu(), 1e-6, "f32 input logits")
+
+
+def test_row_gather_equals_dense_batch():
+    import vnav
+    from vnav.policy import PolicyNet, frames_from_batch, frames_from_rows
+    sc = [vnav.synthetic_scene(k) for k in range(2)]
+    env = vnav.VectorEnv(sc, 50, seed=4)
+    (img, gl) = env.observe()
+    net = PolicyNet((84, 84), 4)
+    params = net.init_params(3)
+    out1, _ = run_forward(net, params, img, gl)
+    arena, fb, _, _ = env.frame_arena()
+    acts = net.new_acts(50)
+    out2 = torch.zeros_like(out1)
+    net.forward(params, frames_from_rows(arena, fb, env._info["img_row"], env._info["goal_row"]), 50, acts, 50, 0, out2)
+    assert torch.equal(out1, out2)
+
+
+def test_a2c_kernels_vs_oracle():
+    from vnav import _lib
+    lib = _lib.load()
+    st = _lib.stream_ptr(torch.device("cuda", 0))
+    T, E = 7, 33
+    g = torch.Generator().manual_seed(0)
+    rewards = (torch.rand(T, E, generator=g) < 0.2).float()
+    dones = torch.rand(T, E, generator=g) < 0.1
+    boot = torch.randn(E, 8, generator=g)
+    R = torch.zeros(T * E, device="cuda")
+    rw_d, dn_d, bt_d = rewards.cuda(), dones.cuda(), boot.cuda()  # keep device tensors alive
+    _lib.check(lib.vn_a2c_returns(_lib.ptr(rw_d), _lib.ptr(dn_d), _lib.ptr(bt_d), T, E, 4,
+                                  ctypes.c_float(0.99), _lib.ptr(R), st), "returns")
+    vext = torch.zeros(T + 1, E)
+    vext[T] = boot[:, 4]
+    Rref = oa2c.returns(rewards, dones, vext, 0.99)
+    _close(R.cpu().view(T, E), Rref, 1e-6, "returns")
+    # loss gradient vs autograd on the oracle loss
+    N = T * E
+    out = torch.randn(N, 8, generator=g)
+    acts = torch.randint(0, 4, (N,), generator=g)
+    out_d, acts_d, R_d = out.cuda(), acts.int().cuda(), Rref.view(-1).cuda()
+    dout, stats = loss_grad_dev(out_d, acts_d, R_d)
+    lg = out[:, :4].clone().requires_grad_(True)
+    v = out[:, 4].clone().requires_grad_(True)
+    loss, parts = oa2c.loss(lg, v, acts, Rref.view(-1))
+    loss.backward()
+    _close(dout.cpu()[:, :4], lg.grad, 1e-5, "dlogits")
+    _close(dout.cpu()[:, 4], v.grad, 1e-5, "dvalue")
+    s = stats.cpu() / N
+    np.testing.assert_allclose(s[0].item(), parts["value_loss"].item(), rtol=1e-5)
+    np.testing.assert_allclose(s[1].item(), parts["action_loss"].item(), rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(s[2].item(), parts["entropy"].item(), rtol=1e-5)
+    # clip + RMSprop vs the torch restatement, two steps
+    P = 10001
+    p0 = torch.randn(P, generator=g)
+    gr = torch.randn(P, generator=g) * 0.01
+    pd, sq = p0.clone().cuda(), torch.zeros(P, device="cuda")
+    gr_d = gr.cuda()
+    part = torch.zeros(512, dtype=torch.float64, device="cuda")
+    sc = torch.zeros(2, device="cuda")
+    pr, sr = [p0.clone()], [torch.zeros(P)]
+    for it in range(2):
+        _lib.check(lib.vn_grad_norm(_lib.ptr(gr_d), P, ctypes.c_float(0.5), ctypes.c_float(0.5), _lib.ptr(part),
+                                    _lib.ptr(sc), st), "norm")
+        _lib.check(lib.vn_rmsprop_step(_lib.ptr(pd), _lib.ptr(gr_d), _lib.ptr(sq), P, ctypes.c_float(0.5),
+                                       _lib.ptr(sc), ctypes.c_float(7e-4), ctypes.c_float(0.99),
+                                       ctypes.c_float(1e-5), st), "rmsprop")
+        norm = oa2c.clip_and_rmsprop(pr, [gr * 0.5], sr, 7e-4)
+        np.testing.assert_allclose(sc[0].item(), norm.item(), rtol=1e-5)
+    _close(pd.cpu(), pr[0], 1e-6, "params after RMSprop")
+
+
+def test_sampling_distribution():
+    from vnav import _lib
+    from oracle import philox
+    lib = _lib.load()
+    n = 200000
+    logits = torch.tensor([[0.5, -1.0, 2.0, 0.0]]).repeat(n, 1)
+    out = torch.zeros(n, 8)
+    out[:, :4] = logits
+    a = torch.zeros(n, dtype=torch.int32, device="cuda")
+    out_d = out.cuda()
+    _lib.check(lib.vn_policy_sample(_lib.ptr(out_d), n, 4, ctypes.c_uint64(5), ctypes.c_uint64(9), _lib.ptr(a),
+                                    None, None, None, _lib.stream_ptr(a.device)), "sample")
+    a = a.cpu().numpy()
+    p = torch.softmax(logits[0], 0).numpy()
+    freq = np.bincount(a, minlength=4) / n
+    assert np.abs(freq - p).max() < 5e-3
+    # the inverse-CDF draw restated on the host (Philox stream 3) picks the same actions
+    r = philox.philox4x32_10(np.arange(n), 9, 0, philox.STREAM_POLICY, 5, 0)[0]
+    u = (r >> 8).astype(np.float64) * (1.0 / 16777216.0)
+    cdf = np.cumsum(p)
+    ref = np.minimum(np.searchsorted(cdf[:-1], u, side="right"), 3)
+    assert (ref == a).mean() > 0.999
