@@ -28,6 +28,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+FP32_MFMA_PEAK_TFLOPS = 157.3  # dense f32 MFMA = f32 vector peak (MI355X_MICROARCH.md)
 
 
 def alg_bytes_per_env_step(frame_bytes):
@@ -44,7 +45,59 @@ def parse():
     p.add_argument("--scenes", type=int, default=20)
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--train-steps", type=int, default=6, help="timed A2C updates (0 = skip the train leg)")
+    p.add_argument("--train-warmup", type=int, default=2)
+    p.add_argument("--num-steps", type=int, default=20, help="A2C rollout length (reference: 20)")
     return p.parse_args()
+
+
+def train_flops_per_env_step(h=84, w=84, A=4, T=20):
+    """Algorithmic FLOPs of one A2C env-step: policy forward (kept activations serve the
+    backward), weight gradients of every layer, input gradients of all but conv1, and the
+    bootstrap forward amortised over the rollout."""
+    o1 = ((h - 7) // 4 + 1, (w - 7) // 4 + 1)
+    o2 = ((o1[0] - 4) // 2 + 1, (o1[1] - 4) // 2 + 1)
+    o3 = ((o2[0] - 4) // 2 + 1, (o2[1] - 4) // 2 + 1)
+    p1, p2, p3 = o1[0] * o1[1], o2[0] * o2[1], o3[0] * o3[1]
+    macs = [2 * p1 * 32 * 147, 2 * p2 * 32 * 512, p3 * 64 * 1024, p3 * 32 * 64, 512 * 32 * p3, (A + 1) * 512]
+    fwd = 2 * sum(macs)
+    return fwd + fwd + 2 * sum(macs[1:]) + fwd / T, fwd
+
+
+def bench_train(args, scenes, dev, world, rank):
+    """A2C training throughput: one step = rollout of num_steps on every local env (policy
+    forward + sampling + env step) + backward + one RCCL all-reduce of the flat gradient +
+    clip + RMSprop."""
+    import vnav
+    E, T = args.envs, args.num_steps
+    env = vnav.VectorEnv(scenes, E, seed=2000 + rank, device=dev)
+    tr = vnav.A2CTrainer(env, num_steps=T, seed=7, max_time_steps=1e12)
+    for _ in range(args.train_warmup):
+        tr.step(sync=False)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        torch.distributed.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.train_steps):
+        tr.step(sync=False)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        torch.distributed.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        el = float(t[0])
+    steps = E * T * args.train_steps * world
+    flops, fwd = train_flops_per_env_step(T=T)
+    tflops = E * T * args.train_steps * flops / el / 1e12
+    res = {"value": steps / el, "unit": "env-steps/s", "updates": args.train_steps, "envs_per_gpu": E,
+           "num_steps": T, "ms_per_update": el / args.train_steps * 1e3, "dtype": "f32",
+           "roofline": {"bound": "mfma", "achieved": tflops, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": tflops / FP32_MFMA_PEAK_TFLOPS, "flops_per_env_step": flops,
+                        "scope": "whole update (all kernels), algorithmic FLOPs"}}
+    del tr, env
+    return res
 
 
 # ---------------------------------------------------------------- CPU baseline
@@ -154,6 +207,11 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
     flags = env.error_flags()
+    del env, out
+    train = None
+    if args.train_steps > 0:
+        torch.cuda.empty_cache()
+        train = bench_train(args, scenes, dev, world, rank)
     if rank == 0:
         env_steps = E * K * world
         value = env_steps / elapsed
@@ -178,13 +236,14 @@ def main():
                                    "TimeLimit 900" % (args.scenes, cache_mb,
                                                       "HBM-resident" if cache_mb > 256 else "LLC-resident",
                                                       E),
-                       "envs_per_gpu": E, "scenes": args.scenes, "frame": list(env.frame_shape),
+                       "envs_per_gpu": E, "scenes": args.scenes, "frame": list(scenes[0].frame_shape),
                        "parallelism": "dp%d (independent env shards, replicated scene cache)" % world},
             "roofline": {"bound": "hbm", "kernel": "vn_step (env_kernel<MODE_STEP,16>)",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                          "bytes_per_env_step": bpe, "kernel_ms": kern_ms},
             "cpu_baseline": cpu,
+            "train": train,
             "error_flags": flags,
         }
         print(json.dumps(line))
