@@ -20,6 +20,7 @@ import time
 import torch
 
 from . import _lib
+from . import dist as vdist
 from .policy import OUT_LD, PolicyNet, frames_from_rows
 
 
@@ -41,16 +42,11 @@ class A2CTrainer:
         self.entropy_coefficient = float(entropy_coefficient)
         self.seed = int(seed)
         self.group = process_group
-        self.world = 1
-        self.rank = 0
-        if torch.distributed.is_available() and torch.distributed.is_initialized():
-            self.world = torch.distributed.get_world_size(process_group)
-            self.rank = torch.distributed.get_rank(process_group)
+        self.world, self.rank = vdist.world_of(process_group)
         self.net = net if net is not None else PolicyNet(env.frame_shape[:2], env.num_actions, self.device)
         self.A = self.net.num_actions
         self.params = params if params is not None else self.net.init_params(self.seed)
-        if self.world > 1:
-            torch.distributed.broadcast(self.params, src=0, group=self.group)
+        vdist.broadcast_params_(self.params, group=self.group)
         P = self.net.n_params
         E, T = env.num_envs, self.num_steps
         N = T * E
@@ -111,7 +107,7 @@ class A2CTrainer:
             net.forward(self.params, self._frames(self.rows_img[sl], self.rows_goal[sl]), E, self.acts, N, t * E,
                         self.out[sl])
             counter = (self.num_updates * T + t) & (2 ** 64 - 1)
-            _lib.check(lib.vn_policy_sample(_lib.ptr(self.out[sl]), E, A, ctypes.c_uint64(self.seed * 7919 + self.rank),
+            _lib.check(lib.vn_policy_sample(_lib.ptr(self.out[sl]), E, A, ctypes.c_uint64(vdist.rank_seed(self.seed, self.rank)),
                                             ctypes.c_uint64(counter), _lib.ptr(self.actions[sl]), None, None, None,
                                             self._stream()), "vn_policy_sample")
             env.step(self.actions[sl], out=dict(reward=self.rewards[t], done=self.dones[t], state=self.states),
@@ -137,10 +133,7 @@ class A2CTrainer:
                                         _lib.ptr(self.stats), st), "vn_a2c_loss_grad")
         net.backward(self.params, self._frames(self.rows_img, self.rows_goal), N, self.acts, N, self.dout, self.grads,
                      self.workspace)
-        scale = 1.0
-        if self.world > 1:
-            torch.distributed.all_reduce(self.grads, group=self.group)  # RCCL, one flat bucket
-            scale = 1.0 / self.world
+        scale = vdist.allreduce_gradients_(self.grads, self.group)  # RCCL, one flat bucket
         P = net.n_params
         _lib.check(lib.vn_grad_norm(_lib.ptr(self.grads), P, ctypes.c_float(scale),
                                     ctypes.c_float(self.max_gradient_norm), _lib.ptr(self.norm_partial),
@@ -159,15 +152,12 @@ class A2CTrainer:
         N = self.num_steps * self.env.num_envs
         self.total_steps += N * self.world
         self.num_updates += 1
-        m = torch.cat([self.stats / N, self.episode_stats, self.scalars[:1]])
-        if self.world > 1:
-            torch.distributed.all_reduce(m, group=self.group)
-            m[:4] /= self.world
-            m[7] /= self.world
+        m = torch.cat([self.stats / N, self.scalars[:1], self.episode_stats])
+        vdist.reduce_metrics_(m, 5, self.group)
         if not sync:
             return {"raw": m}
         vals = m.tolist()
-        vl, al, ent, ret_mean, eps, rsum, lsum, gnorm = vals
+        vl, al, ent, ret_mean, gnorm, eps, rsum, lsum = vals
         dt = time.perf_counter() - t0
         return {
             "step": self.total_steps, "updates": self.num_updates,

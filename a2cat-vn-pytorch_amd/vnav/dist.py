@@ -1,0 +1,76 @@
+"""Data parallelism: one process per GPU, torch.distributed over RCCL ("nccl" on ROCm).
+
+Envs are independent, so each rank owns its own env shard and a full replica of the
+scene cache; the only data-path exchange is ONE all-reduce of the flat
+fp32 gradient buffer per update (0.96 MB for the 84x84 policy: latency-bound on xGMI,
+issued as a single call), plus one tiny all-reduce of the episode/loss statistics.
+The reference has no distributed code at all (it runs 4 SubprocVecEnv processes on
+one GPU, experiments/thor_cached_auxiliary.py:58-71).
+"""
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def env_rank():
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def init_distributed(backend=None):
+    """Initialise from torchrun's environment. Returns (rank, world, local_rank)."""
+    rank, world, local = env_rank()
+    if world > 1 and not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        kw = {}
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            kw["device_id"] = torch.device("cuda", local)
+        dist.init_process_group(backend, rank=rank, world_size=world, **kw)
+    return rank, world, local
+
+
+def world_of(group=None):
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(group), dist.get_rank(group)
+    return 1, 0
+
+
+def allreduce_gradients_(flat, group=None):
+    """SUM-all-reduce the flat gradient in place; returns the 1/world scale the update
+    kernels fold into the gradient norm and the RMSprop step (no extra pass)."""
+    world, _ = world_of(group)
+    if world > 1:
+        dist.all_reduce(flat, group=group)
+    return 1.0 / world
+
+
+def reduce_metrics_(m, n_mean, group=None):
+    """m = [mean stats (n_mean entries) | summed counters]: average the first n_mean
+    entries over ranks and sum the rest."""
+    world, _ = world_of(group)
+    if world > 1:
+        dist.all_reduce(m, group=group)
+        m[:n_mean] /= world
+    return m
+
+
+def broadcast_params_(flat, src=0, group=None):
+    world, _ = world_of(group)
+    if world > 1:
+        dist.broadcast(flat, src=src, group=group)
+    return flat
+
+
+def rank_seed(seed, rank):
+    """Distinct, reproducible per-rank seeds for env resets and policy sampling."""
+    return (int(seed) * 1000003 + int(rank) * 7919 + 1) & (2**63 - 1)
+
+
+def shard(n_total, world, rank):
+    """Contiguous env shard [start, start+count) of rank (envs e -> GPU e // per)."""
+    per, extra = divmod(int(n_total), int(world))
+    start = rank * per + min(rank, extra)
+    return start, per + (1 if rank < extra else 0)

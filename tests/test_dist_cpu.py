@@ -1,0 +1,101 @@
+"""Multi-process data parallelism on the CPU (gloo, world_size 2): the product's DP
+helpers (vnav/dist.py) average gradients so that the per-rank A2C gradients of two env
+shards equal the single-process gradient over the concatenated batch (computed with the
+CPU oracle model), and reduce the metrics as the trainer expects."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from conftest import PKG, REPO
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, q):
+    import sys
+    for p in (REPO, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+    from oracle import a2c
+    from oracle.policy import GoalNetOracle
+    from vnav import dist as vdist
+    r, w, _ = vdist.init_distributed(backend="gloo")
+    assert (r, w) == (rank, world)
+    torch.manual_seed(0)
+    net = GoalNetOracle((84, 84))
+    g = torch.Generator().manual_seed(1)
+    N = 8
+    img = torch.rand(N, 3, 84, 84, generator=g)
+    goal = torch.rand(N, 3, 84, 84, generator=g)
+    acts = torch.randint(0, 4, (N,), generator=g)
+    rets = torch.randn(N, generator=g)
+    start, count = vdist.shard(N, world, rank)
+    sl = slice(start, start + count)
+    lg, v = net(img[sl], goal[sl])
+    loss, parts = a2c.loss(lg, v.view(-1), acts[sl], rets[sl])
+    loss.backward()
+    flat = torch.cat([p.grad.reshape(-1) for p in net.parameters()])
+    scale = vdist.allreduce_gradients_(flat)
+    m = torch.tensor([parts["value_loss"].item(), 0.0, 0.0, 0.0, 1.0, float(count), 2.0, 3.0])
+    vdist.reduce_metrics_(m, 5)
+    seeds = [vdist.rank_seed(5, rr) for rr in range(world)]
+    q.put((rank, (flat * scale).numpy(), m.numpy(), len(set(seeds))))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_gradient_average_equals_full_batch():
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort()
+    g0, g1 = res[0][1], res[1][1]
+    np.testing.assert_array_equal(g0, g1)  # every rank holds the same averaged gradient
+    # single process, concatenated batch
+    from oracle import a2c
+    from oracle.policy import GoalNetOracle
+    torch.manual_seed(0)
+    net = GoalNetOracle((84, 84))
+    g = torch.Generator().manual_seed(1)
+    N = 8
+    img = torch.rand(N, 3, 84, 84, generator=g)
+    goal = torch.rand(N, 3, 84, 84, generator=g)
+    acts = torch.randint(0, 4, (N,), generator=g)
+    rets = torch.randn(N, generator=g)
+    lg, v = net(img, goal)
+    loss, _ = a2c.loss(lg, v.view(-1), acts, rets)
+    loss.backward()
+    full = torch.cat([p.grad.reshape(-1) for p in net.parameters()]).numpy()
+    np.testing.assert_allclose(g0, full, rtol=1e-4, atol=1e-7)
+    m = res[0][2]
+    assert m[4] == 1.0 and m[5] == 8.0 and m[6] == 4.0  # means averaged, counters summed
+    assert res[0][3] == world
+
+
+def test_shard_covers_all_envs():
+    from vnav.dist import shard
+    for n, w in ((32768, 8), (10, 3), (4096, 1)):
+        spans = [shard(n, w, r) for r in range(w)]
+        assert spans[0][0] == 0 and sum(c for _, c in spans) == n
+        for (s0, c0), (s1, _) in zip(spans, spans[1:]):
+            assert s0 + c0 == s1
