@@ -1,0 +1,165 @@
+// vn_conv1.h — conv1 (Conv2d(3->32, k7, s4) on uint8 frames) forward and weight
+// gradient, specialised for gfx950 (included by vn_policy.hip after FrameSrc).
+//
+// The frame(s) of a workgroup are staged once into LDS with 16-B (or 4-B) loads from
+// the scene-cache arena rows; operands are then read byte-wise from LDS and converted
+// with v_cvt_f32_ubyte (exact integers). Because the conv is linear in x = u/255, the
+// 1/255 is applied once to each accumulated sum (epilogue / reduce) instead of to every
+// operand — the same fp32 result up to rounding order (parity tests at 1e-5 rel).
+// MFMA: v_mfma_f32_32x32x2_f32 (64-cycle issue = 64-cycle dependent latency, so one
+// accumulator chain per wave runs at the full rate).
+//   forward: D[pixel 32][co 32] += A[pixel][k] * B[k][co]; the 74 B fragments (all of K)
+//            stay in registers for the whole kernel; one LDS byte per lane per MFMA.
+//   wgrad:   D[co 32][k 32] += A[co][pixel] * B[pixel][k] over 5 k-tiles (148 + bias
+//            column); A is read straight from dZ (NHWC: 256 contiguous bytes per wave
+//            and step), B from the LDS frame; per-wave partial sums go to slabs that a
+//            deterministic reduce sums (and scales by 1/255).
+#pragma once
+
+namespace vn {
+
+typedef float f16v __attribute__((ext_vector_type(16)));
+
+template <int W>
+__host__ __device__ constexpr int conv1_koff(int k) {
+  return k >= 147 ? 0 : (k / 21) * W * 3 + ((k / 3) % 7) * 3 + (k % 3);
+}
+
+__device__ __forceinline__ const uint8_t* frame_ptr(const FrameSrc& src, int f) {
+  const int smp = f >> 1, h = f & 1;
+  const int64_t row = src.rows[h] ? (int64_t)src.rows[h][smp] : (int64_t)smp;
+  return src.base[h] + row * src.stride;
+}
+
+// Copy FB bytes of one frame into LDS with NT threads.
+template <int FB, int NT>
+__device__ __forceinline__ void stage_frame(uint8_t* dst, const uint8_t* src, int tid) {
+  if constexpr (FB % 16 == 0) {
+    const uint4* s = reinterpret_cast<const uint4*>(src);
+    uint4* d = reinterpret_cast<uint4*>(dst);
+#pragma unroll 4
+    for (int i = tid; i < FB / 16; i += NT) d[i] = s[i];
+  } else {
+    static_assert(FB % 4 == 0, "frame bytes must be a multiple of 4");
+    const uint32_t* s = reinterpret_cast<const uint32_t*>(src);
+    uint32_t* d = reinterpret_cast<uint32_t*>(dst);
+#pragma unroll 4
+    for (int i = tid; i < FB / 4; i += NT) d[i] = s[i];
+  }
+}
+
+__device__ __forceinline__ float u8f(const uint8_t* p) { return (float)(*p); }
+
+// ---- forward ------------------------------------------------------------------
+// NF frames per workgroup iteration, 5 waves; rows = pixels of the NF frames.
+template <int H, int W, int OH, int OW, int NF>
+__global__ __launch_bounds__(320) void conv1_fwd_kernel(FrameSrc src, int n_frames, const float* __restrict__ Wt,
+                                                        const float* __restrict__ bias, float* __restrict__ Y) {
+  constexpr int FB = H * W * 3;
+  constexpr int FBP = (FB + 15) / 16 * 16;
+  constexpr int NPIX = OH * OW;
+  constexpr int TILES = (NF * NPIX + 31) / 32;
+  constexpr int NW = 5;
+  __shared__ __attribute__((aligned(16))) uint8_t fr[NF * FBP];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, c32 = lane & 31;
+  float b[74];
+#pragma unroll
+  for (int s = 0; s < 74; ++s) b[s] = (2 * s + h < 147) ? Wt[c32 * 148 + 2 * s + h] : 0.0f;  // k = 147 is padding
+  const float bs = bias[c32];
+  for (int f0 = blockIdx.x * NF; f0 < n_frames; f0 += gridDim.x * NF) {
+    const int nf = min(NF, n_frames - f0);
+    for (int j = 0; j < nf; ++j) stage_frame<FB, 320>(fr + j * FBP, frame_ptr(src, f0 + j), tid);
+    __syncthreads();
+    for (int t = wave; t < TILES; t += NW) {
+      const int row = t * 32 + c32;
+      const int sel = row / NPIX, px = row - (row / NPIX) * NPIX;
+      const int oy = px / OW, ox = px - (px / OW) * OW;
+      const uint8_t* base = fr + (sel < nf ? sel : 0) * FBP + (oy * 4 * W + ox * 4) * 3;
+      f16v acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+#pragma unroll
+      for (int s = 0; s < 74; ++s) {
+        const int k0 = conv1_koff<W>(2 * s), k1 = conv1_koff<W>(2 * s + 1);
+        const float a = u8f(base + (h ? k1 : k0));
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b[s], acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rr = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (rr < nf * NPIX) Y[((int64_t)f0 * NPIX + rr) * 32 + c32] = fmaxf(acc[r] * (1.0f / 255.0f) + bs, 0.0f);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ---- weight gradient ----------------------------------------------------------
+// One frame per workgroup iteration; each of the 4 waves reduces over a quarter of its
+// pixels, two pixels per MFMA step. Columns: k in [0,147) data, 147 pad, 148 = bias (ones).
+template <int H, int W, int OH, int OW>
+__global__ __launch_bounds__(256) void conv1_wgrad_kernel(FrameSrc src, int n_frames, const float* __restrict__ dZ,
+                                                          float* __restrict__ slab) {
+  constexpr int FB = H * W * 3;
+  constexpr int NPIX = OH * OW;
+  constexpr int PPW = (NPIX + 7) / 8 * 2;  // pixels per wave (even), 4 waves cover NPIX
+  constexpr int STEPS = PPW / 2;
+  __shared__ __attribute__((aligned(16))) uint8_t fr[(FB + 15) / 16 * 16 + 16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, c32 = lane & 31;
+  int koff[5];
+#pragma unroll
+  for (int nt = 0; nt < 5; ++nt) koff[nt] = conv1_koff<W>(nt * 32 + c32);
+  const int k4 = 128 + c32;
+  const float mul4 = k4 < 147 ? 1.0f : 0.0f;
+  const float add4 = k4 == 148 ? 1.0f : 0.0f;
+  f16v acc[5];
+#pragma unroll
+  for (int nt = 0; nt < 5; ++nt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[nt][r] = 0.0f;
+  for (int f = blockIdx.x; f < n_frames; f += gridDim.x) {
+    stage_frame<FB, 256>(fr, frame_ptr(src, f), tid);
+    __syncthreads();
+    const float* dzf = dZ + (int64_t)f * NPIX * 32;
+#pragma unroll 2
+    for (int s = 0; s < STEPS; ++s) {
+      const int p = wave * PPW + 2 * s + h;
+      const bool valid = p < NPIX && (2 * s + h) < PPW;
+      const float a = valid ? dzf[(int64_t)p * 32 + c32] : 0.0f;
+      const int pp = valid ? p : 0;
+      const int oy = pp / OW, ox = pp - (pp / OW) * OW;
+      const uint8_t* pb = fr + (oy * 4 * W + ox * 4) * 3;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) acc[nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, u8f(pb + koff[nt]), acc[nt], 0, 0, 0);
+      const float b4 = fmaf(u8f(pb + koff[4]), mul4, add4);
+      acc[4] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b4, acc[4], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  // D[co = row][k = nt*32 + c32]
+  float* out = slab + ((int64_t)blockIdx.x * 4 + wave) * (32 * 160);
+#pragma unroll
+  for (int nt = 0; nt < 5; ++nt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = (r & 3) + 8 * (r >> 2) + 4 * h;
+      out[co * 160 + nt * 32 + c32] = acc[nt][r];
+    }
+}
+
+__global__ void conv1_wgrad_reduce_kernel(const float* __restrict__ slab, int nslab, float* dW, float* db) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;  // co*160 + k
+  if (idx >= 32 * 160) return;
+  const int co = idx / 160, k = idx - (idx / 160) * 160;
+  if (k > 148) return;
+  float s = 0.0f;
+  for (int z = 0; z < nslab; ++z) s += slab[(int64_t)z * 32 * 160 + idx];
+  if (k < 148)
+    dW[co * 148 + k] = k < 147 ? s * (1.0f / 255.0f) : 0.0f;
+  else
+    db[co] = s;
+}
+
+}  // namespace vn

@@ -29,6 +29,10 @@ struct FrameSrc {
   const float* f32[2];  // optional dense float NCHW frames (TransposeImage+ScaledFloatFrame output)
 };
 
+}  // namespace vn
+#include "vn_conv1.h"
+namespace vn {
+
 // ---- operand loaders ---------------------------------------------------------
 // conv1 im2col over 3-channel frames; k = (ky*7 + kx)*3 + c, K = 147 (padded 148).
 template <int H, int W, int OH, int OW>
@@ -310,6 +314,7 @@ inline PolicyLayout make_layout(int H, int W, int A) {
 }
 
 constexpr int OUT_LD = 8;  // [n][8]: logits 0..A-1, value at A
+constexpr int kConv1WgradBlocks = 384;  // x 4 wave slabs x 32 x 160 floats fits the slab
 
 inline dim3 grid_for(int M, int N, int BM, int BN, int splits = 1) {
   return dim3((M + BM - 1) / BM, (N + BN - 1) / BN, splits);
@@ -370,11 +375,17 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
   using G = Geo<H0, W0>;
   const int A1 = L.A + 1;
   // conv1 (frames -> X1), 2n frames
-  {
+  if (src.f32[0] || src.f32[1]) {  // dense float frames: generic im2col path
     FramesIm2col<H0, W0, G::OH1, G::OW1> fa{src, 2 * n * G::OH1 * G::OW1};
     DenseRows fb{P + L.l[0].w, 148, 32};
     EpiBiasAct ep{a.X[0], 32, P + L.l[0].b, 1};
     launch_gemm<64, 32, 32, 4, 1>(fa, fb, ep, fa.M, 32, 148, st);
+  } else {
+    constexpr int NF = (2 * H0 * W0 * 3 <= 64 * 1024) ? 2 : 1;
+    const int frames = 2 * n;
+    const int blocks = std::min((frames + NF - 1) / NF, 2048);
+    hipLaunchKernelGGL((conv1_fwd_kernel<H0, W0, G::OH1, G::OW1, NF>), dim3(blocks), dim3(320), 0, st, src, frames,
+                       P + L.l[0].w, P + L.l[0].b, a.X[0]);
   }
   // conv2 (X1 -> X2)
   {
@@ -525,11 +536,18 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
       }
   }
   // ---- conv1: wgrad from dz1 (in X1's storage) and the frames
-  {
+  if (src.f32[0] || src.f32[1]) {
     using Im = FramesIm2col<H0, W0, G::OH1, G::OW1>;
     const int P1 = 2 * n * G::OH1 * G::OW1;
     Im2colT<Im> fbw{Im{src, P1}, 148};
     launch_wgrad<32, 64, 2, 2>(a.X[0], 32, 32, fbw, 148, P1, w.slab, w.slab_cap, Gr + L.l[0].w, Gr + L.l[0].b, st);
+  } else {
+    const int frames = 2 * n;
+    const int blocks = std::min(frames, kConv1WgradBlocks);
+    hipLaunchKernelGGL((conv1_wgrad_kernel<H0, W0, G::OH1, G::OW1>), dim3(blocks), dim3(256), 0, st, src, frames,
+                       a.X[0], w.slab);
+    hipLaunchKernelGGL(conv1_wgrad_reduce_kernel, dim3((32 * 160 + 255) / 256), dim3(256), 0, st, w.slab, blocks * 4,
+                       Gr + L.l[0].w, Gr + L.l[0].b);
   }
   VN_HIP(hipGetLastError());
   return VN_OK;

@@ -142,7 +142,7 @@ def test_autograd_policy_vs_torch_oracle():
         _close(mine[k + ".bias"].numpy(), mod.bias.grad.numpy(), 1e-4, k + ".bias")
     # float CHW input (the reference wrapper format) gives the same outputs
     lf, vf, _ = pol(((frames_to_float(img).cuda(), frames_to_float(gl).cuda()), None), None, None)
-    _close(lf.detach().cpu(), logits.detach().cpu(), 1e-6, "f32 input logits")
+    _close(lf.detach().cpu(), logits.detach().cpu(), 1e-5, "f32 input logits")
 
 
 def test_row_gather_equals_dense_batch():
