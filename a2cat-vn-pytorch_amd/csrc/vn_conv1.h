@@ -96,16 +96,21 @@ __global__ __launch_bounds__(320) void conv1_fwd_kernel(FrameSrc src, int n_fram
 }
 
 // ---- weight gradient ----------------------------------------------------------
-// One frame per workgroup iteration; each of the 4 waves reduces over a quarter of its
-// pixels, two pixels per MFMA step. Columns: k in [0,147) data, 147 pad, 148 = bias (ones).
-template <int H, int W, int OH, int OW>
+// One frame per workgroup iteration, its pixels in chunks of CP: the chunk's dZ rows
+// (CP x 32 fp32, 16-B loads) and the frame bytes are staged into LDS together, then each
+// of the 4 waves reduces over a quarter of the chunk, two pixels per MFMA step.
+// Columns: k in [0,147) data, 147 pad, 148 = bias (ones), 149..159 zero.
+template <int H, int W, int OH, int OW, int CP>
 __global__ __launch_bounds__(256) void conv1_wgrad_kernel(FrameSrc src, int n_frames, const float* __restrict__ dZ,
                                                           float* __restrict__ slab) {
   constexpr int FB = H * W * 3;
+  constexpr int FBP = (FB + 15) / 16 * 16;
   constexpr int NPIX = OH * OW;
-  constexpr int PPW = (NPIX + 7) / 8 * 2;  // pixels per wave (even), 4 waves cover NPIX
-  constexpr int STEPS = PPW / 2;
-  __shared__ __attribute__((aligned(16))) uint8_t fr[(FB + 15) / 16 * 16 + 16];
+  static_assert(CP % 8 == 0, "chunk must split into 4 waves x 2 pixels");
+  constexpr int SPW = CP / 8;  // MFMA steps per wave per chunk
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint8_t* fr = smem;
+  float* dzs = reinterpret_cast<float*>(smem + FBP);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, c32 = lane & 31;
   int koff[5];
@@ -120,23 +125,32 @@ __global__ __launch_bounds__(256) void conv1_wgrad_kernel(FrameSrc src, int n_fr
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[nt][r] = 0.0f;
   for (int f = blockIdx.x; f < n_frames; f += gridDim.x) {
-    stage_frame<FB, 256>(fr, frame_ptr(src, f), tid);
-    __syncthreads();
     const float* dzf = dZ + (int64_t)f * NPIX * 32;
-#pragma unroll 2
-    for (int s = 0; s < STEPS; ++s) {
-      const int p = wave * PPW + 2 * s + h;
-      const bool valid = p < NPIX && (2 * s + h) < PPW;
-      const float a = valid ? dzf[(int64_t)p * 32 + c32] : 0.0f;
-      const int pp = valid ? p : 0;
-      const int oy = pp / OW, ox = pp - (pp / OW) * OW;
-      const uint8_t* pb = fr + (oy * 4 * W + ox * 4) * 3;
+    for (int c0 = 0; c0 < NPIX; c0 += CP) {
+      const int np = min(CP, NPIX - c0);
+      {
+        const f4* s4 = reinterpret_cast<const f4*>(dzf + (int64_t)c0 * 32);
+        f4* d4 = reinterpret_cast<f4*>(dzs);
+        for (int i = tid; i < np * 8; i += 256) d4[i] = s4[i];
+      }
+      if (c0 == 0) stage_frame<FB, 256>(fr, frame_ptr(src, f), tid);
+      __syncthreads();
+#pragma unroll 5
+      for (int s = 0; s < SPW; ++s) {
+        const int pl = wave * (CP / 4) + 2 * s + h;
+        const bool valid = pl < np;
+        const float a = valid ? dzs[pl * 32 + c32] : 0.0f;
+        const int p = valid ? c0 + pl : 0;
+        const int oy = p / OW, ox = p - (p / OW) * OW;
+        const uint8_t* pb = fr + (oy * 4 * W + ox * 4) * 3;
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) acc[nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, u8f(pb + koff[nt]), acc[nt], 0, 0, 0);
-      const float b4 = fmaf(u8f(pb + koff[4]), mul4, add4);
-      acc[4] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b4, acc[4], 0, 0, 0);
+        for (int nt = 0; nt < 4; ++nt)
+          acc[nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, u8f(pb + koff[nt]), acc[nt], 0, 0, 0);
+        const float b4 = fmaf(u8f(pb + koff[4]), mul4, add4);
+        acc[4] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b4, acc[4], 0, 0, 0);
+      }
+      __syncthreads();
     }
-    __syncthreads();
   }
   // D[co = row][k = nt*32 + c32]
   float* out = slab + ((int64_t)blockIdx.x * 4 + wave) * (32 * 160);
@@ -147,6 +161,11 @@ __global__ __launch_bounds__(256) void conv1_wgrad_kernel(FrameSrc src, int n_fr
       const int co = (r & 3) + 8 * (r >> 2) + 4 * h;
       out[co * 160 + nt * 32 + c32] = acc[nt][r];
     }
+}
+
+template <int H, int W, int CP>
+constexpr size_t conv1_wgrad_lds() {
+  return (size_t)(H * W * 3 + 15) / 16 * 16 + (size_t)CP * 32 * 4;
 }
 
 __global__ void conv1_wgrad_reduce_kernel(const float* __restrict__ slab, int nslab, float* dW, float* db) {

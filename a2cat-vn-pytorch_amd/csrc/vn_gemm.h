@@ -2,9 +2,11 @@
 //
 // C[M][N] = sum_k A[m][k] * B[k][n], one 256-thread workgroup (4 waves, WM x WN) per
 // BM x BN tile and K range. Both operands are staged in LDS k-contiguous
-// ([row][k], row stride BK+4 floats) by "fill" functors that gather them straight
+// ([row][k], row stride BK+4 floats) by loader functors that gather them straight
 // from their producers (im2col of NHWC activations, uint8 frames addressed through
-// scene-cache rows, transposed weights, ...). Each wave reads 16 B per lane
+// scene-cache rows, transposed weights, ...): fetch() issues the next K tile's global
+// loads into registers before the current tile's MFMAs, commit() writes them to LDS
+// after the barrier (a register-staged software pipeline). Each wave reads 16 B per lane
 // (ds_read_b128: 4 consecutive k of one row) and issues four
 // v_mfma_f32_16x16x4_f32 per read — MFMA j of a group covers k = {j, 4+j, 8+j, 12+j},
 // the same permutation on both operands, so the product is unchanged. f32 in/f32
@@ -28,6 +30,8 @@ __global__ __launch_bounds__(256) void gemm_kernel(FA fa, FB fb, EP ep, int M, i
   constexpr int LD = BK + 4;
   constexpr int TM = BM / (WM * 16), TN = BN / (WN * 16);
   static_assert(TM >= 1 && TN >= 1, "tile too small for the wave layout");
+  constexpr int NA = (FA::template slots<BM, BK>() + 255) / 256;
+  constexpr int NB = (FB::template slots<BN, BK>() + 255) / 256;
   __shared__ __attribute__((aligned(16))) float As[BM * LD];
   __shared__ __attribute__((aligned(16))) float Bs[BN * LD];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -42,10 +46,20 @@ __global__ __launch_bounds__(256) void gemm_kernel(FA fa, FB fb, EP ep, int M, i
     for (int j = 0; j < TN; ++j) acc[i][j] = f4zero();
   const int ra = (wm * TM * 16 + (lane & 15)) * LD + 4 * (lane >> 4);
   const int rb = (wn * TN * 16 + (lane & 15)) * LD + 4 * (lane >> 4);
+  // software pipeline: the next K tile's global loads are in flight while this one computes
+  f4 pa[NA], pb[NB];
+  if (kb < ke) {
+    fa.template fetch<BM, BK>(pa, m0, kb, ke, tid);
+    fb.template fetch<BN, BK>(pb, n0, kb, ke, tid);
+  }
   for (int k0 = kb; k0 < ke; k0 += BK) {
-    fa.template fill<BM, BK>(As, m0, k0, ke, tid);
-    fb.template fill<BN, BK>(Bs, n0, k0, ke, tid);
+    FA::template commit<BM, BK>(pa, As, tid);
+    FB::template commit<BN, BK>(pb, Bs, tid);
     __syncthreads();
+    if (k0 + BK < ke) {
+      fa.template fetch<BM, BK>(pa, m0, k0 + BK, ke, tid);
+      fb.template fetch<BN, BK>(pb, n0, k0 + BK, ke, tid);
+    }
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 16) {
       f4 a[TM], b[TN];
@@ -75,32 +89,86 @@ __global__ __launch_bounds__(256) void gemm_kernel(FA fa, FB fb, EP ep, int M, i
       }
 }
 
-// ---- fill helpers -----------------------------------------------------------
+// ---- fill helpers: fetch (global -> registers) then commit (registers -> LDS) ----
 // Row-major source: L::load4(row, k, kend) -> 4 consecutive k of one row (zeros past kend).
 template <int ROWS, int BK, class L>
-__device__ __forceinline__ void fill_rows(const L& l, float* s, int row0, int k0, int kend, int tid) {
-  constexpr int LD = BK + 4, Q = BK / 4, SLOTS = ROWS * Q;
+__device__ __forceinline__ void fetch_rows(const L& l, f4* r, int row0, int k0, int kend, int tid) {
+  constexpr int Q = BK / 4, T = ROWS * Q, NS = (T + 255) / 256;
 #pragma unroll
-  for (int i = tid; i < SLOTS; i += 256) {
-    const int r = i / Q, q = i - r * Q;
-    *reinterpret_cast<f4*>(&s[r * LD + 4 * q]) = l.load4(row0 + r, k0 + 4 * q, kend);
+  for (int j = 0; j < NS; ++j) {
+    const int i = tid + j * 256;
+    if (T % 256 == 0 || i < T) {
+      const int rr = i / Q, q = i - (i / Q) * Q;
+      r[j] = l.load4(row0 + rr, k0 + 4 * q, kend);
+    }
+  }
+}
+template <int ROWS, int BK>
+__device__ __forceinline__ void commit_rows(const f4* r, float* s, int tid) {
+  constexpr int LD = BK + 4, Q = BK / 4, T = ROWS * Q, NS = (T + 255) / 256;
+#pragma unroll
+  for (int j = 0; j < NS; ++j) {
+    const int i = tid + j * 256;
+    if (T % 256 == 0 || i < T) {
+      const int rr = i / Q, q = i - (i / Q) * Q;
+      *reinterpret_cast<f4*>(&s[rr * LD + 4 * q]) = r[j];
+    }
   }
 }
 
 // Transposing source (wgrad): L::load4t(p, r) -> rows r..r+3 at reduction index p.
 template <int ROWS, int BK, class L>
-__device__ __forceinline__ void fill_trans(const L& l, float* s, int row0, int k0, int kend, int tid) {
-  constexpr int LD = BK + 4, R4 = ROWS / 4, SLOTS = R4 * BK;
+__device__ __forceinline__ void fetch_trans(const L& l, f4* r, int row0, int k0, int kend, int tid) {
+  constexpr int R4 = ROWS / 4, T = R4 * BK, NS = (T + 255) / 256;
 #pragma unroll
-  for (int i = tid; i < SLOTS; i += 256) {
-    const int kk = i / R4, rq = i - kk * R4;
-    const int p = k0 + kk;
-    const f4 v = (p < kend) ? l.load4t(p, row0 + 4 * rq) : f4zero();
-    s[(4 * rq + 0) * LD + kk] = v[0];
-    s[(4 * rq + 1) * LD + kk] = v[1];
-    s[(4 * rq + 2) * LD + kk] = v[2];
-    s[(4 * rq + 3) * LD + kk] = v[3];
+  for (int j = 0; j < NS; ++j) {
+    const int i = tid + j * 256;
+    if (T % 256 == 0 || i < T) {
+      const int kk = i / R4, rq = i - (i / R4) * R4;
+      const int p = k0 + kk;
+      r[j] = (p < kend) ? l.load4t(p, row0 + 4 * rq) : f4zero();
+    }
   }
 }
+template <int ROWS, int BK>
+__device__ __forceinline__ void commit_trans(const f4* r, float* s, int tid) {
+  constexpr int LD = BK + 4, R4 = ROWS / 4, T = R4 * BK, NS = (T + 255) / 256;
+#pragma unroll
+  for (int j = 0; j < NS; ++j) {
+    const int i = tid + j * 256;
+    if (T % 256 == 0 || i < T) {
+      const int kk = i / R4, rq = i - (i / R4) * R4;
+      s[(4 * rq + 0) * LD + kk] = r[j][0];
+      s[(4 * rq + 1) * LD + kk] = r[j][1];
+      s[(4 * rq + 2) * LD + kk] = r[j][2];
+      s[(4 * rq + 3) * LD + kk] = r[j][3];
+    }
+  }
+}
+
+// Mix-ins giving a loader the fetch/commit/slots interface of the GEMM core.
+#define VN_ROWS_LOADER                                                                     \
+  template <int ROWS, int BK>                                                              \
+  static constexpr int slots() { return ROWS * (BK / 4); }                                 \
+  template <int ROWS, int BK>                                                              \
+  __device__ __forceinline__ void fetch(f4* r, int r0, int k0, int ke, int tid) const {    \
+    fetch_rows<ROWS, BK>(*this, r, r0, k0, ke, tid);                                       \
+  }                                                                                        \
+  template <int ROWS, int BK>                                                              \
+  __device__ __forceinline__ static void commit(const f4* r, float* s, int tid) {          \
+    commit_rows<ROWS, BK>(r, s, tid);                                                      \
+  }
+
+#define VN_TRANS_LOADER                                                                    \
+  template <int ROWS, int BK>                                                              \
+  static constexpr int slots() { return (ROWS / 4) * BK; }                                 \
+  template <int ROWS, int BK>                                                              \
+  __device__ __forceinline__ void fetch(f4* r, int r0, int k0, int ke, int tid) const {    \
+    fetch_trans<ROWS, BK>(*this, r, r0, k0, ke, tid);                                      \
+  }                                                                                        \
+  template <int ROWS, int BK>                                                              \
+  __device__ __forceinline__ static void commit(const f4* r, float* s, int tid) {          \
+    commit_trans<ROWS, BK>(r, s, tid);                                                     \
+  }
 
 }  // namespace vn

@@ -71,10 +71,7 @@ struct FramesIm2col {
     }
     return v;
   }
-  template <int ROWS, int BK>
-  __device__ __forceinline__ void fill(float* s, int r0, int k0, int ke, int tid) const {
-    fill_rows<ROWS, BK>(*this, s, r0, k0, ke, tid);
-  }
+  VN_ROWS_LOADER
 };
 
 // im2col over NHWC fp32 with G channel-concatenated input groups (C % 4 == 0).
@@ -94,10 +91,7 @@ struct NhwcIm2col {
     const int ky = t / KW, kx = t % KW;
     return *reinterpret_cast<const f4*>(X + ((((int64_t)n * G + g) * H + oy * S + ky) * W + ox * S + kx) * C + c);
   }
-  template <int ROWS, int BK>
-  __device__ __forceinline__ void fill(float* s, int r0, int k0, int ke, int tid) const {
-    fill_rows<ROWS, BK>(*this, s, r0, k0, ke, tid);
-  }
+  VN_ROWS_LOADER
 };
 
 // Dense row-major matrix [rows][ld] (ld % 4 == 0, 16-B aligned).
@@ -113,10 +107,7 @@ struct DenseRows {
     for (int j = 0; j < 4 && k + j < kend; ++j) v[j] = p[j];
     return v;
   }
-  template <int ROWS, int BK>
-  __device__ __forceinline__ void fill(float* s, int r0, int k0, int ke, int tid) const {
-    fill_rows<ROWS, BK>(*this, s, r0, k0, ke, tid);
-  }
+  VN_ROWS_LOADER
 };
 
 // wgrad A operand: dZ [P][ld] read as rows r..r+3 (output channels) at pixel p.
@@ -131,10 +122,7 @@ struct DenseT {
     for (int j = 0; j < 4 && r + j < ncols; ++j) v[j] = q[j];
     return v;
   }
-  template <int ROWS, int BK>
-  __device__ __forceinline__ void fill(float* s, int r0, int k0, int ke, int tid) const {
-    fill_trans<ROWS, BK>(*this, s, r0, k0, ke, tid);
-  }
+  VN_TRANS_LOADER
 };
 
 // wgrad B operand: an im2col loader read transposed, plus a ones column at k == KP
@@ -150,10 +138,7 @@ struct Im2colT {
       if (r + j == KP) v[j] = 1.0f;
     return v;
   }
-  template <int ROWS, int BK>
-  __device__ __forceinline__ void fill(float* s, int r0, int k0, int ke, int tid) const {
-    fill_trans<ROWS, BK>(*this, s, r0, k0, ke, tid);
-  }
+  VN_TRANS_LOADER
 };
 
 // dgrad of a strided conv, one (group g, parity py, px) class per launch: rows are the
@@ -176,10 +161,7 @@ struct DgradA {
     if (oy < 0 || oy >= OH || ox < 0 || ox >= OW) return f4zero();
     return *reinterpret_cast<const f4*>(dZ + (((int64_t)n * OH + oy) * OW + ox) * COUT + co);
   }
-  template <int ROWS, int BK>
-  __device__ __forceinline__ void fill(float* s, int r0, int k0, int ke, int tid) const {
-    fill_rows<ROWS, BK>(*this, s, r0, k0, ke, tid);
-  }
+  VN_ROWS_LOADER
 };
 
 template <int COUT, int KW, int S, int CINF>
@@ -193,10 +175,7 @@ struct DgradB {
     const int ky = py + (t / (KW / S)) * S, kx = px + (t % (KW / S)) * S;
     return *reinterpret_cast<const f4*>(WT + ((int64_t)(ky * KW + kx) * CINF + g_off + j) * COUT + co);
   }
-  template <int ROWS, int BK>
-  __device__ __forceinline__ void fill(float* s, int r0, int k0, int ke, int tid) const {
-    fill_rows<ROWS, BK>(*this, s, r0, k0, ke, tid);
-  }
+  VN_ROWS_LOADER
 };
 
 // ---- epilogues ----------------------------------------------------------------
@@ -544,7 +523,15 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
   } else {
     const int frames = 2 * n;
     const int blocks = std::min(frames, kConv1WgradBlocks);
-    hipLaunchKernelGGL((conv1_wgrad_kernel<H0, W0, G::OH1, G::OW1>), dim3(blocks), dim3(256), 0, st, src, frames,
+    constexpr int CP = (G::OH1 * G::OW1 <= 400) ? (G::OH1 * G::OW1 + 7) / 8 * 8 : 448;
+    constexpr size_t lds = conv1_wgrad_lds<H0, W0, CP>();
+    static bool attr = false;  // > 64 KiB of dynamic LDS needs the opt-in attribute
+    if (!attr) {
+      VN_HIP(hipFuncSetAttribute((const void*)conv1_wgrad_kernel<H0, W0, G::OH1, G::OW1, CP>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      attr = true;
+    }
+    hipLaunchKernelGGL((conv1_wgrad_kernel<H0, W0, G::OH1, G::OW1, CP>), dim3(blocks), dim3(256), lds, st, src, frames,
                        a.X[0], w.slab);
     hipLaunchKernelGGL(conv1_wgrad_reduce_kernel, dim3((32 * 160 + 255) / 256), dim3(256), 0, st, w.slab, blocks * 4,
                        Gr + L.l[0].w, Gr + L.l[0].b);
