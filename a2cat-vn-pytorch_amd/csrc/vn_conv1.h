@@ -181,4 +181,163 @@ __global__ void conv1_wgrad_reduce_kernel(const float* __restrict__ slab, int ns
     db[co] = s;
 }
 
+// ---- conv2 weight gradient ----------------------------------------------------
+// dW2[co][(ky*4+kx)*32 + ci] = sum over frames and output pixels p of
+// dZ2[f][p][co] * X1[f][(2oy+ky)*IW + 2ox+kx][ci]. One frame per workgroup iteration:
+// X1_f (IH*IW*32 fp32) and dZ2_f are staged in LDS; wave w owns taps 4w..4w+3 (four
+// 32x32 accumulators: co x ci), two output pixels per MFMA step. Bias gradient: colsum.
+template <int IH, int IW, int OH, int OW>
+__global__ __launch_bounds__(256) void conv2_wgrad_kernel(const float* __restrict__ X1, const float* __restrict__ dZ2,
+                                                          int n_frames, float* __restrict__ slab,
+                                                          float* __restrict__ bias_slab) {
+  constexpr int NX = IH * IW * 32, NP = OH * OW, NPE = (NP + 1) / 2 * 2;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  float* xs = reinterpret_cast<float*>(smem);
+  float* ds = xs + NX;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, c32 = lane & 31;
+  f16v acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.0f;
+  float bacc = 0.0f;  // bias gradient: column sums of dZ2 (wave 0 only)
+  for (int f = blockIdx.x; f < n_frames; f += gridDim.x) {
+    {
+      const f4* s4 = reinterpret_cast<const f4*>(X1 + (int64_t)f * NX);
+      f4* d4 = reinterpret_cast<f4*>(xs);
+#pragma unroll 4
+      for (int i = tid; i < NX / 4; i += 256) d4[i] = s4[i];
+      const f4* z4 = reinterpret_cast<const f4*>(dZ2 + (int64_t)f * NP * 32);
+      f4* e4 = reinterpret_cast<f4*>(ds);
+      for (int i = tid; i < NPE * 8; i += 256) e4[i] = i < NP * 8 ? z4[i] : f4zero();
+    }
+    __syncthreads();
+#pragma unroll 3
+    for (int s = 0; s < NPE / 2; ++s) {
+      const int p = 2 * s + h;
+      const float a = ds[p * 32 + c32];
+      if (wave == 0) bacc += a;
+      const int pp = p < NP ? p : 0;
+      const int oy = pp / OW, ox = pp - (pp / OW) * OW;
+      const float* xb = xs + ((2 * oy) * IW + 2 * ox) * 32 + c32;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int tap = wave * 4 + j, ky = tap >> 2, kx = tap & 3;
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, xb[(ky * IW + kx) * 32], acc[j], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  float* out = slab + (int64_t)blockIdx.x * (32 * 512);
+  if (wave == 0) {
+    bacc += __shfl_xor(bacc, 32);
+    if (h == 0) bias_slab[(int64_t)blockIdx.x * 32 + c32] = bacc;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = (r & 3) + 8 * (r >> 2) + 4 * h;
+      out[co * 512 + (wave * 4 + j) * 32 + c32] = acc[j][r];
+    }
+}
+
+// ---- conv2 input gradient -------------------------------------------------------
+// dX1[f][y][x][ci] = [X1 > 0] * sum over the (ky, kx) taps reaching (y, x) and co of
+// dZ2[f][oy][ox][co] * W2[co][ky][kx][ci]  (k4 s2). Wave w owns the input-parity class
+// (py, px) = (w >> 1, w & 1): its (KH/S)^2 = 4 taps are fixed, so its 64 B fragments (k =
+// tap*32 + co, 16x16x4 MFMA, 2 column tiles of ci) stay in registers for the whole kernel.
+// dZ2_f is staged in LDS with one extra zero row that out-of-range taps point at.
+template <int IH, int IW, int OH, int OW>
+__global__ __launch_bounds__(256) void conv2_dgrad_kernel(const float* __restrict__ dZ2, const float* __restrict__ WT,
+                                                          const float* __restrict__ X1, float* __restrict__ dX1,
+                                                          int n_frames) {
+  constexpr int NP = OH * OW;
+  constexpr int HYC = IH / 2, WXC = IW / 2;  // even input sizes: every class has HYC x WXC pixels
+  static_assert(IH % 2 == 0 && IW % 2 == 0, "even conv1 maps");
+  constexpr int NPC = HYC * WXC;
+  constexpr int TILES = (NPC + 15) / 16;
+  __shared__ __attribute__((aligned(16))) float ds[(NP + 1) * 32];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int py = wave >> 1, px = wave & 1;
+  const int i16 = lane & 15, q = lane >> 4;
+  // B fragments: step s covers k = 4s..4s+3 -> tap = s / 8, co = 4*(s % 8) + q
+  float b[32][2];
+#pragma unroll
+  for (int s = 0; s < 32; ++s) {
+    const int tap = s >> 3, co = 4 * (s & 7) + q;
+    const int ky = py + 2 * (tap >> 1), kx = px + 2 * (tap & 1);
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) b[s][ct] = WT[((ky * 4 + kx) * 32 + ct * 16 + i16) * 32 + co];
+  }
+  if (tid < 32) ds[NP * 32 + tid] = 0.0f;
+  for (int f = blockIdx.x; f < n_frames; f += gridDim.x) {
+    {
+      const f4* z4 = reinterpret_cast<const f4*>(dZ2 + (int64_t)f * NP * 32);
+      f4* e4 = reinterpret_cast<f4*>(ds);
+      for (int i = tid; i < NP * 8; i += 256) e4[i] = z4[i];
+    }
+    __syncthreads();
+    for (int t = 0; t < TILES; ++t) {
+      const int pc = t * 16 + i16;  // this lane's pixel of the class (A row)
+      const int yy = pc / WXC, xx = pc - (pc / WXC) * WXC;
+      int off[4];
+#pragma unroll
+      for (int tap = 0; tap < 4; ++tap) {
+        const int oy = yy - (tap >> 1), ox = xx - (tap & 1);
+        const bool ok = pc < NPC && oy >= 0 && oy < OH && ox >= 0 && ox < OW;
+        off[tap] = (ok ? (oy * OW + ox) : NP) * 32 + q;
+      }
+      f4 acc0 = f4zero(), acc1 = f4zero();
+#pragma unroll
+      for (int s = 0; s < 32; ++s) {
+        const float a = ds[off[s >> 3] + 4 * (s & 7)];
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b[s][0], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b[s][1], acc1, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int pr = t * 16 + q * 4 + r;
+        if (pr < NPC) {
+          const int y = (pr / WXC) * 2 + py, x = (pr % WXC) * 2 + px;
+          const int64_t base = (((int64_t)f * IH + y) * IW + x) * 32 + i16;
+          dX1[base] = X1[base] > 0.0f ? acc0[r] : 0.0f;
+          dX1[base + 16] = X1[base + 16] > 0.0f ? acc1[r] : 0.0f;
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <int IH, int IW, int OH, int OW>
+constexpr size_t conv2_wgrad_lds() {
+  return ((size_t)IH * IW * 32 + (size_t)(OH * OW + 1) / 2 * 2 * 32) * 4;
+}
+
+// Deterministic column sums of a [rows][32] matrix: per-block partials, then one block.
+__global__ __launch_bounds__(256) void colsum32_partial_kernel(const float* __restrict__ A, int64_t rows,
+                                                               float* __restrict__ partial) {
+  const int c = threadIdx.x & 31, r0 = threadIdx.x >> 5;  // 8 row lanes per block
+  float s = 0.0f;
+  for (int64_t r = (int64_t)blockIdx.x * 8 + r0; r < rows; r += (int64_t)gridDim.x * 8) s += A[r * 32 + c];
+  __shared__ float red[8][32];
+  red[r0][c] = s;
+  __syncthreads();
+  if (threadIdx.x < 32) {
+    float t = 0.0f;
+    for (int i = 0; i < 8; ++i) t += red[i][threadIdx.x];
+    partial[(int64_t)blockIdx.x * 32 + threadIdx.x] = t;
+  }
+}
+
+__global__ void sum_slabs_kernel(const float* __restrict__ slab, int nslab, int64_t n, float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float s = 0.0f;
+  for (int z = 0; z < nslab; ++z) s += slab[(int64_t)z * n + i];
+  out[i] = s;
+}
+
 }  // namespace vn

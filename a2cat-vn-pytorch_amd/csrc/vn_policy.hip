@@ -15,7 +15,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <mutex>
 #include <new>
+#include <unordered_map>
 
 #include "vn_common.h"
 #include "vn_gemm.h"
@@ -144,16 +146,16 @@ struct Im2colT {
 // dgrad of a strided conv, one (group g, parity py, px) class per launch: rows are the
 // input pixels y = yy*S + py, x = xx*S + px; k = (tky, tkx, co) over the KH/S x KW/S taps
 // that reach them (ky = py + tky*S, oy = yy - tky).
-template <int COUT, int KW, int S, int OH, int OW>
+template <int COUT, int KW, int S, int OH, int OW, int HYC, int WXC>
 struct DgradA {
   const float* dZ;
-  int M, HYc, WXc;
+  int M;
   __device__ __forceinline__ f4 load4(int m, int k, int kend) const {
     if (m >= M || k >= kend) return f4zero();
-    const int per = HYc * WXc;
+    constexpr int per = HYC * WXC;
     const int n = m / per;
     const int r = m - n * per;
-    const int yy = r / WXc, xx = r - (r / WXc) * WXc;
+    const int yy = r / WXC, xx = r - (r / WXC) * WXC;
     const int co = k % COUT;
     const int t = k / COUT;
     const int tky = t / (KW / S), tkx = t % (KW / S);
@@ -201,16 +203,16 @@ struct EpiMask {
   }
 };
 
-template <int H, int W, int S>
+template <int H, int W, int S, int PY, int PX, int HYC, int WXC>
 struct EpiMaskParity {
   float* out;
   const float* X;
-  int WXc, HYc, py, px, g, G, cin;
+  int g, G, cin;
   __device__ __forceinline__ void operator()(int row, int col, float v, int) const {
-    const int per = HYc * WXc;
+    constexpr int per = HYC * WXC;
     const int n = row / per;
     const int r = row - n * per;
-    const int y = (r / WXc) * S + py, x = (r % WXc) * S + px;
+    const int y = (r / WXC) * S + PY, x = (r % WXC) * S + PX;
     const int64_t i = ((((int64_t)n * G + g) * H + y) * W + x) * cin + col;
     out[i] = X[i] > 0.0f ? v : 0.0f;
   }
@@ -293,7 +295,24 @@ inline PolicyLayout make_layout(int H, int W, int A) {
 }
 
 constexpr int OUT_LD = 8;  // [n][8]: logits 0..A-1, value at A
-constexpr int kConv1WgradBlocks = 384;  // x 4 wave slabs x 32 x 160 floats fits the slab
+constexpr int kConv1WgradBlocks = 512;  // x 4 wave slabs x 32 x 160 floats (fits the slab)
+constexpr int kConv2WgradBlocks = 512;  // x (32 x 512 + 32) floats (fits the slab)
+
+// Resident workgroups of a persistent kernel on the current device (cached per kernel).
+inline int resident_blocks(const void* kernel, int threads, size_t lds) {
+  static std::mutex mu;
+  static std::unordered_map<const void*, int> cache;
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = cache.find(kernel);
+  if (it != cache.end()) return it->second;
+  int dev = 0, cus = 0, per = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, threads, lds) != hipSuccess || per < 1) per = 1;
+  const int blocks = std::max(1, per * std::max(cus, 1));
+  cache[kernel] = blocks;
+  return blocks;
+}
 
 inline dim3 grid_for(int M, int N, int BM, int BN, int splits = 1) {
   return dim3((M + BM - 1) / BM, (N + BN - 1) / BN, splits);
@@ -324,6 +343,28 @@ inline void launch_wgrad(const float* dZ, int64_t ldz, int M, FB fb, int KP, int
   launch_gemm<BM, BN, BK, WM, WN>(fa, fb, ep, M, N, P, st, splits, kchunk);
   const int total = M * N;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, slab, splits, M, N, dW, db);
+}
+
+// dgrad of one (group, parity) class of a k4 s2 conv: input pixels (y, x) with
+// y % 2 == PY, x % 2 == PX of nimg images, masked by the ReLU of their producer.
+template <int COUT, int CINF, int H, int W, int OH, int OW, int PY, int PX>
+inline void dgrad_class(const float* dz, const float* WT, float* out, const float* X, int nimg, int g, int G, int cin,
+                        hipStream_t st) {
+  constexpr int HYC = (H - PY + 1) / 2, WXC = (W - PX + 1) / 2;
+  const int M = nimg * HYC * WXC;
+  DgradA<COUT, 4, 2, OH, OW, HYC, WXC> fa{dz, M};
+  DgradB<COUT, 4, 2, CINF> fb{WT, cin, g * cin, PY, PX};
+  EpiMaskParity<H, W, 2, PY, PX, HYC, WXC> ep{out, X, g, G, cin};
+  launch_gemm<64, 32, 32, 4, 1>(fa, fb, ep, M, cin, 4 * COUT, st);
+}
+
+template <int COUT, int CINF, int H, int W, int OH, int OW>
+inline void dgrad_all_classes(const float* dz, const float* WT, float* out, const float* X, int nimg, int g, int G,
+                              int cin, hipStream_t st) {
+  dgrad_class<COUT, CINF, H, W, OH, OW, 0, 0>(dz, WT, out, X, nimg, g, G, cin, st);
+  dgrad_class<COUT, CINF, H, W, OH, OW, 0, 1>(dz, WT, out, X, nimg, g, G, cin, st);
+  dgrad_class<COUT, CINF, H, W, OH, OW, 1, 0>(dz, WT, out, X, nimg, g, G, cin, st);
+  dgrad_class<COUT, CINF, H, W, OH, OW, 1, 1>(dz, WT, out, X, nimg, g, G, cin, st);
 }
 
 template <int H0, int W0>
@@ -362,7 +403,8 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
   } else {
     constexpr int NF = (2 * H0 * W0 * 3 <= 64 * 1024) ? 2 : 1;
     const int frames = 2 * n;
-    const int blocks = std::min((frames + NF - 1) / NF, 2048);
+    const int blocks =
+        std::min((frames + NF - 1) / NF, resident_blocks((const void*)conv1_fwd_kernel<H0, W0, G::OH1, G::OW1, NF>, 320, 0));
     hipLaunchKernelGGL((conv1_fwd_kernel<H0, W0, G::OH1, G::OW1, NF>), dim3(blocks), dim3(320), 0, st, src, frames,
                        P + L.l[0].w, P + L.l[0].b, a.X[0]);
   }
@@ -416,7 +458,7 @@ struct BwdWork {
 };
 
 inline int64_t slab_floats(const PolicyLayout& L) {
-  return 8ll << 20;  // split-K slab capacity (launch_wgrad halves the split count to fit)
+  return 12ll << 20;  // split-K slab capacity (launch_wgrad halves the split count to fit)
 }
 
 inline int64_t workspace_floats(const PolicyLayout& L, int64_t n) {
@@ -488,31 +530,40 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
     Im2colT<Im> fbw{Im{a.X[1], n9}, 1024};
     launch_wgrad<64, 64, 2, 2>(w.dz3, 64, 64, fbw, 1024, n9, w.slab, w.slab_cap, Gr + L.l[2].w, Gr + L.l[2].b, st);
     for (int g = 0; g < 2; ++g)
-      for (int py = 0; py < 2; ++py)
-        for (int px = 0; px < 2; ++px) {
-          const int HYc = (G::OH2 - py + 1) / 2, WXc = (G::OW2 - px + 1) / 2;
-          const int M = n * HYc * WXc;
-          DgradA<64, 4, 2, G::OH3, G::OW3> fa{w.dz3, M, HYc, WXc};
-          DgradB<64, 4, 2, 64> fb{T(2), 32, g * 32, py, px};
-          EpiMaskParity<G::OH2, G::OW2, 2> ep{w.dz2, a.X[1], WXc, HYc, py, px, g, 2, 32};
-          launch_gemm<64, 32, 32, 4, 1>(fa, fb, ep, M, 32, 4 * 64, st);
-        }
+      dgrad_all_classes<64, 64, G::OH2, G::OW2, G::OH3, G::OW3>(w.dz3, T(2), w.dz2, a.X[1], n, g, 2, 32, st);
   }
   // ---- conv2 (k4 s2): wgrad (needs X1), then dgrad into dz1 written over X1
   {
-    using Im = NhwcIm2col<32, 4, 4, 2, G::OH1, G::OW1, G::OH2, G::OW2, 1>;
-    const int P2 = 2 * n * G::OH2 * G::OW2;
-    Im2colT<Im> fbw{Im{a.X[0], P2}, 512};
-    launch_wgrad<32, 64, 2, 2>(w.dz2, 32, 32, fbw, 512, P2, w.slab, w.slab_cap, Gr + L.l[1].w, Gr + L.l[1].b, st);
-    for (int py = 0; py < 2; ++py)
-      for (int px = 0; px < 2; ++px) {
-        const int HYc = (G::OH1 - py + 1) / 2, WXc = (G::OW1 - px + 1) / 2;
-        const int M = 2 * n * HYc * WXc;
-        DgradA<32, 4, 2, G::OH2, G::OW2> fa{w.dz2, M, HYc, WXc};
-        DgradB<32, 4, 2, 32> fb{T(1), 32, 0, py, px};
-        EpiMaskParity<G::OH1, G::OW1, 2> ep{a.X[0], a.X[0], WXc, HYc, py, px, 0, 1, 32};
-        launch_gemm<64, 32, 32, 4, 1>(fa, fb, ep, M, 32, 4 * 32, st);
+    const int frames = 2 * n;
+    const int blocks = std::min(frames, kConv2WgradBlocks);
+    constexpr size_t lds = conv2_wgrad_lds<G::OH1, G::OW1, G::OH2, G::OW2>();
+    if constexpr (lds <= 160 * 1024) {
+      static bool attr = false;
+      if (!attr) {
+        VN_HIP(hipFuncSetAttribute((const void*)conv2_wgrad_kernel<G::OH1, G::OW1, G::OH2, G::OW2>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        attr = true;
       }
+      float* bias_slab = w.slab + (int64_t)blocks * 32 * 512;
+      hipLaunchKernelGGL((conv2_wgrad_kernel<G::OH1, G::OW1, G::OH2, G::OW2>), dim3(blocks), dim3(256), lds, st,
+                         a.X[0], w.dz2, frames, w.slab, bias_slab);
+      hipLaunchKernelGGL(sum_slabs_kernel, dim3((32 * 512 + 255) / 256), dim3(256), 0, st, w.slab, blocks,
+                         (int64_t)32 * 512, Gr + L.l[1].w);
+      hipLaunchKernelGGL(sum_slabs_kernel, dim3(1), dim3(32), 0, st, bias_slab, blocks, (int64_t)32, Gr + L.l[1].b);
+    } else {  // frames whose conv1 map does not fit the LDS (174x174): generic split-K path
+      using Im = NhwcIm2col<32, 4, 4, 2, G::OH1, G::OW1, G::OH2, G::OW2, 1>;
+      const int P2 = 2 * n * G::OH2 * G::OW2;
+      Im2colT<Im> fbw{Im{a.X[0], P2}, 512};
+      launch_wgrad<32, 64, 2, 2>(w.dz2, 32, 32, fbw, 512, P2, w.slab, w.slab_cap, Gr + L.l[1].w, Gr + L.l[1].b, st);
+    }
+    if constexpr (G::OH1 % 2 == 0 && G::OW1 % 2 == 0) {
+      const int blocks = std::min(frames, resident_blocks((const void*)conv2_dgrad_kernel<G::OH1, G::OW1, G::OH2, G::OW2>,
+                                                          256, 0));
+      hipLaunchKernelGGL((conv2_dgrad_kernel<G::OH1, G::OW1, G::OH2, G::OW2>), dim3(blocks), dim3(256), 0, st, w.dz2,
+                         T(1), a.X[0], a.X[0], frames);
+    } else {
+      dgrad_all_classes<32, 32, G::OH1, G::OW1, G::OH2, G::OW2>(w.dz2, T(1), a.X[0], a.X[0], 2 * n, 0, 1, 32, st);
+    }
   }
   // ---- conv1: wgrad from dz1 (in X1's storage) and the frames
   if (src.f32[0] || src.f32[1]) {
@@ -522,7 +573,6 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
     launch_wgrad<32, 64, 2, 2>(a.X[0], 32, 32, fbw, 148, P1, w.slab, w.slab_cap, Gr + L.l[0].w, Gr + L.l[0].b, st);
   } else {
     const int frames = 2 * n;
-    const int blocks = std::min(frames, kConv1WgradBlocks);
     constexpr int CP = (G::OH1 * G::OW1 <= 400) ? (G::OH1 * G::OW1 + 7) / 8 * 8 : 448;
     constexpr size_t lds = conv1_wgrad_lds<H0, W0, CP>();
     static bool attr = false;  // > 64 KiB of dynamic LDS needs the opt-in attribute
@@ -531,6 +581,8 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       attr = true;
     }
+    const int blocks = std::min(
+        {frames, kConv1WgradBlocks, resident_blocks((const void*)conv1_wgrad_kernel<H0, W0, G::OH1, G::OW1, CP>, 256, lds)});
     hipLaunchKernelGGL((conv1_wgrad_kernel<H0, W0, G::OH1, G::OW1, CP>), dim3(blocks), dim3(256), lds, st, src, frames,
                        a.X[0], w.slab);
     hipLaunchKernelGGL(conv1_wgrad_reduce_kernel, dim3((32 * 160 + 255) / 256), dim3(256), 0, st, w.slab, blocks * 4,
