@@ -40,9 +40,12 @@ const std::string& last_error() { return g_last_error; }
 
 struct SceneDev {
   int64_t row_base;  // first arena row (frame) of the scene
-  int64_t spd_off;   // element offset of the scene's [N][N] spd block
+  int64_t spd_off;   // element offset of the scene's [N][N] spd block (and curriculum order block)
+  int64_t cnt_off;   // element offset of the scene's [N][maxd+2] curriculum count block
   int32_t graph_off; // first row of the scene's [N][4] adjacency block
   int32_t n;         // states
+  int32_t maxd;      // largest spd value of the scene
+  int32_t cur_oi;    // curriculum threshold floor(c*(maxd+offset)+1) clamped to [0, maxd] (host, fp64)
   float r_goal, r_step, r_coll;
   int32_t terminal_obs;
 };
@@ -60,8 +63,11 @@ struct EnvArgs {
   const int32_t* env_scene;
   const int32_t* tasks;
   const int32_t* sched;
+  const int32_t* cur_order;  // per scene, per goal: states sorted by spd[s][g] (stable)
+  const int32_t* cur_count;  // per scene, per goal: #states with clamp(spd,-1,maxd)+1 <= b
   uint32_t* flags;
   int n_tasks, sched_len, max_steps, autoreset, n_envs;
+  int cur_mode;  // 0 off, 1 uniform over 0 < spd <= opt, 2 0.9 / 0.1 split (graph/util.py:88-117)
   uint32_t k0, k1;
   // per call
   const int32_t* actions;
@@ -116,7 +122,20 @@ __device__ void reset_env(const EnvArgs& a, int e, int lane, int& sc, int& s, in
   const SceneDev S = a.scenes[sc];
   const int32_t* spd = a.spd + S.spd_off;
   s = -1;
-  for (int round = 0; round < kStartRounds; ++round) {
+  if (a.cur_mode > 0) {
+    // curriculum (graph/util.py:88-143, environments/gym_graph/graph.py:43-52):
+    // opt = c * (maxd + offset) + 1 (S.cur_oi = its floor); candidates 0 < spd <= opt, uniform (mode 1) or
+    // 0.9 over them / 0.1 over the farther ones (mode 2); one O(1) draw from the sorted table
+    const int oi = S.cur_oi;
+    const int32_t* cnt = a.cur_count + S.cnt_off + (int64_t)g * (S.maxd + 2);
+    const int lo = cnt[1], hi = cnt[oi + 1], n = S.n;
+    const u32x4 r = philox4x32_10(u32x4{(uint32_t)e, (uint32_t)k, 0u, STREAM_START}, a.k0, a.k1);
+    // far set when the 0.1 coin says so (and it is not empty) or when the near set is empty
+    const bool use_far = (a.cur_mode == 2 && r.y >= 3865470566u && hi < n) || hi <= lo;  // 0.9 * 2^32
+    const int b0 = use_far ? hi : lo, b1 = use_far ? n : hi;
+    if (b1 > b0) s = a.cur_order[S.spd_off + (int64_t)g * n + b0 + (int)uniform_below(r.x, (uint32_t)(b1 - b0))];
+  }
+  for (int round = 0; round < kStartRounds && s < 0; ++round) {
     const uint32_t att = (uint32_t)(round * 64 + lane);
     const u32x4 r = philox4x32_10(u32x4{(uint32_t)e, (uint32_t)k, att, STREAM_START}, a.k0, a.k1);
     const int cand = (int)uniform_below(r.x, (uint32_t)S.n);
@@ -311,6 +330,11 @@ struct vn_ctx {
   int n_tasks = 0;
   int32_t* sched = nullptr;
   int sched_len = 0;
+  std::vector<int32_t> spd_host;  // kept for building curriculum tables on demand
+  int32_t* cur_order = nullptr;
+  int32_t* cur_count = nullptr;
+  int cur_mode = 0;
+  float cur_c = 0.f, cur_offset = 0.f;
   uint32_t* flags = nullptr;
   int max_steps = 900, autoreset = 1;
   float* info_ret = nullptr;
@@ -347,6 +371,9 @@ EnvArgs make_args(vn_ctx* c) {
   a.env_scene = c->env_scene;
   a.tasks = c->tasks;
   a.sched = c->sched;
+  a.cur_order = c->cur_order;
+  a.cur_count = c->cur_count;
+  a.cur_mode = c->cur_mode;
   a.flags = c->flags;
   a.n_tasks = c->n_tasks;
   a.sched_len = c->sched_len;
@@ -383,7 +410,7 @@ int launch_env(vn_ctx* c, const EnvArgs& a, hipStream_t stream) {
 void free_ctx(vn_ctx* c) {
   if (!c) return;
   void* ptrs[] = {c->arena, c->graph, c->spd, c->scenes, c->st, c->ep_ret, c->env_scene,
-                  c->tasks, c->sched, c->flags};
+                  c->tasks, c->sched, c->flags, c->cur_order, c->cur_count};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   delete c;
@@ -446,10 +473,19 @@ int vn_create(const vn_scene_desc* scenes, int n_scenes, int n_envs, uint64_t se
       if (v < -1 || v >= n) return fail(VN_EINVAL, "vn_create: graph entry out of range");
       g32[(int64_t)sh[k].graph_off * 4 + i] = (int32_t)v;
     }
+    int32_t mx = 0;
     for (int64_t i = 0; i < n * n; ++i) {
       const int64_t v = d.spd[i];
       spd32[sh[k].spd_off + i] = (int32_t)std::max<int64_t>(std::min<int64_t>(v, INT32_MAX), INT32_MIN);
+      mx = std::max(mx, spd32[sh[k].spd_off + i]);
     }
+    if (mx > (1 << 20)) return fail(VN_EINVAL, "vn_create: spd values above 2^20");
+    sh[k].maxd = mx;
+  }
+  int64_t cnt_elems = 0;
+  for (int k = 0; k < n_scenes; ++k) {
+    sh[k].cnt_off = cnt_elems;
+    cnt_elems += (int64_t)sh[k].n * (sh[k].maxd + 2);
   }
   DeviceGuard guard(device);
   vn_ctx* c = new (std::nothrow) vn_ctx();
@@ -461,6 +497,7 @@ int vn_create(const vn_scene_desc* scenes, int n_scenes, int n_envs, uint64_t se
   c->frame_bytes = F;
   c->n_rows = rows;
   c->scenes_host = sh;
+  c->spd_host = spd32;
   auto alloc = [&](void** p, size_t bytes) -> bool {
     return hipMalloc(p, std::max<size_t>(bytes, 16)) == hipSuccess;
   };
@@ -616,6 +653,54 @@ int vn_set_env_scenes(vn_ctx* c, const int32_t* env_scene_host) {
       return fail(VN_EINVAL, "vn_set_env_scenes: scene out of range");
   DeviceGuard guard(c->device);
   VN_HIP(hipMemcpy(c->env_scene, env_scene_host, (size_t)c->n_envs * 4, hipMemcpyHostToDevice));
+  return VN_OK;
+}
+
+int vn_set_curriculum(vn_ctx* c, float complexity, int mode, float offset) {
+  if (!c) return fail(VN_EINVAL, "vn_set_curriculum: NULL ctx");
+  if (mode < 0 || mode > 2 || !(complexity >= 0.0f)) return fail(VN_EINVAL, "vn_set_curriculum: bad mode/complexity");
+  DeviceGuard guard(c->device);
+  if (mode > 0 && !c->cur_order) {
+    // per scene and goal: states sorted by spd[s][g] (stable counting sort) + inclusive counts
+    int64_t n_order = 0, n_cnt = 0;
+    for (const SceneDev& S : c->scenes_host) {
+      n_order += (int64_t)S.n * S.n;
+      n_cnt += (int64_t)S.n * (S.maxd + 2);
+    }
+    std::vector<int32_t> order(n_order), cnt(n_cnt);
+    for (const SceneDev& S : c->scenes_host) {
+      const int n = S.n, B = S.maxd + 2;
+      const int32_t* spd = c->spd_host.data() + S.spd_off;
+      std::vector<int32_t> hist(B);
+      for (int g = 0; g < n; ++g) {
+        std::fill(hist.begin(), hist.end(), 0);
+        for (int s = 0; s < n; ++s) hist[std::min(std::max(spd[(int64_t)s * n + g], -1), S.maxd) + 1]++;
+        int32_t* cg = cnt.data() + S.cnt_off + (int64_t)g * B;
+        int run = 0;
+        for (int b = 0; b < B; ++b) {
+          const int h = hist[b];
+          hist[b] = run;  // start of bucket b
+          run += h;
+          cg[b] = run;    // inclusive count
+        }
+        int32_t* og = order.data() + S.spd_off + (int64_t)g * n;
+        for (int s = 0; s < n; ++s) og[hist[std::min(std::max(spd[(int64_t)s * n + g], -1), S.maxd) + 1]++] = s;
+      }
+    }
+    if (hipMalloc((void**)&c->cur_order, std::max<size_t>(order.size() * 4, 16)) != hipSuccess ||
+        hipMalloc((void**)&c->cur_count, std::max<size_t>(cnt.size() * 4, 16)) != hipSuccess)
+      return fail(VN_ENOMEM, "vn_set_curriculum: device allocation failed");
+    VN_HIP(hipMemcpy(c->cur_order, order.data(), order.size() * 4, hipMemcpyHostToDevice));
+    VN_HIP(hipMemcpy(c->cur_count, cnt.data(), cnt.size() * 4, hipMemcpyHostToDevice));
+  }
+  for (SceneDev& S : c->scenes_host) {  // the reference computes opt in Python floats (fp64)
+    const double opt = (double)complexity * ((double)S.maxd + (double)offset) + 1.0;
+    S.cur_oi = (int32_t)std::min<double>(std::max<double>(std::floor(opt), 0.0), (double)S.maxd);
+  }
+  VN_HIP(hipMemcpy(c->scenes, c->scenes_host.data(), c->scenes_host.size() * sizeof(SceneDev), hipMemcpyHostToDevice));
+  c->cur_mode = mode;
+  c->cur_c = complexity;
+  c->cur_offset = offset;
   return VN_OK;
 }
 

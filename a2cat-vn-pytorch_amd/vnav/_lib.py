@@ -55,6 +55,7 @@ SIGNATURES = {
     "vn_set_tasks": (c_int, [c_void_p, P(c_int32), c_int]),
     "vn_set_env_scenes": (c_int, [c_void_p, P(c_int32)]),
     "vn_set_max_episode_steps": (c_int, [c_void_p, c_int]),
+    "vn_set_curriculum": (c_int, [c_void_p, c_float, c_int, c_float]),
     "vn_set_autoreset": (c_int, [c_void_p, c_int]),
     "vn_random_actions": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p]),
     "vn_get_state": (c_int, [c_void_p, c_void_p, c_void_p]),

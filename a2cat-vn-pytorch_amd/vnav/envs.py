@@ -120,10 +120,19 @@ class VectorEnv:
         _lib.check(self.lib.vn_set_schedule(self._ctx, _lib.ptr(sched), sched.shape[1]), "vn_set_schedule")
         self._schedule = sched
 
-    def set_complexity(self, complexity=None):
-        """Curriculum hook (graph/env.py:98-99, experiments/thor_cached_auxiliary.py:68-70).
-        Recorded only: on-device curriculum sampling is a SURVEY §8f 'next' item."""
+    def set_complexity(self, complexity=None, mode=None, offset=None):
+        """Curriculum hook (graph/env.py:98-99, environments/gym_graph/graph.py:40-52,
+        experiments/thor_cached_auxiliary.py:68-70): subsequent resets draw starts near the
+        goal on the device (vn_set_curriculum); None switches back to uniform starts.
+        mode/offset default to the first scene's semantics (Scene.curriculum)."""
         self.complexity = complexity
+        if complexity is None:
+            _lib.check(self.lib.vn_set_curriculum(self._ctx, 0.0, 0, 0.0), "vn_set_curriculum")
+            return
+        dm, do = self.scenes[0].curriculum
+        m = dm if mode is None else int(mode)
+        o = do if offset is None else float(offset)
+        _lib.check(self.lib.vn_set_curriculum(self._ctx, float(complexity), m, o), "vn_set_curriculum")
 
     set_hardness = set_complexity
 

@@ -37,6 +37,10 @@ class Scene:
     synth_id: int = 0
     rewards: Tuple[float, float, float] = CACHED_REWARDS
     terminal_obs: int = 0  # 0: re-emit previous obs on terminal (cached.py:90-96); 1: current
+    # set_complexity semantics: (mode, offset) of vn_set_curriculum. Oriented h5 scenes follow
+    # OrientedGraphEnv (uniform over d <= c*(maxd_cell+3)+1; spd carries the rotation term, so
+    # maxd_cell + 3 = max spd + 1); maze scenes follow SimpleGraphEnv (0.9/0.1, c*(maxd-1)+1).
+    curriculum: Tuple[int, float] = (1, 1.0)
     name: str = ""
     maze: Optional[np.ndarray] = None
     locations: Optional[list] = None
@@ -154,7 +158,7 @@ def maze_scene(maze, goal, name="maze"):
     g = lookup[tuple(goal)]
     return Scene(graph=graph, spd=base, frame_shape=(X, Y, 3), observations=frames,
                  rewards=GRAPH_REWARDS, terminal_obs=1, name=name, maze=maze, locations=locs,
-                 goals=[g])
+                 goals=[g], curriculum=(2, -1.0))
 
 
 def scene_from_arrays(graph, spd, observations, rewards=CACHED_REWARDS, name=""):

@@ -123,6 +123,16 @@ int vn_set_tasks(vn_ctx* ctx, const int32_t* tasks_host, int n_tasks);
 /* Fixed env -> scene assignment (default e mod n_scenes). */
 int vn_set_env_scenes(vn_ctx* ctx, const int32_t* env_scene_host);
 int vn_set_max_episode_steps(vn_ctx* ctx, int max_steps); /* <= 0: no limit */
+
+/* Curriculum start sampling (set_complexity / set_hardness: graph/util.py:88-143,
+ * environments/gym_graph/graph.py:43-52, graph/env.py:101-106,
+ * experiments/thor_cached_auxiliary.py:68-70). opt = complexity*(maxd + offset) + 1 with
+ * maxd the scene's largest spd; starts with 0 < spd[s][g] <= opt are drawn uniformly
+ * (mode 1, OrientedGraphEnv/sample_initial_state) or with probability 0.9 among them and
+ * 0.1 among the farther ones (mode 2, SimpleGraphEnv/sample_initial_position); mode 0 =
+ * off (uniform rejection sampling of cached.py). One O(1) draw from per-goal sorted tables
+ * built on the first call. */
+int vn_set_curriculum(vn_ctx* ctx, float complexity, int mode, float offset);
 int vn_set_autoreset(vn_ctx* ctx, int on);                /* default on */
 
 /* Synthetic uniform actions in [0,4) from Philox(seed, env, step). */

@@ -93,12 +93,35 @@ class VectorEnvOracle:
         self.env_scene = (np.arange(n_envs) % len(scenes)) if env_scene is None else np.asarray(env_scene)
         self.tasks = None if not tasks else np.asarray(tasks, dtype=np.int64)
         self.schedule = None
+        self.cur_mode, self.cur_c, self.cur_offset = 0, 0.0, 0.0
         z = lambda: np.zeros(n_envs, dtype=np.int64)  # noqa: E731
         self.scene, self.state, self.goal, self.obs_state = z(), z(), z(), z()
         self.elapsed, self.episode, self.sched_pos = z(), z(), z()
         self.ep_ret = np.zeros(n_envs, dtype=np.float32)
         self.flags = 0
         self.reset()
+
+    def set_curriculum(self, complexity, mode, offset):
+        """The engine's curriculum draw (restated from DESIGN.md "Curriculum"): per goal,
+        states sorted stably by spd; near = 0 < spd <= floor(opt), far = spd > opt."""
+        self.cur_mode, self.cur_c, self.cur_offset = int(mode), float(complexity), float(offset)
+
+    def _curriculum_start(self, e, k, sc, g):
+        spd = np.asarray(self.scenes[sc]["spd"])
+        n = spd.shape[0]
+        maxd = int(spd.max())
+        col = np.clip(spd[:, g], -1, maxd)
+        order = np.argsort(col, kind="stable")
+        opt = self.cur_c * (maxd + self.cur_offset) + 1.0  # Python floats, as the reference
+        oi = min(max(int(np.floor(opt)), 0), maxd)
+        lo = int((col <= 0).sum())
+        hi = int((col <= oi).sum())
+        rx, ry, _, _ = philox.philox4x32_10(e, k, 0, philox.STREAM_START, self.k0, self.k1)
+        use_far = (self.cur_mode == 2 and int(ry) >= 3865470566 and hi < n) or hi <= lo
+        b0, b1 = (hi, n) if use_far else (lo, hi)
+        if b1 <= b0:
+            return None
+        return int(order[b0 + int(philox.uniform_below(rx, b1 - b0))])
 
     def set_schedule(self, schedule):
         """schedule [n_envs, L, 2] of (start, goal)."""
@@ -117,31 +140,39 @@ class VectorEnvOracle:
                 s, g = min(max(s, 0), n - 1), min(max(g, 0), n - 1)
             self.sched_pos[e] = sp + 1
         else:
-            rx, ry, _, _ = philox.philox4x32_10(e, k, 0, philox.STREAM_GOAL, self.k0, self.k1)
-            if self.tasks is not None:
-                t = int(philox.uniform_below(rx, len(self.tasks)))
-                sc, g = int(self.tasks[t, 0]), int(self.tasks[t, 1])
-                if g < 0:
-                    g = int(philox.uniform_below(ry, self.sizes[sc]))
-            else:
-                sc = int(self.env_scene[e])
-                g = int(philox.uniform_below(rx, self.sizes[sc]))
-            n = int(self.sizes[sc])
-            spd = self.scenes[sc]["spd"]
-            att = np.arange(START_ATTEMPTS)
-            r = philox.philox4x32_10(e, k, att, philox.STREAM_START, self.k0, self.k1)[0]
-            cand = philox.uniform_below(r, n)
-            ok = np.asarray(spd)[cand, g] > 0
-            if ok.any():
-                s = int(cand[int(np.argmax(ok))])
-            else:
-                self.flags |= FLAG_RESET_EXHAUSTED
-                s = int(cand[0])
+            sc, g = self._draw_goal(e, k)
+            s = self._curriculum_start(e, k, sc, g) if self.cur_mode > 0 else None
+            if s is None:
+                s = self._rejection_start(e, k, sc, g)
         self.scene[e], self.state[e], self.goal[e] = sc, s, g
         self.obs_state[e] = s
         self.elapsed[e] = 0
         self.ep_ret[e] = 0.0
         self.episode[e] = k + 1
+
+    def _draw_goal(self, e, k):
+        rx, ry, _, _ = philox.philox4x32_10(e, k, 0, philox.STREAM_GOAL, self.k0, self.k1)
+        if self.tasks is not None:
+            t = int(philox.uniform_below(rx, len(self.tasks)))
+            sc, g = int(self.tasks[t, 0]), int(self.tasks[t, 1])
+            if g < 0:
+                g = int(philox.uniform_below(ry, self.sizes[sc]))
+        else:
+            sc = int(self.env_scene[e])
+            g = int(philox.uniform_below(rx, self.sizes[sc]))
+        return sc, g
+
+    def _rejection_start(self, e, k, sc, g):
+        """cached.py:41-44 over Philox attempts: first candidate with spd[s][g] > 0."""
+        n = int(self.sizes[sc])
+        att = np.arange(START_ATTEMPTS)
+        r = philox.philox4x32_10(e, k, att, philox.STREAM_START, self.k0, self.k1)[0]
+        cand = philox.uniform_below(r, n)
+        ok = np.asarray(self.scenes[sc]["spd"])[cand, g] > 0
+        if ok.any():
+            return int(cand[int(np.argmax(ok))])
+        self.flags |= FLAG_RESET_EXHAUSTED
+        return int(cand[0])
 
     def reset(self, mask=None):
         for e in range(self.n_envs):

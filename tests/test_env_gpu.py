@@ -260,3 +260,60 @@ def test_state_checkpoint_roundtrip():
         r0, d0, s0 = first[t - 10]
         assert torch.equal(r, r0) and torch.equal(d, d0) and torch.equal(i["state"], s0)
     assert ret.shape[0] == 257
+
+
+@pytest.mark.parametrize("mode,c", [(1, 0.05), (1, 0.3), (2, 0.1), (2, 0.6)])
+def test_curriculum_matches_oracle(mode, c):
+    vnav = _vnav()
+    sc = small_scenes()
+    arena = np.concatenate([s.observations for s in sc])
+    n = 700
+    env = vnav.VectorEnv(sc, n, seed=99, max_episode_steps=7)
+    o = oracle_of(sc, n, 99, max_steps=7)
+    env.set_complexity(c, mode=mode, offset=1.0)
+    o.set_curriculum(c, mode, 1.0)
+    env.reset()
+    o.reset()
+    rng = np.random.RandomState(7)
+    for t in range(40):
+        a = rng.randint(0, 4, size=n).astype(np.int32)
+        compare_step(env.step(torch.as_tensor(a, device="cuda")), o.step(a), arena, (mode, c, t))
+
+
+def test_curriculum_maze_distribution_matches_reference(golden):
+    """SimpleGraphEnv's set_complexity (graph/env.py:101-106): starts ~ sample_initial_position
+    (graph/util.py:88-117) with the 0.9/0.1 split; GPU frequencies vs the reference weights."""
+    vnav = _vnav()
+    m = golden("maze.npz")
+    maze, goal = m["maze"], tuple(m["goal"].tolist())
+    dist = m["distances"]
+    scene = vnav.maze_scene(maze, goal)
+    g = scene.goals[0]
+    E = 4096
+    env = vnav.VectorEnv([scene], E, seed=3, tasks=[(0, g)], max_episode_steps=0)
+    c = 0.3
+    env.set_complexity(c)
+    counts = np.zeros(scene.n_states)
+    for _ in range(12):
+        env.reset()
+        st = env.get_state()[1].cpu().numpy()
+        counts += np.bincount(st, minlength=scene.n_states)
+    # reference weights (graph/util.py:103-112) with opt = c*(largest-1)+1 (graph/env.py:105)
+    opt = c * (dist.max() - 1) + 1
+    d = np.array([dist[p + goal] for p in scene.locations])
+    pos, neg = (d > 0) & (d <= opt), d > opt
+    w = np.where(pos, 0.9 / pos.sum(), 0.0) + np.where(neg, 0.1 / neg.sum(), 0.0)
+    expect = w * counts.sum()
+    assert counts[w == 0].sum() == 0
+    nz = w > 0
+    chi2 = (((counts[nz] - expect[nz]) ** 2) / expect[nz]).sum()
+    dof = nz.sum() - 1
+    assert chi2 < dof + 6 * np.sqrt(2 * dof), (chi2, dof)
+    # the reference's own sampler (oracle restatement pinned by goldens) agrees with w
+    rng = np.random.RandomState(0)
+    ref = np.zeros(scene.n_states)
+    lookup = {p: i for i, p in enumerate(scene.locations)}
+    for _ in range(4000):
+        ref[lookup[oe.sample_initial_position(maze, dist, goal, opt, rng=rng)]] += 1
+    chi2r = (((ref[nz] - w[nz] * 4000) ** 2) / (w[nz] * 4000)).sum()
+    assert chi2r < dof + 6 * np.sqrt(2 * dof)
