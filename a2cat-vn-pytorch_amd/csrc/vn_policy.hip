@@ -21,6 +21,7 @@
 
 #include "vn_common.h"
 #include "vn_gemm.h"
+#include "vn_lstm.h"
 
 namespace vn {
 
@@ -257,9 +258,12 @@ struct PolicyLayout {
   int64_t n_params;
   int64_t sz[5];  // per-sample floats of X1..X5
   int64_t wt_off[6], wt_total;
+  // recurrent core (BigGoalHouseModel, models/goal.py:61-67): W_cat [2048][xcat] = [W_ih | 0 | W_hh]
+  int lstm, lin, xoff, xcat;
+  int64_t lw, lbih, lbhh;
 };
 
-inline PolicyLayout make_layout(int H, int W, int A) {
+inline PolicyLayout make_layout(int H, int W, int A, int lstm = 0) {
   PolicyLayout L{};
   L.H = H;
   L.W = W;
@@ -283,6 +287,18 @@ inline PolicyLayout make_layout(int H, int W, int A) {
     off += couts[i];
     L.wt_off[i] = wt;
     if (i > 0) wt += (int64_t)couts[i] * ks[i];
+  }
+  L.lstm = lstm;
+  L.lin = 512 + A + 1;
+  L.xoff = (L.lin + 3) / 4 * 4;
+  L.xcat = L.xoff + 512;
+  if (lstm) {
+    L.lw = off;
+    off += 2048ll * L.xcat;
+    L.lbih = off;
+    off += 2048;
+    L.lbhh = off;
+    off += 2048;
   }
   L.n_params = off;
   L.wt_total = wt;
@@ -436,8 +452,8 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
     EpiBiasAct ep{a.X[4], 512, P + L.l[4].b, 1};
     launch_gemm<64, 64, 32, 2, 2>(fa, fb, ep, n, 512, G::FCIN, st);
   }
-  // heads (X5 -> out[n][8]: logits, value)
-  {
+  // heads (X5 -> out[n][8]: logits, value); out == NULL runs the trunk only (recurrent policy)
+  if (out) {
     DenseRows fa{a.X[4], 512, n};
     DenseRows fb{P + L.l[5].w, 512, A1};
     EpiBiasAct ep{out, OUT_LD, P + L.l[5].b, 0};
@@ -485,10 +501,12 @@ inline BwdWork carve(const PolicyLayout& L, float* ws, int64_t n) {
 
 template <int H0, int W0>
 int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int n, const Acts& a,
-                  const float* dout, float* Gr, const BwdWork& w, hipStream_t st) {
+                  const float* dout, const float* dz5_in, float* Gr, const BwdWork& w, hipStream_t st) {
   using G = Geo<H0, W0>;
   const int A1 = L.A + 1;
   auto T = [&](int i) { return w.wt + L.wt_off[i]; };
+  // dz5_in != NULL: the trunk backward of the recurrent policy (heads and LSTM already done)
+  const float* dz5 = dz5_in ? dz5_in : w.dz5;
   // transposed weights for the dgrad products
   for (int i = 1; i < 6; ++i) {
     const int rows = L.l[i].cout, cols = L.l[i].kp;
@@ -497,7 +515,7 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
   }
   const int n9 = n * G::OH3 * G::OW3;
   // ---- head: dX5 = dout x Whead, masked by X5 ; dWhead = dout^T x X5
-  {
+  if (!dz5_in) {
     DenseRows fa{dout, OUT_LD, n};
     DenseRows fb{T(5), A1, 512};  // WT [512][A1]
     EpiMask ep{w.dz5, a.X[4], 512};
@@ -507,12 +525,12 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
   }
   // ---- conv_merge Linear: dX4 = dz5 x Wfc masked by X4 ; dWfc = dz5^T x X4
   {
-    DenseRows fa{w.dz5, 512, n};
+    DenseRows fa{dz5, 512, n};
     DenseRows fb{T(4), 512, G::FCIN};  // WT [FCIN][512]
     EpiMask ep{w.dz4, a.X[3], G::FCIN};
     launch_gemm<64, 64, 32, 2, 2>(fa, fb, ep, n, G::FCIN, 512, st);
     Im2colT<DenseRows> fbw{DenseRows{a.X[3], G::FCIN, n}, G::FCIN};
-    launch_wgrad<64, 64, 2, 2>(w.dz5, 512, 512, fbw, G::FCIN, n, w.slab, w.slab_cap, Gr + L.l[4].w, Gr + L.l[4].b,
+    launch_wgrad<64, 64, 2, 2>(dz5, 512, 512, fbw, G::FCIN, n, w.slab, w.slab_cap, Gr + L.l[4].w, Gr + L.l[4].b,
                                st);
   }
   // ---- conv4 (1x1): dX3 = dz4 x W4 masked by X3 ; dW4 = dz4^T x X3
@@ -592,6 +610,118 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
   return VN_OK;
 }
 
+// ---- recurrent core (vn_lstm.h) --------------------------------------------------
+inline int lstm_forward_step(const PolicyLayout& L, const float* P, int E, const float* x5, const float* lra,
+                             const float* mask, const float* h_prev, const float* c_prev, float* xc, float* gates,
+                             float* acts, float* c_out, float* h_out, hipStream_t st) {
+  const int64_t nx = (int64_t)E * L.xcat;
+  hipLaunchKernelGGL(lstm_prep_kernel, dim3((unsigned)((nx + 255) / 256)), dim3(256), 0, st, E, L.A, L.xcat, L.xoff,
+                     x5, lra, mask, h_prev, xc);
+  {
+    DenseRows fa{xc, L.xcat, E};
+    DenseRows fb{P + L.lw, L.xcat, 2048};
+    EpiBias2 ep{gates, 2048, P + L.lbih, P + L.lbhh};
+    launch_gemm<64, 64, 32, 2, 2>(fa, fb, ep, E, 2048, L.xcat, st);
+  }
+  const int64_t nc = (int64_t)E * 512;
+  hipLaunchKernelGGL(lstm_cell_kernel, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, st, E, gates, c_prev, mask,
+                     acts, c_out, h_out);
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
+
+inline int heads_forward(const PolicyLayout& L, const float* P, const float* feat, int n, float* out, hipStream_t st) {
+  DenseRows fa{feat, 512, n};
+  DenseRows fb{P + L.l[5].w, 512, L.A + 1};
+  EpiBiasAct ep{out, OUT_LD, P + L.l[5].b, 0};
+  launch_gemm<64, 16, 32, 4, 1>(fa, fb, ep, n, L.A + 1, 512, st);
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
+
+struct LstmWork {
+  float* wcat_t;   // [xcat][2048]
+  float* head_t;   // [512][A+1]
+  float* dh_heads; // [T*E][512]
+  float* dgates;   // [T*E][2048]
+  float* dh[2];    // [E][512]
+  float* dc[2];    // [E][512]
+  float* slab;
+};
+
+inline int64_t lstm_workspace_floats(const PolicyLayout& L, int64_t T, int64_t E) {
+  const int64_t n = T * E;
+  return 2048ll * L.xcat + 512ll * 8 + n * 512 + n * 2048 + 4 * E * 512 + slab_floats(L) + 64;
+}
+
+inline LstmWork lstm_carve(const PolicyLayout& L, float* ws, int64_t T, int64_t E) {
+  LstmWork w;
+  float* p = ws;
+  w.wcat_t = p;
+  p += 2048ll * L.xcat;
+  w.head_t = p;
+  p += 512ll * 8;
+  w.dh_heads = p;
+  p += T * E * 512;
+  w.dgates = p;
+  p += T * E * 2048;
+  for (int i = 0; i < 2; ++i) {
+    w.dh[i] = p;
+    p += E * 512;
+    w.dc[i] = p;
+    p += E * 512;
+  }
+  w.slab = p;
+  return w;
+}
+
+// BPTT over one rollout of T steps x E envs (rows t*E + e), from dL/d(out) [T*E][8].
+// Writes the head and LSTM gradients into Gr and dL/dX5 (masked by conv_merge's ReLU)
+// into dz5 for the trunk backward.
+inline int lstm_backward(const PolicyLayout& L, const float* P, int T, int E, const float* dout, const float* h_all,
+                         const float* xcat_all, const float* acts_all, const float* c_all, const float* c_init,
+                         const float* mask_all, const float* x5_all, float* dz5, float* Gr, const LstmWork& w,
+                         hipStream_t st) {
+  const int A1 = L.A + 1;
+  const int N = T * E;
+  const int64_t e512 = (int64_t)E * 512;
+  hipLaunchKernelGGL(transpose_kernel, dim3((2048 * L.xcat + 255) / 256), dim3(256), 0, st, P + L.lw, 2048, L.xcat,
+                     w.wcat_t);
+  hipLaunchKernelGGL(transpose_kernel, dim3((A1 * 512 + 255) / 256), dim3(256), 0, st, P + L.l[5].w, A1, 512,
+                     w.head_t);
+  {  // heads: dh_heads = dout x Whead ; dWhead = dout^T x h
+    DenseRows fa{dout, OUT_LD, N};
+    DenseRows fb{w.head_t, A1, 512};
+    EpiStore ep{w.dh_heads, 512};
+    launch_gemm<64, 64, 32, 2, 2>(fa, fb, ep, N, 512, A1, st);
+    Im2colT<DenseRows> fbw{DenseRows{h_all, 512, N}, 512};
+    launch_wgrad<32, 64, 2, 2>(dout, OUT_LD, A1, fbw, 512, N, w.slab, slab_floats(L), Gr + L.l[5].w, Gr + L.l[5].b,
+                               st);
+  }
+  const unsigned cb = (unsigned)((e512 + 255) / 256);
+  for (int t = T - 1, cur = 0; t >= 0; --t, cur ^= 1) {
+    const bool last = (t == T - 1);
+    const float* mask = mask_all ? mask_all + (int64_t)t * E : nullptr;
+    const float* cprev = t > 0 ? c_all + (int64_t)(t - 1) * e512 : c_init;
+    float* dg = w.dgates + (int64_t)t * E * 2048;
+    hipLaunchKernelGGL(lstm_cell_bwd_kernel, dim3(cb), dim3(256), 0, st, E, w.dh_heads + (int64_t)t * e512,
+                       last ? nullptr : w.dh[cur ^ 1], last ? nullptr : w.dc[cur ^ 1], acts_all + (int64_t)t * E * 2048,
+                       c_all + (int64_t)t * e512, cprev, mask, dg, w.dc[cur]);
+    DenseRows fa{dg, 2048, E};
+    DenseRows fb{w.wcat_t, 2048, L.xcat};
+    EpiLstmDx ep{dz5 + (int64_t)t * e512, x5_all + (int64_t)t * e512, w.dh[cur], mask, L.xoff};
+    launch_gemm<64, 64, 32, 2, 2>(fa, fb, ep, E, L.xcat, 2048, st);
+  }
+  {  // dW_cat = dgates^T x xcat over all T*E rows; b_ih and b_hh share the bias gradient
+    Im2colT<DenseRows> fbw{DenseRows{xcat_all, L.xcat, N}, L.xcat};
+    launch_wgrad<64, 64, 2, 2>(w.dgates, 2048, 2048, fbw, L.xcat, N, w.slab, slab_floats(L), Gr + L.lw, Gr + L.lbih,
+                               st);
+    VN_HIP(hipMemcpyAsync(Gr + L.lbhh, Gr + L.lbih, 2048 * sizeof(float), hipMemcpyDeviceToDevice, st));
+  }
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
+
 }  // namespace vn
 
 using namespace vn;
@@ -619,14 +749,19 @@ FrameSrc to_src(const vn_frames* f) {
 extern "C" {
 
 int vn_policy_create(int frame_h, int frame_w, int num_actions, vn_policy** out) {
+  return vn_policy_create_ex(frame_h, frame_w, num_actions, 0, out);
+}
+
+int vn_policy_create_ex(int frame_h, int frame_w, int num_actions, int flags, vn_policy** out) {
   if (!out) return fail(VN_EINVAL, "vn_policy_create: out is NULL");
+  if (flags & ~VN_POLICY_LSTM) return fail(VN_EINVAL, "vn_policy_create: unknown flags");
   *out = nullptr;
   if (!supported(frame_h, frame_w))
     return fail(VN_EINVAL, "vn_policy_create: frame size must be 84x84 or 174x174");
   if (num_actions < 1 || num_actions + 1 > OUT_LD) return fail(VN_EINVAL, "vn_policy_create: 1..7 actions");
   vn_policy* p = new (std::nothrow) vn_policy();
   if (!p) return fail(VN_ENOMEM, "vn_policy_create: host allocation");
-  p->L = make_layout(frame_h, frame_w, num_actions);
+  p->L = make_layout(frame_h, frame_w, num_actions, (flags & VN_POLICY_LSTM) ? 1 : 0);
   *out = p;
   return VN_OK;
 }
@@ -660,7 +795,8 @@ int vn_policy_workspace_floats(vn_policy* p, int64_t n, int64_t* floats) {
 
 int vn_policy_forward(vn_policy* p, const float* params, const vn_frames* frames, int n, float* acts,
                       int64_t act_capacity, int64_t act_offset, float* out, vn_stream_t stream) {
-  if (!p || !params || !frames || !acts || !out || n <= 0) return fail(VN_EINVAL, "vn_policy_forward: bad args");
+  if (!p || !params || !frames || !acts || n <= 0) return fail(VN_EINVAL, "vn_policy_forward: bad args");
+  if (!out && !p->L.lstm) return fail(VN_EINVAL, "vn_policy_forward: out is NULL");
   if (act_offset < 0 || act_offset + n > act_capacity)
     return fail(VN_EINVAL, "vn_policy_forward: samples exceed the activation capacity");
   const FrameSrc src = to_src(frames);
@@ -682,8 +818,64 @@ int vn_policy_backward(vn_policy* p, const float* params, const vn_frames* frame
   const Acts a = acts_at(p->L, acts, act_capacity, 0);
   const BwdWork w = carve(p->L, workspace, n);
   hipStream_t st = (hipStream_t)stream;
-  if (p->L.H == 84) return backward_impl<84, 84>(p->L, params, src, n, a, dout, grads, w, st);
-  return backward_impl<174, 174>(p->L, params, src, n, a, dout, grads, w, st);
+  if (p->L.H == 84) return backward_impl<84, 84>(p->L, params, src, n, a, dout, nullptr, grads, w, st);
+  return backward_impl<174, 174>(p->L, params, src, n, a, dout, nullptr, grads, w, st);
+}
+
+int vn_policy_backward_trunk(vn_policy* p, const float* params, const vn_frames* frames, int n, float* acts,
+                             int64_t act_capacity, const float* dz5, float* grads, float* workspace,
+                             vn_stream_t stream) {
+  if (!p || !params || !frames || !acts || !dz5 || !grads || !workspace || n <= 0)
+    return fail(VN_EINVAL, "vn_policy_backward_trunk: bad args");
+  if (n > act_capacity) return fail(VN_EINVAL, "vn_policy_backward_trunk: n exceeds the activation capacity");
+  const FrameSrc src = to_src(frames);
+  const Acts a = acts_at(p->L, acts, act_capacity, 0);
+  const BwdWork w = carve(p->L, workspace, n);
+  hipStream_t st = (hipStream_t)stream;
+  if (p->L.H == 84) return backward_impl<84, 84>(p->L, params, src, n, a, nullptr, dz5, grads, w, st);
+  return backward_impl<174, 174>(p->L, params, src, n, a, nullptr, dz5, grads, w, st);
+}
+
+int vn_policy_lstm_info(vn_policy* p, int64_t* info8) {
+  if (!p || !info8) return fail(VN_EINVAL, "vn_policy_lstm_info: bad args");
+  if (!p->L.lstm) return fail(VN_EINVAL, "vn_policy_lstm_info: policy has no recurrent core");
+  const PolicyLayout& L = p->L;
+  const int64_t v[8] = {L.lw, L.lbih, L.lbhh, L.xcat, L.xoff, L.lin, 512, 0};
+  for (int i = 0; i < 8; ++i) info8[i] = v[i];
+  return VN_OK;
+}
+
+int vn_lstm_workspace_floats(vn_policy* p, int T, int E, int64_t* floats) {
+  if (!p || !floats || T <= 0 || E <= 0 || !p->L.lstm) return fail(VN_EINVAL, "vn_lstm_workspace_floats: bad args");
+  *floats = lstm_workspace_floats(p->L, T, E);
+  return VN_OK;
+}
+
+int vn_lstm_forward_step(vn_policy* p, const float* params, int E, const float* x5, const float* lra,
+                         const float* mask, const float* h_prev, const float* c_prev, float* xcat, float* gates,
+                         float* acts, float* c_out, float* h_out, vn_stream_t stream) {
+  if (!p || !p->L.lstm || !params || E <= 0 || !x5 || !xcat || !gates || !acts || !c_out || !h_out)
+    return fail(VN_EINVAL, "vn_lstm_forward_step: bad args");
+  return lstm_forward_step(p->L, params, E, x5, lra, mask, h_prev, c_prev, xcat, gates, acts, c_out, h_out,
+                           (hipStream_t)stream);
+}
+
+int vn_policy_heads(vn_policy* p, const float* params, const float* feat, int n, float* out, vn_stream_t stream) {
+  if (!p || !params || !feat || !out || n <= 0) return fail(VN_EINVAL, "vn_policy_heads: bad args");
+  return heads_forward(p->L, params, feat, n, out, (hipStream_t)stream);
+}
+
+int vn_lstm_backward(vn_policy* p, const float* params, int T, int E, const float* dout, const float* h_all,
+                     const float* xcat_all, const float* acts_all, const float* c_all, const float* c_init,
+                     const float* mask_all, const float* x5_all, float* dz5_all, float* grads, float* workspace,
+                     vn_stream_t stream) {
+  if (!p || !p->L.lstm || !params || T <= 0 || E <= 0 || !dout || !h_all || !xcat_all || !acts_all || !c_all ||
+      !x5_all || !dz5_all || !grads || !workspace)
+    return fail(VN_EINVAL, "vn_lstm_backward: bad args");
+  if ((int64_t)T * E > (int64_t)1 << 30) return fail(VN_EINVAL, "vn_lstm_backward: T*E too large");
+  const LstmWork w = lstm_carve(p->L, workspace, T, E);
+  return lstm_backward(p->L, params, T, E, dout, h_all, xcat_all, acts_all, c_all, c_init, mask_all, x5_all, dz5_all,
+                       grads, w, (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -78,6 +78,14 @@ SIGNATURES.update({
     "vn_policy_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_int,
                                           c_void_p, c_int64, c_void_p, c_void_p,
                                           c_void_p, c_void_p]),
+    "vn_policy_create_ex": (c_int, [c_int, c_int, c_int, c_int, P(c_void_p)]),
+    "vn_policy_lstm_info": (c_int, [c_void_p, P(c_int64)]),
+    "vn_lstm_workspace_floats": (c_int, [c_void_p, c_int, c_int, P(c_int64)]),
+    "vn_lstm_forward_step": (c_int, [c_void_p, c_void_p, c_int] + [c_void_p] * 10 + [c_void_p]),
+    "vn_policy_heads": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "vn_lstm_backward": (c_int, [c_void_p, c_void_p, c_int, c_int] + [c_void_p] * 11 + [c_void_p]),
+    "vn_policy_backward_trunk": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int64, c_void_p,
+                                         c_void_p, c_void_p, c_void_p]),
     "vn_policy_sample": (c_int, [c_void_p, c_int, c_int, c_uint64, c_uint64,
                                         c_void_p, c_void_p, c_void_p, c_void_p,
                                         c_void_p]),

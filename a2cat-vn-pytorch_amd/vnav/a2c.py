@@ -13,6 +13,11 @@ Everything per step is a device launch: policy forward on frames gathered zero-c
 from the scene cache by row index, categorical sampling, env step (index-only), then
 returns, loss gradient, backward, one flat-buffer all-reduce, norm, clip + RMSprop. No
 host synchronisation inside ``step(sync=False)``.
+
+With a recurrent net (``recurrent=True``) each step also runs the LSTM core: the input is
+[conv_merge features | one-hot last action | last reward] and the carried (h, c), both
+zeroed where an episode starts (mask m_t = 1 - done_{t-1}); the update back-propagates
+through the T steps of the rollout (truncated BPTT) and (h, c) carry on to the next.
 """
 import ctypes
 import time
@@ -27,7 +32,7 @@ from .policy import OUT_LD, PolicyNet, frames_from_rows
 class A2CTrainer:
     def __init__(self, env, net=None, params=None, num_steps=20, gamma=0.99, learning_rate=7e-4,
                  max_time_steps=2e6, rms_alpha=0.99, rms_epsilon=1e-5, max_gradient_norm=0.5,
-                 value_coefficient=0.5, entropy_coefficient=0.01, seed=0, process_group=None):
+                 value_coefficient=0.5, entropy_coefficient=0.01, seed=0, process_group=None, recurrent=False):
         self.env = env
         self.lib = _lib.load()
         self.device = env.device
@@ -43,7 +48,9 @@ class A2CTrainer:
         self.seed = int(seed)
         self.group = process_group
         self.world, self.rank = vdist.world_of(process_group)
-        self.net = net if net is not None else PolicyNet(env.frame_shape[:2], env.num_actions, self.device)
+        self.net = net if net is not None else PolicyNet(env.frame_shape[:2], env.num_actions, self.device,
+                                                         recurrent=recurrent)
+        self.recurrent = self.net.recurrent
         self.A = self.net.num_actions
         self.params = params if params is not None else self.net.init_params(self.seed)
         vdist.broadcast_params_(self.params, group=self.group)
@@ -70,6 +77,30 @@ class A2CTrainer:
         self.scalars = torch.zeros(2, dtype=torch.float32, **kw)
         self.episode_stats = torch.zeros(3, dtype=torch.float32, **kw)  # count, return sum, length sum
         self.workspace = torch.empty(self.net.workspace_floats(N), dtype=torch.float32, **kw)
+        if self.recurrent:
+            X = self.net.lstm["xcat"]
+            A1 = self.A + 1
+            f32 = dict(dtype=torch.float32, **kw)
+            self.xcat = torch.zeros((N, X), **f32)
+            self.lstm_acts = torch.zeros((N, 2048), **f32)
+            self.c_all = torch.zeros((N, 512), **f32)
+            self.h_all = torch.zeros((N, 512), **f32)
+            self.gates = torch.zeros((E, 2048), **f32)
+            self.masks = torch.ones((T, E), **f32)
+            self.lra = torch.zeros((T, E, A1), **f32)
+            self.h0 = torch.zeros((E, 512), **f32)    # state entering the rollout
+            self.c0 = torch.zeros((E, 512), **f32)
+            self.prev_action = torch.zeros(E, dtype=torch.int64, **kw)
+            self.prev_reward = torch.zeros(E, **f32)
+            self.prev_mask = torch.zeros(E, **f32)    # 0: the first step starts every episode
+            self.boot_xcat = torch.zeros((E, X), **f32)
+            self.boot_la = torch.zeros((E, 2048), **f32)
+            self.boot_c = torch.zeros((E, 512), **f32)
+            self.boot_h = torch.zeros((E, 512), **f32)
+            self.boot_mask = torch.zeros(E, **f32)
+            self.boot_lra = torch.zeros((E, A1), **f32)
+            self.dz5 = torch.zeros((N, 512), **f32)
+            self.lstm_ws = torch.empty(self.net.lstm_workspace_floats(T, E), **f32)
         arena, fb, _, _ = env.frame_arena()
         self._arena, self._fb = arena, fb
         env.observe(gather=False)  # refresh the obs row buffers for the first forward
@@ -94,6 +125,44 @@ class A2CTrainer:
         frac = min(self.total_steps / self.max_time_steps, 1.0) if self.max_time_steps > 0 else 0.0
         return self.learning_rate * (1.0 - frac)
 
+    def _last_reward_action(self, lra, mask):
+        """[one_hot(a_{t-1}) | r_{t-1}] * m_t (goal.py:63: last action, reward)."""
+        A = self.A
+        lra.zero_()
+        lra[:, :A].scatter_(1, self.prev_action[:, None], 1.0)
+        lra[:, A] = self.prev_reward
+        lra.mul_(mask[:, None])
+
+    def _policy_step(self, t, frames):
+        """Forward of step t of the rollout into self.out[t*E:(t+1)*E]."""
+        net, E, N = self.net, self.env.num_envs, self.num_steps * self.env.num_envs
+        sl = slice(t * E, (t + 1) * E)
+        if not self.recurrent:
+            net.forward(self.params, frames, E, self.acts, N, t * E, self.out[sl])
+            return
+        net.forward(self.params, frames, E, self.acts, N, t * E, None)
+        self.masks[t].copy_(self.prev_mask)
+        self._last_reward_action(self.lra[t], self.masks[t])
+        hp = self.h0 if t == 0 else self.h_all[(t - 1) * E:t * E]
+        cp = self.c0 if t == 0 else self.c_all[(t - 1) * E:t * E]
+        net.lstm_step(self.params, E, net.x5(self.acts, N)[sl], self.lra[t], self.masks[t], hp, cp, self.xcat[sl],
+                      self.gates, self.lstm_acts[sl], self.c_all[sl], self.h_all[sl])
+        net.heads(self.params, self.h_all[sl], E, self.out[sl])
+
+    def _bootstrap(self, frames):
+        net, E = self.net, self.env.num_envs
+        if not self.recurrent:
+            net.forward(self.params, frames, E, self.boot_acts, E, 0, self.boot_out)
+            return
+        T = self.num_steps
+        net.forward(self.params, frames, E, self.boot_acts, E, 0, None)
+        self.boot_mask.copy_(self.prev_mask)
+        self._last_reward_action(self.boot_lra, self.boot_mask)
+        last = slice((T - 1) * E, T * E)
+        net.lstm_step(self.params, E, net.x5(self.boot_acts, E), self.boot_lra, self.boot_mask, self.h_all[last],
+                      self.c_all[last], self.boot_xcat, self.gates, self.boot_la, self.boot_c, self.boot_h)
+        net.heads(self.params, self.boot_h, E, self.boot_out)
+
     def rollout(self):
         env, net, lib = self.env, self.net, self.lib
         E, T, A = env.num_envs, self.num_steps, self.A
@@ -104,8 +173,7 @@ class A2CTrainer:
             sl = slice(t * E, (t + 1) * E)
             self.rows_img[sl].copy_(info["img_row"])
             self.rows_goal[sl].copy_(info["goal_row"])
-            net.forward(self.params, self._frames(self.rows_img[sl], self.rows_goal[sl]), E, self.acts, N, t * E,
-                        self.out[sl])
+            self._policy_step(t, self._frames(self.rows_img[sl], self.rows_goal[sl]))
             counter = (self.num_updates * T + t) & (2 ** 64 - 1)
             _lib.check(lib.vn_policy_sample(_lib.ptr(self.out[sl]), E, A, ctypes.c_uint64(vdist.rank_seed(self.seed, self.rank)),
                                             ctypes.c_uint64(counter), _lib.ptr(self.actions[sl]), None, None, None,
@@ -113,12 +181,15 @@ class A2CTrainer:
             env.step(self.actions[sl], out=dict(reward=self.rewards[t], done=self.dones[t], state=self.states),
                      gather=False)
             d = self.dones[t].to(torch.float32)
+            if self.recurrent:
+                self.prev_action.copy_(self.actions[sl])
+                self.prev_reward.copy_(self.rewards[t])
+                torch.sub(1.0, d, out=self.prev_mask)
             self.episode_stats[0] += d.sum()
             self.episode_stats[1] += (info["ep_return"] * d).sum()
             self.episode_stats[2] += (info["ep_length"].to(torch.float32) * d).sum()
         # bootstrap value of the final observation
-        net.forward(self.params, self._frames(info["img_row"], info["goal_row"]), E, self.boot_acts, E, 0,
-                    self.boot_out)
+        self._bootstrap(self._frames(info["img_row"], info["goal_row"]))
 
     def update(self):
         lib, net = self.lib, self.net
@@ -131,8 +202,17 @@ class A2CTrainer:
                                         ctypes.c_float(self.value_coefficient),
                                         ctypes.c_float(self.entropy_coefficient), _lib.ptr(self.dout),
                                         _lib.ptr(self.stats), st), "vn_a2c_loss_grad")
-        net.backward(self.params, self._frames(self.rows_img, self.rows_goal), N, self.acts, N, self.dout, self.grads,
-                     self.workspace)
+        if self.recurrent:
+            net.lstm_backward(self.params, T, E, self.dout, self.h_all, self.xcat, self.lstm_acts, self.c_all, self.c0,
+                              self.masks, net.x5(self.acts, N), self.dz5, self.grads, self.lstm_ws)
+            net.backward_trunk(self.params, self._frames(self.rows_img, self.rows_goal), N, self.acts, N, self.dz5,
+                               self.grads, self.workspace)
+            # (h, c) after the last step carry into the next rollout
+            self.h0.copy_(self.h_all[(T - 1) * E:])
+            self.c0.copy_(self.c_all[(T - 1) * E:])
+        else:
+            net.backward(self.params, self._frames(self.rows_img, self.rows_goal), N, self.acts, N, self.dout,
+                         self.grads, self.workspace)
         scale = vdist.allreduce_gradients_(self.grads, self.group)  # RCCL, one flat bucket
         P = net.n_params
         _lib.check(lib.vn_grad_norm(_lib.ptr(self.grads), P, ctypes.c_float(scale),
@@ -175,10 +255,16 @@ class A2CTrainer:
                 logger(metrics)
         return self
 
+    _RECURRENT_STATE = ("h0", "c0", "prev_action", "prev_reward", "prev_mask")
+
     def state_dict(self):
-        return {"params": self.params.detach().cpu(), "square_avg": self.square_avg.cpu(),
-                "env_state": self.env.get_state().cpu(), "num_updates": self.num_updates,
-                "total_steps": self.total_steps, "seed": self.seed}
+        sd = {"params": self.params.detach().cpu(), "square_avg": self.square_avg.cpu(),
+              "env_state": self.env.get_state().cpu(), "num_updates": self.num_updates,
+              "total_steps": self.total_steps, "seed": self.seed}
+        if self.recurrent:
+            for k in self._RECURRENT_STATE:
+                sd[k] = getattr(self, k).cpu()
+        return sd
 
     def load_state_dict(self, sd):
         self.params.copy_(sd["params"].to(self.device))
@@ -186,4 +272,7 @@ class A2CTrainer:
         self.env.set_state(sd["env_state"])
         self.num_updates = int(sd["num_updates"])
         self.total_steps = int(sd["total_steps"])
+        if self.recurrent:
+            for k in self._RECURRENT_STATE:
+                getattr(self, k).copy_(sd[k].to(self.device))
         self.env.observe(gather=False)

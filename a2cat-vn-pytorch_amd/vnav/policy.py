@@ -3,8 +3,11 @@
 GoalNavPolicy mirrors BigGoalHouseModel's interface (models/goal.py:15-92):
 ``forward(inputs, masks, states) -> [policy_logits, critic, states]`` and
 ``initial_states(batch)``, with the trunk + heads (goal.py:36-59) computed by the HIP
-kernels. The recurrent core (MaskedRNN/LSTM, goal.py:61-67) is outside this slice
-("next"): features feed the heads directly and ``states`` pass through.
+kernels. ``recurrent=True`` adds the recurrent core MaskedRNN(nn.LSTM(512 + A + 1, 512))
+(goal.py:61-67, 91-92): conv_merge features concatenated with the last (one-hot action,
+reward) feed the LSTM, whose output feeds the heads, and ``states`` = (h, c) [B,1,512]
+are carried; masks [B,T] zero the carried state where an episode starts. Without it the
+features feed the heads directly and ``states`` pass through (the feed-forward slice).
 
 All parameters live in ONE flat fp32 device buffer (layout in include/vnav.h), so the
 optimizer, the gradient norm and the RCCL all-reduce each touch one contiguous tensor.
@@ -60,15 +63,16 @@ def trunk_sizes(h, w):
 class PolicyNet:
     """Handle on a vn_policy: flat parameter layout, forward/backward launches."""
 
-    def __init__(self, frame_hw=(84, 84), num_actions=4, device=None):
+    def __init__(self, frame_hw=(84, 84), num_actions=4, device=None, recurrent=False):
         self.lib = _lib.load()
+        self.recurrent = bool(recurrent)
         self.frame_hw = tuple(frame_hw)
         self.num_actions = int(num_actions)
         self.device = torch.device("cuda", torch.cuda.current_device() if device is None else
                                    torch.device(device).index or 0)
         h = ctypes.c_void_p()
-        _lib.check(self.lib.vn_policy_create(frame_hw[0], frame_hw[1], num_actions, ctypes.byref(h)),
-                   "vn_policy_create")
+        _lib.check(self.lib.vn_policy_create_ex(frame_hw[0], frame_hw[1], num_actions, 1 if recurrent else 0,
+                                                ctypes.byref(h)), "vn_policy_create_ex")
         self._h = h
         n, a = ctypes.c_int64(), ctypes.c_int64()
         lay = (ctypes.c_int64 * 12)()
@@ -80,6 +84,12 @@ class PolicyNet:
         self.fc_in = 32 * o3[0] * o3[1]
         self.shapes = {"conv1": (32, 148), "conv2": (32, 512), "conv3": (64, 1024), "conv4": (32, 64),
                        "fc": (512, self.fc_in), "head": (num_actions + 1, 512)}
+        self.lstm = None
+        if self.recurrent:
+            info = (ctypes.c_int64 * 8)()
+            _lib.check(self.lib.vn_policy_lstm_info(h, info), "vn_policy_lstm_info")
+            self.lstm = dict(w=info[0], bih=info[1], bhh=info[2], xcat=info[3], xoff=info[4], lin=info[5],
+                             hidden=info[6])
 
     def __del__(self):
         try:
@@ -97,6 +107,10 @@ class PolicyNet:
             w, b = self.offsets[name]
             co, k = self.shapes[name]
             out[name] = (flat[w:w + co * k].view(co, k), flat[b:b + co])
+        if self.lstm:
+            L = self.lstm
+            out["lstm"] = (flat[L["w"]:L["w"] + 2048 * L["xcat"]].view(2048, L["xcat"]),
+                           flat[L["bih"]:L["bih"] + 2048], flat[L["bhh"]:L["bhh"] + 2048])
         return out
 
     def new_params(self):
@@ -113,6 +127,15 @@ class PolicyNet:
             d = 1.0 / math.sqrt(fan_in[name])
             k = 147 if name == "conv1" else w.shape[1]
             w[:, :k].uniform_(-d, d, generator=g)
+        if self.lstm:  # goal.py:17-24: xavier_uniform W_ih, orthogonal W_hh, zero biases
+            L = self.lstm
+            wcat, _, _ = v["lstm"]
+            wih = torch.empty(2048, L["lin"])
+            torch.nn.init.xavier_uniform_(wih, generator=g)
+            whh = torch.empty(2048, 512)
+            torch.nn.init.orthogonal_(whh, generator=g)
+            wcat[:, :L["lin"]] = wih
+            wcat[:, L["xoff"]:] = whh
         return flat.to(self.device)
 
     def from_reference(self, sd):
@@ -143,6 +166,13 @@ class PolicyNet:
         b[:A] = t(pick("policy_logits", 0, "bias"))
         w[A] = t(pick("critic", 0, "weight")).view(-1)
         b[A] = t(pick("critic", 0, "bias")).view(())
+        if self.lstm:
+            L = self.lstm
+            wcat, bih, bhh = v["lstm"]
+            wcat[:, :L["lin"]] = t(_lstm_param(sd, "weight_ih_l0"))
+            wcat[:, L["xoff"]:] = t(_lstm_param(sd, "weight_hh_l0"))
+            bih[:] = t(_lstm_param(sd, "bias_ih_l0"))
+            bhh[:] = t(_lstm_param(sd, "bias_hh_l0"))
         return flat.to(self.device)
 
     def to_reference(self, flat):
@@ -171,6 +201,13 @@ class PolicyNet:
         out["policy_logits.0.bias"] = b[:A].clone()
         out["critic.0.weight"] = w[A:A + 1].clone()
         out["critic.0.bias"] = b[A:A + 1].clone()
+        if self.lstm:
+            L = self.lstm
+            wcat, bih, bhh = v["lstm"]
+            out["rnn.inner.weight_ih_l0"] = wcat[:, :L["lin"]].clone()
+            out["rnn.inner.weight_hh_l0"] = wcat[:, L["xoff"]:].clone()
+            out["rnn.inner.bias_ih_l0"] = bih.clone()
+            out["rnn.inner.bias_hh_l0"] = bhh.clone()
         return out
 
     # -- launches -------------------------------------------------------------------
@@ -182,7 +219,13 @@ class PolicyNet:
     def new_acts(self, capacity):
         return torch.empty(int(capacity) * self.act_floats, dtype=torch.float32, device=self.device)
 
+    def x5(self, acts, capacity):
+        """[capacity, 512] view of the conv_merge features in an activation store."""
+        c = int(capacity)
+        return acts[c * (self.act_floats - 512):c * self.act_floats].view(c, 512)
+
     def forward(self, params, frames, n, acts, capacity, offset, out):
+        """out=None (recurrent nets only): trunk only, features kept in acts."""
         _lib.check(self.lib.vn_policy_forward(self._h, _lib.ptr(params), ctypes.byref(frames), int(n), _lib.ptr(acts),
                                               int(capacity), int(offset), _lib.ptr(out),
                                               _lib.stream_ptr(self.device)), "vn_policy_forward")
@@ -191,6 +234,44 @@ class PolicyNet:
         _lib.check(self.lib.vn_policy_backward(self._h, _lib.ptr(params), ctypes.byref(frames), int(n), _lib.ptr(acts),
                                                int(capacity), _lib.ptr(dout), _lib.ptr(grads), _lib.ptr(workspace),
                                                _lib.stream_ptr(self.device)), "vn_policy_backward")
+
+    def backward_trunk(self, params, frames, n, acts, capacity, dz5, grads, workspace):
+        _lib.check(self.lib.vn_policy_backward_trunk(self._h, _lib.ptr(params), ctypes.byref(frames), int(n),
+                                                     _lib.ptr(acts), int(capacity), _lib.ptr(dz5), _lib.ptr(grads),
+                                                     _lib.ptr(workspace), _lib.stream_ptr(self.device)),
+                   "vn_policy_backward_trunk")
+
+    # -- recurrent core -------------------------------------------------------------
+    def lstm_workspace_floats(self, T, E):
+        f = ctypes.c_int64()
+        _lib.check(self.lib.vn_lstm_workspace_floats(self._h, int(T), int(E), ctypes.byref(f)),
+                   "vn_lstm_workspace_floats")
+        return f.value
+
+    def lstm_step(self, params, E, x5, lra, mask, h_prev, c_prev, xcat, gates, acts, c_out, h_out):
+        P = _lib.ptr
+        _lib.check(self.lib.vn_lstm_forward_step(self._h, P(params), int(E), P(x5), P(lra), P(mask), P(h_prev),
+                                                 P(c_prev), P(xcat), P(gates), P(acts), P(c_out), P(h_out),
+                                                 _lib.stream_ptr(self.device)), "vn_lstm_forward_step")
+
+    def heads(self, params, feat, n, out):
+        _lib.check(self.lib.vn_policy_heads(self._h, _lib.ptr(params), _lib.ptr(feat), int(n), _lib.ptr(out),
+                                            _lib.stream_ptr(self.device)), "vn_policy_heads")
+
+    def lstm_backward(self, params, T, E, dout, h_all, xcat_all, acts_all, c_all, c_init, mask_all, x5_all, dz5_all,
+                      grads, workspace):
+        P = _lib.ptr
+        _lib.check(self.lib.vn_lstm_backward(self._h, P(params), int(T), int(E), P(dout), P(h_all), P(xcat_all),
+                                             P(acts_all), P(c_all), P(c_init), P(mask_all), P(x5_all), P(dz5_all),
+                                             P(grads), P(workspace), _lib.stream_ptr(self.device)),
+                   "vn_lstm_backward")
+
+
+def _lstm_param(sd, suffix):
+    keys = [k for k in sd if k.endswith(suffix)]
+    if len(keys) != 1:
+        raise KeyError("expected one LSTM parameter *%s in the state dict, found %s" % (suffix, keys))
+    return sd[keys[0]]
 
 
 class _ReferenceNames:
@@ -239,14 +320,64 @@ class _GoalNavFunction(torch.autograd.Function):
         return grads, None, None, None
 
 
+class _RecurrentGoalNavFunction(torch.autograd.Function):
+    """Trunk over all T*B samples (time-major rows t*B + b), LSTM steps, heads on h.
+    Gradients reach the parameters only: BPTT stops at the states entering the sequence
+    (and lra / masks are inputs), as in a truncated-BPTT rollout."""
+
+    @staticmethod
+    def forward(ctx, params, image, goal, lra, masks, h0, c0, net, T, B):
+        n = T * B
+        dev = params.device
+        acts = net.new_acts(n)
+        frames = frames_from_batch(image, goal)
+        net.forward(params, frames, n, acts, n, 0, None)
+        x5 = net.x5(acts, n)
+        L = net.lstm
+        xcat = torch.empty((n, L["xcat"]), dtype=torch.float32, device=dev)
+        gates = torch.empty((B, 2048), dtype=torch.float32, device=dev)
+        la = torch.empty((n, 2048), dtype=torch.float32, device=dev)
+        c_all = torch.empty((n, 512), dtype=torch.float32, device=dev)
+        h_all = torch.empty((n, 512), dtype=torch.float32, device=dev)
+        hp, cp = h0, c0
+        for t in range(T):
+            sl = slice(t * B, (t + 1) * B)
+            net.lstm_step(params, B, x5[sl], lra[sl], masks[t], hp, cp, xcat[sl], gates, la[sl], c_all[sl], h_all[sl])
+            hp, cp = h_all[sl], c_all[sl]
+        out = torch.empty((n, OUT_LD), dtype=torch.float32, device=dev)
+        net.heads(params, h_all, n, out)
+        ctx.save_for_backward(params, image, goal, acts, xcat, la, c_all, h_all, c0, masks)
+        ctx.net, ctx.T, ctx.B = net, T, B
+        hT, cT = h_all[(T - 1) * B:].clone(), c_all[(T - 1) * B:].clone()
+        ctx.mark_non_differentiable(hT, cT)
+        return out[:, : net.num_actions + 1], hT, cT
+
+    @staticmethod
+    def backward(ctx, dout, _dh, _dc):
+        params, image, goal, acts, xcat, la, c_all, h_all, c0, masks = ctx.saved_tensors
+        net, T, B = ctx.net, ctx.T, ctx.B
+        n = T * B
+        dev = params.device
+        d = torch.zeros((n, OUT_LD), dtype=torch.float32, device=dev)
+        d[:, : net.num_actions + 1] = dout
+        grads = torch.zeros_like(params)
+        dz5 = torch.empty((n, 512), dtype=torch.float32, device=dev)
+        ws = torch.empty(net.lstm_workspace_floats(T, B), dtype=torch.float32, device=dev)
+        net.lstm_backward(params, T, B, d, h_all, xcat, la, c_all, c0, masks, net.x5(acts, n), dz5, grads, ws)
+        del ws
+        ws = torch.empty(net.workspace_floats(n), dtype=torch.float32, device=dev)
+        net.backward_trunk(params, frames_from_batch(image, goal), n, acts, n, dz5, grads, ws)
+        return (grads,) + (None,) * 9
+
+
 class GoalNavPolicy(torch.nn.Module):
     """Drop-in for BigGoalHouseModel's trunk + heads (see module docstring)."""
 
-    def __init__(self, num_inputs=3, num_outputs=4, frame_hw=(84, 84), device=None, seed=0):
+    def __init__(self, num_inputs=3, num_outputs=4, frame_hw=(84, 84), device=None, seed=0, recurrent=False):
         super().__init__()
         if num_inputs != 3:
             raise ValueError("frames are RGB (num_inputs=3)")
-        self.net = PolicyNet(frame_hw, num_outputs, device)
+        self.net = PolicyNet(frame_hw, num_outputs, device, recurrent=recurrent)
         self.params = torch.nn.Parameter(self.net.init_params(seed))
         self.lstm_layers, self.lstm_hidden_size = 1, 512  # goal.py:61-62 (state shape contract)
 
@@ -266,6 +397,8 @@ class GoalNavPolicy(torch.nn.Module):
         observations, _last_reward_action = inputs if isinstance(inputs, tuple) and len(inputs) == 2 and \
             isinstance(inputs[0], (tuple, list)) else (inputs, None)
         image, goal = observations[0], observations[1]
+        if self.net.recurrent:
+            return self._forward_recurrent(image, goal, _last_reward_action, masks, states)
         lead = image.shape[:2]
         if image.dtype == torch.uint8:   # env frames [B,T,H,W,3]
             img = image.reshape(-1, *image.shape[2:]).contiguous()
@@ -276,3 +409,32 @@ class GoalNavPolicy(torch.nn.Module):
         out = _GoalNavFunction.apply(self.params, img, gl, self.net)
         A = self.net.num_actions
         return [out[:, :A].reshape(*lead, A), out[:, A:A + 1].reshape(*lead, 1), states]
+
+    def _forward_recurrent(self, image, goal, lra, masks, states):
+        """goal.py:84-92 with the recurrent core: inputs [B,T,...] batch-first."""
+        B, T = image.shape[:2]
+        dev = self.params.device
+        A = self.net.num_actions
+
+        def time_major(x, dtype=None):
+            x = x.to(dev).transpose(0, 1)
+            return x.reshape(T * B, *x.shape[2:]).to(dtype or x.dtype).contiguous()
+
+        if image.dtype == torch.uint8:
+            img, gl = time_major(image), time_major(goal)
+        else:
+            img, gl = time_major(image, torch.float32), time_major(goal, torch.float32)
+        if lra is None:
+            lra = torch.zeros((B, T, A + 1), dtype=torch.float32, device=dev)
+        if lra.shape[-1] != A + 1:
+            raise ValueError("last_reward_action must be [B,T,%d]" % (A + 1))
+        lr = time_major(lra, torch.float32)
+        m = torch.ones((B, T), dtype=torch.float32, device=dev) if masks is None else masks
+        m = m.to(dev).reshape(B, T).to(torch.float32).t().contiguous()
+        if states is None:
+            states = self.initial_states(B)
+        h0 = states[0].to(dev, torch.float32).reshape(B, 512).contiguous()
+        c0 = states[1].to(dev, torch.float32).reshape(B, 512).contiguous()
+        out, hT, cT = _RecurrentGoalNavFunction.apply(self.params, img, gl, lr, m, h0, c0, self.net, T, B)
+        out = out.view(T, B, A + 1).transpose(0, 1)
+        return [out[..., :A], out[..., A:A + 1], (hT.view(B, 1, 512), cT.view(B, 1, 512))]

@@ -48,6 +48,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--train-steps", type=int, default=6, help="timed A2C updates (0 = skip the train leg)")
     p.add_argument("--train-warmup", type=int, default=2)
+    p.add_argument("--no-train-ff", action="store_true", help="skip the feed-forward (no LSTM) train leg")
     p.add_argument("--num-steps", type=int, default=20, help="A2C rollout length (reference: 20)")
     p.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
     p.add_argument("--dist-backend", default="nccl", help="torch.distributed backend (nccl = RCCL on ROCm)")
@@ -99,7 +100,7 @@ def pmc_traffic(envs, scenes):
                                        "source": "live rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes"}
 
 
-def train_flops_per_env_step(h=84, w=84, A=4, T=20):
+def train_flops_per_env_step(h=84, w=84, A=4, T=20, recurrent=False):
     """Algorithmic FLOPs of one A2C env-step: policy forward (kept activations serve the
     backward), weight gradients of every layer, input gradients of all but conv1, and the
     bootstrap forward amortised over the rollout."""
@@ -108,18 +109,21 @@ def train_flops_per_env_step(h=84, w=84, A=4, T=20):
     o3 = ((o2[0] - 4) // 2 + 1, (o2[1] - 4) // 2 + 1)
     p1, p2, p3 = o1[0] * o1[1], o2[0] * o2[1], o3[0] * o3[1]
     macs = [2 * p1 * 32 * 147, 2 * p2 * 32 * 512, p3 * 64 * 1024, p3 * 32 * 64, 512 * 32 * p3, (A + 1) * 512]
+    if recurrent:  # LSTM gates GEMM [xcat=512+A+1 padded to 4, +512] x 2048: fwd, dgrad, wgrad
+        macs.append(2048 * ((512 + A + 1 + 3) // 4 * 4 + 512))
     fwd = 2 * sum(macs)
     return fwd + fwd + 2 * sum(macs[1:]) + fwd / T, fwd
 
 
-def bench_train(args, scenes, dev, world, rank):
+def bench_train(args, scenes, dev, world, rank, recurrent):
     """A2C training throughput: one step = rollout of num_steps on every local env (policy
     forward + sampling + env step) + backward + one RCCL all-reduce of the flat gradient +
-    clip + RMSprop."""
+    clip + RMSprop. recurrent: the full BigGoalHouseModel (LSTM core, BPTT over the rollout);
+    else the feed-forward trunk + heads."""
     import vnav
     E, T = args.envs, args.num_steps
     env = vnav.VectorEnv(scenes, E, seed=2000 + rank, device=dev)
-    tr = vnav.A2CTrainer(env, num_steps=T, seed=7, max_time_steps=1e12)
+    tr = vnav.A2CTrainer(env, num_steps=T, seed=7, max_time_steps=1e12, recurrent=recurrent)
     for _ in range(args.train_warmup):
         tr.step(sync=False)
     torch.cuda.synchronize(dev)
@@ -137,9 +141,10 @@ def bench_train(args, scenes, dev, world, rank):
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         el = float(t[0])
     steps = E * T * args.train_steps * world
-    flops, fwd = train_flops_per_env_step(T=T)
+    flops, fwd = train_flops_per_env_step(T=T, recurrent=recurrent)
     tflops = E * T * args.train_steps * flops / el / 1e12
-    res = {"value": steps / el, "unit": "env-steps/s", "updates": args.train_steps, "envs_per_gpu": E,
+    res = {"model": "BigGoalHouseModel (LSTM core)" if recurrent else "BigGoalHouseModel trunk + heads (no LSTM)",
+           "value": steps / el, "unit": "env-steps/s", "updates": args.train_steps, "envs_per_gpu": E,
            "num_steps": T, "ms_per_update": el / args.train_steps * 1e3, "dtype": "f32",
            "roofline": {"bound": "mfma", "achieved": tflops, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                         "frac": tflops / FP32_MFMA_PEAK_TFLOPS, "flops_per_env_step": flops,
@@ -263,10 +268,13 @@ def main():
         elapsed, kern_ms = float(t[0]), float(t[1])
     flags = env.error_flags()
     del env, out
-    train = None
+    train = train_ff = None
     if args.train_steps > 0:
         torch.cuda.empty_cache()
-        train = bench_train(args, scenes, dev, world, rank)
+        train = bench_train(args, scenes, dev, world, rank, recurrent=True)
+        torch.cuda.empty_cache()
+        if not args.no_train_ff:
+            train_ff = bench_train(args, scenes, dev, world, rank, recurrent=False)
     if rank == 0:
         env_steps = E * K * world
         value = env_steps / elapsed
@@ -300,6 +308,7 @@ def main():
                          "bytes_per_launch": bpe * E, "kernel_ms": kern_ms},
             "cpu_baseline": cpu,
             "train": train,
+            "train_feedforward": train_ff,
             "error_flags": flags,
         }
         print(json.dumps(line))

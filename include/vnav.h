@@ -180,7 +180,8 @@ int vn_policy_create(int frame_h, int frame_w, int num_actions, vn_policy** out)
 int vn_policy_destroy(vn_policy* p);
 int vn_policy_info(vn_policy* p, int64_t* n_params, int64_t* act_floats_per_sample, int64_t* layout12);
 int vn_policy_workspace_floats(vn_policy* p, int64_t n_samples, int64_t* floats);
-/* out [n][8]: logits in 0..A-1, value at A. Activations of the n samples are kept at
+/* out [n][8]: logits in 0..A-1, value at A (out may be NULL for a VN_POLICY_LSTM policy:
+ * trunk only, features kept in the activation store). Activations of the n samples are kept at
  * sample offset act_offset of an activation store holding act_capacity samples. */
 int vn_policy_forward(vn_policy* p, const float* params, const vn_frames* frames, int n, float* acts,
                       int64_t act_capacity, int64_t act_offset, float* out, vn_stream_t stream);
@@ -189,6 +190,37 @@ int vn_policy_forward(vn_policy* p, const float* params, const vn_frames* frames
 int vn_policy_backward(vn_policy* p, const float* params, const vn_frames* frames, int n, float* acts,
                        int64_t act_capacity, const float* dout, float* grads, float* workspace,
                        vn_stream_t stream);
+
+/* ---- recurrent core: MaskedRNN(nn.LSTM(512 + A + 1, 512)) (models/goal.py:61-67, 91-92) ----
+ * A policy created with VN_POLICY_LSTM appends W_cat [2048][xcat] = [W_ih | 0 pad | W_hh]
+ * (torch gate order i, f, g, o), b_ih [2048], b_hh [2048] to the flat parameters; its heads
+ * read h_t instead of the conv_merge features. info8 = (W_cat, b_ih, b_hh offsets, xcat,
+ * xoff = column of h in W_cat, lin = 512 + A + 1, hidden 512, 0).
+ * Step t of a batch of E: x5 [E][512] conv_merge features (the trunk activations stored
+ * by vn_policy_forward with out == NULL), lra [E][A+1] (one-hot last action, last reward;
+ * NULL = zeros), mask [E] (0 resets the carried state: m * h_prev, m * c_prev; NULL = 1),
+ * h_prev/c_prev [E][512] (NULL = zeros). Writes xcat [E][xcat], gates scratch [E][2048],
+ * acts [E][2048] (i, f, g, o), c_out, h_out [E][512] — keep xcat/acts/c/h of every step of a
+ * rollout (rows t*E + e) for vn_lstm_backward. */
+#define VN_POLICY_LSTM 1
+int vn_policy_create_ex(int frame_h, int frame_w, int num_actions, int flags, vn_policy** out);
+int vn_policy_lstm_info(vn_policy* p, int64_t* info8);
+int vn_lstm_forward_step(vn_policy* p, const float* params, int E, const float* x5, const float* lra,
+                         const float* mask, const float* h_prev, const float* c_prev, float* xcat, float* gates,
+                         float* acts, float* c_out, float* h_out, vn_stream_t stream);
+/* Heads on n feature rows [n][512] -> out [n][8]. */
+int vn_policy_heads(vn_policy* p, const float* params, const float* feat, int n, float* out, vn_stream_t stream);
+int vn_lstm_workspace_floats(vn_policy* p, int T, int E, int64_t* floats);
+/* BPTT within one rollout (the state entering it is a constant): writes the head and LSTM
+ * gradients into grads and dL/d(conv_merge pre-activation) [T*E][512] into dz5_all. */
+int vn_lstm_backward(vn_policy* p, const float* params, int T, int E, const float* dout, const float* h_all,
+                     const float* xcat_all, const float* acts_all, const float* c_all, const float* c_init,
+                     const float* mask_all, const float* x5_all, float* dz5_all, float* grads, float* workspace,
+                     vn_stream_t stream);
+/* Trunk gradients (conv1..conv_merge) of the n stored samples from dz5 [n][512]. */
+int vn_policy_backward_trunk(vn_policy* p, const float* params, const vn_frames* frames, int n, float* acts,
+                             int64_t act_capacity, const float* dz5, float* grads, float* workspace,
+                             vn_stream_t stream);
 
 /* ---- A2C (the deep_rl trainer contract; DESIGN.md "A2C contract") ---- */
 int vn_policy_sample(const float* out, int n, int num_actions, uint64_t seed, uint64_t counter,

@@ -55,6 +55,41 @@ class GoalNetOracle(nn.Module):
         return self
 
 
+class RecurrentGoalNetOracle(GoalNetOracle):
+    """BigGoalHouseModel with its recurrent core: features ++ last_reward_action feed
+    MaskedRNN(nn.LSTM(512 + A + 1, 512, batch_first=True)) (goal.py:61-67, 84-92) and the
+    heads read the LSTM output. The LSTM cell is torch's own nn.LSTM (the reference's
+    inner module). MaskedRNN lives in the absent deep-rl 0.2.9; restated here as: before
+    step t, (h, c) *= masks[:, t] (0 where an episode starts) — parity unpinned for that
+    convention (DESIGN.md)."""
+
+    def __init__(self, frame_hw=(84, 84), num_inputs=3, num_outputs=4):
+        super().__init__(frame_hw, num_inputs, num_outputs)
+        self.lstm = nn.LSTM(512 + num_outputs + 1, 512, num_layers=1, batch_first=True)
+
+    def forward_seq(self, image, goal, last_reward_action, masks, states):
+        """image, goal float [B,T,3,H,W]; last_reward_action [B,T,A+1]; masks [B,T];
+        states (h, c) [B,1,512] -> (logits [B,T,A], value [B,T,1], (h, c))."""
+        B, T = image.shape[:2]
+        f = self.features(image.flatten(0, 1), goal.flatten(0, 1)).view(B, T, 512)
+        x = torch.cat((f, last_reward_action), 2)
+        h, c = states[0].transpose(0, 1), states[1].transpose(0, 1)
+        outs = []
+        for t in range(T):
+            m = masks[:, t].reshape(1, B, 1)
+            o, (h, c) = self.lstm(x[:, t:t + 1], (h * m, c * m))
+            outs.append(o)
+        y = torch.cat(outs, 1)
+        return self.policy_logits(y), self.critic(y), (h.transpose(0, 1), c.transpose(0, 1))
+
+    def load_reference(self, sd):
+        super().load_reference(sd)
+        for name in ("weight_ih_l0", "weight_hh_l0", "bias_ih_l0", "bias_hh_l0"):
+            keys = [k for k in sd if k.endswith(name)]
+            getattr(self.lstm, name).data.copy_(torch.as_tensor(sd[keys[0]]))
+        return self
+
+
 def frames_to_float(u8):
     """uint8 [...,H,W,C] -> float32 [...,C,H,W] / 255 (TransposeImage + ScaledFloatFrame)."""
     x = torch.as_tensor(u8)

@@ -35,3 +35,27 @@ def test_ctypes_signatures_cover_header(built_lib):
     # error path without a device: NULL ctx is rejected with a message
     assert lib.vn_step(None, None, None, None, None, None, None, None) != 0
     assert "NULL" in _lib.last_error()
+
+
+def test_recurrent_policy_layout(built_lib):
+    """VN_POLICY_LSTM appends W_cat [2048][xcat] (W_ih | pad | W_hh), b_ih, b_hh to the flat
+    parameters (host-side layout only: no device call)."""
+    from vnav import _lib
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    n, a = ctypes.c_int64(), ctypes.c_int64()
+    assert lib.vn_policy_create_ex(84, 84, 4, 0, ctypes.byref(h)) == 0
+    assert lib.vn_policy_info(h, ctypes.byref(n), ctypes.byref(a), None) == 0
+    base = n.value
+    assert base == 239397
+    assert lib.vn_policy_lstm_info(h, (ctypes.c_int64 * 8)()) != 0  # feed-forward policy has no core
+    lib.vn_policy_destroy(h)
+    assert lib.vn_policy_create_ex(84, 84, 4, 1, ctypes.byref(h)) == 0
+    info = (ctypes.c_int64 * 8)()
+    assert lib.vn_policy_lstm_info(h, info) == 0
+    lin, xoff, xcat = 512 + 4 + 1, 520, 1032
+    assert list(info) == [base, base + 2048 * xcat, base + 2048 * xcat + 2048, xcat, xoff, lin, 512, 0]
+    assert lib.vn_policy_info(h, ctypes.byref(n), None, None) == 0
+    assert n.value == base + 2048 * xcat + 4096
+    lib.vn_policy_destroy(h)
+    assert lib.vn_policy_create_ex(84, 84, 4, 2, ctypes.byref(h)) != 0

@@ -1,0 +1,196 @@
+"""Recurrent core (MaskedRNN(nn.LSTM(512 + A + 1, 512)), models/goal.py:61-67, 84-92) on the
+HIP kernels vs torch's nn.LSTM in the CPU oracle (oracle/policy.py RecurrentGoalNetOracle).
+Tolerances as test_policy_gpu.py: outputs/states rtol 1e-5 of scale, parameter gradients
+rtol 1e-4 of each tensor's scale. The state-masking convention is the restated MaskedRNN
+(parity unpinned)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import a2c as oa2c
+from oracle.frames import synth_frames
+from oracle.policy import RecurrentGoalNetOracle, frames_to_float
+
+pytestmark = pytest.mark.gpu
+
+LSTM_KEYS = ("weight_ih_l0", "weight_hh_l0", "bias_ih_l0", "bias_hh_l0")
+TRUNK = {"shared_base.0.0": "conv1", "shared_base.0.2": "conv2", "conv_base.0.0": "conv3",
+         "conv_base.0.2": "conv4", "conv_merge.0.1": "fc", "policy_logits.0": "policy_logits", "critic.0": "critic"}
+
+
+def _close(a, b, rtol, what):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    scale = max(np.abs(b).max(), 1e-30)
+    err = np.abs(a - b).max() / scale
+    assert err <= rtol, "%s: max err %.3g of scale %.3g" % (what, err, scale)
+
+
+def _perturbed_policy(seed=0):
+    from vnav.policy import GoalNavPolicy
+    torch.manual_seed(seed)
+    pol = GoalNavPolicy(3, 4, (84, 84), recurrent=True)
+    with torch.no_grad():
+        pol.params.add_(torch.randn_like(pol.params) * 0.01)
+        L = pol.net.lstm
+        wcat = pol.params[L["w"]:L["w"] + 2048 * L["xcat"]].view(2048, L["xcat"])
+        wcat[:, L["lin"]:L["xoff"]] = 0.0  # the pad columns are not parameters
+    return pol
+
+
+def _grad_check(pol, ref, what):
+    mine = pol.net.to_reference(pol.params.grad)
+    for k, attr in TRUNK.items():
+        mod = getattr(ref, attr)
+        _close(mine[k + ".weight"].numpy(), mod.weight.grad.numpy(), 1e-4, what + k + ".weight")
+        _close(mine[k + ".bias"].numpy(), mod.bias.grad.numpy(), 1e-4, what + k + ".bias")
+    for k in LSTM_KEYS:
+        _close(mine["rnn.inner." + k].numpy(), getattr(ref.lstm, k).grad.numpy(), 1e-4, what + k)
+
+
+def test_recurrent_policy_forward_backward_vs_torch_lstm():
+    pol = _perturbed_policy(0)
+    ref = RecurrentGoalNetOracle((84, 84)).load_reference(pol.reference_state_dict())
+    B, T, A = 5, 6, 4
+    rng = np.random.RandomState(2)
+    img = torch.as_tensor(rng.randint(0, 256, size=(B, T, 84, 84, 3)).astype(np.uint8))
+    gl = torch.as_tensor(rng.randint(0, 256, size=(B, T, 84, 84, 3)).astype(np.uint8))
+    lra = torch.zeros(B, T, A + 1)
+    lra[torch.arange(B)[:, None], torch.arange(T)[None, :], torch.as_tensor(rng.randint(0, A, size=(B, T)))] = 1.0
+    lra[..., A] = torch.as_tensor(rng.randn(B, T).astype(np.float32))
+    masks = torch.as_tensor((rng.rand(B, T) > 0.3).astype(np.float32))
+    masks[:, 0] = torch.tensor([0.0, 1.0, 1.0, 0.0, 1.0])
+    h0 = torch.as_tensor(rng.randn(B, 1, 512).astype(np.float32)) * 0.5
+    c0 = torch.as_tensor(rng.randn(B, 1, 512).astype(np.float32)) * 0.5
+
+    logits, value, (hT, cT) = pol(((img.cuda(), gl.cuda()), lra.cuda()), masks.cuda(), (h0.cuda(), c0.cuda()))
+    rl, rv, (rh, rc) = ref.forward_seq(frames_to_float(img), frames_to_float(gl), lra, masks, (h0, c0))
+    _close(logits.detach().cpu(), rl.detach(), 1e-5, "logits")
+    _close(value.detach().cpu(), rv.detach(), 1e-5, "value")
+    _close(hT.cpu(), rh.detach(), 1e-5, "h_T")
+    _close(cT.cpu(), rc.detach(), 1e-5, "c_T")
+
+    actions = torch.as_tensor(rng.randint(0, A, size=B * T))
+    rets = torch.as_tensor(rng.randn(B * T).astype(np.float32))
+    loss, _ = oa2c.loss(logits.reshape(-1, A), value.reshape(-1), actions.cuda(), rets.cuda())
+    loss.backward()
+    rloss, _ = oa2c.loss(rl.reshape(-1, A), rv.reshape(-1), actions, rets)
+    rloss.backward()
+    np.testing.assert_allclose(loss.item(), rloss.item(), rtol=1e-5)
+    _grad_check(pol, ref, "")
+
+
+def test_recurrent_policy_float_input_and_defaults():
+    """Float CHW frames give the u8 results; masks/states/lra default to ones/zeros/zeros."""
+    pol = _perturbed_policy(1)
+    B, T = 3, 4
+    rng = np.random.RandomState(3)
+    img = torch.as_tensor(rng.randint(0, 256, size=(B, T, 84, 84, 3)).astype(np.uint8))
+    gl = torch.as_tensor(rng.randint(0, 256, size=(B, T, 84, 84, 3)).astype(np.uint8))
+    with torch.no_grad():
+        l1, v1, s1 = pol(((img.cuda(), gl.cuda()), None), None, None)
+        l2, v2, s2 = pol(((frames_to_float(img).cuda(), frames_to_float(gl).cuda()),
+                          torch.zeros(B, T, 5).cuda()), torch.ones(B, T).cuda(), pol.initial_states(B))
+    _close(l2.cpu(), l1.cpu(), 1e-5, "logits")
+    _close(v2.cpu(), v1.cpu(), 1e-5, "value")
+    _close(s2[0].cpu(), s1[0].cpu(), 1e-5, "h")
+
+
+def _small_env(n_envs=12, seed=21):
+    import vnav
+    sc = [vnav.synthetic_scene(k) for k in range(2)]
+    for s in sc:
+        s.observations = synth_frames(s.synth_id, np.arange(s.n_states), s.frame_shape)
+    env = vnav.VectorEnv(sc, n_envs, seed=seed, max_episode_steps=6)
+    return env, np.concatenate([s.observations for s in sc])
+
+
+def test_recurrent_trainer_update_matches_cpu_oracle():
+    """Two rollouts + updates of the recurrent A2CTrainer; the second (carried state, masks
+    from episode ends, last action/reward inputs) is restated on the torch oracle."""
+    import vnav
+    env, arena = _small_env()
+    T, E, A = 5, 12, 4
+    tr = vnav.A2CTrainer(env, num_steps=T, seed=3, max_time_steps=1e6, recurrent=True)
+    tr.step(sync=True)
+    p0 = tr.params.detach().clone()
+    sq0 = tr.square_avg.detach().clone()
+    h0 = tr.h0.cpu().clone()
+    c0 = tr.c0.cpu().clone()
+    prev_a, prev_r, prev_m = tr.prev_action.cpu().clone(), tr.prev_reward.cpu().clone(), tr.prev_mask.cpu().clone()
+    tr.rollout()
+    rows_img, rows_goal = tr.rows_img.cpu().numpy(), tr.rows_goal.cpu().numpy()
+    actions = tr.actions.cpu().long()
+    rewards, dones = tr.rewards.cpu(), tr.dones.cpu()
+    boot_rows = (env._info["img_row"].cpu().numpy(), env._info["goal_row"].cpu().numpy())
+    out_gpu = tr.out.cpu()
+    boot_gpu = tr.boot_out.cpu()
+    lr = tr.current_lr()
+    tr.update()
+    torch.cuda.synchronize()
+
+    # masks / last reward-action the trainer should have fed, rebuilt from the rollout
+    masks = torch.empty(T + 1, E)
+    lra = torch.zeros(T + 1, E, A + 1)
+    a_prev, r_prev, m = prev_a, prev_r, prev_m
+    for t in range(T + 1):
+        masks[t] = m
+        lra[t, torch.arange(E), a_prev] = 1.0
+        lra[t, :, A] = r_prev
+        lra[t] *= m[:, None]
+        if t < T:
+            a_prev, r_prev = actions[t * E:(t + 1) * E], rewards[t]
+            m = 1.0 - dones[t].float()
+    np.testing.assert_array_equal(tr.masks.cpu().numpy(), masks[:T].numpy())
+
+    ref = RecurrentGoalNetOracle((84, 84)).load_reference(tr.net.to_reference(p0))
+    img = np.concatenate([arena[rows_img].reshape(T, E, 84, 84, 3), arena[boot_rows[0]][None]]).transpose(1, 0, 2, 3, 4)
+    gl = np.concatenate([arena[rows_goal].reshape(T, E, 84, 84, 3), arena[boot_rows[1]][None]]).transpose(1, 0, 2, 3, 4)
+    logits, value, _ = ref.forward_seq(frames_to_float(img), frames_to_float(gl), lra.transpose(0, 1),
+                                       masks.t(), (h0[:, None], c0[:, None]))
+    lt = logits.transpose(0, 1)  # [T+1, E, A]
+    vt = value.transpose(0, 1)[..., 0]
+    _close(out_gpu[:, :A].numpy(), lt[:T].reshape(-1, A).detach().numpy(), 1e-5, "rollout logits")
+    _close(out_gpu[:, A].numpy(), vt[:T].reshape(-1).detach().numpy(), 1e-5, "rollout values")
+    _close(boot_gpu[:, A].numpy(), vt[T].detach().numpy(), 1e-5, "bootstrap value")
+
+    vext = torch.cat([vt[:T], vt[T:].detach()])
+    R = oa2c.returns(rewards, dones, vext.detach(), 0.99)
+    loss, _ = oa2c.loss(lt[:T].reshape(-1, A), vt[:T].reshape(-1), actions, R.view(-1))
+    loss.backward()
+    mods = [getattr(ref, a) for a in TRUNK.values()]
+    params = [m.weight for m in mods] + [m.bias for m in mods] + [getattr(ref.lstm, k) for k in LSTM_KEYS]
+    keys = [k + ".weight" for k in TRUNK] + [k + ".bias" for k in TRUNK] + ["rnn.inner." + k for k in LSTM_KEYS]
+    old = tr.net.to_reference(p0)
+    sq_old = tr.net.to_reference(sq0)
+    grads = [p.grad.clone() for p in params]
+    sq = [sq_old[k].clone().view_as(p) for k, p in zip(keys, params)]
+    with torch.no_grad():
+        oa2c.clip_and_rmsprop([p.data for p in params], grads, sq, lr)
+    new = tr.net.to_reference(tr.params)
+    for k, p in zip(keys, params):
+        step_ref = p.data - old[k].view_as(p)
+        step_gpu = new[k].view_as(p) - old[k].view_as(p)
+        scale = step_ref.abs().max().item()
+        assert (step_gpu - step_ref).abs().max().item() <= 2e-3 * scale + 1e-9, k
+    # the state after the rollout's last step carries into the next rollout
+    np.testing.assert_array_equal(tr.h0.cpu().numpy(), tr.h_all[(T - 1) * E:].cpu().numpy())
+
+
+def test_recurrent_trainer_learns_on_small_scene():
+    """As test_trainer_gpu.test_trainer_learns_on_small_scene, with the recurrent core."""
+    import vnav
+    from oracle.graph import h5_tables
+    graph, spd, _ = h5_tables(np.ones((3, 3), dtype=bool))
+    frames = synth_frames(3, np.arange(len(graph)), (84, 84, 3))
+    scene = vnav.scene_from_arrays(graph, spd, frames)
+    env = vnav.VectorEnv([scene], 256, seed=1, max_episode_steps=60, tasks=[(0, 5)])
+    tr = vnav.A2CTrainer(env, num_steps=20, seed=0, max_time_steps=1e9, recurrent=True)
+    lengths = []
+    for u in range(250):
+        m = tr.step(sync=(u < 20 or u >= 240))
+        if "raw" not in m:
+            lengths.append(m["episode_length"])
+    early = np.nanmean(lengths[5:20])
+    late = np.nanmean(lengths[-10:])
+    assert np.isfinite(late) and late < 0.8 * early, (early, late)

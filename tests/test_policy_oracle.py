@@ -49,3 +49,28 @@ def test_returns_recursion():
     # env 0: t2 = .5 + .9*2 = 2.3; t1 = 0 (done); t0 = 1 + .9*0 = 1
     np.testing.assert_allclose(R[:, 0].numpy(), [1.0, 0.0, 2.3], rtol=1e-6)
     np.testing.assert_allclose(R[:, 1].numpy(), [0.9 * (1 + 0.9 * 2.7), 1 + 0.9 * 2.7, 2.7], rtol=1e-6)
+
+
+def test_recurrent_oracle_mask_semantics():
+    """RecurrentGoalNetOracle: masks of ones = nn.LSTM over the whole sequence; a zero mask
+    at step t = restarting the LSTM from zero state at t."""
+    from oracle.policy import RecurrentGoalNetOracle
+    torch.manual_seed(0)
+    net = RecurrentGoalNetOracle((84, 84))
+    B, T, A = 2, 5, 4
+    img = torch.rand(B, T, 3, 84, 84)
+    gl = torch.rand(B, T, 3, 84, 84)
+    lra = torch.randn(B, T, A + 1)
+    h0, c0 = torch.randn(B, 1, 512), torch.randn(B, 1, 512)
+    with torch.no_grad():
+        x = torch.cat((net.features(img.flatten(0, 1), gl.flatten(0, 1)).view(B, T, 512), lra), 2)
+        y, (h, c) = net.lstm(x, (h0.transpose(0, 1), c0.transpose(0, 1)))
+        l1, v1, (h1, c1) = net.forward_seq(img, gl, lra, torch.ones(B, T), (h0, c0))
+        np.testing.assert_allclose(l1.numpy(), net.policy_logits(y).numpy(), rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(h1.numpy(), h.transpose(0, 1).numpy(), rtol=1e-5, atol=1e-6)
+        m = torch.ones(B, T)
+        m[:, 2] = 0
+        l2, _, _ = net.forward_seq(img, gl, lra, m, (h0, c0))
+        y2, _ = net.lstm(x[:, 2:])
+        np.testing.assert_allclose(l2[:, 2:].numpy(), net.policy_logits(y2).numpy(), rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(l2[:, :2].numpy(), l1[:, :2].numpy(), rtol=1e-6, atol=1e-7)
