@@ -42,10 +42,12 @@ struct SceneDev {
   int64_t row_base;  // first arena row (frame) of the scene
   int64_t spd_off;   // element offset of the scene's [N][N] spd block (and curriculum order block)
   int64_t cnt_off;   // element offset of the scene's [N][maxd+2] curriculum count block
+  int64_t comp_base; // first arena row of the scene's companion frames, -1 = second output is the goal frame
   int32_t graph_off; // first row of the scene's [N][4] adjacency block
   int32_t n;         // states
   int32_t maxd;      // largest spd value of the scene
   int32_t cur_oi;    // curriculum threshold floor(c*(maxd+offset)+1) clamped to [0, maxd] (host, fp64)
+  int32_t cur_mode;  // 0 off, 1 uniform over 0 < spd <= opt, 2 0.9 / 0.1 split (graph/util.py:88-117)
   float r_goal, r_step, r_coll;
   int32_t terminal_obs;
 };
@@ -67,7 +69,7 @@ struct EnvArgs {
   const int32_t* cur_count;  // per scene, per goal: #states with clamp(spd,-1,maxd)+1 <= b
   uint32_t* flags;
   int n_tasks, sched_len, max_steps, autoreset, n_envs;
-  int cur_mode;  // 0 off, 1 uniform over 0 < spd <= opt, 2 0.9 / 0.1 split (graph/util.py:88-117)
+  int cur_mode;  // any scene with a curriculum (the per-scene mode is SceneDev::cur_mode)
   uint32_t k0, k1;
   // per call
   const int32_t* actions;
@@ -122,7 +124,7 @@ __device__ void reset_env(const EnvArgs& a, int e, int lane, int& sc, int& s, in
   const SceneDev S = a.scenes[sc];
   const int32_t* spd = a.spd + S.spd_off;
   s = -1;
-  if (a.cur_mode > 0) {
+  if (a.cur_mode > 0 && S.cur_mode > 0) {
     // curriculum (graph/util.py:88-143, environments/gym_graph/graph.py:43-52):
     // opt = c * (maxd + offset) + 1 (S.cur_oi = its floor); candidates 0 < spd <= opt, uniform (mode 1) or
     // 0.9 over them / 0.1 over the farther ones (mode 2); one O(1) draw from the sorted table
@@ -131,7 +133,7 @@ __device__ void reset_env(const EnvArgs& a, int e, int lane, int& sc, int& s, in
     const int lo = cnt[1], hi = cnt[oi + 1], n = S.n;
     const u32x4 r = philox4x32_10(u32x4{(uint32_t)e, (uint32_t)k, 0u, STREAM_START}, a.k0, a.k1);
     // far set when the 0.1 coin says so (and it is not empty) or when the near set is empty
-    const bool use_far = (a.cur_mode == 2 && r.y >= 3865470566u && hi < n) || hi <= lo;  // 0.9 * 2^32
+    const bool use_far = (S.cur_mode == 2 && r.y >= 3865470566u && hi < n) || hi <= lo;  // 0.9 * 2^32
     const int b0 = use_far ? hi : lo, b1 = use_far ? n : hi;
     if (b1 > b0) s = a.cur_order[S.spd_off + (int64_t)g * n + b0 + (int)uniform_below(r.x, (uint32_t)(b1 - b0))];
   }
@@ -272,8 +274,8 @@ __global__ __launch_bounds__(256) void env_kernel(EnvArgs a) {
     if (lane == 0 && a.state_out) a.state_out[e] = s;
   }
 
-  const int64_t base = a.scenes[sc].row_base;
-  const int64_t img_row = base + os, goal_row = base + g;
+  const int64_t base = a.scenes[sc].row_base, comp = a.scenes[sc].comp_base;
+  const int64_t img_row = base + os, goal_row = comp >= 0 ? comp + os : base + g;
   if (lane == 0) {
     if (a.info_img_row) a.info_img_row[e] = (int32_t)img_row;
     if (a.info_goal_row) a.info_goal_row[e] = (int32_t)goal_row;
@@ -334,7 +336,7 @@ struct vn_ctx {
   int32_t* cur_order = nullptr;
   int32_t* cur_count = nullptr;
   int cur_mode = 0;
-  float cur_c = 0.f, cur_offset = 0.f;
+  double cur_c = 0.0;
   uint32_t* flags = nullptr;
   int max_steps = 900, autoreset = 1;
   float* info_ret = nullptr;
@@ -458,6 +460,11 @@ int vn_create(const vn_scene_desc* scenes, int n_scenes, int n_envs, uint64_t se
     sh[k].r_coll = d.reward_collision;
     sh[k].terminal_obs = d.terminal_obs;
     rows += d.n_states;
+    sh[k].comp_base = -1;
+    if (d.companion) {
+      sh[k].comp_base = rows;
+      rows += d.n_states;
+    }
     graph_rows += d.n_states;
     spd_elems += (int64_t)d.n_states * d.n_states;
   }
@@ -521,6 +528,9 @@ int vn_create(const vn_scene_desc* scenes, int n_scenes, int n_envs, uint64_t se
   if (e == hipSuccess) e = hipMemset(c->flags, 0, 4);
   for (int k = 0; k < n_scenes && e == hipSuccess; ++k) {
     const vn_scene_desc& d = scenes[k];
+    if (d.companion)
+      e = hipMemcpy(c->arena + sh[k].comp_base * F, d.companion, (size_t)d.n_states * F, hipMemcpyHostToDevice);
+    if (e != hipSuccess) break;
     if (d.observations) {
       e = hipMemcpy(c->arena + sh[k].row_base * F, d.observations, (size_t)d.n_states * F, hipMemcpyHostToDevice);
     } else {
@@ -656,11 +666,16 @@ int vn_set_env_scenes(vn_ctx* c, const int32_t* env_scene_host) {
   return VN_OK;
 }
 
-int vn_set_curriculum(vn_ctx* c, float complexity, int mode, float offset) {
-  if (!c) return fail(VN_EINVAL, "vn_set_curriculum: NULL ctx");
-  if (mode < 0 || mode > 2 || !(complexity >= 0.0f)) return fail(VN_EINVAL, "vn_set_curriculum: bad mode/complexity");
+int vn_set_curriculum_scenes(vn_ctx* c, double complexity, const int32_t* modes_host, const double* offsets_host) {
+  if (!c || !modes_host || !offsets_host) return fail(VN_EINVAL, "vn_set_curriculum_scenes: NULL argument");
+  if (!(complexity >= 0.0)) return fail(VN_EINVAL, "vn_set_curriculum: bad complexity");
+  int any = 0;
+  for (int i = 0; i < c->n_scenes; ++i) {
+    if (modes_host[i] < 0 || modes_host[i] > 2) return fail(VN_EINVAL, "vn_set_curriculum: bad mode");
+    any |= modes_host[i];
+  }
   DeviceGuard guard(c->device);
-  if (mode > 0 && !c->cur_order) {
+  if (any && !c->cur_order) {
     // per scene and goal: states sorted by spd[s][g] (stable counting sort) + inclusive counts
     int64_t n_order = 0, n_cnt = 0;
     for (const SceneDev& S : c->scenes_host) {
@@ -693,16 +708,25 @@ int vn_set_curriculum(vn_ctx* c, float complexity, int mode, float offset) {
     VN_HIP(hipMemcpy(c->cur_order, order.data(), order.size() * 4, hipMemcpyHostToDevice));
     VN_HIP(hipMemcpy(c->cur_count, cnt.data(), cnt.size() * 4, hipMemcpyHostToDevice));
   }
-  for (SceneDev& S : c->scenes_host) {  // the reference computes opt in Python floats (fp64)
-    const double opt = (double)complexity * ((double)S.maxd + (double)offset) + 1.0;
+  for (int i = 0; i < c->n_scenes; ++i) {  // the reference computes opt in Python floats (fp64)
+    SceneDev& S = c->scenes_host[i];
+    const double opt = complexity * ((double)S.maxd + offsets_host[i]) + 1.0;
     S.cur_oi = (int32_t)std::min<double>(std::max<double>(std::floor(opt), 0.0), (double)S.maxd);
+    S.cur_mode = modes_host[i];
   }
   VN_HIP(hipMemcpy(c->scenes, c->scenes_host.data(), c->scenes_host.size() * sizeof(SceneDev), hipMemcpyHostToDevice));
-  c->cur_mode = mode;
+  c->cur_mode = any ? 1 : 0;
   c->cur_c = complexity;
-  c->cur_offset = offset;
   return VN_OK;
 }
+
+int vn_set_curriculum(vn_ctx* c, double complexity, int mode, double offset) {
+  if (!c) return fail(VN_EINVAL, "vn_set_curriculum: NULL ctx");
+  std::vector<int32_t> modes(c->n_scenes, mode);
+  std::vector<double> offsets(c->n_scenes, offset);
+  return vn_set_curriculum_scenes(c, complexity, modes.data(), offsets.data());
+}
+
 
 int vn_set_max_episode_steps(vn_ctx* c, int max_steps) {
   if (!c) return fail(VN_EINVAL, "vn_set_max_episode_steps: NULL ctx");

@@ -19,6 +19,7 @@ c_int64 = ctypes.c_int64
 c_uint32 = ctypes.c_uint32
 c_uint64 = ctypes.c_uint64
 c_float = ctypes.c_float
+c_double = ctypes.c_double
 c_void_p = ctypes.c_void_p
 c_size_t = ctypes.c_size_t
 P = ctypes.POINTER
@@ -38,6 +39,7 @@ class SceneDesc(ctypes.Structure):
         ("reward_collision", c_float),
         ("terminal_obs", c_int32),
         ("synth_id", c_uint32),
+        ("companion", P(ctypes.c_uint8)),
     ]
 
 
@@ -55,7 +57,8 @@ SIGNATURES = {
     "vn_set_tasks": (c_int, [c_void_p, P(c_int32), c_int]),
     "vn_set_env_scenes": (c_int, [c_void_p, P(c_int32)]),
     "vn_set_max_episode_steps": (c_int, [c_void_p, c_int]),
-    "vn_set_curriculum": (c_int, [c_void_p, c_float, c_int, c_float]),
+    "vn_set_curriculum": (c_int, [c_void_p, c_double, c_int, c_double]),
+    "vn_set_curriculum_scenes": (c_int, [c_void_p, c_double, c_void_p, c_void_p]),
     "vn_set_autoreset": (c_int, [c_void_p, c_int]),
     "vn_random_actions": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p]),
     "vn_get_state": (c_int, [c_void_p, c_void_p, c_void_p]),

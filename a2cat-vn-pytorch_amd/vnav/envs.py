@@ -57,6 +57,8 @@ class VectorEnv:
                 d.observations = s.observations.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
             d.reward_goal, d.reward_step, d.reward_collision = s.rewards
             d.terminal_obs = s.terminal_obs
+            if s.companion is not None:
+                d.companion = s.companion.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
             d.synth_id = s.synth_id
             self._keep.append(s)
         handle = ctypes.c_void_p()
@@ -85,6 +87,9 @@ class VectorEnv:
             _lib.check(self.lib.vn_set_autoreset(self._ctx, 0), "vn_set_autoreset")
         if env_scenes is not None:
             self.set_env_scenes(env_scenes)
+        if tasks is None and all(s.goals for s in self.scenes):
+            # the scenes' own fixed goal lists (OrientedGraphEnv goals, MazeGraph goal)
+            tasks = [(i, g) for i, s in enumerate(self.scenes) for g in s.goals]
         if tasks:
             self.set_tasks(tasks)
         self.complexity = None
@@ -124,15 +129,15 @@ class VectorEnv:
         """Curriculum hook (graph/env.py:98-99, environments/gym_graph/graph.py:40-52,
         experiments/thor_cached_auxiliary.py:68-70): subsequent resets draw starts near the
         goal on the device (vn_set_curriculum); None switches back to uniform starts.
-        mode/offset default to the first scene's semantics (Scene.curriculum)."""
+        mode/offset default to each scene's own semantics (Scene.curriculum)."""
         self.complexity = complexity
         if complexity is None:
             _lib.check(self.lib.vn_set_curriculum(self._ctx, 0.0, 0, 0.0), "vn_set_curriculum")
             return
-        dm, do = self.scenes[0].curriculum
-        m = dm if mode is None else int(mode)
-        o = do if offset is None else float(offset)
-        _lib.check(self.lib.vn_set_curriculum(self._ctx, float(complexity), m, o), "vn_set_curriculum")
+        modes = np.array([s.curriculum[0] if mode is None else int(mode) for s in self.scenes], dtype=np.int32)
+        offs = np.array([s.curriculum[1] if offset is None else float(offset) for s in self.scenes], dtype=np.float64)
+        _lib.check(self.lib.vn_set_curriculum_scenes(self._ctx, float(complexity), modes.ctypes.data_as(ctypes.c_void_p),
+                                                     offs.ctypes.data_as(ctypes.c_void_p)), "vn_set_curriculum_scenes")
 
     set_hardness = set_complexity
 

@@ -14,8 +14,15 @@ Builders
                             4-connected component, hash frames
   maze_scene(maze, goal)    graph/env.py SimpleGraphEnv maze as a cached scene
                             (absolute-direction actions, MazeGraph frames)
-  scene_from_arrays(...)    h5 datasets already in memory (see tools/h5_to_npz.py)
+  oriented_scene(...)       environments/gym_graph/graph.py OrientedGraphEnv over a
+                            ThorGridWorld grid (oriented actions, fixed goal list)
+  load_graph_pickle(path)   a pickled ThorGridWorld (environments/gym_graph/download.py:
+                            37-75) through an allow-list unpickler -> oriented_scene
+  scene_from_arrays(...)    h5 datasets already in memory; load_h5 / load_npz read them
+                            (tools/h5_to_npz.py converts + optionally resizes offline)
 """
+import io
+import pickle
 from dataclasses import dataclass, field
 from typing import Optional, Tuple
 
@@ -26,6 +33,8 @@ from scipy.sparse.csgraph import connected_components, shortest_path
 DIRECTIONS = ((1, 0), (0, 1), (-1, 0), (0, -1))  # graph/util.py:4-13
 CACHED_REWARDS = (1.0, -0.0, 0.0)   # cached.py:84-88: step reward is -reward_configuration[1]
 GRAPH_REWARDS = (1.0, 0.0, 0.0)     # graph/env.py rewards=[1.0, 0.0, 0.0]
+ORIENTED_REWARDS = (1.0, 0.0, 0.0)  # environments/gym_graph/graph.py:10
+_ROT_COST = np.array([0, 1, 2, 1])  # compute_rotation_steps: (r - (gr + d)) % 4 with 3 -> 1
 
 
 @dataclass
@@ -45,6 +54,9 @@ class Scene:
     maze: Optional[np.ndarray] = None
     locations: Optional[list] = None
     goals: list = field(default_factory=list)
+    # [N,H,W,C] frames emitted as the second output for the current state instead of the goal
+    # frame (OrientedGraphEnv's (rgb, third-person rgb) observation)
+    companion: Optional[np.ndarray] = None
 
     @property
     def n_states(self):
@@ -62,6 +74,10 @@ class Scene:
             self.observations = np.ascontiguousarray(self.observations, dtype=np.uint8)
             if self.observations.shape != (n,) + tuple(self.frame_shape):
                 raise ValueError("observations must be [N,H,W,C] matching frame_shape")
+        if self.companion is not None:
+            self.companion = np.ascontiguousarray(self.companion, dtype=np.uint8)
+            if self.companion.shape != (n,) + tuple(self.frame_shape):
+                raise ValueError("companion frames must be [N,H,W,C] matching frame_shape")
 
 
 def positions(maze):
@@ -172,3 +188,135 @@ def load_npz(path, name=None):
     d = np.load(path, allow_pickle=False)
     return scene_from_arrays(d["graph"], d["shortest_path_distance"], d["observation"],
                              name=name or path)
+
+
+def load_h5(path, name=None):
+    """A reference h5 scene (graph/util.py:222-227 layout; read as cached.py:26-32). Needs
+    h5py; without it convert offline with tools/h5_to_npz.py and use load_npz."""
+    try:
+        import h5py
+    except ImportError as e:
+        raise ImportError("h5py is not importable here: convert %s with tools/h5_to_npz.py "
+                          "(/opt/conda/bin/python3.9) and load the .npz" % path) from e
+    with h5py.File(path, "r") as f:
+        return scene_from_arrays(f["graph"][()], f["shortest_path_distance"][()], f["observation"][()],
+                                 name=name or path)
+
+
+def oriented_tables(maze):
+    """(graph [N,4], spd [N,N], locations) of OrientedGraphEnv (environments/gym_graph/graph.py:
+    9-93) on a grid maze. State = point*4 + rotation over enumerate_positions (graph/util.py:
+    27-31). Actions per graph/util.py:15-25: 0 forward along rotation r, 1 rot+1, 2 backward,
+    3 rot-1 (rotations are always valid; a move off the free cells is a collision).
+    spd[s][g] is the distance sample_initial_state ranks starts by (graph/util.py:119-143):
+    cell distance d + compute_rotation_steps (:82-86) where d > 0, 0 on the goal's own cell
+    (never a start) and -1 where unreachable."""
+    base, locs, lookup = cell_distances(maze)
+    P = len(locs)
+    n = 4 * P
+    nbr = np.full((P, 4), -1, dtype=np.int64)
+    for p, (x, y) in enumerate(locs):
+        for d, (dx, dy) in enumerate(DIRECTIONS):
+            nbr[p, d] = lookup.get((x + dx, y + dy), -1)
+    graph = np.empty((n, 4), dtype=np.int64)
+    for p in range(P):
+        for r in range(4):
+            f, b = nbr[p, r], nbr[p, (r + 2) % 4]
+            graph[p * 4 + r] = (f * 4 + r if f >= 0 else -1, p * 4 + (r + 1) % 4,
+                                b * 4 + r if b >= 0 else -1, p * 4 + (r + 3) % 4)
+    # optimal first directions (compute_shortest_path_data, util.py:146-176): the free
+    # neighbours one step closer to the goal cell
+    rot = np.full((P, P, 4, 4), 99, dtype=np.int64)  # [p, q, r, gr]
+    r_idx = np.arange(4)[:, None]
+    gr_idx = np.arange(4)[None, :]
+    for d in range(4):
+        valid = nbr[:, d] >= 0
+        nd = np.where(valid[:, None], base[np.maximum(nbr[:, d], 0)], -2)
+        opt = valid[:, None] & (nd == base - 1) & (base > 0)
+        cost = _ROT_COST[(r_idx - (gr_idx + d)) % 4]
+        rot = np.where(opt[:, :, None, None], np.minimum(rot, cost[None, None]), rot)
+    spd4 = np.where(base[:, :, None, None] > 0, base[:, :, None, None] + rot,
+                    np.where(base[:, :, None, None] == 0, 0, -1))
+    spd = spd4.transpose(0, 2, 1, 3).reshape(n, n)
+    return graph, np.ascontiguousarray(spd), locs, base
+
+
+def oriented_scene(maze, observations, goals=(), name="oriented", rewards=ORIENTED_REWARDS,
+                   tp_observations=None):
+    """OrientedGraphEnv over a ThorGridWorld-style grid. observations [X, Y, 4, H, W, C]
+    uint8 indexed (x, y, rotation) as ThorGridWorld.render (graph/thor_graph.py:15-18);
+    tp_observations (same shape, optional) are the third-person frames render() appends
+    (:26-27), emitted as the second output instead of the goal frame; goals are
+    (x, y, rotation) triples (the env's fixed goal list, graph.py:20-23).
+    Terminal steps emit the current frame (graph.py:86-88); set_complexity follows
+    graph.py:51 (opt = c * (largest cell distance + 3) + 1, uniform over the starts)."""
+    maze = np.asarray(maze, dtype=bool)
+    graph, spd, locs, base = oriented_tables(maze)
+    obs = np.asarray(observations)
+    if obs.shape[:3] != maze.shape + (4,):
+        raise ValueError("observations must be [X, Y, 4, H, W, C] over the maze")
+    xs = np.array([p[0] for p in locs])
+    ys = np.array([p[1] for p in locs])
+    frames = np.ascontiguousarray(obs[xs, ys].reshape((-1,) + obs.shape[3:]), dtype=np.uint8)
+    comp = None
+    if tp_observations is not None:
+        tp = np.asarray(tp_observations)
+        if tp.shape != obs.shape:
+            raise ValueError("tp_observations must match observations")
+        comp = np.ascontiguousarray(tp[xs, ys].reshape((-1,) + tp.shape[3:]), dtype=np.uint8)
+    lookup = {p: i for i, p in enumerate(locs)}
+    goal_states = [lookup[(int(g[0]), int(g[1]))] * 4 + int(g[2]) for g in goals]
+    offset = float(base.max() + 3 - spd.max())  # c*(maxd + offset) + 1 == c*(largest + 3) + 1
+    return Scene(graph=graph, spd=spd, frame_shape=tuple(frames.shape[1:]), observations=frames,
+                 rewards=tuple(rewards), terminal_obs=1, curriculum=(1, offset), name=name, maze=maze,
+                 locations=locs, goals=goal_states, companion=comp)
+
+
+class _GridWorld:
+    """Attribute holder standing in for graph.thor_graph.ThorGridWorld when unpickling."""
+
+    def __setstate__(self, state):
+        self.__dict__.update(state)
+
+
+class _GraphUnpickler(pickle.Unpickler):
+    """Allow-list unpickler for ThorGridWorld pickles (graph/util.py:40-79 dump_graph /
+    load_graph): only numpy array reconstruction, builtin containers and the grid-world
+    class (mapped to a plain attribute holder) resolve — nothing else is importable, so
+    loading executes no code from the file."""
+
+    _ALLOWED = {
+        ("numpy.core.multiarray", "_reconstruct"), ("numpy._core.multiarray", "_reconstruct"),
+        ("numpy.core.multiarray", "scalar"), ("numpy._core.multiarray", "scalar"),
+        ("numpy", "ndarray"), ("numpy", "dtype"),
+        ("builtins", "tuple"), ("builtins", "list"), ("builtins", "dict"), ("builtins", "set"),
+        ("builtins", "frozenset"), ("builtins", "slice"), ("_codecs", "encode"),
+    }
+    _GRID = {("graph.thor_graph", "ThorGridWorld"), ("graph.core", "GridWorldScene"),
+             ("graph.maze_graph", "MazeGraph")}
+
+    def find_class(self, module, name):
+        if (module, name) in self._GRID:
+            return _GridWorld
+        if (module, name) in self._ALLOWED:
+            import importlib
+            return getattr(importlib.import_module(module), name)
+        raise pickle.UnpicklingError("refusing to load %s.%s from a scene pickle" % (module, name))
+
+
+def load_graph_pickle(path, goals=None, name=None):
+    """A pickled ThorGridWorld (``~/.visual_navigation/scenes/<name>.pkl``,
+    environments/gym_graph/download.py:37-75) as an OrientedGraphEnv scene. goals default to
+    the pickle's own ``goals`` attribute (download.py:11)."""
+    with open(path, "rb") as f:
+        g = _GraphUnpickler(io.BytesIO(f.read())).load()
+    if not isinstance(g, _GridWorld) or "_maze" not in g.__dict__ or "_observations" not in g.__dict__:
+        raise ValueError("%s does not hold a ThorGridWorld" % path)
+    if goals is None:
+        goals = g.__dict__.get("goals") or []
+        if isinstance(goals, tuple) and len(goals) == 3 and all(np.isscalar(v) for v in goals):
+            goals = [goals]
+    tp = g.__dict__.get("_tp_observations")
+    if tp is not None and np.shape(tp) != np.shape(g._observations):
+        tp = None  # render() would resize it to the screen size (graph/core.py:29-39): not emitted
+    return oriented_scene(g._maze, g._observations, goals, name=name or path, tp_observations=tp)

@@ -78,6 +78,11 @@ typedef struct vn_scene_desc {
   float reward_collision;
   int32_t terminal_obs;
   uint32_t synth_id; /* scene id fed to the frame hash when observations == NULL */
+  /* [n_states][H][W][C] or NULL. When set, the second output of every observation is the
+   * companion frame of the emitted state instead of the goal frame: OrientedGraphEnv's
+   * observation (rgb, third-person rgb) of ThorGridWorld.render (graph/thor_graph.py:15-33,
+   * environments/gym_graph/graph.py:56-58). */
+  const uint8_t* companion;
 } vn_scene_desc;
 
 /* ---- environment ------------------------------------------------------- */
@@ -131,8 +136,12 @@ int vn_set_max_episode_steps(vn_ctx* ctx, int max_steps); /* <= 0: no limit */
  * (mode 1, OrientedGraphEnv/sample_initial_state) or with probability 0.9 among them and
  * 0.1 among the farther ones (mode 2, SimpleGraphEnv/sample_initial_position); mode 0 =
  * off (uniform rejection sampling of cached.py). One O(1) draw from per-goal sorted tables
- * built on the first call. */
-int vn_set_curriculum(vn_ctx* ctx, float complexity, int mode, float offset);
+ * built on the first call. complexity and offset are fp64 (the reference computes opt in
+ * Python floats, so floor(opt) matches it bit for bit). */
+int vn_set_curriculum(vn_ctx* ctx, double complexity, int mode, double offset);
+/* Per-scene (mode, offset) arrays of n_scenes entries (host memory). */
+int vn_set_curriculum_scenes(vn_ctx* ctx, double complexity, const int32_t* modes_host,
+                             const double* offsets_host);
 int vn_set_autoreset(vn_ctx* ctx, int on);                /* default on */
 
 /* Synthetic uniform actions in [0,4) from Philox(seed, env, step). */

@@ -104,7 +104,11 @@ class VectorEnvOracle:
     def set_curriculum(self, complexity, mode, offset):
         """The engine's curriculum draw (restated from DESIGN.md "Curriculum"): per goal,
         states sorted stably by spd; near = 0 < spd <= floor(opt), far = spd > opt."""
-        self.cur_mode, self.cur_c, self.cur_offset = int(mode), float(complexity), float(offset)
+        n = len(self.scenes)
+        self.cur_c = float(complexity)
+        self.cur_modes = [int(m) for m in (mode if np.ndim(mode) else [mode] * n)]
+        self.cur_offsets = [float(o) for o in (offset if np.ndim(offset) else [offset] * n)]
+        self.cur_mode = int(any(self.cur_modes))
 
     def _curriculum_start(self, e, k, sc, g):
         spd = np.asarray(self.scenes[sc]["spd"])
@@ -112,12 +116,14 @@ class VectorEnvOracle:
         maxd = int(spd.max())
         col = np.clip(spd[:, g], -1, maxd)
         order = np.argsort(col, kind="stable")
-        opt = self.cur_c * (maxd + self.cur_offset) + 1.0  # Python floats, as the reference
+        if not self.cur_modes[sc]:
+            return None
+        opt = self.cur_c * (maxd + self.cur_offsets[sc]) + 1.0  # Python floats, as the reference
         oi = min(max(int(np.floor(opt)), 0), maxd)
         lo = int((col <= 0).sum())
         hi = int((col <= oi).sum())
         rx, ry, _, _ = philox.philox4x32_10(e, k, 0, philox.STREAM_START, self.k0, self.k1)
-        use_far = (self.cur_mode == 2 and int(ry) >= 3865470566 and hi < n) or hi <= lo
+        use_far = (self.cur_modes[sc] == 2 and int(ry) >= 3865470566 and hi < n) or hi <= lo
         b0, b1 = (hi, n) if use_far else (lo, hi)
         if b1 <= b0:
             return None
