@@ -304,6 +304,24 @@ __global__ void synth_frames_kernel(uint8_t* arena, int64_t row_base, int n_rows
   }
 }
 
+// dst[i] = src[rows[i]] for rows of row_bytes (one wave per row, 16-B lanes when aligned).
+__global__ __launch_bounds__(256) void gather_rows_kernel(const uint8_t* __restrict__ src, int64_t row_bytes,
+                                                          const int32_t* __restrict__ rows, int n,
+                                                          uint8_t* __restrict__ dst) {
+  const int lane = threadIdx.x & 63;
+  const int i = uni(blockIdx.x * 4 + (threadIdx.x >> 6));
+  if (i >= n) return;
+  const uint8_t* s = src + (int64_t)rows[i] * row_bytes;
+  uint8_t* d = dst + (int64_t)i * row_bytes;
+  if ((row_bytes & 15) == 0) {
+    const uint4* a = reinterpret_cast<const uint4*>(s);
+    uint4* b = reinterpret_cast<uint4*>(d);
+    for (int64_t j = lane; j < (row_bytes >> 4); j += 64) b[j] = a[j];
+  } else {
+    for (int64_t j = lane; j < row_bytes; j += 64) d[j] = s[j];
+  }
+}
+
 __global__ void random_actions_kernel(int32_t* actions, int n, uint32_t k0, uint32_t k1, uint64_t step) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
@@ -745,6 +763,16 @@ int vn_random_actions(vn_ctx* c, int32_t* actions_dev, uint64_t step, vn_stream_
   DeviceGuard guard(c->device);
   hipLaunchKernelGGL(random_actions_kernel, dim3((c->n_envs + 255) / 256), dim3(256), 0, (hipStream_t)stream,
                      actions_dev, c->n_envs, (uint32_t)c->seed ^ 0xA5A5A5A5u, (uint32_t)(c->seed >> 32), step);
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
+
+int vn_gather_rows(const uint8_t* src_dev, int64_t row_bytes, const int32_t* rows_dev, int n, uint8_t* dst_dev,
+                   vn_stream_t stream) {
+  if (!src_dev || !rows_dev || !dst_dev || row_bytes <= 0 || n < 0) return fail(VN_EINVAL, "vn_gather_rows: bad args");
+  if (n == 0) return VN_OK;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream, src_dev, row_bytes,
+                     rows_dev, n, dst_dev);
   VN_HIP(hipGetLastError());
   return VN_OK;
 }

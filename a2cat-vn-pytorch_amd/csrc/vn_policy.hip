@@ -22,6 +22,7 @@
 #include "vn_common.h"
 #include "vn_gemm.h"
 #include "vn_lstm.h"
+#include "vn_aux.h"
 
 namespace vn {
 
@@ -261,9 +262,13 @@ struct PolicyLayout {
   // recurrent core (BigGoalHouseModel, models/goal.py:61-67): W_cat [2048][xcat] = [W_ih | 0 | W_hh]
   int lstm, lin, xoff, xcat;
   int64_t lw, lbih, lbhh;
+  // aux deconv heads (AuxiliaryBigGoalHouseModel, goal.py:144-189): W1 [32][4][4][48], b1 [48],
+  // W2 [48][4][4][8] (block diagonal), b2 [8]; maps X4 [h3][w3] -> A1 [AH][AW] -> P [PH][PW]
+  int aux, AH, AW, PH, PW;
+  int64_t aw1, ab1, aw2, ab2;
 };
 
-inline PolicyLayout make_layout(int H, int W, int A, int lstm = 0) {
+inline PolicyLayout make_layout(int H, int W, int A, int lstm = 0, int aux = 0) {
   PolicyLayout L{};
   L.H = H;
   L.W = W;
@@ -299,6 +304,21 @@ inline PolicyLayout make_layout(int H, int W, int A, int lstm = 0) {
     off += 2048;
     L.lbhh = off;
     off += 2048;
+  }
+  L.aux = aux;
+  L.AH = 2 * L.OH3 + 2;
+  L.AW = 2 * L.OW3 + 2;
+  L.PH = 2 * L.AH + 2;
+  L.PW = 2 * L.AW + 2;
+  if (aux) {
+    L.aw1 = off;
+    off += 32ll * 16 * kAuxC1;
+    L.ab1 = off;
+    off += kAuxC1;
+    L.aw2 = off;
+    off += (int64_t)kAuxC1 * 16 * kAuxC2;
+    L.ab2 = off;
+    off += kAuxC2;
   }
   L.n_params = off;
   L.wt_total = wt;
@@ -501,7 +521,8 @@ inline BwdWork carve(const PolicyLayout& L, float* ws, int64_t n) {
 
 template <int H0, int W0>
 int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int n, const Acts& a,
-                  const float* dout, const float* dz5_in, float* Gr, const BwdWork& w, hipStream_t st) {
+                  const float* dout, const float* dz5_in, const float* dx4_extra, float* Gr, const BwdWork& w,
+                  hipStream_t st) {
   using G = Geo<H0, W0>;
   const int A1 = L.A + 1;
   auto T = [&](int i) { return w.wt + L.wt_off[i]; };
@@ -527,8 +548,13 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
   {
     DenseRows fa{dz5, 512, n};
     DenseRows fb{T(4), 512, G::FCIN};  // WT [FCIN][512]
-    EpiMask ep{w.dz4, a.X[3], G::FCIN};
-    launch_gemm<64, 64, 32, 2, 2>(fa, fb, ep, n, G::FCIN, 512, st);
+    if (dx4_extra) {  // + the aux heads' gradient w.r.t. X4, under the same ReLU mask
+      EpiMaskAdd ep{w.dz4, a.X[3], G::FCIN, dx4_extra};
+      launch_gemm<64, 64, 32, 2, 2>(fa, fb, ep, n, G::FCIN, 512, st);
+    } else {
+      EpiMask ep{w.dz4, a.X[3], G::FCIN};
+      launch_gemm<64, 64, 32, 2, 2>(fa, fb, ep, n, G::FCIN, 512, st);
+    }
     Im2colT<DenseRows> fbw{DenseRows{a.X[3], G::FCIN, n}, G::FCIN};
     launch_wgrad<64, 64, 2, 2>(dz5, 512, 512, fbw, G::FCIN, n, w.slab, w.slab_cap, Gr + L.l[4].w, Gr + L.l[4].b,
                                st);
@@ -722,6 +748,115 @@ inline int lstm_backward(const PolicyLayout& L, const float* P, int T, int E, co
   return VN_OK;
 }
 
+// ---- aux deconv heads (vn_aux.h) ---------------------------------------------------
+// One parity class (PY, PX) of a k4 s2 transposed conv in [n][IH][IW][CIN] -> out
+// [n][OH][OW][COUT] (OH = 2 IH + 2): the trunk's dgrad loaders with a bias/ReLU epilogue.
+template <int CIN, int COUT, int IH, int IW, int OH, int OW, int PY, int PX>
+inline void deconv_class(const float* in, const float* WT, float* out, const float* bias, int relu, int nimg,
+                         hipStream_t st) {
+  constexpr int HYC = OH / 2, WXC = OW / 2;
+  const int M = nimg * HYC * WXC;
+  DgradA<CIN, 4, 2, IH, IW, HYC, WXC> fa{in, M};
+  DgradB<CIN, 4, 2, COUT> fb{WT, COUT, 0, PY, PX};
+  EpiDeconv<OH, OW, PY, PX, HYC, WXC> ep{out, COUT, bias, relu};
+  if constexpr (COUT >= 32)
+    launch_gemm<64, 32, 32, 4, 1>(fa, fb, ep, M, COUT, 4 * CIN, st);
+  else
+    launch_gemm<64, 16, 32, 4, 1>(fa, fb, ep, M, COUT, 4 * CIN, st);
+}
+
+template <int CIN, int COUT, int IH, int IW, int OH, int OW>
+inline void deconv_all(const float* in, const float* WT, float* out, const float* bias, int relu, int nimg,
+                       hipStream_t st) {
+  static_assert(OH == 2 * IH + 2 && OW == 2 * IW + 2, "k4 s2 transposed conv geometry");
+  deconv_class<CIN, COUT, IH, IW, OH, OW, 0, 0>(in, WT, out, bias, relu, nimg, st);
+  deconv_class<CIN, COUT, IH, IW, OH, OW, 0, 1>(in, WT, out, bias, relu, nimg, st);
+  deconv_class<CIN, COUT, IH, IW, OH, OW, 1, 0>(in, WT, out, bias, relu, nimg, st);
+  deconv_class<CIN, COUT, IH, IW, OH, OW, 1, 1>(in, WT, out, bias, relu, nimg, st);
+}
+
+struct AuxWork {
+  float* w1t;    // [16*48][32]
+  float* w2t;    // [16*8][48]
+  float* slab;
+  float* colsum; // [kColsumBlocks][48]
+  float* db;     // [48] scratch (the ones-column output of the weight-gradient products)
+};
+constexpr int kColsumBlocks = 512;
+
+inline int64_t aux_workspace_floats(const PolicyLayout& L) {
+  return 768ll * 32 + 128ll * 48 + slab_floats(L) + (int64_t)kColsumBlocks * 48 + 64 + 64;
+}
+
+inline AuxWork aux_carve(const PolicyLayout& L, float* ws) {
+  AuxWork w;
+  float* p = ws;
+  w.w1t = p;
+  p += 768ll * 32;
+  w.w2t = p;
+  p += 128ll * 48;
+  w.slab = p;
+  p += slab_floats(L);
+  w.colsum = p;
+  p += (int64_t)kColsumBlocks * 48;
+  w.db = p;
+  return w;
+}
+
+inline void colsum(const float* src, int64_t rows, int cols, float* partial, float* out, hipStream_t st) {
+  const int lanes = 256 / cols;
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(kColsumBlocks, (rows + lanes - 1) / lanes));
+  hipLaunchKernelGGL(colsum_partial_kernel, dim3(blocks), dim3(256), 0, st, src, rows, cols, partial);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3(1), dim3(64), 0, st, partial, blocks, cols, out);
+}
+
+template <int H0, int W0>
+int aux_forward_impl(const PolicyLayout& L, const float* P, const float* X4, int n, float* A1, float* Pout,
+                     const AuxWork& w, hipStream_t st) {
+  using G = Geo<H0, W0>;
+  constexpr int IH = G::OH3, IW = G::OW3, AH = 2 * IH + 2, AW = 2 * IW + 2, PH = 2 * AH + 2, PW = 2 * AW + 2;
+  hipLaunchKernelGGL(transpose_kernel, dim3((32 * 768 + 255) / 256), dim3(256), 0, st, P + L.aw1, 32, 768, w.w1t);
+  hipLaunchKernelGGL(transpose_kernel, dim3((48 * 128 + 255) / 256), dim3(256), 0, st, P + L.aw2, 48, 128, w.w2t);
+  deconv_all<32, kAuxC1, IH, IW, AH, AW>(X4, w.w1t, A1, P + L.ab1, 1, n, st);
+  deconv_all<kAuxC1, kAuxC2, AH, AW, PH, PW>(A1, w.w2t, Pout, P + L.ab2, 0, n, st);
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
+
+// Gradients of the heads' parameters and dX4 [n][IH][IW][32] (unmasked) from dP; A1 is
+// overwritten by its own gradient.
+template <int H0, int W0>
+int aux_backward_impl(const PolicyLayout& L, const float* P, const float* X4, int n, float* A1, const float* dP,
+                      float* Gr, float* dX4, const AuxWork& w, hipStream_t st) {
+  using G = Geo<H0, W0>;
+  constexpr int IH = G::OH3, IW = G::OW3, AH = 2 * IH + 2, AW = 2 * IW + 2, PH = 2 * AH + 2, PW = 2 * AW + 2;
+  const int P1 = n * AH * AW, P0 = n * IH * IW;
+  using Im2 = NhwcIm2col<kAuxC2, 4, 4, 2, PH, PW, AH, AW, 1>;  // dP windows per A1 pixel
+  using Im1 = NhwcIm2col<kAuxC1, 4, 4, 2, AH, AW, IH, IW, 1>;  // dA1 windows per X4 pixel
+  // second layer: dW2 = A1^T x im2col(dP) (block-diagonal mask), db2 = column sums of dP
+  launch_wgrad<32, 64, 2, 2>(A1, kAuxC1, kAuxC1, Im2colT<Im2>{Im2{dP, P1}, 16 * kAuxC2}, 16 * kAuxC2, P1, w.slab,
+                             slab_floats(L), Gr + L.aw2, w.db, st);
+  hipLaunchKernelGGL(aux_blockdiag_mask_kernel, dim3((kAuxC1 * 16 * kAuxC2 + 255) / 256), dim3(256), 0, st,
+                     Gr + L.aw2);
+  colsum(dP, (int64_t)n * PH * PW, kAuxC2, w.colsum, Gr + L.ab2, st);
+  {  // dA1 = conv(dP, W2) masked by the ReLU of A1, in place
+    DenseRows fb{P + L.aw2, 16 * kAuxC2, kAuxC1};
+    EpiMask ep{A1, A1, kAuxC1};
+    launch_gemm<64, 32, 32, 4, 1>(Im2{dP, P1}, fb, ep, P1, kAuxC1, 16 * kAuxC2, st);
+  }
+  colsum(A1, (int64_t)P1, kAuxC1, w.colsum, Gr + L.ab1, st);
+  // first layer: dW1 = X4^T x im2col(dA1); dX4 = conv(dA1, W1)
+  launch_wgrad<32, 64, 2, 2>(X4, 32, 32, Im2colT<Im1>{Im1{A1, P0}, 16 * kAuxC1}, 16 * kAuxC1, P0, w.slab,
+                             slab_floats(L), Gr + L.aw1, w.db, st);
+  {
+    DenseRows fb{P + L.aw1, 16 * kAuxC1, 32};
+    EpiStore ep{dX4, 32};
+    launch_gemm<64, 32, 32, 4, 1>(Im1{A1, P0}, fb, ep, P0, 32, 16 * kAuxC1, st);
+  }
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
+
 }  // namespace vn
 
 using namespace vn;
@@ -754,14 +889,14 @@ int vn_policy_create(int frame_h, int frame_w, int num_actions, vn_policy** out)
 
 int vn_policy_create_ex(int frame_h, int frame_w, int num_actions, int flags, vn_policy** out) {
   if (!out) return fail(VN_EINVAL, "vn_policy_create: out is NULL");
-  if (flags & ~VN_POLICY_LSTM) return fail(VN_EINVAL, "vn_policy_create: unknown flags");
+  if (flags & ~(VN_POLICY_LSTM | VN_POLICY_AUX)) return fail(VN_EINVAL, "vn_policy_create: unknown flags");
   *out = nullptr;
   if (!supported(frame_h, frame_w))
     return fail(VN_EINVAL, "vn_policy_create: frame size must be 84x84 or 174x174");
   if (num_actions < 1 || num_actions + 1 > OUT_LD) return fail(VN_EINVAL, "vn_policy_create: 1..7 actions");
   vn_policy* p = new (std::nothrow) vn_policy();
   if (!p) return fail(VN_ENOMEM, "vn_policy_create: host allocation");
-  p->L = make_layout(frame_h, frame_w, num_actions, (flags & VN_POLICY_LSTM) ? 1 : 0);
+  p->L = make_layout(frame_h, frame_w, num_actions, (flags & VN_POLICY_LSTM) ? 1 : 0, (flags & VN_POLICY_AUX) ? 1 : 0);
   *out = p;
   return VN_OK;
 }
@@ -808,32 +943,90 @@ int vn_policy_forward(vn_policy* p, const float* params, const vn_frames* frames
   return forward_impl<174, 174>(p->L, params, src, n, a, out, st);
 }
 
-int vn_policy_backward(vn_policy* p, const float* params, const vn_frames* frames, int n, float* acts,
-                       int64_t act_capacity, const float* dout, float* grads, float* workspace,
-                       vn_stream_t stream) {
-  if (!p || !params || !frames || !acts || !dout || !grads || !workspace || n <= 0)
+int vn_policy_backward_ex(vn_policy* p, const float* params, const vn_frames* frames, int n, float* acts,
+                          int64_t act_capacity, const float* dout, const float* dz5, const float* dx4_extra,
+                          float* grads, float* workspace, vn_stream_t stream) {
+  if (!p || !params || !frames || !acts || !grads || !workspace || n <= 0 || (!dout && !dz5))
     return fail(VN_EINVAL, "vn_policy_backward: bad args");
   if (n > act_capacity) return fail(VN_EINVAL, "vn_policy_backward: n exceeds the activation capacity");
   const FrameSrc src = to_src(frames);
   const Acts a = acts_at(p->L, acts, act_capacity, 0);
   const BwdWork w = carve(p->L, workspace, n);
   hipStream_t st = (hipStream_t)stream;
-  if (p->L.H == 84) return backward_impl<84, 84>(p->L, params, src, n, a, dout, nullptr, grads, w, st);
-  return backward_impl<174, 174>(p->L, params, src, n, a, dout, nullptr, grads, w, st);
+  const float* d = dz5 ? nullptr : dout;
+  if (p->L.H == 84) return backward_impl<84, 84>(p->L, params, src, n, a, d, dz5, dx4_extra, grads, w, st);
+  return backward_impl<174, 174>(p->L, params, src, n, a, d, dz5, dx4_extra, grads, w, st);
+}
+
+int vn_policy_backward(vn_policy* p, const float* params, const vn_frames* frames, int n, float* acts,
+                       int64_t act_capacity, const float* dout, float* grads, float* workspace,
+                       vn_stream_t stream) {
+  if (!dout) return fail(VN_EINVAL, "vn_policy_backward: dout is NULL");
+  return vn_policy_backward_ex(p, params, frames, n, acts, act_capacity, dout, nullptr, nullptr, grads, workspace,
+                               stream);
 }
 
 int vn_policy_backward_trunk(vn_policy* p, const float* params, const vn_frames* frames, int n, float* acts,
                              int64_t act_capacity, const float* dz5, float* grads, float* workspace,
                              vn_stream_t stream) {
-  if (!p || !params || !frames || !acts || !dz5 || !grads || !workspace || n <= 0)
-    return fail(VN_EINVAL, "vn_policy_backward_trunk: bad args");
-  if (n > act_capacity) return fail(VN_EINVAL, "vn_policy_backward_trunk: n exceeds the activation capacity");
-  const FrameSrc src = to_src(frames);
+  if (!dz5) return fail(VN_EINVAL, "vn_policy_backward_trunk: dz5 is NULL");
+  return vn_policy_backward_ex(p, params, frames, n, acts, act_capacity, nullptr, dz5, nullptr, grads, workspace,
+                               stream);
+}
+
+int vn_policy_aux_info(vn_policy* p, int64_t* info8) {
+  if (!p || !info8) return fail(VN_EINVAL, "vn_policy_aux_info: bad args");
+  if (!p->L.aux) return fail(VN_EINVAL, "vn_policy_aux_info: policy has no aux heads");
+  const PolicyLayout& L = p->L;
+  const int64_t v[8] = {L.aw1, L.ab1, L.aw2, L.ab2, L.AH, L.AW, L.PH, L.PW};
+  for (int i = 0; i < 8; ++i) info8[i] = v[i];
+  return VN_OK;
+}
+
+int vn_aux_workspace_floats(vn_policy* p, int64_t* floats) {
+  if (!p || !floats || !p->L.aux) return fail(VN_EINVAL, "vn_aux_workspace_floats: bad args");
+  *floats = aux_workspace_floats(p->L);
+  return VN_OK;
+}
+
+int vn_aux_forward(vn_policy* p, const float* params, float* acts, int64_t act_capacity, int n, float* a1,
+                   float* pred, float* workspace, vn_stream_t stream) {
+  if (!p || !p->L.aux || !params || !acts || !a1 || !pred || !workspace || n <= 0 || n > act_capacity)
+    return fail(VN_EINVAL, "vn_aux_forward: bad args");
   const Acts a = acts_at(p->L, acts, act_capacity, 0);
-  const BwdWork w = carve(p->L, workspace, n);
+  const AuxWork w = aux_carve(p->L, workspace);
   hipStream_t st = (hipStream_t)stream;
-  if (p->L.H == 84) return backward_impl<84, 84>(p->L, params, src, n, a, nullptr, dz5, grads, w, st);
-  return backward_impl<174, 174>(p->L, params, src, n, a, nullptr, dz5, grads, w, st);
+  if (p->L.H == 84) return aux_forward_impl<84, 84>(p->L, params, a.X[3], n, a1, pred, w, st);
+  return aux_forward_impl<174, 174>(p->L, params, a.X[3], n, a1, pred, w, st);
+}
+
+int vn_aux_loss_grad(vn_policy* p, const float* pred, int n, const vn_aux_targets* targets, float weight,
+                     float* dpred, float* stats4, vn_stream_t stream) {
+  if (!p || !p->L.aux || !pred || !targets || !dpred || !stats4 || n <= 0 || !targets->depth ||
+      !targets->segmentation || !targets->image_rows || !targets->goal_rows)
+    return fail(VN_EINVAL, "vn_aux_loss_grad: bad args");
+  const PolicyLayout& L = p->L;
+  if (targets->height < L.PH * kAuxCell || targets->width < L.PW * kAuxCell)
+    return fail(VN_EINVAL, "vn_aux_loss_grad: target frames smaller than the crop");
+  AuxTargets tg{targets->depth, targets->segmentation, targets->image_rows, targets->goal_rows, targets->height,
+                targets->width};
+  const int64_t total = (int64_t)n * L.PH * L.PW;
+  hipLaunchKernelGGL(aux_loss_grad_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     n, L.PH, L.PW, pred, tg, weight, dpred, stats4);
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
+
+int vn_aux_backward(vn_policy* p, const float* params, float* acts, int64_t act_capacity, int n, float* a1,
+                    const float* dpred, float* grads, float* dx4, float* workspace, vn_stream_t stream) {
+  if (!p || !p->L.aux || !params || !acts || !a1 || !dpred || !grads || !dx4 || !workspace || n <= 0 ||
+      n > act_capacity)
+    return fail(VN_EINVAL, "vn_aux_backward: bad args");
+  const Acts a = acts_at(p->L, acts, act_capacity, 0);
+  const AuxWork w = aux_carve(p->L, workspace);
+  hipStream_t st = (hipStream_t)stream;
+  if (p->L.H == 84) return aux_backward_impl<84, 84>(p->L, params, a.X[3], n, a1, dpred, grads, dx4, w, st);
+  return aux_backward_impl<174, 174>(p->L, params, a.X[3], n, a1, dpred, grads, dx4, w, st);
 }
 
 int vn_policy_lstm_info(vn_policy* p, int64_t* info8) {

@@ -4,7 +4,8 @@ Hot path of felipefelixarias/a2cat-vn-pytorch rebuilt for gfx950: the cached-sce
 env.step (VectorEnv, libvnav.so) and the A2C rollout/update of the goal-conditioned
 CNN policy. See DESIGN.md at the repository root.
 """
-from .scenes import Scene, grid_tables, maze_scene, synthetic_scene, scene_from_arrays  # noqa: F401
+from .scenes import (Scene, grid_tables, load_graph_pickle, load_h5, load_npz, maze_scene, oriented_scene,  # noqa: F401
+                     oriented_tables, scene_from_arrays, synthetic_scene)
 from .envs import VectorEnv, make, to_float_chw  # noqa: F401
 from .policy import GoalNavPolicy, PolicyNet  # noqa: F401
 from .a2c import A2CTrainer  # noqa: F401

@@ -67,6 +67,7 @@ SIGNATURES = {
     "vn_scene_row_base": (c_int, [c_void_p, c_int, P(c_int64)]),
     "vn_error_flags_sync": (c_int, [c_void_p, P(c_uint32), c_int]),
     "vn_num_envs": (c_int, [c_void_p]),
+    "vn_gather_rows": (c_int, [c_void_p, c_int64, c_void_p, c_int, c_void_p, c_void_p]),
 }
 
 SIGNATURES.update({
@@ -89,6 +90,15 @@ SIGNATURES.update({
     "vn_lstm_backward": (c_int, [c_void_p, c_void_p, c_int, c_int] + [c_void_p] * 11 + [c_void_p]),
     "vn_policy_backward_trunk": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int64, c_void_p,
                                          c_void_p, c_void_p, c_void_p]),
+    "vn_policy_aux_info": (c_int, [c_void_p, P(c_int64)]),
+    "vn_aux_workspace_floats": (c_int, [c_void_p, P(c_int64)]),
+    "vn_aux_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p,
+                               c_void_p]),
+    "vn_aux_loss_grad": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_float, c_void_p, c_void_p, c_void_p]),
+    "vn_aux_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p,
+                                c_void_p, c_void_p, c_void_p]),
+    "vn_policy_backward_ex": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int64, c_void_p, c_void_p,
+                                      c_void_p, c_void_p, c_void_p, c_void_p]),
     "vn_policy_sample": (c_int, [c_void_p, c_int, c_int, c_uint64, c_uint64,
                                         c_void_p, c_void_p, c_void_p, c_void_p,
                                         c_void_p]),

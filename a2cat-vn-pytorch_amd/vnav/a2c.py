@@ -18,6 +18,13 @@ With a recurrent net (``recurrent=True``) each step also runs the LSTM core: the
 [conv_merge features | one-hot last action | last reward] and the carried (h, c), both
 zeroed where an episode starts (mask m_t = 1 - done_{t-1}); the update back-propagates
 through the T steps of the rollout (truncated BPTT) and (h, c) carry on to the next.
+
+With ``aux_weight > 0`` (AuxiliaryTrainer, experiments/ai2_auxiliary/trainer.py:21-55:
+auxiliary_weight 0.05) the update adds the deconv loss of AuxiliaryBigGoalHouseModel's
+depth / segmentation / goal-segmentation heads against avg-pooled targets gathered from
+the env's aux arena by row. The reference computes it on a sequence sampled from
+UnrealTrainer's replay buffer (deep_rl, absent); here it uses the on-policy rollout batch
+(documented deviation, parity unpinned at the trainer level).
 """
 import ctypes
 import time
@@ -32,7 +39,8 @@ from .policy import OUT_LD, PolicyNet, frames_from_rows
 class A2CTrainer:
     def __init__(self, env, net=None, params=None, num_steps=20, gamma=0.99, learning_rate=7e-4,
                  max_time_steps=2e6, rms_alpha=0.99, rms_epsilon=1e-5, max_gradient_norm=0.5,
-                 value_coefficient=0.5, entropy_coefficient=0.01, seed=0, process_group=None, recurrent=False):
+                 value_coefficient=0.5, entropy_coefficient=0.01, seed=0, process_group=None, recurrent=False,
+                 aux_weight=0.0):
         self.env = env
         self.lib = _lib.load()
         self.device = env.device
@@ -48,9 +56,12 @@ class A2CTrainer:
         self.seed = int(seed)
         self.group = process_group
         self.world, self.rank = vdist.world_of(process_group)
+        self.aux_weight = float(aux_weight)
         self.net = net if net is not None else PolicyNet(env.frame_shape[:2], env.num_actions, self.device,
-                                                         recurrent=recurrent)
+                                                         recurrent=recurrent, aux=self.aux_weight > 0)
         self.recurrent = self.net.recurrent
+        if self.aux_weight > 0 and (not self.net.aux or getattr(env, "aux_arena", None) is None):
+            raise ValueError("aux_weight > 0 needs an aux policy (aux=True) and scenes with depth + segmentation")
         self.A = self.net.num_actions
         self.params = params if params is not None else self.net.init_params(self.seed)
         vdist.broadcast_params_(self.params, group=self.group)
@@ -101,6 +112,16 @@ class A2CTrainer:
             self.boot_lra = torch.zeros((E, A1), **f32)
             self.dz5 = torch.zeros((N, 512), **f32)
             self.lstm_ws = torch.empty(self.net.lstm_workspace_floats(T, E), **f32)
+        if self.aux_weight > 0:
+            self.a1, self.pred = self.net.aux_buffers(N)
+            self.dpred = torch.empty_like(self.pred)
+            self.dx4 = torch.zeros((N, self.net.fc_in), dtype=torch.float32, **kw)
+            self.aux_stats = torch.zeros(4, dtype=torch.float32, **kw)
+            self.aux_ws = torch.empty(self.net.aux_workspace_floats(), dtype=torch.float32, **kw)
+            from .policy import AuxTargets
+            depth, seg = env.aux_arena
+            self._aux_targets = AuxTargets(depth.data_ptr(), seg.data_ptr(), self.rows_img.data_ptr(),
+                                           self.rows_goal.data_ptr(), env.frame_shape[0], env.frame_shape[1])
         arena, fb, _, _ = env.frame_arena()
         self._arena, self._fb = arena, fb
         env.observe(gather=False)  # refresh the obs row buffers for the first forward
@@ -202,17 +223,23 @@ class A2CTrainer:
                                         ctypes.c_float(self.value_coefficient),
                                         ctypes.c_float(self.entropy_coefficient), _lib.ptr(self.dout),
                                         _lib.ptr(self.stats), st), "vn_a2c_loss_grad")
+        dx4 = None
+        if self.aux_weight > 0:  # deconv heads: forward, loss gradient, backward -> dL/dX4
+            self.aux_stats.zero_()
+            net.aux_forward(self.params, self.acts, N, N, self.a1, self.pred, self.aux_ws)
+            net.aux_loss_grad(self.pred, N, self._aux_targets, self.aux_weight, self.dpred, self.aux_stats)
+            net.aux_backward(self.params, self.acts, N, N, self.a1, self.dpred, self.grads, self.dx4, self.aux_ws)
+            dx4 = self.dx4
+        frames = self._frames(self.rows_img, self.rows_goal)
         if self.recurrent:
             net.lstm_backward(self.params, T, E, self.dout, self.h_all, self.xcat, self.lstm_acts, self.c_all, self.c0,
                               self.masks, net.x5(self.acts, N), self.dz5, self.grads, self.lstm_ws)
-            net.backward_trunk(self.params, self._frames(self.rows_img, self.rows_goal), N, self.acts, N, self.dz5,
-                               self.grads, self.workspace)
+            net.backward_ex(self.params, frames, N, self.acts, N, None, self.dz5, dx4, self.grads, self.workspace)
             # (h, c) after the last step carry into the next rollout
             self.h0.copy_(self.h_all[(T - 1) * E:])
             self.c0.copy_(self.c_all[(T - 1) * E:])
         else:
-            net.backward(self.params, self._frames(self.rows_img, self.rows_goal), N, self.acts, N, self.dout,
-                         self.grads, self.workspace)
+            net.backward_ex(self.params, frames, N, self.acts, N, self.dout, None, dx4, self.grads, self.workspace)
         scale = vdist.allreduce_gradients_(self.grads, self.group)  # RCCL, one flat bucket
         P = net.n_params
         _lib.check(lib.vn_grad_norm(_lib.ptr(self.grads), P, ctypes.c_float(scale),
@@ -232,12 +259,18 @@ class A2CTrainer:
         N = self.num_steps * self.env.num_envs
         self.total_steps += N * self.world
         self.num_updates += 1
-        m = torch.cat([self.stats / N, self.scalars[:1], self.episode_stats])
-        vdist.reduce_metrics_(m, 5, self.group)
+        if self.aux_weight > 0:  # sum of the per-head MSEs (trainer.py:51-54)
+            ph, pw = self.net.aux_layout["p_hw"]
+            numel = torch.tensor([1.0, 3.0, 3.0], device=self.device) * (N * ph * pw)
+            aux = (self.aux_stats[:3] / numel).sum().view(1)
+        else:
+            aux = torch.zeros(1, device=self.device)
+        m = torch.cat([self.stats / N, self.scalars[:1], aux, self.episode_stats])
+        vdist.reduce_metrics_(m, 6, self.group)
         if not sync:
             return {"raw": m}
         vals = m.tolist()
-        vl, al, ent, ret_mean, gnorm, eps, rsum, lsum = vals
+        vl, al, ent, ret_mean, gnorm, aux_loss, eps, rsum, lsum = vals
         dt = time.perf_counter() - t0
         return {
             "step": self.total_steps, "updates": self.num_updates,
@@ -246,6 +279,7 @@ class A2CTrainer:
             "episodes": eps, "reward": rsum / eps if eps else float("nan"),
             "episode_length": lsum / eps if eps else float("nan"),
             "grad_norm": gnorm, "return_mean": ret_mean, "fps": N * self.world / dt,
+            **({"aux_loss": aux_loss} if self.aux_weight > 0 else {}),
         }
 
     def run(self, log_every=10, logger=print):

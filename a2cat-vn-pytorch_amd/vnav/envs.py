@@ -31,7 +31,7 @@ class VectorEnv:
     num_actions = 4  # THORDiscreteCachedEnv.get_action_size (cached.py:66-68)
 
     def __init__(self, scenes, num_envs, seed=0, device=None, max_episode_steps=900, tasks=None,
-                 env_scenes=None, autoreset=True):
+                 env_scenes=None, autoreset=True, aux_observations=False):
         if isinstance(scenes, Scene):
             scenes = [scenes]
         if not scenes:
@@ -94,6 +94,36 @@ class VectorEnv:
             self.set_tasks(tasks)
         self.complexity = None
         self._schedule = None
+        self.aux_arena = None
+        if all(s.depth is not None and s.segmentation is not None for s in self.scenes):
+            self.aux_arena = self._build_aux_arena()
+        self.aux_observations = bool(aux_observations)
+        if self.aux_observations and self.aux_arena is None:
+            raise ValueError("aux_observations needs depth + segmentation on every scene")
+
+    def _build_aux_arena(self):
+        """Depth [rows,H,W,1] and segmentation [rows,H,W,3] uint8 on the device, indexed by
+        the frame arena's rows (so info img_row / goal_row address them too)."""
+        _, _, rows, bases = self.frame_arena()
+        H, W = self.frame_shape[:2]
+        depth = torch.zeros((rows, H, W, 1), dtype=torch.uint8, device=self.device)
+        seg = torch.zeros((rows, H, W, 3), dtype=torch.uint8, device=self.device)
+        for s, b in zip(self.scenes, bases):
+            depth[b:b + s.n_states].copy_(torch.from_numpy(s.depth))
+            seg[b:b + s.n_states].copy_(torch.from_numpy(s.segmentation))
+        return depth, seg
+
+    def _gather_aux(self):
+        """(depth, segmentation, goal segmentation) of the current observation by row."""
+        depth, seg = self.aux_arena
+        E = self.num_envs
+        out = []
+        for src, rows in ((depth, self._info["img_row"]), (seg, self._info["img_row"]), (seg, self._info["goal_row"])):
+            dst = torch.empty((E,) + tuple(src.shape[1:]), dtype=torch.uint8, device=self.device)
+            _lib.check(self.lib.vn_gather_rows(_lib.ptr(src), int(src[0].numel()), _lib.ptr(rows), E, _lib.ptr(dst),
+                                               self._stream()), "vn_gather_rows")
+            out.append(dst)
+        return tuple(out)
 
     # -- configuration -------------------------------------------------------
     def set_max_episode_steps(self, n):
@@ -167,6 +197,8 @@ class VectorEnv:
             return None, None
         img, goal = out if out is not None else self._frames()
         _lib.check(self.lib.vn_observe(self._ctx, _lib.ptr(img), _lib.ptr(goal), None, self._stream()), "vn_observe")
+        if self.aux_observations:
+            return (img, goal) + self._gather_aux()
         return img, goal
 
     def step(self, actions, out=None, gather=True):
@@ -193,6 +225,8 @@ class VectorEnv:
                                     _lib.ptr(done), _lib.ptr(state), self._stream()), "vn_step")
         info = dict(self._info)
         info["state"] = state
+        if self.aux_observations and gather:
+            return (img, goal) + self._gather_aux(), reward, done, info
         return (img, goal), reward, done, info
 
     def random_actions(self, step, out=None):
@@ -244,7 +278,7 @@ class VectorEnv:
 # environments/gym_ai2thor/__init__.py:45-49, environments/gym_graph/__init__.py:18-27)
 REGISTRY = {
     "CachedThor-v0": dict(max_episode_steps=900),
-    "AuxiliaryGraph-v0": dict(max_episode_steps=900),
+    "AuxiliaryGraph-v0": dict(max_episode_steps=900, aux_observations=True),
     "OrientedGraph-v0": dict(max_episode_steps=900),
 }
 

@@ -60,19 +60,30 @@ def trunk_sizes(h, w):
     return o1, o2, o3
 
 
+class AuxTargets(ctypes.Structure):
+    """vn_aux_targets (include/vnav.h)."""
+    _fields_ = [("depth", ctypes.c_void_p), ("segmentation", ctypes.c_void_p), ("image_rows", ctypes.c_void_p),
+                ("goal_rows", ctypes.c_void_p), ("height", ctypes.c_int32), ("width", ctypes.c_int32)]
+
+
+AUX_HEADS = (("deconv_depth", 1, 0), ("deconv_mask", 3, 1), ("deconv_mask_goal", 3, 4))  # name, C, first out ch
+
+
 class PolicyNet:
     """Handle on a vn_policy: flat parameter layout, forward/backward launches."""
 
-    def __init__(self, frame_hw=(84, 84), num_actions=4, device=None, recurrent=False):
+    def __init__(self, frame_hw=(84, 84), num_actions=4, device=None, recurrent=False, aux=False):
         self.lib = _lib.load()
         self.recurrent = bool(recurrent)
+        self.aux = bool(aux)
         self.frame_hw = tuple(frame_hw)
         self.num_actions = int(num_actions)
         self.device = torch.device("cuda", torch.cuda.current_device() if device is None else
                                    torch.device(device).index or 0)
         h = ctypes.c_void_p()
-        _lib.check(self.lib.vn_policy_create_ex(frame_hw[0], frame_hw[1], num_actions, 1 if recurrent else 0,
-                                                ctypes.byref(h)), "vn_policy_create_ex")
+        flags = (1 if recurrent else 0) | (2 if aux else 0)  # VN_POLICY_LSTM | VN_POLICY_AUX
+        _lib.check(self.lib.vn_policy_create_ex(frame_hw[0], frame_hw[1], num_actions, flags, ctypes.byref(h)),
+                   "vn_policy_create_ex")
         self._h = h
         n, a = ctypes.c_int64(), ctypes.c_int64()
         lay = (ctypes.c_int64 * 12)()
@@ -90,6 +101,12 @@ class PolicyNet:
             _lib.check(self.lib.vn_policy_lstm_info(h, info), "vn_policy_lstm_info")
             self.lstm = dict(w=info[0], bih=info[1], bhh=info[2], xcat=info[3], xoff=info[4], lin=info[5],
                              hidden=info[6])
+        self.aux_layout = None
+        if self.aux:
+            info = (ctypes.c_int64 * 8)()
+            _lib.check(self.lib.vn_policy_aux_info(h, info), "vn_policy_aux_info")
+            self.aux_layout = dict(w1=info[0], b1=info[1], w2=info[2], b2=info[3], a_hw=(info[4], info[5]),
+                                   p_hw=(info[6], info[7]))
 
     def __del__(self):
         try:
@@ -111,6 +128,10 @@ class PolicyNet:
             L = self.lstm
             out["lstm"] = (flat[L["w"]:L["w"] + 2048 * L["xcat"]].view(2048, L["xcat"]),
                            flat[L["bih"]:L["bih"] + 2048], flat[L["bhh"]:L["bhh"] + 2048])
+        if self.aux_layout:
+            X = self.aux_layout
+            out["aux"] = (flat[X["w1"]:X["w1"] + 32 * 16 * 48].view(32, 4, 4, 48), flat[X["b1"]:X["b1"] + 48],
+                          flat[X["w2"]:X["w2"] + 48 * 16 * 8].view(48, 4, 4, 8), flat[X["b2"]:X["b2"] + 8])
         return out
 
     def new_params(self):
@@ -136,6 +157,12 @@ class PolicyNet:
             torch.nn.init.orthogonal_(whh, generator=g)
             wcat[:, :L["lin"]] = wih
             wcat[:, L["xoff"]:] = whh
+        if self.aux_layout:  # init_weights on ConvTranspose2d: fan_in = out_channels * k * k (torch's convention)
+            w1, _, w2, _ = v["aux"]
+            for hd, (_, c, o) in enumerate(AUX_HEADS):
+                d1, d2 = 1.0 / math.sqrt(16 * 16), 1.0 / math.sqrt(c * 16)
+                w1[:, :, :, 16 * hd:16 * hd + 16].uniform_(-d1, d1, generator=g)
+                w2[16 * hd:16 * hd + 16, :, :, o:o + c].uniform_(-d2, d2, generator=g)
         return flat.to(self.device)
 
     def from_reference(self, sd):
@@ -173,6 +200,13 @@ class PolicyNet:
             wcat[:, L["xoff"]:] = t(_lstm_param(sd, "weight_hh_l0"))
             bih[:] = t(_lstm_param(sd, "bias_ih_l0"))
             bhh[:] = t(_lstm_param(sd, "bias_hh_l0"))
+        if self.aux_layout:
+            w1, b1, w2, b2 = v["aux"]
+            for hd, (name, c, o) in enumerate(AUX_HEADS):
+                w1[:, :, :, 16 * hd:16 * hd + 16] = t(sd["%s.0.1.weight" % name]).permute(0, 2, 3, 1)
+                b1[16 * hd:16 * hd + 16] = t(sd["%s.0.1.bias" % name])
+                w2[16 * hd:16 * hd + 16, :, :, o:o + c] = t(sd["%s.0.3.weight" % name]).permute(0, 2, 3, 1)
+                b2[o:o + c] = t(sd["%s.0.3.bias" % name])
         return flat.to(self.device)
 
     def to_reference(self, flat):
@@ -208,6 +242,13 @@ class PolicyNet:
             out["rnn.inner.weight_hh_l0"] = wcat[:, L["xoff"]:].clone()
             out["rnn.inner.bias_ih_l0"] = bih.clone()
             out["rnn.inner.bias_hh_l0"] = bhh.clone()
+        if self.aux_layout:
+            w1, b1, w2, b2 = v["aux"]
+            for hd, (name, c, o) in enumerate(AUX_HEADS):
+                out["%s.0.1.weight" % name] = w1[:, :, :, 16 * hd:16 * hd + 16].permute(0, 3, 1, 2).contiguous()
+                out["%s.0.1.bias" % name] = b1[16 * hd:16 * hd + 16].clone()
+                out["%s.0.3.weight" % name] = w2[16 * hd:16 * hd + 16, :, :, o:o + c].permute(0, 3, 1, 2).contiguous()
+                out["%s.0.3.bias" % name] = b2[o:o + c].clone()
         return out
 
     # -- launches -------------------------------------------------------------------
@@ -234,6 +275,47 @@ class PolicyNet:
         _lib.check(self.lib.vn_policy_backward(self._h, _lib.ptr(params), ctypes.byref(frames), int(n), _lib.ptr(acts),
                                                int(capacity), _lib.ptr(dout), _lib.ptr(grads), _lib.ptr(workspace),
                                                _lib.stream_ptr(self.device)), "vn_policy_backward")
+
+    def backward_ex(self, params, frames, n, acts, capacity, dout, dz5, dx4, grads, workspace):
+        P = _lib.ptr
+        _lib.check(self.lib.vn_policy_backward_ex(self._h, P(params), ctypes.byref(frames), int(n), P(acts),
+                                                  int(capacity), P(dout), P(dz5), P(dx4), P(grads), P(workspace),
+                                                  _lib.stream_ptr(self.device)), "vn_policy_backward_ex")
+
+    # -- aux deconv heads ------------------------------------------------------------
+    def aux_workspace_floats(self):
+        f = ctypes.c_int64()
+        _lib.check(self.lib.vn_aux_workspace_floats(self._h, ctypes.byref(f)), "vn_aux_workspace_floats")
+        return f.value
+
+    def aux_buffers(self, n):
+        ah, aw = self.aux_layout["a_hw"]
+        ph, pw = self.aux_layout["p_hw"]
+        kw = dict(dtype=torch.float32, device=self.device)
+        return torch.empty((n, ah, aw, 48), **kw), torch.empty((n, ph, pw, 8), **kw)
+
+    def aux_forward(self, params, acts, capacity, n, a1, pred, workspace):
+        P = _lib.ptr
+        _lib.check(self.lib.vn_aux_forward(self._h, P(params), P(acts), int(capacity), int(n), P(a1), P(pred),
+                                           P(workspace), _lib.stream_ptr(self.device)), "vn_aux_forward")
+
+    def aux_loss_grad(self, pred, n, targets, weight, dpred, stats):
+        P = _lib.ptr
+        _lib.check(self.lib.vn_aux_loss_grad(self._h, P(pred), int(n), ctypes.byref(targets), ctypes.c_float(weight),
+                                             P(dpred), P(stats), _lib.stream_ptr(self.device)), "vn_aux_loss_grad")
+
+    def aux_backward(self, params, acts, capacity, n, a1, dpred, grads, dx4, workspace):
+        P = _lib.ptr
+        _lib.check(self.lib.vn_aux_backward(self._h, P(params), P(acts), int(capacity), int(n), P(a1), P(dpred),
+                                            P(grads), P(dx4), P(workspace), _lib.stream_ptr(self.device)),
+                   "vn_aux_backward")
+
+    def x4(self, acts, capacity):
+        """[capacity, h3*w3*32] view of conv_base's output (X4) in an activation store."""
+        c = int(capacity)
+        s4 = self.fc_in
+        off = c * (self.act_floats - 512 - s4)
+        return acts[off:off + c * s4].view(c, s4)
 
     def backward_trunk(self, params, frames, n, acts, capacity, dz5, grads, workspace):
         _lib.check(self.lib.vn_policy_backward_trunk(self._h, _lib.ptr(params), ctypes.byref(frames), int(n),
@@ -370,14 +452,50 @@ class _RecurrentGoalNavFunction(torch.autograd.Function):
         return (grads,) + (None,) * 9
 
 
+class _AuxDeconvFunction(torch.autograd.Function):
+    """Trunk to conv_base (X4) + the three deconv heads; gradients reach the parameters."""
+
+    @staticmethod
+    def forward(ctx, params, image, goal, net):
+        n = image.shape[0]
+        dev = params.device
+        acts = net.new_acts(n)
+        frames = frames_from_batch(image, goal)
+        out = None if net.recurrent else torch.empty((n, OUT_LD), dtype=torch.float32, device=dev)
+        net.forward(params, frames, n, acts, n, 0, out)
+        a1, pred = net.aux_buffers(n)
+        ws = torch.empty(net.aux_workspace_floats(), dtype=torch.float32, device=dev)
+        net.aux_forward(params, acts, n, n, a1, pred, ws)
+        ctx.save_for_backward(params, image, goal, acts, a1)
+        ctx.net = net
+        return pred
+
+    @staticmethod
+    def backward(ctx, dpred):
+        params, image, goal, acts, a1 = ctx.saved_tensors
+        net = ctx.net
+        n = image.shape[0]
+        dev = params.device
+        grads = torch.zeros_like(params)
+        dx4 = torch.empty((n, net.fc_in), dtype=torch.float32, device=dev)
+        ws = torch.empty(net.aux_workspace_floats(), dtype=torch.float32, device=dev)
+        net.aux_backward(params, acts, n, n, a1.clone(), dpred.contiguous(), grads, dx4, ws)
+        dz5 = torch.zeros((n, 512), dtype=torch.float32, device=dev)  # heads / LSTM take no gradient here
+        ws = torch.empty(net.workspace_floats(n), dtype=torch.float32, device=dev)
+        net.backward_ex(params, frames_from_batch(image, goal), n, acts, n, None, dz5, dx4, grads, ws)
+        return grads, None, None, None
+
+
 class GoalNavPolicy(torch.nn.Module):
     """Drop-in for BigGoalHouseModel's trunk + heads (see module docstring)."""
 
-    def __init__(self, num_inputs=3, num_outputs=4, frame_hw=(84, 84), device=None, seed=0, recurrent=False):
+    def __init__(self, num_inputs=3, num_outputs=4, frame_hw=(84, 84), device=None, seed=0, recurrent=False,
+                 aux=False):
         super().__init__()
         if num_inputs != 3:
             raise ValueError("frames are RGB (num_inputs=3)")
-        self.net = PolicyNet(frame_hw, num_outputs, device, recurrent=recurrent)
+        self.net = PolicyNet(frame_hw, num_outputs, device, recurrent=recurrent, aux=aux)
+        self.deconv_cell_size = 4  # goal.py:70,148
         self.params = torch.nn.Parameter(self.net.init_params(seed))
         self.lstm_layers, self.lstm_hidden_size = 1, 512  # goal.py:61-62 (state shape contract)
 
@@ -438,3 +556,25 @@ class GoalNavPolicy(torch.nn.Module):
         out, hT, cT = _RecurrentGoalNavFunction.apply(self.params, img, gl, lr, m, h0, c0, self.net, T, B)
         out = out.view(T, B, A + 1).transpose(0, 1)
         return [out[..., :A], out[..., A:A + 1], (hT.view(B, 1, 512), cT.view(B, 1, 512))]
+
+    def forward_deconv(self, inputs, masks=None, states=None):
+        """AuxiliaryBigGoalHouseModel.forward_deconv (goal.py:177-189): (depth [B,T,1,h,w],
+        mask [B,T,3,h,w], goal mask [B,T,3,h,w]) from conv_base's map, states unchanged."""
+        if not self.net.aux:
+            raise ValueError("forward_deconv needs GoalNavPolicy(aux=True)")
+        observations = inputs[0] if isinstance(inputs, tuple) and len(inputs) == 2 and \
+            isinstance(inputs[0], (tuple, list)) else inputs
+        image, goal = observations[0], observations[1]
+        lead = image.shape[:2]
+        dev = self.params.device
+        if image.dtype == torch.uint8:
+            img = image.to(dev).reshape(-1, *image.shape[2:]).contiguous()
+            gl = goal.to(dev).reshape(-1, *goal.shape[2:]).contiguous()
+        else:
+            img = image.to(dev).reshape(-1, *image.shape[2:]).float().contiguous()
+            gl = goal.to(dev).reshape(-1, *goal.shape[2:]).float().contiguous()
+        pred = _AuxDeconvFunction.apply(self.params, img, gl, self.net)  # [n, h, w, 8] NHWC
+        p = pred.permute(0, 3, 1, 2)
+        h, w = p.shape[-2:]
+        heads = tuple(p[:, o:o + c].reshape(*lead, c, h, w) for _, c, o in AUX_HEADS)
+        return heads, states

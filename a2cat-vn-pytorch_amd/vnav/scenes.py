@@ -57,6 +57,10 @@ class Scene:
     # [N,H,W,C] frames emitted as the second output for the current state instead of the goal
     # frame (OrientedGraphEnv's (rgb, third-person rgb) observation)
     companion: Optional[np.ndarray] = None
+    # auxiliary observations of GoalGymGraphAuxiliaryEnv (environments/gym_graph/graph.py:96-120):
+    # depth [N,H,W,1] and segmentation [N,H,W,3] uint8 per state
+    depth: Optional[np.ndarray] = None
+    segmentation: Optional[np.ndarray] = None
 
     @property
     def n_states(self):
@@ -78,6 +82,16 @@ class Scene:
             self.companion = np.ascontiguousarray(self.companion, dtype=np.uint8)
             if self.companion.shape != (n,) + tuple(self.frame_shape):
                 raise ValueError("companion frames must be [N,H,W,C] matching frame_shape")
+        hw = tuple(self.frame_shape[:2])
+        for name, ch in (("depth", 1), ("segmentation", 3)):
+            v = getattr(self, name)
+            if v is not None:
+                v = np.ascontiguousarray(v, dtype=np.uint8)
+                if v.ndim == 3:
+                    v = v[..., None]
+                if v.shape != (n,) + hw + (ch,):
+                    raise ValueError("%s must be [N,H,W,%d]" % (name, ch))
+                setattr(self, name, v)
 
 
 def positions(maze):
@@ -242,12 +256,14 @@ def oriented_tables(maze):
 
 
 def oriented_scene(maze, observations, goals=(), name="oriented", rewards=ORIENTED_REWARDS,
-                   tp_observations=None):
+                   tp_observations=None, depths=None, segmentations=None):
     """OrientedGraphEnv over a ThorGridWorld-style grid. observations [X, Y, 4, H, W, C]
     uint8 indexed (x, y, rotation) as ThorGridWorld.render (graph/thor_graph.py:15-18);
     tp_observations (same shape, optional) are the third-person frames render() appends
     (:26-27), emitted as the second output instead of the goal frame; goals are
-    (x, y, rotation) triples (the env's fixed goal list, graph.py:20-23).
+    (x, y, rotation) triples (the env's fixed goal list, graph.py:20-23). depths /
+    segmentations ([X, Y, 4, H, W, 1|3]) make it GoalGymGraphAuxiliaryEnv's scene
+    (graph.py:96-120: rgb, goal rgb, depth, segmentation, goal segmentation).
     Terminal steps emit the current frame (graph.py:86-88); set_complexity follows
     graph.py:51 (opt = c * (largest cell distance + 3) + 1, uniform over the starts)."""
     maze = np.asarray(maze, dtype=bool)
@@ -264,12 +280,17 @@ def oriented_scene(maze, observations, goals=(), name="oriented", rewards=ORIENT
         if tp.shape != obs.shape:
             raise ValueError("tp_observations must match observations")
         comp = np.ascontiguousarray(tp[xs, ys].reshape((-1,) + tp.shape[3:]), dtype=np.uint8)
+    aux = {}
+    for key, arr in (("depth", depths), ("segmentation", segmentations)):
+        if arr is not None:
+            a = np.asarray(arr)
+            aux[key] = np.ascontiguousarray(a[xs, ys].reshape((-1,) + a.shape[3:]), dtype=np.uint8)
     lookup = {p: i for i, p in enumerate(locs)}
     goal_states = [lookup[(int(g[0]), int(g[1]))] * 4 + int(g[2]) for g in goals]
     offset = float(base.max() + 3 - spd.max())  # c*(maxd + offset) + 1 == c*(largest + 3) + 1
     return Scene(graph=graph, spd=spd, frame_shape=tuple(frames.shape[1:]), observations=frames,
                  rewards=tuple(rewards), terminal_obs=1, curriculum=(1, offset), name=name, maze=maze,
-                 locations=locs, goals=goal_states, companion=comp)
+                 locations=locs, goals=goal_states, companion=comp, **aux)
 
 
 class _GridWorld:
@@ -304,10 +325,11 @@ class _GraphUnpickler(pickle.Unpickler):
         raise pickle.UnpicklingError("refusing to load %s.%s from a scene pickle" % (module, name))
 
 
-def load_graph_pickle(path, goals=None, name=None):
+def load_graph_pickle(path, goals=None, name=None, auxiliary=False):
     """A pickled ThorGridWorld (``~/.visual_navigation/scenes/<name>.pkl``,
-    environments/gym_graph/download.py:37-75) as an OrientedGraphEnv scene. goals default to
-    the pickle's own ``goals`` attribute (download.py:11)."""
+    environments/gym_graph/download.py:37-75) as an OrientedGraphEnv scene (or, with
+    auxiliary=True, GoalGymGraphAuxiliaryEnv's: goal frame second, depth + segmentation
+    attached). goals default to the pickle's own ``goals`` attribute (download.py:11)."""
     with open(path, "rb") as f:
         g = _GraphUnpickler(io.BytesIO(f.read())).load()
     if not isinstance(g, _GridWorld) or "_maze" not in g.__dict__ or "_observations" not in g.__dict__:
@@ -316,6 +338,9 @@ def load_graph_pickle(path, goals=None, name=None):
         goals = g.__dict__.get("goals") or []
         if isinstance(goals, tuple) and len(goals) == 3 and all(np.isscalar(v) for v in goals):
             goals = [goals]
+    if auxiliary:
+        return oriented_scene(g._maze, g._observations, goals, name=name or path, depths=g._depths,
+                              segmentations=g._segmentations)
     tp = g.__dict__.get("_tp_observations")
     if tp is not None and np.shape(tp) != np.shape(g._observations):
         tp = None  # render() would resize it to the screen size (graph/core.py:29-39): not emitted

@@ -146,6 +146,11 @@ int vn_set_autoreset(vn_ctx* ctx, int on);                /* default on */
 
 /* Synthetic uniform actions in [0,4) from Philox(seed, env, step). */
 int vn_random_actions(vn_ctx* ctx, int32_t* actions_dev, uint64_t step, vn_stream_t stream);
+/* dst[i] = src[rows[i]] (rows of row_bytes, device memory): gathers the auxiliary frames
+ * (depth, segmentation) of AuxiliaryGraph's 5-tuple observation (environments/gym_graph/
+ * graph.py:96-120) by the env's img_row/goal_row indices. */
+int vn_gather_rows(const uint8_t* src_dev, int64_t row_bytes, const int32_t* rows_dev, int n, uint8_t* dst_dev,
+                   vn_stream_t stream);
 
 /* Per-env state tensors (device, [n_envs] int32 each): for checkpoint/resume and tests.
  * Order: scene, state, goal, obs_state, elapsed, episode(reset count), sched_pos. */
@@ -230,6 +235,42 @@ int vn_lstm_backward(vn_policy* p, const float* params, int T, int E, const floa
 int vn_policy_backward_trunk(vn_policy* p, const float* params, const vn_frames* frames, int n, float* acts,
                              int64_t act_capacity, const float* dz5, float* grads, float* workspace,
                              vn_stream_t stream);
+
+/* ---- aux deconv heads: AuxiliaryBigGoalHouseModel (models/goal.py:144-189) and the
+ * auxiliary deconv loss (experiments/ai2_auxiliary/trainer.py:9-55) ----
+ * A policy created with VN_POLICY_AUX appends W1 [32][4][4][48], b1 [48] (the three heads'
+ * ConvTranspose2d(32,16,4,2) side by side: depth 0-15, mask 16-31, goal mask 32-47) and
+ * W2 [48][4][4][8], b2 [8] (ConvTranspose2d(16,C,4,2) per head, block diagonal: depth ->
+ * channel 0, mask -> 1-3, goal mask -> 4-6, 7 padding). info8 = (W1, b1, W2, b2 offsets,
+ * AH, AW = first deconv map, PH, PW = prediction map). Heads read conv_base's output (X4)
+ * from the activation store of vn_policy_forward; a1 [n][AH][AW][48], pred [n][PH][PW][8]. */
+#define VN_POLICY_AUX 2
+typedef struct vn_aux_targets {
+  const uint8_t* depth;         /* [rows][H][W][1] uint8, row-indexed like the frame arena */
+  const uint8_t* segmentation;  /* [rows][H][W][3] uint8 */
+  const int32_t* image_rows;    /* [n] row of each sample's state (vn_frames.image_rows) */
+  const int32_t* goal_rows;     /* [n] row of each sample's goal */
+  int32_t height, width;
+} vn_aux_targets;
+int vn_policy_aux_info(vn_policy* p, int64_t* info8);
+int vn_aux_workspace_floats(vn_policy* p, int64_t* floats);
+int vn_aux_forward(vn_policy* p, const float* params, float* acts, int64_t act_capacity, int n, float* a1,
+                   float* pred, float* workspace, vn_stream_t stream);
+/* targets = avg_pool(centre crop(obs/255), 4) of depth, segmentation and the goal's
+ * segmentation; dpred = weight * d(sum of per-head MSE)/dpred; stats4[0..2] += per-head
+ * sums of squared errors. */
+int vn_aux_loss_grad(vn_policy* p, const float* pred, int n, const vn_aux_targets* targets, float weight,
+                     float* dpred, float* stats4, vn_stream_t stream);
+/* Head gradients into grads and dL/dX4 [n][h3][w3][32] (before conv_base's ReLU mask) into
+ * dx4; consumes a1. */
+int vn_aux_backward(vn_policy* p, const float* params, float* acts, int64_t act_capacity, int n, float* a1,
+                    const float* dpred, float* grads, float* dx4, float* workspace, vn_stream_t stream);
+/* General backward: from dL/d(out) [n][8] (dz5 == NULL) or from dz5 [n][512] (recurrent
+ * policies, heads and LSTM done by vn_lstm_backward); dx4_extra [n][h3][w3][32] (aux heads,
+ * may be NULL) is added to conv_base's output gradient under its ReLU mask. */
+int vn_policy_backward_ex(vn_policy* p, const float* params, const vn_frames* frames, int n, float* acts,
+                          int64_t act_capacity, const float* dout, const float* dz5, const float* dx4_extra,
+                          float* grads, float* workspace, vn_stream_t stream);
 
 /* ---- A2C (the deep_rl trainer contract; DESIGN.md "A2C contract") ---- */
 int vn_policy_sample(const float* out, int n, int num_actions, uint64_t seed, uint64_t counter,

@@ -90,6 +90,56 @@ class RecurrentGoalNetOracle(GoalNetOracle):
         return self
 
 
+class AuxHeadsOracle(nn.Module):
+    """AuxiliaryBigGoalHouseModel's deconv heads (models/goal.py:144-189): from the
+    conv_base features [N,32,h3,w3], three TimeDistributed(ConvTranspose2d(32,16,4,2), ReLU,
+    ConvTranspose2d(16,C,4,2)) heads for depth (C=1), segmentation (3) and goal
+    segmentation (3). Init as init_weights (goal.py:26-30: bias 0, U(+-1/sqrt(fan_in)))."""
+
+    def __init__(self):
+        super().__init__()
+        self.heads = nn.ModuleList()
+        for c in (1, 3, 3):
+            self.heads.append(nn.Sequential(nn.ConvTranspose2d(32, 16, 4, stride=2), nn.ReLU(),
+                                            nn.ConvTranspose2d(16, c, 4, stride=2)))
+
+    def forward(self, features):
+        return tuple(h(features) for h in self.heads)
+
+    def load_reference(self, sd):
+        for h, name in zip(self.heads, ("deconv_depth", "deconv_mask", "deconv_mask_goal")):
+            for i, layer in ((1, h[0]), (3, h[2])):
+                layer.weight.data.copy_(torch.as_tensor(sd["%s.0.%d.weight" % (name, i)]))
+                layer.bias.data.copy_(torch.as_tensor(sd["%s.0.%d.bias" % (name, i)]))
+        return self
+
+
+def autocrop(x, cell, output_size):
+    """Centre crop of [..., H, W] to output_size * cell (restatement of deep_rl's
+    autocrop_observations as called at experiments/ai2_auxiliary/trainer.py:11; deep-rl is
+    absent, so the centring convention is parity unpinned)."""
+    H, W = x.shape[-2:]
+    nh, nw = output_size[0] * cell, output_size[1] * cell
+    top, left = (H - nh) // 2, (W - nw) // 2
+    return x[..., top:top + nh, left:left + nw]
+
+
+def aux_targets(depth_u8, seg_u8, goal_seg_u8, cell, output_size):
+    """compute_auxiliary_target (experiments/ai2_auxiliary/trainer.py:9-15) for the three
+    aux observations (uint8 [N,H,W,C], scaled by 1/255 as the float observation wrappers
+    do): autocrop, then avg_pool2d(cell, stride=cell) -> [N,C,oh,ow]."""
+    out = []
+    for x in (depth_u8, seg_u8, goal_seg_u8):
+        t = torch.as_tensor(x).permute(0, 3, 1, 2).to(torch.float32) / 255.0
+        out.append(F.avg_pool2d(autocrop(t, cell, output_size), cell, stride=cell))
+    return tuple(out)
+
+
+def aux_loss(predictions, targets):
+    """_deconv_loss (experiments/ai2_auxiliary/trainer.py:45-55): sum of per-head MSE."""
+    return sum(F.mse_loss(p, t) for p, t in zip(predictions, targets))
+
+
 def frames_to_float(u8):
     """uint8 [...,H,W,C] -> float32 [...,C,H,W] / 255 (TransposeImage + ScaledFloatFrame)."""
     x = torch.as_tensor(u8)
@@ -104,9 +154,17 @@ REFERENCE_PARAM_ORDER = (  # BigGoalHouseModel.named_parameters() order for the 
 )
 
 
+AUX_PARAM_ORDER = tuple("%s.0.%d.%s" % (h, i, k) for h in ("deconv_depth", "deconv_mask", "deconv_mask_goal")
+                        for i in (1, 3) for k in ("weight", "bias"))
+
+
 def reference_shapes(frame_hw=(84, 84), num_outputs=4):
     _, _, o3 = trunk_sizes(*frame_hw)
-    return {
+    aux = {}
+    for h, c in (("deconv_depth", 1), ("deconv_mask", 3), ("deconv_mask_goal", 3)):
+        aux.update({h + ".0.1.weight": (32, 16, 4, 4), h + ".0.1.bias": (16,),
+                    h + ".0.3.weight": (16, c, 4, 4), h + ".0.3.bias": (c,)})
+    return {**aux,
         "shared_base.0.0.weight": (32, 3, 7, 7), "shared_base.0.0.bias": (32,),
         "shared_base.0.2.weight": (32, 32, 4, 4), "shared_base.0.2.bias": (32,),
         "conv_base.0.0.weight": (64, 64, 4, 4), "conv_base.0.0.bias": (64,),
@@ -117,13 +175,14 @@ def reference_shapes(frame_hw=(84, 84), num_outputs=4):
     }
 
 
-def seeded_reference_state(frame_hw, seed):
-    """The weights tests/golden/gen_model_goldens.py:seeded_weights draws (PCG64)."""
+def seeded_reference_state(frame_hw, seed, aux=False):
+    """The weights tests/golden/gen_model_goldens.py:seeded_weights draws (PCG64); aux adds
+    the deconv heads (drawn after the trunk and heads, named_parameters order)."""
     import numpy as np
     rng = np.random.default_rng(seed)
     shapes = reference_shapes(frame_hw)
     out = {}
-    for name in REFERENCE_PARAM_ORDER:
+    for name in REFERENCE_PARAM_ORDER + (AUX_PARAM_ORDER if aux else ()):
         shape = shapes[name]
         if name.endswith("bias"):
             v = rng.uniform(-0.05, 0.05, size=shape)

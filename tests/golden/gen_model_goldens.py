@@ -25,7 +25,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 sys.path[:0] = [os.path.join(HERE, "stubs"), "/root/reference", REPO]
 
-from models.goal import BigGoalHouseModel  # noqa: E402  (the reference module)
+from models.goal import AuxiliaryBigGoalHouseModel, BigGoalHouseModel  # noqa: E402  (the reference modules)
 
 from oracle import a2c  # noqa: E402
 
@@ -60,13 +60,13 @@ def reference_forward(model, image_u8, goal_u8):
 USED = ("shared_base", "conv_base", "conv_merge", "policy_logits", "critic")
 
 
-def seeded_weights(model, seed):
+def seeded_weights(model, seed, used=USED):
     """Deterministic weights from numpy's PCG64 (stable across versions) in the reference's
     init distribution U(-1/sqrt(fan_in), 1/sqrt(fan_in)); lets a large case be regenerated
     from its seed instead of being stored."""
     rng = np.random.default_rng(seed)
     for name, p in model.named_parameters():
-        if name.split(".")[0] not in USED:
+        if name.split(".")[0] not in used:
             continue
         if name.endswith("bias"):
             v = rng.uniform(-0.05, 0.05, size=p.shape)
@@ -104,9 +104,52 @@ def case(frame, B, T, seed, store_weights=True):
     return out
 
 
+AUX = ("deconv_depth", "deconv_mask", "deconv_mask_goal")
+
+
+def aux_case(frame, B, T, seed):
+    """AuxiliaryBigGoalHouseModel.forward_deconv (models/goal.py:177-189) at 174x174 (the
+    reference topology: Unflatten(32, 9, 9)), weights from the seed (PCG64, trunk + deconv
+    heads). Stores the inputs, the three head outputs and, for the summed per-head MSE
+    against stored random targets (the _deconv_loss form, ai2_auxiliary/trainer.py:45-55),
+    the gradients of the deconv parameters and of the conv_base features."""
+    torch.manual_seed(seed)
+    model = AuxiliaryBigGoalHouseModel(3, 4)
+    seeded_weights(model, seed, USED + AUX)
+    rng = np.random.RandomState(seed)
+    image = torch.as_tensor(rng.randint(0, 256, size=(B, T, frame, frame, 3)).astype(np.uint8))
+    goal = torch.as_tensor(rng.randint(0, 256, size=(B, T, frame, frame, 3)).astype(np.uint8))
+    img = image.permute(0, 1, 4, 2, 3).float() / 255.0
+    gl = goal.permute(0, 1, 4, 2, 3).float() / 255.0
+    a, b = model.shared_base(img), model.shared_base(gl)
+    feats = model.conv_base(torch.cat((a, b), 2))
+    feats.retain_grad()
+    preds = (model.deconv_depth(feats), model.deconv_mask(feats), model.deconv_mask_goal(feats))
+    # forward_deconv itself must agree with the staged computation above
+    with torch.no_grad():
+        ref_preds, _ = model.forward_deconv(((img, gl), None), None, None)
+    for p, q in zip(preds, ref_preds):
+        assert torch.equal(p, q)
+    targets = [torch.as_tensor(rng.rand(*p.shape).astype(np.float32)) for p in preds]
+    loss = sum(nn.functional.mse_loss(p, t) for p, t in zip(preds, targets))
+    model.zero_grad()
+    loss.backward()
+    out = {"image": image.numpy(), "goal": goal.numpy(), "seed": np.array([seed]),
+           "features": feats.detach().numpy(), "d_features": feats.grad.numpy(),
+           "loss": np.array([loss.item()], dtype=np.float32)}
+    for k, (p, t) in enumerate(zip(preds, targets)):
+        out["pred%d" % k] = p.detach().numpy()
+        out["target%d" % k] = t.numpy()
+    for name, p in model.named_parameters():
+        if name.split(".")[0] in AUX:
+            out["g:" + name] = p.grad.numpy()
+    return out
+
+
 def main():
     np.savez_compressed(os.path.join(HERE, "policy84.npz"), **case(84, 3, 2, 11))
     np.savez_compressed(os.path.join(HERE, "policy174.npz"), **case(174, 2, 1, 12, store_weights=False))
+    np.savez_compressed(os.path.join(HERE, "aux174.npz"), **aux_case(174, 2, 1, 13))
     n_params = sum(p.numel() for n, p in build(84, 0).named_parameters() if n.split(".")[0] in USED)
     print("84x84 trunk+heads parameters:", n_params)
 

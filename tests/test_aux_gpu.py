@@ -1,0 +1,181 @@
+"""Aux deconv heads (AuxiliaryBigGoalHouseModel.forward_deconv, models/goal.py:144-189) and
+the auxiliary deconv loss (experiments/ai2_auxiliary/trainer.py:9-55) on the HIP kernels.
+Outputs rtol 1e-5 of scale, gradients rtol 1e-4 of scale (as test_policy_gpu.py):
+vs the REFERENCE modules' goldens at 174x174 (tests/golden/aux174.npz) and vs the torch
+oracle at 84x84; the fused target/MSE kernel vs oracle/policy.py aux_targets/aux_loss
+(the autocrop centring convention is deep_rl's and unpinned)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle.frames import synth_frames
+from oracle.policy import (AuxHeadsOracle, GoalNetOracle, aux_loss, aux_targets, frames_to_float,
+                           seeded_reference_state)
+
+pytestmark = pytest.mark.gpu
+
+AUX_NAMES = ("deconv_depth", "deconv_mask", "deconv_mask_goal")
+
+
+def _close(a, b, rtol, what):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    scale = max(np.abs(b).max(), 1e-30)
+    err = np.abs(a - b).max() / scale
+    assert err <= rtol, "%s: max err %.3g of scale %.3g" % (what, err, scale)
+
+
+def test_aux_heads_match_reference_174(golden):
+    from vnav.policy import GoalNavPolicy
+    d = golden("aux174.npz")
+    pol = GoalNavPolicy(3, 4, (174, 174), aux=True)
+    pol.load_reference_state_dict(seeded_reference_state((174, 174), int(d["seed"][0]), aux=True))
+    img, gl = torch.as_tensor(d["image"]).cuda(), torch.as_tensor(d["goal"]).cuda()
+    preds, _ = pol.forward_deconv(((img, gl), None), None, None)
+    for k, p in enumerate(preds):
+        _close(p.detach().cpu().numpy(), d["pred%d" % k], 1e-5, "pred%d" % k)
+    loss = sum(torch.nn.functional.mse_loss(p, torch.as_tensor(d["target%d" % k]).cuda()) for k, p in enumerate(preds))
+    np.testing.assert_allclose(loss.item(), d["loss"][0], rtol=1e-5)
+    loss.backward()
+    g = pol.net.to_reference(pol.params.grad)
+    for name in AUX_NAMES:
+        for i in (1, 3):
+            for kind in ("weight", "bias"):
+                key = "%s.0.%d.%s" % (name, i, kind)
+                _close(g[key].numpy(), d["g:" + key], 1e-4, key)
+
+
+def test_aux_grads_reach_trunk_vs_oracle_84():
+    """Random weights at 84x84 (3x3 -> 8x8 -> 18x18): every parameter gradient of the
+    summed head MSE, trunk included (dX4 enters conv_base's backward under its ReLU)."""
+    from vnav.policy import GoalNavPolicy
+    torch.manual_seed(0)
+    pol = GoalNavPolicy(3, 4, (84, 84), aux=True)
+    with torch.no_grad():
+        pol.params.add_(torch.randn_like(pol.params) * 0.01)
+        w1, b1, w2, b2 = pol.net.views(pol.params.data)["aux"]
+        mask = torch.zeros(48, 8, device=w2.device)
+        mask[0:16, 0] = 1
+        mask[16:32, 1:4] = 1
+        mask[32:48, 4:7] = 1
+        w2.mul_(mask[:, None, None, :])  # block-diagonal structure
+        b2[7] = 0.0
+    sd = pol.reference_state_dict()
+    net = GoalNetOracle((84, 84)).load_reference(sd)
+    heads = AuxHeadsOracle().load_reference(sd)
+    B, T = 3, 2
+    rng = np.random.RandomState(4)
+    img = torch.as_tensor(rng.randint(0, 256, size=(B, T, 84, 84, 3)).astype(np.uint8))
+    gl = torch.as_tensor(rng.randint(0, 256, size=(B, T, 84, 84, 3)).astype(np.uint8))
+    preds, _ = pol.forward_deconv(((img.cuda(), gl.cuda()), None))
+    targets = [torch.rand(p.shape) for p in preds]
+    loss = sum(torch.nn.functional.mse_loss(p, t.cuda()) for p, t in zip(preds, targets))
+    loss.backward()
+    import torch.nn.functional as F
+    fi, fg = frames_to_float(img.reshape(-1, 84, 84, 3)), frames_to_float(gl.reshape(-1, 84, 84, 3))
+    x = torch.cat((F.relu(net.conv2(F.relu(net.conv1(fi)))), F.relu(net.conv2(F.relu(net.conv1(fg))))), 1)
+    x4 = F.relu(net.conv4(F.relu(net.conv3(x))))
+    rp = heads(x4)
+    for p, q in zip(preds, rp):
+        _close(p.detach().cpu().reshape(q.shape), q.detach(), 1e-5, "pred")
+    rloss = aux_loss(rp, [t.reshape(q.shape) for t, q in zip(targets, rp)])
+    rloss.backward()
+    mine = pol.net.to_reference(pol.params.grad)
+    for k, mod in {"shared_base.0.0": net.conv1, "shared_base.0.2": net.conv2, "conv_base.0.0": net.conv3,
+                   "conv_base.0.2": net.conv4}.items():
+        _close(mine[k + ".weight"].numpy(), mod.weight.grad.numpy(), 1e-4, k + ".weight")
+        _close(mine[k + ".bias"].numpy(), mod.bias.grad.numpy(), 1e-4, k + ".bias")
+    for h, name in zip(heads.heads, AUX_NAMES):
+        for i, layer in ((1, h[0]), (3, h[2])):
+            _close(mine["%s.0.%d.weight" % (name, i)].numpy(), layer.weight.grad.numpy(), 1e-4, name)
+            _close(mine["%s.0.%d.bias" % (name, i)].numpy(), layer.bias.grad.numpy(), 1e-4, name)
+    # heads and conv_merge receive no gradient from the aux loss
+    assert float(mine["conv_merge.0.1.weight"].abs().max()) == 0.0
+
+
+def _aux_scene(k, frame=(84, 84, 3)):
+    import vnav
+    sc = vnav.synthetic_scene(k, frame_shape=frame)
+    n = sc.n_states
+    sc.observations = synth_frames(k, np.arange(n), frame)
+    sc.depth = synth_frames(50 + k, np.arange(n), frame[:2] + (1,))
+    sc.segmentation = synth_frames(70 + k, np.arange(n), frame[:2] + (3,))
+    sc.goals = []
+    return sc
+
+
+def test_aux_loss_kernel_vs_oracle():
+    """Fused target (centre crop + 4x4 avg pool of u8/255) + per-head MSE gradient."""
+    import vnav
+    from vnav.policy import AuxTargets, PolicyNet
+    sc = [_aux_scene(0), _aux_scene(1)]
+    env = vnav.VectorEnv(sc, 64, seed=3)
+    net = PolicyNet((84, 84), 4, aux=True)
+    n = 64
+    ph, pw = net.aux_layout["p_hw"]
+    torch.manual_seed(1)
+    pred = torch.rand((n, ph, pw, 8), device="cuda")
+    rows_i = env._info["img_row"].clone()
+    rows_g = env._info["goal_row"].clone()
+    depth, seg = env.aux_arena
+    tg = AuxTargets(depth.data_ptr(), seg.data_ptr(), rows_i.data_ptr(), rows_g.data_ptr(), 84, 84)
+    dpred = torch.empty_like(pred)
+    stats = torch.zeros(4, device="cuda")
+    w = 0.05
+    net.aux_loss_grad(pred, n, tg, w, dpred, stats)
+    torch.cuda.synchronize()
+    dd, ss = depth.cpu().numpy(), seg.cpu().numpy()
+    ri, rg = rows_i.cpu().numpy(), rows_g.cpu().numpy()
+    t = aux_targets(dd[ri], ss[ri], ss[rg], 4, (ph, pw))
+    p = pred.cpu().permute(0, 3, 1, 2).requires_grad_()
+    heads = (p[:, 0:1], p[:, 1:4], p[:, 4:7])
+    losses = [torch.nn.functional.mse_loss(h, tt) for h, tt in zip(heads, t)]
+    (w * sum(losses)).backward()
+    _close(dpred.cpu().permute(0, 3, 1, 2)[:, :7].numpy(), p.grad[:, :7].numpy(), 1e-5, "dpred")
+    assert float(dpred[..., 7].abs().max()) == 0.0
+    numel = np.array([1, 3, 3]) * n * ph * pw
+    _close(stats[:3].cpu().numpy() / numel, np.array([x.item() for x in losses]), 1e-5, "per-head MSE")
+
+
+def test_auxiliary_graph_five_tuple_observation():
+    """AuxiliaryGraph-v0 (GoalGymGraphAuxiliaryEnv.observe, environments/gym_graph/graph.py:
+    115-120): (rgb, goal rgb, depth, segmentation, goal segmentation) by state / goal row."""
+    import vnav
+    rng = np.random.RandomState(0)
+    maze = rng.rand(5, 5) > 0.2
+    maze[0, 0] = True
+    X, Y = maze.shape
+    obs = rng.randint(0, 256, size=(X, Y, 4, 16, 16, 3)).astype(np.uint8)
+    dep = rng.randint(0, 256, size=(X, Y, 4, 16, 16, 1)).astype(np.uint8)
+    seg = rng.randint(0, 256, size=(X, Y, 4, 16, 16, 3)).astype(np.uint8)
+    sc = vnav.oriented_scene(maze, obs, [(0, 0, 1)], depths=dep, segmentations=seg)
+    env = vnav.make("AuxiliaryGraph-v0", [sc], 32, seed=5)
+    o = env.reset()
+    assert len(o) == 5
+    g = sc.goals[0]
+    for t in range(20):
+        a = env.random_actions(t)
+        (img, goal, d, s, gs), _, _, info = env.step(a)
+        st = info["state"].cpu().numpy()
+        assert np.array_equal(img.cpu().numpy(), sc.observations[st])
+        assert np.array_equal(goal.cpu().numpy(), np.repeat(sc.observations[g][None], 32, 0))
+        assert np.array_equal(d.cpu().numpy(), sc.depth[st])
+        assert np.array_equal(s.cpu().numpy(), sc.segmentation[st])
+        assert np.array_equal(gs.cpu().numpy(), np.repeat(sc.segmentation[g][None], 32, 0))
+
+
+@pytest.mark.parametrize("recurrent", [False, True])
+def test_trainer_with_aux_loss(recurrent):
+    """A2CTrainer(aux_weight=0.05): the update runs heads + aux loss + backward into the
+    trunk; the aux loss falls while the heads fit the (fixed) depth/segmentation targets."""
+    import vnav
+    env = vnav.VectorEnv([_aux_scene(0)], 256, seed=2, max_episode_steps=50)
+    tr = vnav.A2CTrainer(env, num_steps=10, seed=1, max_time_steps=1e9, aux_weight=0.05, recurrent=recurrent,
+                         learning_rate=2e-3)
+    first = tr.step(sync=True)
+    for _ in range(40):
+        m = tr.step(sync=False)
+    last = tr.step(sync=True)
+    assert np.isfinite(last["aux_loss"]) and np.isfinite(last["value_loss"])
+    assert last["aux_loss"] < 0.7 * first["aux_loss"], (first["aux_loss"], last["aux_loss"])
+    assert env.error_flags() == 0

@@ -58,4 +58,28 @@ def test_recurrent_policy_layout(built_lib):
     assert lib.vn_policy_info(h, ctypes.byref(n), None, None) == 0
     assert n.value == base + 2048 * xcat + 4096
     lib.vn_policy_destroy(h)
-    assert lib.vn_policy_create_ex(84, 84, 4, 2, ctypes.byref(h)) != 0
+    assert lib.vn_policy_create_ex(84, 84, 4, 4, ctypes.byref(h)) != 0  # unknown flag
+
+
+def test_aux_policy_layout(built_lib):
+    """VN_POLICY_AUX appends the deconv heads (W1 [32][4][4][48], b1, W2 [48][4][4][8], b2);
+    maps 3x3 -> 8x8 -> 18x18 at 84x84 and 9x9 -> 20x20 -> 42x42 at 174x174 (goal.py:150-170)."""
+    from vnav import _lib
+    lib = _lib.load()
+    for hw, base, a_hw, p_hw in ((84, 239397, 8, 18), (174, None, 20, 42)):
+        h = ctypes.c_void_p()
+        n = ctypes.c_int64()
+        assert lib.vn_policy_create_ex(hw, hw, 4, 0, ctypes.byref(h)) == 0
+        assert lib.vn_policy_info(h, ctypes.byref(n), None, None) == 0
+        plain = n.value
+        lib.vn_policy_destroy(h)
+        if base is not None:
+            assert plain == base
+        assert lib.vn_policy_create_ex(hw, hw, 4, 2, ctypes.byref(h)) == 0
+        info = (ctypes.c_int64 * 8)()
+        assert lib.vn_policy_aux_info(h, info) == 0
+        w1 = plain
+        assert list(info) == [w1, w1 + 24576, w1 + 24576 + 48, w1 + 24576 + 48 + 6144, a_hw, a_hw, p_hw, p_hw]
+        assert lib.vn_policy_info(h, ctypes.byref(n), None, None) == 0
+        assert n.value == plain + 24576 + 48 + 6144 + 8
+        lib.vn_policy_destroy(h)
