@@ -403,6 +403,10 @@ inline void dgrad_all_classes(const float* dz, const float* WT, float* out, cons
   dgrad_class<COUT, CINF, H, W, OH, OW, 1, 1>(dz, WT, out, X, nimg, g, G, cin, st);
 }
 
+// Frames small enough for the LDS-staged conv1 kernels (84x84, 174x174; not 300x400).
+template <int H0, int W0>
+constexpr bool kConv1LdsFrame = (size_t)H0 * W0 * 3 <= 96 * 1024;
+
 template <int H0, int W0>
 struct Geo {
   static constexpr int OH1 = (H0 - 7) / 4 + 1, OW1 = (W0 - 7) / 4 + 1;
@@ -430,13 +434,15 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
                  hipStream_t st) {
   using G = Geo<H0, W0>;
   const int A1 = L.A + 1;
-  // conv1 (frames -> X1), 2n frames
-  if (src.f32[0] || src.f32[1]) {  // dense float frames: generic im2col path
+  // conv1 (frames -> X1), 2n frames. The specialised kernel stages whole u8 frames in LDS;
+  // dense float frames and frames too large for LDS (300x400) take the generic im2col path.
+  constexpr bool kConv1Lds = kConv1LdsFrame<H0, W0>;
+  if (!kConv1Lds || src.f32[0] || src.f32[1]) {
     FramesIm2col<H0, W0, G::OH1, G::OW1> fa{src, 2 * n * G::OH1 * G::OW1};
     DenseRows fb{P + L.l[0].w, 148, 32};
     EpiBiasAct ep{a.X[0], 32, P + L.l[0].b, 1};
     launch_gemm<64, 32, 32, 4, 1>(fa, fb, ep, fa.M, 32, 148, st);
-  } else {
+  } else if constexpr (kConv1Lds) {
     constexpr int NF = (2 * H0 * W0 * 3 <= 64 * 1024) ? 2 : 1;
     const int frames = 2 * n;
     const int blocks =
@@ -610,12 +616,13 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
     }
   }
   // ---- conv1: wgrad from dz1 (in X1's storage) and the frames
-  if (src.f32[0] || src.f32[1]) {
+  constexpr bool kConv1Lds = kConv1LdsFrame<H0, W0>;
+  if (!kConv1Lds || src.f32[0] || src.f32[1]) {
     using Im = FramesIm2col<H0, W0, G::OH1, G::OW1>;
     const int P1 = 2 * n * G::OH1 * G::OW1;
     Im2colT<Im> fbw{Im{src, P1}, 148};
     launch_wgrad<32, 64, 2, 2>(a.X[0], 32, 32, fbw, 148, P1, w.slab, w.slab_cap, Gr + L.l[0].w, Gr + L.l[0].b, st);
-  } else {
+  } else if constexpr (kConv1Lds) {
     const int frames = 2 * n;
     constexpr int CP = (G::OH1 * G::OW1 <= 400) ? (G::OH1 * G::OW1 + 7) / 8 * 8 : 448;
     constexpr size_t lds = conv1_wgrad_lds<H0, W0, CP>();
@@ -866,7 +873,23 @@ struct vn_policy {
 };
 
 namespace {
-bool supported(int H, int W) { return (H == 84 && W == 84) || (H == 174 && W == 174); }
+bool supported(int H, int W) {
+  return (H == 84 && W == 84) || (H == 174 && W == 174) || (H == 300 && W == 400);
+}
+
+template <int H_, int W_>
+struct GeoTag {
+  static constexpr int H = H_, W = W_;
+};
+
+// Call f(GeoTag<H, W>{}) for the policy's frame geometry (the instantiated set).
+template <class F>
+int dispatch_geo(const PolicyLayout& L, F&& f) {
+  if (L.H == 84 && L.W == 84) return f(GeoTag<84, 84>{});
+  if (L.H == 174 && L.W == 174) return f(GeoTag<174, 174>{});
+  if (L.H == 300 && L.W == 400) return f(GeoTag<300, 400>{});
+  return fail(VN_EINVAL, "policy: unsupported frame geometry");
+}
 
 FrameSrc to_src(const vn_frames* f) {
   FrameSrc s{};
@@ -892,7 +915,7 @@ int vn_policy_create_ex(int frame_h, int frame_w, int num_actions, int flags, vn
   if (flags & ~(VN_POLICY_LSTM | VN_POLICY_AUX)) return fail(VN_EINVAL, "vn_policy_create: unknown flags");
   *out = nullptr;
   if (!supported(frame_h, frame_w))
-    return fail(VN_EINVAL, "vn_policy_create: frame size must be 84x84 or 174x174");
+    return fail(VN_EINVAL, "vn_policy_create: frame size must be 84x84, 174x174 or 300x400");
   if (num_actions < 1 || num_actions + 1 > OUT_LD) return fail(VN_EINVAL, "vn_policy_create: 1..7 actions");
   vn_policy* p = new (std::nothrow) vn_policy();
   if (!p) return fail(VN_ENOMEM, "vn_policy_create: host allocation");
@@ -939,8 +962,9 @@ int vn_policy_forward(vn_policy* p, const float* params, const vn_frames* frames
     return fail(VN_EINVAL, "vn_policy_forward: missing frames");
   const Acts a = acts_at(p->L, acts, act_capacity, act_offset);
   hipStream_t st = (hipStream_t)stream;
-  if (p->L.H == 84) return forward_impl<84, 84>(p->L, params, src, n, a, out, st);
-  return forward_impl<174, 174>(p->L, params, src, n, a, out, st);
+  return dispatch_geo(p->L, [&](auto g) {
+    return forward_impl<decltype(g)::H, decltype(g)::W>(p->L, params, src, n, a, out, st);
+  });
 }
 
 int vn_policy_backward_ex(vn_policy* p, const float* params, const vn_frames* frames, int n, float* acts,
@@ -954,8 +978,9 @@ int vn_policy_backward_ex(vn_policy* p, const float* params, const vn_frames* fr
   const BwdWork w = carve(p->L, workspace, n);
   hipStream_t st = (hipStream_t)stream;
   const float* d = dz5 ? nullptr : dout;
-  if (p->L.H == 84) return backward_impl<84, 84>(p->L, params, src, n, a, d, dz5, dx4_extra, grads, w, st);
-  return backward_impl<174, 174>(p->L, params, src, n, a, d, dz5, dx4_extra, grads, w, st);
+  return dispatch_geo(p->L, [&](auto g) {
+    return backward_impl<decltype(g)::H, decltype(g)::W>(p->L, params, src, n, a, d, dz5, dx4_extra, grads, w, st);
+  });
 }
 
 int vn_policy_backward(vn_policy* p, const float* params, const vn_frames* frames, int n, float* acts,
@@ -996,8 +1021,9 @@ int vn_aux_forward(vn_policy* p, const float* params, float* acts, int64_t act_c
   const Acts a = acts_at(p->L, acts, act_capacity, 0);
   const AuxWork w = aux_carve(p->L, workspace);
   hipStream_t st = (hipStream_t)stream;
-  if (p->L.H == 84) return aux_forward_impl<84, 84>(p->L, params, a.X[3], n, a1, pred, w, st);
-  return aux_forward_impl<174, 174>(p->L, params, a.X[3], n, a1, pred, w, st);
+  return dispatch_geo(p->L, [&](auto g) {
+    return aux_forward_impl<decltype(g)::H, decltype(g)::W>(p->L, params, a.X[3], n, a1, pred, w, st);
+  });
 }
 
 int vn_aux_loss_grad(vn_policy* p, const float* pred, int n, const vn_aux_targets* targets, float weight,
@@ -1025,8 +1051,9 @@ int vn_aux_backward(vn_policy* p, const float* params, float* acts, int64_t act_
   const Acts a = acts_at(p->L, acts, act_capacity, 0);
   const AuxWork w = aux_carve(p->L, workspace);
   hipStream_t st = (hipStream_t)stream;
-  if (p->L.H == 84) return aux_backward_impl<84, 84>(p->L, params, a.X[3], n, a1, dpred, grads, dx4, w, st);
-  return aux_backward_impl<174, 174>(p->L, params, a.X[3], n, a1, dpred, grads, dx4, w, st);
+  return dispatch_geo(p->L, [&](auto g) {
+    return aux_backward_impl<decltype(g)::H, decltype(g)::W>(p->L, params, a.X[3], n, a1, dpred, grads, dx4, w, st);
+  });
 }
 
 int vn_policy_lstm_info(vn_policy* p, int64_t* info8) {
