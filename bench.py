@@ -30,6 +30,9 @@ import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 FP32_MFMA_PEAK_TFLOPS = 157.3  # dense f32 MFMA = f32 vector peak (MI355X_MICROARCH.md)
+# the reference's only throughput record: deep_rl fps of thor-cached-auxiliary (174x174, LSTM +
+# aux deconv, 4 envs, 1 GPU), steady-state median, BASELINE.md §2 / outputs/output.txt
+REFERENCE_LOG_FPS = 106.0
 
 
 def alg_bytes_per_env_step(frame_bytes):
@@ -49,6 +52,9 @@ def parse():
     p.add_argument("--train-steps", type=int, default=6, help="timed A2C updates (0 = skip the train leg)")
     p.add_argument("--train-warmup", type=int, default=2)
     p.add_argument("--no-train-ff", action="store_true", help="skip the feed-forward (no LSTM) train leg")
+    p.add_argument("--no-train-ref", action="store_true",
+                   help="skip the 174x174 LSTM + aux-deconv train leg (the reference's logged experiment shape)")
+    p.add_argument("--c5", action="store_true", help="add the 300x400 + goal + aux-depth train leg (config C5)")
     p.add_argument("--num-steps", type=int, default=20, help="A2C rollout length (reference: 20)")
     p.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
     p.add_argument("--dist-backend", default="nccl", help="torch.distributed backend (nccl = RCCL on ROCm)")
@@ -100,7 +106,17 @@ def pmc_traffic(envs, scenes):
                                        "source": "live rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes"}
 
 
-def train_flops_per_env_step(h=84, w=84, A=4, T=20, recurrent=False):
+def aux_flops_per_sample(o3):
+    """Algorithmic FLOPs of the deconv heads per sample (forward + both gradients): first
+    layer 32 -> 3x16 over 2x2 taps per output pixel, second layer 16 -> (1, 3, 3) per head."""
+    ah, aw = 2 * o3[0] + 2, 2 * o3[1] + 2
+    ph, pw = 2 * ah + 2, 2 * aw + 2
+    l1 = ah * aw * 48 * 4 * 32                      # MACs, forward (= dX4 = wgrad)
+    l2 = ph * pw * 7 * 4 * 16                       # MACs, forward (= dA1 = wgrad)
+    return 2 * 3 * (l1 + l2)
+
+
+def train_flops_per_env_step(h=84, w=84, A=4, T=20, recurrent=False, aux=False):
     """Algorithmic FLOPs of one A2C env-step: policy forward (kept activations serve the
     backward), weight gradients of every layer, input gradients of all but conv1, and the
     bootstrap forward amortised over the rollout."""
@@ -112,25 +128,45 @@ def train_flops_per_env_step(h=84, w=84, A=4, T=20, recurrent=False):
     if recurrent:  # LSTM gates GEMM [xcat=512+A+1 padded to 4, +512] x 2048: fwd, dgrad, wgrad
         macs.append(2048 * ((512 + A + 1 + 3) // 4 * 4 + 512))
     fwd = 2 * sum(macs)
-    return fwd + fwd + 2 * sum(macs[1:]) + fwd / T, fwd
+    total = fwd + fwd + 2 * sum(macs[1:]) + fwd / T
+    if aux:
+        total += aux_flops_per_sample(o3)
+    return total, fwd
 
 
-def bench_train(args, scenes, dev, world, rank, recurrent):
+def aux_scenes(n, frame, seed=0):
+    """Synthetic scenes with depth + segmentation frames (AuxiliaryGraph / config C5 data)."""
+    import vnav
+    out = []
+    rng = np.random.default_rng(seed)
+    for k in range(n):
+        sc = vnav.synthetic_scene(k, frame_shape=frame)
+        sc.depth = rng.integers(0, 256, size=(sc.n_states,) + frame[:2] + (1,), dtype=np.uint8)
+        sc.segmentation = rng.integers(0, 256, size=(sc.n_states,) + frame[:2] + (3,), dtype=np.uint8)
+        sc.__post_init__()
+        out.append(sc)
+    return out
+
+
+def bench_train(args, scenes, dev, world, rank, recurrent, aux_weight=0.0, envs=None, updates=None, warmup=None,
+                model=None):
     """A2C training throughput: one step = rollout of num_steps on every local env (policy
     forward + sampling + env step) + backward + one RCCL all-reduce of the flat gradient +
     clip + RMSprop. recurrent: the full BigGoalHouseModel (LSTM core, BPTT over the rollout);
-    else the feed-forward trunk + heads."""
+    else the feed-forward trunk + heads. aux_weight > 0 adds the deconv heads + aux loss."""
     import vnav
-    E, T = args.envs, args.num_steps
+    E, T = envs or args.envs, args.num_steps
+    updates = updates or args.train_steps
+    warmup = args.train_warmup if warmup is None else warmup
     env = vnav.VectorEnv(scenes, E, seed=2000 + rank, device=dev)
-    tr = vnav.A2CTrainer(env, num_steps=T, seed=7, max_time_steps=1e12, recurrent=recurrent)
-    for _ in range(args.train_warmup):
+    tr = vnav.A2CTrainer(env, num_steps=T, seed=7, max_time_steps=1e12, recurrent=recurrent, aux_weight=aux_weight)
+    for _ in range(warmup):
         tr.step(sync=False)
     torch.cuda.synchronize(dev)
     if world > 1:
         torch.distributed.barrier()
     t0 = time.perf_counter()
-    for _ in range(args.train_steps):
+    for _ in range(updates):
         tr.step(sync=False)
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -140,12 +176,15 @@ def bench_train(args, scenes, dev, world, rank, recurrent):
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         el = float(t[0])
-    steps = E * T * args.train_steps * world
-    flops, fwd = train_flops_per_env_step(T=T, recurrent=recurrent)
-    tflops = E * T * args.train_steps * flops / el / 1e12
-    res = {"model": "BigGoalHouseModel (LSTM core)" if recurrent else "BigGoalHouseModel trunk + heads (no LSTM)",
-           "value": steps / el, "unit": "env-steps/s", "updates": args.train_steps, "envs_per_gpu": E,
-           "num_steps": T, "ms_per_update": el / args.train_steps * 1e3, "dtype": "f32",
+    steps = E * T * updates * world
+    h, w = env.frame_shape[:2]
+    flops, fwd = train_flops_per_env_step(h, w, T=T, recurrent=recurrent, aux=aux_weight > 0)
+    tflops = E * T * updates * flops / el / 1e12
+    if model is None:
+        model = "BigGoalHouseModel (LSTM core)" if recurrent else "BigGoalHouseModel trunk + heads (no LSTM)"
+    res = {"model": model, "frame": [h, w, 3],
+           "value": steps / el, "unit": "env-steps/s", "updates": updates, "envs_per_gpu": E,
+           "num_steps": T, "ms_per_update": el / updates * 1e3, "dtype": "f32",
            "roofline": {"bound": "mfma", "achieved": tflops, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                         "frac": tflops / FP32_MFMA_PEAK_TFLOPS, "flops_per_env_step": flops,
                         "scope": "whole update (all kernels), algorithmic FLOPs"}}
@@ -268,13 +307,27 @@ def main():
         elapsed, kern_ms = float(t[0]), float(t[1])
     flags = env.error_flags()
     del env, out
-    train = train_ff = None
+    train = train_ff = train_ref = train_c5 = None
     if args.train_steps > 0:
         torch.cuda.empty_cache()
         train = bench_train(args, scenes, dev, world, rank, recurrent=True)
         torch.cuda.empty_cache()
         if not args.no_train_ff:
             train_ff = bench_train(args, scenes, dev, world, rank, recurrent=False)
+            torch.cuda.empty_cache()
+        if not args.no_train_ref:
+            # thor-cached-auxiliary as logged (outputs/output.txt): 174x174 scenes, LSTM policy,
+            # aux deconv loss (weight 0.05, ai2_auxiliary/trainer.py:25), 4 scenes
+            train_ref = bench_train(args, aux_scenes(4, (174, 174, 3)), dev, world, rank, recurrent=True,
+                                    aux_weight=0.05, updates=3, warmup=1,
+                                    model="AuxiliaryBigGoalHouseModel (LSTM + deconv heads), 174x174")
+            train_ref["reference_log_fps"] = REFERENCE_LOG_FPS
+            torch.cuda.empty_cache()
+        if args.c5:
+            train_c5 = bench_train(args, aux_scenes(4, (300, 400, 3)), dev, world, rank, recurrent=True,
+                                   aux_weight=0.05, envs=512, updates=3, warmup=1,
+                                   model="AuxiliaryBigGoalHouseModel (LSTM + deconv heads), 300x400 (config C5)")
+            torch.cuda.empty_cache()
     if rank == 0:
         env_steps = E * K * world
         value = env_steps / elapsed
@@ -309,6 +362,8 @@ def main():
             "cpu_baseline": cpu,
             "train": train,
             "train_feedforward": train_ff,
+            "train_174_lstm_aux": train_ref,
+            **({"train_c5_300x400": train_c5} if train_c5 else {}),
             "error_flags": flags,
         }
         print(json.dumps(line))
