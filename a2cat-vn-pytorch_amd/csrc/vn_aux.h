@@ -62,24 +62,25 @@ __global__ void aux_blockdiag_mask_kernel(float* __restrict__ dW2) {
   if (aux_head_of_out(co) != ci / 16) dW2[idx] = 0.0f;
 }
 
-// Column sums of src [rows][cols] (cols <= 64), deterministic: per-block partials, then a
-// fixed-order reduce.
-__global__ void colsum_partial_kernel(const float* __restrict__ src, int64_t rows, int cols,
-                                      float* __restrict__ partial) {
-  __shared__ float sh[256];
-  const int c = threadIdx.x % cols;
-  const int lanes = blockDim.x / cols;  // row lanes per block
-  const int l = threadIdx.x / cols;
-  float s = 0.0f;
+// Column sums of src [rows][cols] (cols in {8, 16, 32, 48, 64}), deterministic: each
+// thread owns 4 consecutive columns of a row group and streams 16-B loads down the rows;
+// per-block partials are reduced in a fixed order.
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __restrict__ src, int64_t rows, int cols,
+                                                             float* __restrict__ partial) {
+  __shared__ f4 sh[256];
+  const int q = cols / 4;                 // float4 columns
+  const int lanes = 256 / q;              // row lanes per block
+  const int c4 = threadIdx.x % q, l = threadIdx.x / q;
+  f4 s = f4zero();
   if (l < lanes)
     for (int64_t r = (int64_t)blockIdx.x * lanes + l; r < rows; r += (int64_t)gridDim.x * lanes)
-      s += src[r * cols + c];
-  sh[threadIdx.x] = (l < lanes) ? s : 0.0f;
+      s += *reinterpret_cast<const f4*>(src + r * cols + c4 * 4);
+  sh[threadIdx.x] = (l < lanes) ? s : f4zero();
   __syncthreads();
-  if (threadIdx.x < cols) {
-    float t = 0.0f;
-    for (int j = 0; j < lanes; ++j) t += sh[j * cols + threadIdx.x];
-    partial[(int64_t)blockIdx.x * cols + threadIdx.x] = t;
+  if (threadIdx.x < q) {
+    f4 t = f4zero();
+    for (int j = 0; j < lanes; ++j) t += sh[j * q + threadIdx.x];
+    *reinterpret_cast<f4*>(partial + (int64_t)blockIdx.x * cols + threadIdx.x * 4) = t;
   }
 }
 
@@ -91,59 +92,82 @@ __global__ void colsum_final_kernel(const float* __restrict__ partial, int block
   out[c] = t;
 }
 
-struct AuxTargets {
-  const uint8_t* depth;   // [rows][H][W][1]
-  const uint8_t* seg;     // [rows][H][W][3]
-  const int32_t* img_rows;
-  const int32_t* goal_rows;
-  int H, W;
-};
-
-// Targets = avg_pool(centre crop(obs / 255), 4) (trainer.py:9-15) fused with the per-head
-// MSE gradient: dP = weight * 2 (P - target) / numel(head); stats[h] += sum (P - target)^2.
-__global__ void aux_loss_grad_kernel(int n, int PH, int PW, const float* __restrict__ P, AuxTargets tg, float weight,
-                                     float* __restrict__ dP, float* __restrict__ stats) {
+// Per-state target table (built once per scene cache): for every arena row and prediction
+// pixel, (depth, seg0, seg1, seg2) = avg_pool(centre crop(obs / 255), 4)
+// (compute_auxiliary_target, trainer.py:9-15). The goal segmentation target of a sample is
+// the seg part of its goal row's entry.
+__global__ void aux_target_table_kernel(const uint8_t* __restrict__ depth, const uint8_t* __restrict__ seg, int H,
+                                        int W, int64_t n_rows, int PH, int PW, f4* __restrict__ table) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n_rows * PH * PW) return;
+  const int64_t row = idx / (PH * PW);
+  const int pix = (int)(idx - row * PH * PW);
+  const int oy = pix / PW, ox = pix - (pix / PW) * PW;
+  const int top = (H - PH * kAuxCell) / 2, left = (W - PW * kAuxCell) / 2;
+  const int64_t HW = (int64_t)H * W;
+  const uint8_t* d = depth + row * HW;
+  const uint8_t* s = seg + row * HW * 3;
+  float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  for (int dy = 0; dy < kAuxCell; ++dy) {
+    const int64_t rp = (int64_t)(top + oy * kAuxCell + dy) * W + left + ox * kAuxCell;
+    for (int dx = 0; dx < kAuxCell; ++dx) {
+      acc[0] += (float)d[rp + dx];
+      for (int c = 0; c < 3; ++c) acc[1 + c] += (float)s[(rp + dx) * 3 + c];
+    }
+  }
+  constexpr float k = (1.0f / 255.0f) * (1.0f / (kAuxCell * kAuxCell));
+  table[idx] = f4{acc[0] * k, acc[1] * k, acc[2] * k, acc[3] * k};
+}
+
+// Per-head MSE gradient against the table: dP = weight * 2 (P - target) / numel(head);
+// stats[h] += sum (P - target)^2. Grid-stride over (sample, pixel): 2 x 16-B pred loads,
+// 16-B target loads from the image row and the goal row, 2 x 16-B gradient stores; the
+// statistics are reduced per workgroup (one atomic per workgroup and head).
+constexpr int kAuxLossBlocks = 2048;
+
+__global__ __launch_bounds__(256) void aux_loss_grad_kernel(int n, int PH, int PW, const float* __restrict__ P,
+                                                            const f4* __restrict__ table,
+                                                            const int32_t* __restrict__ img_rows,
+                                                            const int32_t* __restrict__ goal_rows, float weight,
+                                                            float* __restrict__ dP, float* __restrict__ stats) {
+  __shared__ float red[3][4];
   float sq[3] = {0.0f, 0.0f, 0.0f};
-  if (idx < (int64_t)n * PH * PW) {
+  const int64_t total = (int64_t)n * PH * PW;
+  const float inv[3] = {2.0f * weight / ((float)n * PH * PW), 2.0f * weight / (3.0f * n * PH * PW),
+                        2.0f * weight / (3.0f * n * PH * PW)};
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
     const int e = (int)(idx / (PH * PW));
     const int pix = (int)(idx - (int64_t)e * PH * PW);
-    const int oy = pix / PW, ox = pix - (pix / PW) * PW;
-    const int top = (tg.H - PH * kAuxCell) / 2, left = (tg.W - PW * kAuxCell) / 2;
-    const int64_t HW = (int64_t)tg.H * tg.W;
-    const uint8_t* dsrc = tg.depth + (int64_t)tg.img_rows[e] * HW;
-    const uint8_t* ssrc = tg.seg + (int64_t)tg.img_rows[e] * HW * 3;
-    const uint8_t* gsrc = tg.seg + (int64_t)tg.goal_rows[e] * HW * 3;
-    float acc[7] = {0, 0, 0, 0, 0, 0, 0};
-    for (int dy = 0; dy < kAuxCell; ++dy) {
-      const int64_t rowp = (int64_t)(top + oy * kAuxCell + dy) * tg.W + left + ox * kAuxCell;
-      for (int dx = 0; dx < kAuxCell; ++dx) {
-        const int64_t p = rowp + dx;
-        acc[0] += (float)dsrc[p];
-        for (int c = 0; c < 3; ++c) {
-          acc[1 + c] += (float)ssrc[p * 3 + c];
-          acc[4 + c] += (float)gsrc[p * 3 + c];
-        }
-      }
-    }
-    const float* pr = P + idx * kAuxC2;
-    float* dp = dP + idx * kAuxC2;
-    const float numel[3] = {(float)n * PH * PW, 3.0f * n * PH * PW, 3.0f * n * PH * PW};
+    const f4 ti = table[(int64_t)img_rows[e] * PH * PW + pix];
+    const f4 tg = table[(int64_t)goal_rows[e] * PH * PW + pix];
+    const f4 p0 = *reinterpret_cast<const f4*>(P + idx * kAuxC2);
+    const f4 p1 = *reinterpret_cast<const f4*>(P + idx * kAuxC2 + 4);
+    const float pr[7] = {p0[0], p0[1], p0[2], p0[3], p1[0], p1[1], p1[2]};
+    const float t[7] = {ti[0], ti[1], ti[2], ti[3], tg[1], tg[2], tg[3]};
+    float g[8];
+#pragma unroll
     for (int c = 0; c < 7; ++c) {
-      // avg_pool2d of x/255: sum / 16 of the float values (the reference divides first)
-      const float t = acc[c] * (1.0f / 255.0f) * (1.0f / (kAuxCell * kAuxCell));
-      const float d = pr[c] - t;
+      const float d = pr[c] - t[c];
       const int h = c == 0 ? 0 : (c <= 3 ? 1 : 2);
       sq[h] += d * d;
-      dp[c] = weight * 2.0f * d / numel[h];
+      g[c] = d * inv[h];
     }
-    dp[7] = 0.0f;
+    g[7] = 0.0f;
+    *reinterpret_cast<f4*>(dP + idx * kAuxC2) = f4{g[0], g[1], g[2], g[3]};
+    *reinterpret_cast<f4*>(dP + idx * kAuxC2 + 4) = f4{g[4], g[5], g[6], g[7]};
   }
-  // wave reduction of the statistics, one atomic per wave and head
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
   for (int h = 0; h < 3; ++h) {
     float v = sq[h];
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    if ((threadIdx.x & 63) == 0 && v != 0.0f) atomicAdd(stats + h, v);
+    if (lane == 0) red[h][wave] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    const float v = red[threadIdx.x][0] + red[threadIdx.x][1] + red[threadIdx.x][2] + red[threadIdx.x][3];
+    if (v != 0.0f) atomicAdd(stats + threadIdx.x, v);
   }
 }
 

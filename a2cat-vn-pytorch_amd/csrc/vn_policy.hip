@@ -1026,19 +1026,32 @@ int vn_aux_forward(vn_policy* p, const float* params, float* acts, int64_t act_c
   });
 }
 
+int vn_aux_target_table(vn_policy* p, const uint8_t* depth, const uint8_t* segmentation, int height, int width,
+                        int64_t n_rows, float* table, vn_stream_t stream) {
+  if (!p || !p->L.aux || !depth || !segmentation || !table || n_rows <= 0)
+    return fail(VN_EINVAL, "vn_aux_target_table: bad args");
+  const PolicyLayout& L = p->L;
+  if (height < L.PH * kAuxCell || width < L.PW * kAuxCell)
+    return fail(VN_EINVAL, "vn_aux_target_table: frames smaller than the crop");
+  const int64_t total = n_rows * L.PH * L.PW;
+  hipLaunchKernelGGL(aux_target_table_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, depth, segmentation, height, width, n_rows, L.PH, L.PW,
+                     reinterpret_cast<f4*>(table));
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
+
 int vn_aux_loss_grad(vn_policy* p, const float* pred, int n, const vn_aux_targets* targets, float weight,
                      float* dpred, float* stats4, vn_stream_t stream) {
-  if (!p || !p->L.aux || !pred || !targets || !dpred || !stats4 || n <= 0 || !targets->depth ||
-      !targets->segmentation || !targets->image_rows || !targets->goal_rows)
+  if (!p || !p->L.aux || !pred || !targets || !dpred || !stats4 || n <= 0 || !targets->table ||
+      !targets->image_rows || !targets->goal_rows)
     return fail(VN_EINVAL, "vn_aux_loss_grad: bad args");
   const PolicyLayout& L = p->L;
-  if (targets->height < L.PH * kAuxCell || targets->width < L.PW * kAuxCell)
-    return fail(VN_EINVAL, "vn_aux_loss_grad: target frames smaller than the crop");
-  AuxTargets tg{targets->depth, targets->segmentation, targets->image_rows, targets->goal_rows, targets->height,
-                targets->width};
   const int64_t total = (int64_t)n * L.PH * L.PW;
-  hipLaunchKernelGGL(aux_loss_grad_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                     n, L.PH, L.PW, pred, tg, weight, dpred, stats4);
+  const unsigned blocks = (unsigned)std::min<int64_t>(kAuxLossBlocks, (total + 255) / 256);
+  hipLaunchKernelGGL(aux_loss_grad_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                     n, L.PH, L.PW, pred, reinterpret_cast<const f4*>(targets->table), targets->image_rows,
+                     targets->goal_rows, weight, dpred, stats4);
   VN_HIP(hipGetLastError());
   return VN_OK;
 }

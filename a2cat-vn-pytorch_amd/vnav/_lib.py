@@ -94,6 +94,7 @@ SIGNATURES.update({
     "vn_aux_workspace_floats": (c_int, [c_void_p, P(c_int64)]),
     "vn_aux_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p,
                                c_void_p]),
+    "vn_aux_target_table": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int64, c_void_p, c_void_p]),
     "vn_aux_loss_grad": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_float, c_void_p, c_void_p, c_void_p]),
     "vn_aux_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p,
                                 c_void_p, c_void_p, c_void_p]),

@@ -119,9 +119,9 @@ class A2CTrainer:
             self.aux_stats = torch.zeros(4, dtype=torch.float32, **kw)
             self.aux_ws = torch.empty(self.net.aux_workspace_floats(), dtype=torch.float32, **kw)
             from .policy import AuxTargets
-            depth, seg = env.aux_arena
-            self._aux_targets = AuxTargets(depth.data_ptr(), seg.data_ptr(), self.rows_img.data_ptr(),
-                                           self.rows_goal.data_ptr(), env.frame_shape[0], env.frame_shape[1])
+            self.aux_table = self.net.aux_target_table(*env.aux_arena)  # once per scene cache
+            self._aux_targets = AuxTargets(self.aux_table.data_ptr(), self.rows_img.data_ptr(),
+                                           self.rows_goal.data_ptr())
         arena, fb, _, _ = env.frame_arena()
         self._arena, self._fb = arena, fb
         env.observe(gather=False)  # refresh the obs row buffers for the first forward

@@ -62,8 +62,7 @@ def trunk_sizes(h, w):
 
 class AuxTargets(ctypes.Structure):
     """vn_aux_targets (include/vnav.h)."""
-    _fields_ = [("depth", ctypes.c_void_p), ("segmentation", ctypes.c_void_p), ("image_rows", ctypes.c_void_p),
-                ("goal_rows", ctypes.c_void_p), ("height", ctypes.c_int32), ("width", ctypes.c_int32)]
+    _fields_ = [("table", ctypes.c_void_p), ("image_rows", ctypes.c_void_p), ("goal_rows", ctypes.c_void_p)]
 
 
 AUX_HEADS = (("deconv_depth", 1, 0), ("deconv_mask", 3, 1), ("deconv_mask_goal", 3, 4))  # name, C, first out ch
@@ -298,6 +297,16 @@ class PolicyNet:
         P = _lib.ptr
         _lib.check(self.lib.vn_aux_forward(self._h, P(params), P(acts), int(capacity), int(n), P(a1), P(pred),
                                            P(workspace), _lib.stream_ptr(self.device)), "vn_aux_forward")
+
+    def aux_target_table(self, depth, segmentation):
+        """[rows, PH, PW, 4] float targets from the env's aux arena (depth, segmentation)."""
+        rows, H, W = depth.shape[:3]
+        ph, pw = self.aux_layout["p_hw"]
+        table = torch.empty((rows, ph, pw, 4), dtype=torch.float32, device=self.device)
+        _lib.check(self.lib.vn_aux_target_table(self._h, _lib.ptr(depth), _lib.ptr(segmentation), int(H), int(W),
+                                                int(rows), _lib.ptr(table), _lib.stream_ptr(self.device)),
+                   "vn_aux_target_table")
+        return table
 
     def aux_loss_grad(self, pred, n, targets, weight, dpred, stats):
         P = _lib.ptr

@@ -246,19 +246,22 @@ int vn_policy_backward_trunk(vn_policy* p, const float* params, const vn_frames*
  * from the activation store of vn_policy_forward; a1 [n][AH][AW][48], pred [n][PH][PW][8]. */
 #define VN_POLICY_AUX 2
 typedef struct vn_aux_targets {
-  const uint8_t* depth;         /* [rows][H][W][1] uint8, row-indexed like the frame arena */
-  const uint8_t* segmentation;  /* [rows][H][W][3] uint8 */
+  const float* table;           /* [rows][PH][PW][4] from vn_aux_target_table */
   const int32_t* image_rows;    /* [n] row of each sample's state (vn_frames.image_rows) */
   const int32_t* goal_rows;     /* [n] row of each sample's goal */
-  int32_t height, width;
 } vn_aux_targets;
 int vn_policy_aux_info(vn_policy* p, int64_t* info8);
 int vn_aux_workspace_floats(vn_policy* p, int64_t* floats);
 int vn_aux_forward(vn_policy* p, const float* params, float* acts, int64_t act_capacity, int n, float* a1,
                    float* pred, float* workspace, vn_stream_t stream);
-/* targets = avg_pool(centre crop(obs/255), 4) of depth, segmentation and the goal's
- * segmentation; dpred = weight * d(sum of per-head MSE)/dpred; stats4[0..2] += per-head
- * sums of squared errors. */
+/* Per-state targets, built once per scene cache: table [n_rows][PH][PW][4] = (depth, seg0-2)
+ * of avg_pool(centre crop(obs/255), 4) (compute_auxiliary_target, trainer.py:9-15) from the
+ * depth [rows][H][W][1] and segmentation [rows][H][W][3] arenas (row-indexed like the frame
+ * arena). */
+int vn_aux_target_table(vn_policy* p, const uint8_t* depth, const uint8_t* segmentation, int height, int width,
+                        int64_t n_rows, float* table, vn_stream_t stream);
+/* dpred = weight * d(sum of per-head MSE)/dpred against the image row's (depth, seg) and the
+ * goal row's seg targets; stats4[0..2] += per-head sums of squared errors. */
 int vn_aux_loss_grad(vn_policy* p, const float* pred, int n, const vn_aux_targets* targets, float weight,
                      float* dpred, float* stats4, vn_stream_t stream);
 /* Head gradients into grads and dL/dX4 [n][h3][w3][32] (before conv_base's ReLU mask) into

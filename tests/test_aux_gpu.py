@@ -118,7 +118,8 @@ def test_aux_loss_kernel_vs_oracle():
     rows_i = env._info["img_row"].clone()
     rows_g = env._info["goal_row"].clone()
     depth, seg = env.aux_arena
-    tg = AuxTargets(depth.data_ptr(), seg.data_ptr(), rows_i.data_ptr(), rows_g.data_ptr(), 84, 84)
+    table = net.aux_target_table(depth, seg)
+    tg = AuxTargets(table.data_ptr(), rows_i.data_ptr(), rows_g.data_ptr())
     dpred = torch.empty_like(pred)
     stats = torch.zeros(4, device="cuda")
     w = 0.05
