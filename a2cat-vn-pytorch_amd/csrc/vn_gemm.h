@@ -2,7 +2,8 @@
 //
 // C[M][N] = sum_k A[m][k] * B[k][n], one 256-thread workgroup (4 waves, WM x WN) per
 // BM x BN tile and K range. Both operands are staged in LDS k-contiguous
-// ([row][k], row stride BK+4 floats) by loader functors that gather them straight
+// ([row][k], row stride BK+8 floats: with it the four 16-lane groups of a
+// ds_read_b128 hit 16 distinct 4-bank slots, MI355X_MICROARCH.md §LDS) by loader functors that gather them straight
 // from their producers (im2col of NHWC activations, uint8 frames addressed through
 // scene-cache rows, transposed weights, ...): fetch() issues the next K tile's global
 // loads into registers before the current tile's MFMAs, commit() writes them to LDS
@@ -17,6 +18,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace vn {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
@@ -27,7 +30,9 @@ template <int BM, int BN, int BK, int WM, int WN, class FA, class FB, class EP>
 __global__ __launch_bounds__(256) void gemm_kernel(FA fa, FB fb, EP ep, int M, int N, int K, int kchunk) {
   static_assert(WM * WN == 4, "4 waves per workgroup");
   static_assert(BK % 16 == 0, "BK multiple of 16");
-  constexpr int LD = BK + 4;
+  // LDS row stride: BK+8 makes the ds_read_b128 groups conflict-free; transposed fills
+  // (wgrad) need BK+4 for conflict-free scalar writes (fetch_trans)
+  constexpr int LD = (FA::kTrans || FB::kTrans) ? BK + 4 : BK + 8;
   constexpr int TM = BM / (WM * 16), TN = BN / (WN * 16);
   static_assert(TM >= 1 && TN >= 1, "tile too small for the wave layout");
   constexpr int NA = (FA::template slots<BM, BK>() + 255) / 256;
@@ -53,8 +58,8 @@ __global__ __launch_bounds__(256) void gemm_kernel(FA fa, FB fb, EP ep, int M, i
     fb.template fetch<BN, BK>(pb, n0, kb, ke, tid);
   }
   for (int k0 = kb; k0 < ke; k0 += BK) {
-    FA::template commit<BM, BK>(pa, As, tid);
-    FB::template commit<BN, BK>(pb, Bs, tid);
+    FA::template commit<BM, BK, LD>(pa, As, tid);
+    FB::template commit<BN, BK, LD>(pb, Bs, tid);
     __syncthreads();
     if (k0 + BK < ke) {
       fa.template fetch<BM, BK>(pa, m0, k0 + BK, ke, tid);
@@ -89,11 +94,104 @@ __global__ __launch_bounds__(256) void gemm_kernel(FA fa, FB fb, EP ep, int M, i
       }
 }
 
+// Same core on v_mfma_f32_32x32x2_f32 (64-cycle issue = 64-cycle latency: one accumulator
+// chain per 32x32 block runs at the full rate). Lane l reads 4 consecutive k of row l&31
+// at k offset 4*(l>>5) (ds_read_b128); MFMA j of a group covers k = {j, 4+j}. With the
+// row stride BK+4 the four 16-lane groups of a ds_read_b128 hit 16 distinct 4-bank slots.
+// C layout: row = (r&3) + 8*(r>>2) + 4*(l>>5), col = l&31.
+template <int BM, int BN, int BK, int WM, int WN, class FA, class FB, class EP>
+__global__ __launch_bounds__(256) void gemm32_kernel(FA fa, FB fb, EP ep, int M, int N, int K, int kchunk) {
+  static_assert(WM * WN == 4, "4 waves per workgroup");
+  static_assert(BK % 8 == 0, "BK multiple of 8");
+  constexpr int LD = BK + 4;
+  constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
+  static_assert(TM >= 1 && TN >= 1, "tile too small for the wave layout");
+  constexpr int NA = (FA::template slots<BM, BK>() + 255) / 256;
+  constexpr int NB = (FB::template slots<BN, BK>() + 255) / 256;
+  __shared__ __attribute__((aligned(16))) float As[BM * LD];
+  __shared__ __attribute__((aligned(16))) float Bs[BN * LD];
+  typedef float f16v_ __attribute__((ext_vector_type(16)));
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WM, wn = wave / WM;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int kb = blockIdx.z * kchunk;
+  const int ke = min(K, kb + kchunk);
+  f16v_ acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+  const int ra = (wm * TM * 32 + (lane & 31)) * LD + 4 * (lane >> 5);
+  const int rb = (wn * TN * 32 + (lane & 31)) * LD + 4 * (lane >> 5);
+  f4 pa[NA], pb[NB];
+  if (kb < ke) {
+    fa.template fetch<BM, BK>(pa, m0, kb, ke, tid);
+    fb.template fetch<BN, BK>(pb, n0, kb, ke, tid);
+  }
+  for (int k0 = kb; k0 < ke; k0 += BK) {
+    FA::template commit<BM, BK, LD>(pa, As, tid);
+    FB::template commit<BN, BK, LD>(pb, Bs, tid);
+    __syncthreads();
+    if (k0 + BK < ke) {
+      fa.template fetch<BM, BK>(pa, m0, k0 + BK, ke, tid);
+      fb.template fetch<BN, BK>(pb, n0, k0 + BK, ke, tid);
+    }
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 8) {
+      f4 a[TM], b[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a[i] = *reinterpret_cast<const f4*>(&As[ra + i * 32 * LD + kk]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) b[j] = *reinterpret_cast<const f4*>(&Bs[rb + j * 32 * LD + kk]);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][q], b[j][q], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int col = n0 + wn * TN * 32 + j * 32 + (lane & 31);
+        if (row < M && col < N) ep(row, col, acc[i][j][r], (int)blockIdx.z);
+      }
+}
+
 // ---- fill helpers: fetch (global -> registers) then commit (registers -> LDS) ----
+// A loader with load4_fast(row, k) (no bounds checks) gets it for tiles wholly inside
+// its rows and the K range (a wave-uniform test): the common case issues plain 16-B loads.
+template <class L, class = void>
+struct has_fast_load : std::false_type {};
+template <class L>
+struct has_fast_load<L, std::void_t<decltype(&L::load4_fast)>> : std::true_type {};
+
 // Row-major source: L::load4(row, k, kend) -> 4 consecutive k of one row (zeros past kend).
 template <int ROWS, int BK, class L>
 __device__ __forceinline__ void fetch_rows(const L& l, f4* r, int row0, int k0, int kend, int tid) {
   constexpr int Q = BK / 4, T = ROWS * Q, NS = (T + 255) / 256;
+  if constexpr (has_fast_load<L>::value) {
+    if (k0 + BK <= kend && row0 + ROWS <= l.M) {
+#pragma unroll
+      for (int j = 0; j < NS; ++j) {
+        const int i = tid + j * 256;
+        if (T % 256 == 0 || i < T) {
+          const int rr = i / Q, q = i - (i / Q) * Q;
+          r[j] = l.load4_fast(row0 + rr, k0 + 4 * q);
+        }
+      }
+      return;
+    }
+  }
 #pragma unroll
   for (int j = 0; j < NS; ++j) {
     const int i = tid + j * 256;
@@ -103,9 +201,9 @@ __device__ __forceinline__ void fetch_rows(const L& l, f4* r, int row0, int k0, 
     }
   }
 }
-template <int ROWS, int BK>
+template <int ROWS, int BK, int LD>
 __device__ __forceinline__ void commit_rows(const f4* r, float* s, int tid) {
-  constexpr int LD = BK + 4, Q = BK / 4, T = ROWS * Q, NS = (T + 255) / 256;
+  constexpr int Q = BK / 4, T = ROWS * Q, NS = (T + 255) / 256;
 #pragma unroll
   for (int j = 0; j < NS; ++j) {
     const int i = tid + j * 256;
@@ -117,27 +215,32 @@ __device__ __forceinline__ void commit_rows(const f4* r, float* s, int tid) {
 }
 
 // Transposing source (wgrad): L::load4t(p, r) -> rows r..r+3 at reduction index p.
+// Slot i holds rows 4*rq..4*rq+3 at k = kk with rq = (i & 1) + 2 * (i / (2*BK)),
+// kk = (i >> 1) % BK: pairs of lanes read 32 contiguous bytes of one k, and the 32 lanes
+// of a ds_write_b32 half cover kk 0..15 x two row quads, whose banks
+// ((4 rq + c) * LD + kk) mod 32 are distinct when LD = BK + 4 (4 LD = 16 mod 32).
 template <int ROWS, int BK, class L>
 __device__ __forceinline__ void fetch_trans(const L& l, f4* r, int row0, int k0, int kend, int tid) {
   constexpr int R4 = ROWS / 4, T = R4 * BK, NS = (T + 255) / 256;
+  static_assert(R4 % 2 == 0, "row quads in pairs");
 #pragma unroll
   for (int j = 0; j < NS; ++j) {
     const int i = tid + j * 256;
     if (T % 256 == 0 || i < T) {
-      const int kk = i / R4, rq = i - (i / R4) * R4;
+      const int kk = (i >> 1) % BK, rq = (i & 1) + 2 * (i / (2 * BK));
       const int p = k0 + kk;
       r[j] = (p < kend) ? l.load4t(p, row0 + 4 * rq) : f4zero();
     }
   }
 }
-template <int ROWS, int BK>
+template <int ROWS, int BK, int LD>
 __device__ __forceinline__ void commit_trans(const f4* r, float* s, int tid) {
-  constexpr int LD = BK + 4, R4 = ROWS / 4, T = R4 * BK, NS = (T + 255) / 256;
+  constexpr int R4 = ROWS / 4, T = R4 * BK, NS = (T + 255) / 256;
 #pragma unroll
   for (int j = 0; j < NS; ++j) {
     const int i = tid + j * 256;
     if (T % 256 == 0 || i < T) {
-      const int kk = i / R4, rq = i - (i / R4) * R4;
+      const int kk = (i >> 1) % BK, rq = (i & 1) + 2 * (i / (2 * BK));
       s[(4 * rq + 0) * LD + kk] = r[j][0];
       s[(4 * rq + 1) * LD + kk] = r[j][1];
       s[(4 * rq + 2) * LD + kk] = r[j][2];
@@ -148,27 +251,29 @@ __device__ __forceinline__ void commit_trans(const f4* r, float* s, int tid) {
 
 // Mix-ins giving a loader the fetch/commit/slots interface of the GEMM core.
 #define VN_ROWS_LOADER                                                                     \
+  static constexpr bool kTrans = false;                                                    \
   template <int ROWS, int BK>                                                              \
   static constexpr int slots() { return ROWS * (BK / 4); }                                 \
   template <int ROWS, int BK>                                                              \
   __device__ __forceinline__ void fetch(f4* r, int r0, int k0, int ke, int tid) const {    \
     fetch_rows<ROWS, BK>(*this, r, r0, k0, ke, tid);                                       \
   }                                                                                        \
-  template <int ROWS, int BK>                                                              \
+  template <int ROWS, int BK, int LD>                                                      \
   __device__ __forceinline__ static void commit(const f4* r, float* s, int tid) {          \
-    commit_rows<ROWS, BK>(r, s, tid);                                                      \
+    commit_rows<ROWS, BK, LD>(r, s, tid);                                                  \
   }
 
 #define VN_TRANS_LOADER                                                                    \
+  static constexpr bool kTrans = true;                                                     \
   template <int ROWS, int BK>                                                              \
   static constexpr int slots() { return (ROWS / 4) * BK; }                                 \
   template <int ROWS, int BK>                                                              \
   __device__ __forceinline__ void fetch(f4* r, int r0, int k0, int ke, int tid) const {    \
     fetch_trans<ROWS, BK>(*this, r, r0, k0, ke, tid);                                      \
   }                                                                                        \
-  template <int ROWS, int BK>                                                              \
+  template <int ROWS, int BK, int LD>                                                      \
   __device__ __forceinline__ static void commit(const f4* r, float* s, int tid) {          \
-    commit_trans<ROWS, BK>(r, s, tid);                                                     \
+    commit_trans<ROWS, BK, LD>(r, s, tid);                                                 \
   }
 
 }  // namespace vn

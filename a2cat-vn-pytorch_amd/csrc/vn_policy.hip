@@ -103,6 +103,9 @@ struct DenseRows {
   const float* A;
   int64_t ld;
   int M;
+  __device__ __forceinline__ f4 load4_fast(int m, int k) const {
+    return *reinterpret_cast<const f4*>(A + (int64_t)m * ld + k);
+  }
   __device__ __forceinline__ f4 load4(int m, int k, int kend) const {
     if (m >= M || k >= kend) return f4zero();
     const float* p = A + (int64_t)m * ld + k;
@@ -359,6 +362,14 @@ inline void launch_gemm(FA fa, FB fb, EP ep, int M, int N, int K, hipStream_t st
   if (M <= 0 || N <= 0) return;
   if (kchunk <= 0) kchunk = K;
   hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, FA, FB, EP>), grid_for(M, N, BM, BN, splits), dim3(256), 0,
+                     st, fa, fb, ep, M, N, K, kchunk);
+}
+
+template <int BM, int BN, int BK, int WM, int WN, class FA, class FB, class EP>
+inline void launch_gemm32(FA fa, FB fb, EP ep, int M, int N, int K, hipStream_t st, int splits = 1, int kchunk = 0) {
+  if (M <= 0 || N <= 0) return;
+  if (kchunk <= 0) kchunk = K;
+  hipLaunchKernelGGL((gemm32_kernel<BM, BN, BK, WM, WN, FA, FB, EP>), grid_for(M, N, BM, BN, splits), dim3(256), 0,
                      st, fa, fb, ep, M, N, K, kchunk);
 }
 
@@ -654,7 +665,7 @@ inline int lstm_forward_step(const PolicyLayout& L, const float* P, int E, const
     DenseRows fa{xc, L.xcat, E};
     DenseRows fb{P + L.lw, L.xcat, 2048};
     EpiBias2 ep{gates, 2048, P + L.lbih, P + L.lbhh};
-    launch_gemm<64, 64, 32, 2, 2>(fa, fb, ep, E, 2048, L.xcat, st);
+    launch_gemm<128, 128, 16, 2, 2>(fa, fb, ep, E, 2048, L.xcat, st);
   }
   const int64_t nc = (int64_t)E * 512;
   hipLaunchKernelGGL(lstm_cell_kernel, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, st, E, gates, c_prev, mask,
@@ -747,8 +758,8 @@ inline int lstm_backward(const PolicyLayout& L, const float* P, int T, int E, co
   }
   {  // dW_cat = dgates^T x xcat over all T*E rows; b_ih and b_hh share the bias gradient
     Im2colT<DenseRows> fbw{DenseRows{xcat_all, L.xcat, N}, L.xcat};
-    launch_wgrad<64, 64, 2, 2>(w.dgates, 2048, 2048, fbw, L.xcat, N, w.slab, slab_floats(L), Gr + L.lw, Gr + L.lbih,
-                               st);
+    launch_wgrad<128, 64, 2, 2>(w.dgates, 2048, 2048, fbw, L.xcat, N, w.slab, slab_floats(L), Gr + L.lw, Gr + L.lbih,
+                                st);
     VN_HIP(hipMemcpyAsync(Gr + L.lbhh, Gr + L.lbih, 2048 * sizeof(float), hipMemcpyDeviceToDevice, st));
   }
   VN_HIP(hipGetLastError());

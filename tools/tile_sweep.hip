@@ -58,6 +58,7 @@ static float timeit(F f, int reps = 5) {
 }
 
 int main(int argc, char** argv) {
+  const bool dense_only = argc > 3 && atoi(argv[3]) == 1;
   const int n = argc > 1 ? atoi(argv[1]) : 81920;    // backward batch (T*E)
   const int nf = argc > 2 ? atoi(argv[2]) : 4096;    // forward batch (E)
   using G = Geo<84, 84>;
@@ -75,7 +76,66 @@ int main(int argc, char** argv) {
   float* dW = dalloc(64 * 1025, 11, 0.f);
   float* db = dalloc(64, 12, 0.f);
   hipStream_t st = 0;
+  {  // LSTM gates GEMM: [4096 x 1032] x [2048 x 1032]^T
+    const int E = nf, XC = 1032;
+    float* xc = dalloc((int64_t)E * XC, 21, -0.5f);
+    float* wc = dalloc(2048ll * XC, 22, -0.05f);
+    float* gt = dalloc((int64_t)E * 2048, 23, 0.f);
+    float* b0 = dalloc(2048, 24, 0.f);
+    const double fl = 2.0 * E * 2048 * XC;
+#define DENSE(BM, BN, BK, WM, WN)                                                                            \
+    {                                                                                                        \
+      DenseRows fa{xc, XC, E};                                                                               \
+      DenseRows fb{wc, XC, 2048};                                                                            \
+      EpiBias2 ep{gt, 2048, b0, b0};                                                                         \
+      float ms = timeit([&] { launch_gemm<BM, BN, BK, WM, WN>(fa, fb, ep, E, 2048, XC, st); });              \
+      printf("lstm gates  <%3d,%3d,%2d,%d,%d> %8.3f ms %7.1f TF\n", BM, BN, BK, WM, WN, ms, fl / ms / 1e9);    \
+    }
+#define DENSE32(BM, BN, BK, WM, WN)                                                                          \
+    {                                                                                                        \
+      DenseRows fa{xc, XC, E};                                                                               \
+      DenseRows fb{wc, XC, 2048};                                                                            \
+      EpiBias2 ep{gt, 2048, b0, b0};                                                                         \
+      float ms = timeit([&] { launch_gemm32<BM, BN, BK, WM, WN>(fa, fb, ep, E, 2048, XC, st); });            \
+      printf("lstm gates32<%3d,%3d,%2d,%d,%d> %8.3f ms %7.1f TF\n", BM, BN, BK, WM, WN, ms, fl / ms / 1e9);    \
+    }
+    {  // LSTM weight gradient: dgates^T [2048 x P] x xcat [P x 1032] (split-K over P)
+      const int P = 4 * E;
+      float* dg = dalloc((int64_t)P * 2048, 25, -0.5f);
+      float* xa = dalloc((int64_t)P * XC, 26, -0.5f);
+      float* slab = dalloc(12ll << 20, 27, 0.f);
+      float* dW = dalloc(2048ll * XC, 28, 0.f);
+      float* db = dalloc(2048, 29, 0.f);
+      const double fw = 2.0 * P * 2048 * XC;
+#define WGL(BM, BN, WM, WN)                                                                                   \
+      {                                                                                                       \
+        Im2colT<DenseRows> fbw{DenseRows{xa, XC, P}, XC};                                                     \
+        float ms = timeit([&] { launch_wgrad<BM, BN, WM, WN>(dg, 2048, 2048, fbw, XC, P, slab, 12ll << 20, dW, db, st); }); \
+        printf("lstm wgrad  <%3d,%3d,32,%d,%d> %8.3f ms %7.1f TF\n", BM, BN, WM, WN, ms, fw / ms / 1e9);        \
+      }
+      WGL(64, 64, 2, 2)
+      WGL(128, 64, 2, 2)
+      WGL(128, 128, 2, 2)
+      WGL(64, 128, 2, 2)
+    }
+    DENSE32(64, 64, 32, 2, 2)
+    DENSE32(128, 128, 32, 2, 2)
+    DENSE32(128, 128, 16, 2, 2)
+    DENSE32(128, 64, 32, 2, 2)
+    DENSE32(64, 128, 32, 2, 2)
+    DENSE32(128, 128, 64, 2, 2)
+    DENSE32(256, 128, 16, 2, 2)
+    DENSE(64, 64, 32, 2, 2)
+    DENSE(128, 64, 32, 2, 2)
+    DENSE(64, 128, 32, 2, 2)
+    DENSE(128, 128, 32, 2, 2)
+    DENSE(128, 128, 16, 2, 2)
+    DENSE(64, 64, 64, 2, 2)
+    DENSE(128, 64, 64, 2, 2)
+  }
+
   const double f2 = 2.0 * 81 * 32 * 512;  // per frame flops of conv2
+  if (dense_only) { hipDeviceSynchronize(); printf("done\n"); return 0; }
 
 #define FWD2(BM, BN, BK, WM, WN)                                                                                  \
   {                                                                                                               \
