@@ -54,7 +54,8 @@ __device__ __forceinline__ float u8f(const uint8_t* p) { return (float)(*p); }
 // NF frames per workgroup iteration, 5 waves; rows = pixels of the NF frames.
 template <int H, int W, int OH, int OW, int NF>
 __global__ __launch_bounds__(320) void conv1_fwd_kernel(FrameSrc src, int n_frames, const float* __restrict__ Wt,
-                                                        const float* __restrict__ bias, float* __restrict__ Y) {
+                                                        const float* __restrict__ bias, float* __restrict__ Y,
+                                                        uint32_t* __restrict__ mask) {
   constexpr int FB = H * W * 3;
   constexpr int FBP = (FB + 15) / 16 * 16;
   constexpr int NPIX = OH * OW;
@@ -88,7 +89,13 @@ __global__ __launch_bounds__(320) void conv1_fwd_kernel(FrameSrc src, int n_fram
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int rr = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (rr < nf * NPIX) Y[((int64_t)f0 * NPIX + rr) * 32 + c32] = fmaxf(acc[r] * (1.0f / 255.0f) + bs, 0.0f);
+        const float y = fmaxf(acc[r] * (1.0f / 255.0f) + bs, 0.0f);
+        // ReLU bitmask: lanes 0-31 (h = 0) and 32-63 (h = 1) are the 32 channels of two pixels
+        const uint64_t bal = __ballot(y > 0.0f);
+        if (rr < nf * NPIX) {
+          Y[((int64_t)f0 * NPIX + rr) * 32 + c32] = y;
+          if (c32 == 0) mask[(int64_t)f0 * NPIX + rr] = (uint32_t)(bal >> (32 * h));
+        }
       }
     }
     __syncthreads();
@@ -248,17 +255,25 @@ __global__ __launch_bounds__(256) void conv2_wgrad_kernel(const float* __restric
 // dZ2[f][oy][ox][co] * W2[co][ky][kx][ci]  (k4 s2). Wave w owns the input-parity class
 // (py, px) = (w >> 1, w & 1): its (KH/S)^2 = 4 taps are fixed, so its 64 B fragments (k =
 // tap*32 + co, 16x16x4 MFMA, 2 column tiles of ci) stay in registers for the whole kernel.
-// dZ2_f is staged in LDS with one extra zero row that out-of-range taps point at.
-template <int IH, int IW, int OH, int OW>
+// dZ2_f is staged in LDS with one extra zero row that out-of-range taps point at, pixel
+// rows padded to 34 floats: the 16 pixels x 2 channel lanes of a ds_read_b32 half then
+// fall on distinct banks (2p + q mod 32), where a 32-float stride put all 16 pixels of a
+// channel on one bank (SQ_LDS_BANK_CONFLICT 3.4e9 per update before). Maps whose padded
+// copy would cost a resident workgroup (174x174: 3 per CU) use 33 (2-way at worst).
+// BITS: the ReLU mask comes from conv1's bitmask (one uint32 of channel bits per pixel)
+// instead of X1 itself — 4 B instead of 128 B of reads per pixel.
+template <int IH, int IW, int OH, int OW, bool BITS>
 __global__ __launch_bounds__(256) void conv2_dgrad_kernel(const float* __restrict__ dZ2, const float* __restrict__ WT,
-                                                          const float* __restrict__ X1, float* __restrict__ dX1,
+                                                          const float* __restrict__ X1,
+                                                          const uint32_t* __restrict__ mask, float* __restrict__ dX1,
                                                           int n_frames) {
   constexpr int NP = OH * OW;
   constexpr int HYC = IH / 2, WXC = IW / 2;  // even input sizes: every class has HYC x WXC pixels
   static_assert(IH % 2 == 0 && IW % 2 == 0, "even conv1 maps");
   constexpr int NPC = HYC * WXC;
   constexpr int TILES = (NPC + 15) / 16;
-  __shared__ __attribute__((aligned(16))) float ds[(NP + 1) * 32];
+  constexpr int PS = ((NP + 1) * 34 * 4 <= 160 * 1024 / 3 || (NP + 1) * 33 * 4 > 160 * 1024 / 3) ? 34 : 33;
+  __shared__ __attribute__((aligned(16))) float ds[(NP + 1) * PS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int py = wave >> 1, px = wave & 1;
   const int i16 = lane & 15, q = lane >> 4;
@@ -271,14 +286,41 @@ __global__ __launch_bounds__(256) void conv2_dgrad_kernel(const float* __restric
 #pragma unroll
     for (int ct = 0; ct < 2; ++ct) b[s][ct] = WT[((ky * 4 + kx) * 32 + ct * 16 + i16) * 32 + co];
   }
-  if (tid < 32) ds[NP * 32 + tid] = 0.0f;
+  if (tid < 32) ds[NP * PS + tid] = 0.0f;
+  // software pipeline: the next frame's dZ2 is loaded into registers while this one computes
+  constexpr int NZ = (NP * 8 + 255) / 256;
+  f4 zr[NZ];
+  auto load_z = [&](int f) {
+    const f4* z4 = reinterpret_cast<const f4*>(dZ2 + (int64_t)f * NP * 32);
+#pragma unroll
+    for (int j = 0; j < NZ; ++j) {
+      const int i = tid + j * 256;
+      if (i < NP * 8) zr[j] = z4[i];
+    }
+  };
+  if (blockIdx.x < n_frames) load_z(blockIdx.x);
   for (int f = blockIdx.x; f < n_frames; f += gridDim.x) {
     {
-      const f4* z4 = reinterpret_cast<const f4*>(dZ2 + (int64_t)f * NP * 32);
-      f4* e4 = reinterpret_cast<f4*>(ds);
-      for (int i = tid; i < NP * 8; i += 256) e4[i] = z4[i];
+      typedef float f2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+      for (int j = 0; j < NZ; ++j) {
+        const int i = tid + j * 256;
+        if (i >= NP * 8) break;
+        const f4 v = zr[j];
+        float* d = ds + (i >> 3) * PS + 4 * (i & 7);
+        if constexpr (PS % 2 == 0) {
+          reinterpret_cast<f2*>(d)[0] = f2{v[0], v[1]};
+          reinterpret_cast<f2*>(d)[1] = f2{v[2], v[3]};
+        } else {
+          d[0] = v[0];
+          d[1] = v[1];
+          d[2] = v[2];
+          d[3] = v[3];
+        }
+      }
     }
     __syncthreads();
+    if (f + (int)gridDim.x < n_frames) load_z(f + gridDim.x);
     for (int t = 0; t < TILES; ++t) {
       const int pc = t * 16 + i16;  // this lane's pixel of the class (A row)
       const int yy = pc / WXC, xx = pc - (pc / WXC) * WXC;
@@ -287,7 +329,7 @@ __global__ __launch_bounds__(256) void conv2_dgrad_kernel(const float* __restric
       for (int tap = 0; tap < 4; ++tap) {
         const int oy = yy - (tap >> 1), ox = xx - (tap & 1);
         const bool ok = pc < NPC && oy >= 0 && oy < OH && ox >= 0 && ox < OW;
-        off[tap] = (ok ? (oy * OW + ox) : NP) * 32 + q;
+        off[tap] = (ok ? (oy * OW + ox) : NP) * PS + q;
       }
       f4 acc0 = f4zero(), acc1 = f4zero();
 #pragma unroll
@@ -301,9 +343,16 @@ __global__ __launch_bounds__(256) void conv2_dgrad_kernel(const float* __restric
         const int pr = t * 16 + q * 4 + r;
         if (pr < NPC) {
           const int y = (pr / WXC) * 2 + py, x = (pr % WXC) * 2 + px;
-          const int64_t base = (((int64_t)f * IH + y) * IW + x) * 32 + i16;
-          dX1[base] = X1[base] > 0.0f ? acc0[r] : 0.0f;
-          dX1[base + 16] = X1[base + 16] > 0.0f ? acc1[r] : 0.0f;
+          const int64_t pix = ((int64_t)f * IH + y) * IW + x;
+          const int64_t base = pix * 32 + i16;
+          if constexpr (BITS) {
+            const uint32_t mw = mask[pix];
+            dX1[base] = (mw >> i16) & 1u ? acc0[r] : 0.0f;
+            dX1[base + 16] = (mw >> (i16 + 16)) & 1u ? acc1[r] : 0.0f;
+          } else {
+            dX1[base] = X1[base] > 0.0f ? acc0[r] : 0.0f;
+            dX1[base + 16] = X1[base + 16] > 0.0f ? acc1[r] : 0.0f;
+          }
         }
       }
     }

@@ -261,6 +261,7 @@ struct PolicyLayout {
   LayerOff l[6];  // conv1, conv2, conv3, conv4, fc, head
   int64_t n_params;
   int64_t sz[5];  // per-sample floats of X1..X5
+  int64_t msz;    // per-sample words of the conv1 ReLU bitmask (one uint32 of channel bits per pixel)
   int64_t wt_off[6], wt_total;
   // recurrent core (BigGoalHouseModel, models/goal.py:61-67): W_cat [2048][xcat] = [W_ih | 0 | W_hh]
   int lstm, lin, xoff, xcat;
@@ -330,6 +331,7 @@ inline PolicyLayout make_layout(int H, int W, int A, int lstm = 0, int aux = 0) 
   L.sz[2] = (int64_t)L.OH3 * L.OW3 * 64;
   L.sz[3] = (int64_t)L.OH3 * L.OW3 * 32;
   L.sz[4] = 512;
+  L.msz = 2ll * L.OH1 * L.OW1;
   return L;
 }
 
@@ -426,13 +428,17 @@ struct Geo {
   static constexpr int FCIN = 32 * OH3 * OW3;
 };
 
+// Activation store of `cap` samples: [conv1 ReLU bitmask | X1 | X2 | X3 | X4 | X5], each
+// region sample-contiguous (X5 last: the recurrent core reads it as [cap][512]).
 struct Acts {
   float* X[5];
+  uint32_t* M1;  // [frames][OH1*OW1] channel bits of X1 > 0 (written by conv1, read by conv2's dgrad)
 };
 
 inline Acts acts_at(const PolicyLayout& L, float* base, int64_t cap, int64_t off) {
   Acts a;
-  float* p = base;
+  a.M1 = reinterpret_cast<uint32_t*>(base) + off * L.msz;
+  float* p = base + cap * L.msz;
   for (int i = 0; i < 5; ++i) {
     a.X[i] = p + off * L.sz[i];
     p += cap * L.sz[i];
@@ -459,7 +465,7 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
     const int blocks =
         std::min((frames + NF - 1) / NF, resident_blocks((const void*)conv1_fwd_kernel<H0, W0, G::OH1, G::OW1, NF>, 320, 0));
     hipLaunchKernelGGL((conv1_fwd_kernel<H0, W0, G::OH1, G::OW1, NF>), dim3(blocks), dim3(320), 0, st, src, frames,
-                       P + L.l[0].w, P + L.l[0].b, a.X[0]);
+                       P + L.l[0].w, P + L.l[0].b, a.X[0], a.M1);
   }
   // conv2 (X1 -> X2)
   {
@@ -618,10 +624,19 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
       launch_wgrad<32, 64, 2, 2>(w.dz2, 32, 32, fbw, 512, P2, w.slab, w.slab_cap, Gr + L.l[1].w, Gr + L.l[1].b, st);
     }
     if constexpr (G::OH1 % 2 == 0 && G::OW1 % 2 == 0) {
-      const int blocks = std::min(frames, resident_blocks((const void*)conv2_dgrad_kernel<G::OH1, G::OW1, G::OH2, G::OW2>,
-                                                          256, 0));
-      hipLaunchKernelGGL((conv2_dgrad_kernel<G::OH1, G::OW1, G::OH2, G::OW2>), dim3(blocks), dim3(256), 0, st, w.dz2,
-                         T(1), a.X[0], a.X[0], frames);
+      // the u8 conv1 kernel left X1's ReLU as a bitmask: read 4 B per pixel instead of X1
+      const bool bits = kConv1LdsFrame<H0, W0> && !(src.f32[0] || src.f32[1]);
+      if (bits) {
+        const int blocks = std::min(
+            frames, resident_blocks((const void*)conv2_dgrad_kernel<G::OH1, G::OW1, G::OH2, G::OW2, true>, 256, 0));
+        hipLaunchKernelGGL((conv2_dgrad_kernel<G::OH1, G::OW1, G::OH2, G::OW2, true>), dim3(blocks), dim3(256), 0, st,
+                           w.dz2, T(1), a.X[0], a.M1, a.X[0], frames);
+      } else {
+        const int blocks = std::min(
+            frames, resident_blocks((const void*)conv2_dgrad_kernel<G::OH1, G::OW1, G::OH2, G::OW2, false>, 256, 0));
+        hipLaunchKernelGGL((conv2_dgrad_kernel<G::OH1, G::OW1, G::OH2, G::OW2, false>), dim3(blocks), dim3(256), 0, st,
+                           w.dz2, T(1), a.X[0], a.M1, a.X[0], frames);
+      }
     } else {
       dgrad_all_classes<32, 32, G::OH1, G::OW1, G::OH2, G::OW2>(w.dz2, T(1), a.X[0], a.X[0], 2 * n, 0, 1, 32, st);
     }
@@ -946,7 +961,7 @@ int vn_policy_info(vn_policy* p, int64_t* n_params, int64_t* act_floats_per_samp
   if (act_floats_per_sample) {
     int64_t s = 0;
     for (int i = 0; i < 5; ++i) s += p->L.sz[i];
-    *act_floats_per_sample = s;
+    *act_floats_per_sample = s + p->L.msz;
   }
   if (layout12)
     for (int i = 0; i < 6; ++i) {

@@ -36,8 +36,7 @@ def run_forward(net, params, image, goal):
 
 
 def x5_of(net, acts, n):
-    off = sum(n * s for s in _act_sizes(net)[:4])
-    return acts[off:off + n * 512].view(n, 512)
+    return net.x5(acts, n)
 
 
 def _act_sizes(net):

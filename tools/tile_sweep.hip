@@ -158,9 +158,9 @@ int main(int argc, char** argv) {
   }
   {
     const int frames = 2 * n;
-    const int blocks = std::min(frames, resident_blocks((const void*)conv2_dgrad_kernel<20, 20, 9, 9>, 256, 0));
+    const int blocks = std::min(frames, resident_blocks((const void*)conv2_dgrad_kernel<20, 20, 9, 9, false>, 256, 0));
     float ms = timeit([&] {
-      hipLaunchKernelGGL((conv2_dgrad_kernel<20, 20, 9, 9>), dim3(blocks), dim3(256), 0, st, dz2, W2T, X1, out, frames);
+      hipLaunchKernelGGL((conv2_dgrad_kernel<20, 20, 9, 9, false>), dim3(blocks), dim3(256), 0, st, dz2, W2T, X1, nullptr, out, frames);
     });
     printf("conv2 dgrad specialised   %8.3f ms %7.1f TF (%d blocks)\n", ms, f2 * 2 * n / ms / 1e9, blocks);
   }
