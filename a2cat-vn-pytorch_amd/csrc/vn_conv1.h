@@ -102,6 +102,128 @@ __global__ __launch_bounds__(320) void conv1_fwd_kernel(FrameSrc src, int n_fram
   }
 }
 
+// ---- forward on bf16 MFMA with split weights ------------------------------------
+// The frame bytes are integers 0..255, exact in bf16; each fp32 weight is split by
+// truncation into three bf16 terms with w == hi + mid + lo exactly, so every product is
+// exact in fp32 and v_mfma_f32_32x32x16_bf16 (16x the f32 MFMA rate) accumulates the same
+// sum of exact products as the f32 path, in a different order (parity at 1e-5 rel, as the
+// f32 kernel). Three accumulators (one per term) keep three independent MFMA chains.
+// K is relaid k' = ky*24 + kr (kr = kx*3 + c < 21, 21..23 and ky = 7 zero-weighted) so
+// the 8 k' of a lane's fragment are 8 consecutive frame bytes of one image row: the
+// frame is staged once per workgroup into LDS as bf16 rows of RS elements and a fragment
+// is two aligned 8-byte LDS reads; the split weights sit in LDS as per-lane fragments
+// (one ds_read_b128 each), and the next frame is prefetched into registers. Frames whose
+// row bytes are not a multiple of 4 or whose bf16 image does not fit use the f32 kernel.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+template <int H, int W>
+constexpr bool conv1_x3_fits() {
+  return (W * 3) % 4 == 0 && (size_t)H * ((W * 3 + 3) / 4 * 4) * 2 + 11 * 3 * 64 * 16 <= 80 * 1024;
+}
+
+__device__ __forceinline__ void split3_bf16(float w, uint16_t& hi, uint16_t& mid, uint16_t& lo) {
+  const uint32_t hb = __float_as_uint(w) & 0xffff0000u;
+  const float r1 = w - __uint_as_float(hb);  // exact: the low 16 mantissa bits of w
+  const uint32_t mb = __float_as_uint(r1) & 0xffff0000u;
+  const float r2 = r1 - __uint_as_float(mb);  // exact, <= 8 significant bits
+  hi = (uint16_t)(hb >> 16);
+  mid = (uint16_t)(mb >> 16);
+  lo = (uint16_t)(__float_as_uint(r2) >> 16);
+}
+
+template <int H, int W, int OH, int OW>
+__global__ __launch_bounds__(256) void conv1_fwd_x3_kernel(FrameSrc src, int n_frames, const float* __restrict__ Wt,
+                                                           const float* __restrict__ bias, float* __restrict__ Y,
+                                                           uint32_t* __restrict__ mask) {
+  constexpr int RB = W * 3;                 // frame row bytes
+  constexpr int RS = (RB + 3) / 4 * 4;      // LDS row stride (bf16 elements)
+  constexpr int NPIX = OH * OW;
+  constexpr int TILES = (NPIX + 31) / 32;
+  constexpr int NS = 11;                    // k' slices of 16 (k' < 176)
+  constexpr int ND = H * RB / 4;            // frame dwords
+  constexpr int NPF = (ND + 255) / 256;     // prefetched dwords per thread
+  static_assert(RB % 4 == 0, "frame rows of whole dwords");
+  // LDS: the bf16 frame image, then the split weights as per-lane 16-B fragments [s][term][lane]
+  __shared__ __attribute__((aligned(16))) uint16_t img[H * RS];
+  __shared__ __attribute__((aligned(16))) bf16x8 bw[NS * 3 * 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, c32 = lane & 31;
+  for (int i = tid; i < NS * 64; i += 256) {  // fragment of slice sl for lane ln
+    const int sl = i >> 6, ln = i & 63, hh = ln >> 5, co = ln & 31;
+    union { uint16_t u[8]; bf16x8 v; } t0, t1, t2;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int kp = 16 * sl + 8 * hh + j, ky = kp / 24, kr = kp % 24;
+      const float w = (ky < 7 && kr < 21) ? Wt[co * 148 + ky * 21 + kr] : 0.0f;
+      split3_bf16(w, t0.u[j], t1.u[j], t2.u[j]);
+    }
+    bw[(sl * 3 + 0) * 64 + ln] = t0.v;
+    bw[(sl * 3 + 1) * 64 + ln] = t1.v;
+    bw[(sl * 3 + 2) * 64 + ln] = t2.v;
+  }
+  const float bs = bias[c32];
+  uint32_t pre[NPF];  // next frame's bytes, in flight while the current frame computes
+  auto load_frame = [&](int f) {
+    const uint32_t* s4 = reinterpret_cast<const uint32_t*>(frame_ptr(src, f));
+#pragma unroll
+    for (int j = 0; j < NPF; ++j) {
+      const int i = tid + j * 256;
+      if (i < ND) pre[j] = s4[i];
+    }
+  };
+  if ((int)blockIdx.x < n_frames) load_frame(blockIdx.x);
+  for (int f = blockIdx.x; f < n_frames; f += gridDim.x) {
+#pragma unroll
+    for (int j = 0; j < NPF; ++j) {  // u8 -> bf16 rows (a dword never straddles a row)
+      const int i = tid + j * 256;
+      if (i < ND) {
+        const uint32_t v = pre[j];
+        const int e = i * 4, row = e / RB, col = e - row * RB;
+        const uint32_t b0 = __float_as_uint((float)(v & 0xffu)) >> 16;
+        const uint32_t b1 = __float_as_uint((float)((v >> 8) & 0xffu)) >> 16;
+        const uint32_t b2 = __float_as_uint((float)((v >> 16) & 0xffu)) >> 16;
+        const uint32_t b3 = __float_as_uint((float)(v >> 24)) >> 16;
+        *reinterpret_cast<uint2*>(img + row * RS + col) = uint2{b0 | (b1 << 16), b2 | (b3 << 16)};
+      }
+    }
+    __syncthreads();
+    if (f + (int)gridDim.x < n_frames) load_frame(f + gridDim.x);
+    for (int t = wave; t < TILES; t += 4) {
+      const int px = min(t * 32 + c32, NPIX - 1);
+      const int oy = px / OW, ox = px - (px / OW) * OW;
+      const uint16_t* base = img + (oy * 4) * RS + ox * 12;
+      f16v acc[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[p][r] = 0.0f;
+#pragma unroll
+      for (int sl = 0; sl < NS; ++sl) {
+        const int k0 = 16 * sl + 8 * h, ky = k0 / 24, kr0 = k0 - (k0 / 24) * 24;
+        const uint2* q = reinterpret_cast<const uint2*>(base + ky * RS + kr0);
+        union { uint2 u[2]; bf16x8 v; } a;
+        a.u[0] = q[0];
+        a.u[1] = q[1];
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.v, bw[(sl * 3 + p) * 64 + lane], acc[p], 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rr = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const float sum = (acc[2][r] + acc[1][r]) + acc[0][r];
+        const float y = fmaxf(sum * (1.0f / 255.0f) + bs, 0.0f);
+        const uint64_t bal = __ballot(y > 0.0f);
+        if (rr < NPIX) {
+          Y[((int64_t)f * NPIX + rr) * 32 + c32] = y;
+          if (c32 == 0) mask[(int64_t)f * NPIX + rr] = (uint32_t)(bal >> (32 * h));
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // ---- weight gradient ----------------------------------------------------------
 // One frame per workgroup iteration, its pixels in chunks of CP: the chunk's dZ rows
 // (CP x 32 fp32, 16-B loads) and the frame bytes are staged into LDS together, then each

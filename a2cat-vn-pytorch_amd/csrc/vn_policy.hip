@@ -459,6 +459,11 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
     DenseRows fb{P + L.l[0].w, 148, 32};
     EpiBiasAct ep{a.X[0], 32, P + L.l[0].b, 1};
     launch_gemm<64, 32, 32, 4, 1>(fa, fb, ep, fa.M, 32, 148, st);
+  } else if constexpr (conv1_x3_fits<H0, W0>()) {  // bf16 MFMA on split weights (exact products)
+    const int frames = 2 * n;
+    const int blocks = std::min(frames, resident_blocks((const void*)conv1_fwd_x3_kernel<H0, W0, G::OH1, G::OW1>, 256, 0));
+    hipLaunchKernelGGL((conv1_fwd_x3_kernel<H0, W0, G::OH1, G::OW1>), dim3(blocks), dim3(256), 0, st, src, frames,
+                       P + L.l[0].w, P + L.l[0].b, a.X[0], a.M1);
   } else if constexpr (kConv1Lds) {
     constexpr int NF = (2 * H0 * W0 * 3 <= 64 * 1024) ? 2 : 1;
     const int frames = 2 * n;
