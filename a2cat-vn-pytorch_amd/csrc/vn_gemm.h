@@ -167,6 +167,124 @@ __global__ __launch_bounds__(256) void gemm32_kernel(FA fa, FB fb, EP ep, int M,
       }
 }
 
+// ---- fp32 GEMM on bf16 MFMA with split operands ("x6") ---------------------------
+// Each fp32 operand value v is split by truncation into three bf16 terms v0 + v1 + v2 == v
+// (exact, split3 below); a*b is summed as the six term products with i + j <= 2 (the three
+// dropped ones are below 2^-24 |a b|), each exact in fp32, on v_mfma_f32_32x32x16_bf16 (16x
+// the f32 MFMA rate; 6 of them cost 0.375 of the f32 path). Row-fill loaders only: commit
+// splits a k-contiguous f4 into three 8-byte bf16 runs of planes [term][row][k] (row
+// stride BK + 8 elements: 20-dword rows put the 16-lane groups of a ds_read_b128 on 16
+// distinct slots). Lane l reads row l&31, k = 8*(l>>5)..+7 (the MFMA A/B layout).
+typedef __bf16 bf16x8_ __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ uint32_t bf16_split_bits(float v, float& rest) {
+  const uint32_t hb = __float_as_uint(v) & 0xffff0000u;
+  rest = v - __uint_as_float(hb);
+  return hb >> 16;
+}
+
+template <int ROWS, int BK, int LDK>
+__device__ __forceinline__ void commit_rows_x6(const f4* r, uint16_t* s, int tid) {
+  constexpr int Q = BK / 4, T = ROWS * Q, NS = (T + 255) / 256, PLANE = ROWS * LDK;
+#pragma unroll
+  for (int j = 0; j < NS; ++j) {
+    const int i = tid + j * 256;
+    if (T % 256 == 0 || i < T) {
+      const int rr = i / Q, q = i - (i / Q) * Q;
+      uint32_t t0[4], t1[4], t2[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float r1, r2, r3;
+        t0[e] = bf16_split_bits(r[j][e], r1);
+        t1[e] = bf16_split_bits(r1, r2);
+        t2[e] = bf16_split_bits(r2, r3);
+      }
+      uint16_t* d = s + rr * LDK + 4 * q;
+      *reinterpret_cast<uint2*>(d) = uint2{t0[0] | (t0[1] << 16), t0[2] | (t0[3] << 16)};
+      *reinterpret_cast<uint2*>(d + PLANE) = uint2{t1[0] | (t1[1] << 16), t1[2] | (t1[3] << 16)};
+      *reinterpret_cast<uint2*>(d + 2 * PLANE) = uint2{t2[0] | (t2[1] << 16), t2[2] | (t2[3] << 16)};
+    }
+  }
+}
+
+template <int BM, int BN, int BK, int WM, int WN, class FA, class FB, class EP>
+__global__ __launch_bounds__(256) void gemm_x6_kernel(FA fa, FB fb, EP ep, int M, int N, int K, int kchunk) {
+  static_assert(WM * WN == 4, "4 waves per workgroup");
+  static_assert(BK % 16 == 0, "BK multiple of 16");
+  static_assert(!FA::kTrans && !FB::kTrans, "row-fill loaders only");
+  constexpr int LDK = BK + 8;
+  constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
+  static_assert(TM >= 1 && TN >= 1, "tile too small for the wave layout");
+  constexpr int NA = (FA::template slots<BM, BK>() + 255) / 256;
+  constexpr int NB = (FB::template slots<BN, BK>() + 255) / 256;
+  __shared__ __attribute__((aligned(16))) uint16_t As[3 * BM * LDK];
+  __shared__ __attribute__((aligned(16))) uint16_t Bs[3 * BN * LDK];
+  typedef float f16v_ __attribute__((ext_vector_type(16)));
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WM, wn = wave / WM;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int kb = blockIdx.z * kchunk;
+  const int ke = min(K, kb + kchunk);
+  f16v_ acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+  const int ra = (wm * TM * 32 + (lane & 31)) * LDK + 8 * (lane >> 5);
+  const int rb = (wn * TN * 32 + (lane & 31)) * LDK + 8 * (lane >> 5);
+  f4 pa[NA], pb[NB];
+  if (kb < ke) {
+    fa.template fetch<BM, BK>(pa, m0, kb, ke, tid);
+    fb.template fetch<BN, BK>(pb, n0, kb, ke, tid);
+  }
+  for (int k0 = kb; k0 < ke; k0 += BK) {
+    commit_rows_x6<BM, BK, LDK>(pa, As, tid);
+    commit_rows_x6<BN, BK, LDK>(pb, Bs, tid);
+    __syncthreads();
+    if (k0 + BK < ke) {
+      fa.template fetch<BM, BK>(pa, m0, k0 + BK, ke, tid);
+      fb.template fetch<BN, BK>(pb, n0, k0 + BK, ke, tid);
+    }
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 16) {
+      bf16x8_ a[3][TM], b[3][TN];
+#pragma unroll
+      for (int t = 0; t < 3; ++t) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          a[t][i] = *reinterpret_cast<const bf16x8_*>(&As[t * BM * LDK + ra + i * 32 * LDK + kk]);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          b[t][j] = *reinterpret_cast<const bf16x8_*>(&Bs[t * BN * LDK + rb + j * 32 * LDK + kk]);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {  // small terms first
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][i], b[0][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[2][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[1][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[0][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[1][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[0][j], acc[i][j], 0, 0, 0);
+        }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int col = n0 + wn * TN * 32 + j * 32 + (lane & 31);
+        if (row < M && col < N) ep(row, col, acc[i][j][r], (int)blockIdx.z);
+      }
+}
+
 // ---- fill helpers: fetch (global -> registers) then commit (registers -> LDS) ----
 // A loader with load4_fast(row, k) (no bounds checks) gets it for tiles wholly inside
 // its rows and the K range (a wave-uniform test): the common case issues plain 16-B loads.

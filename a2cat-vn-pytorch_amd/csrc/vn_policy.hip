@@ -368,6 +368,13 @@ inline void launch_gemm(FA fa, FB fb, EP ep, int M, int N, int K, hipStream_t st
 }
 
 template <int BM, int BN, int BK, int WM, int WN, class FA, class FB, class EP>
+inline void launch_gemm_x6(FA fa, FB fb, EP ep, int M, int N, int K, hipStream_t st) {
+  if (M <= 0 || N <= 0) return;
+  hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, BK, WM, WN, FA, FB, EP>), grid_for(M, N, BM, BN), dim3(256), 0, st, fa, fb,
+                     ep, M, N, K, K);
+}
+
+template <int BM, int BN, int BK, int WM, int WN, class FA, class FB, class EP>
 inline void launch_gemm32(FA fa, FB fb, EP ep, int M, int N, int K, hipStream_t st, int splits = 1, int kchunk = 0) {
   if (M <= 0 || N <= 0) return;
   if (kchunk <= 0) kchunk = K;
@@ -404,7 +411,7 @@ inline void dgrad_class(const float* dz, const float* WT, float* out, const floa
   DgradA<COUT, 4, 2, OH, OW, HYC, WXC> fa{dz, M};
   DgradB<COUT, 4, 2, CINF> fb{WT, cin, g * cin, PY, PX};
   EpiMaskParity<H, W, 2, PY, PX, HYC, WXC> ep{out, X, g, G, cin};
-  launch_gemm<64, 32, 32, 4, 1>(fa, fb, ep, M, cin, 4 * COUT, st);
+  launch_gemm_x6<128, 32, 32, 4, 1>(fa, fb, ep, M, cin, 4 * COUT, st);
 }
 
 template <int COUT, int CINF, int H, int W, int OH, int OW>
@@ -458,7 +465,7 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
     FramesIm2col<H0, W0, G::OH1, G::OW1> fa{src, 2 * n * G::OH1 * G::OW1};
     DenseRows fb{P + L.l[0].w, 148, 32};
     EpiBiasAct ep{a.X[0], 32, P + L.l[0].b, 1};
-    launch_gemm<64, 32, 32, 4, 1>(fa, fb, ep, fa.M, 32, 148, st);
+    launch_gemm_x6<128, 32, 32, 4, 1>(fa, fb, ep, fa.M, 32, 148, st);
   } else if constexpr (conv1_x3_fits<H0, W0>()) {  // bf16 MFMA on split weights (exact products)
     const int frames = 2 * n;
     const int blocks = std::min(frames, resident_blocks((const void*)conv1_fwd_x3_kernel<H0, W0, G::OH1, G::OW1>, 256, 0));
@@ -477,28 +484,28 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
     NhwcIm2col<32, 4, 4, 2, G::OH1, G::OW1, G::OH2, G::OW2, 1> fa{a.X[0], 2 * n * G::OH2 * G::OW2};
     DenseRows fb{P + L.l[1].w, 512, 32};
     EpiBiasAct ep{a.X[1], 32, P + L.l[1].b, 1};
-    launch_gemm<64, 32, 32, 4, 1>(fa, fb, ep, fa.M, 32, 512, st);
+    launch_gemm_x6<128, 32, 32, 4, 1>(fa, fb, ep, fa.M, 32, 512, st);
   }
   // conv3 over concat(image, goal) (X2 -> X3)
   {
     NhwcIm2col<32, 4, 4, 2, G::OH2, G::OW2, G::OH3, G::OW3, 2> fa{a.X[1], n * G::OH3 * G::OW3};
     DenseRows fb{P + L.l[2].w, 1024, 64};
     EpiBiasAct ep{a.X[2], 64, P + L.l[2].b, 1};
-    launch_gemm<64, 64, 32, 2, 2>(fa, fb, ep, fa.M, 64, 1024, st);
+    launch_gemm_x6<64, 64, 32, 2, 2>(fa, fb, ep, fa.M, 64, 1024, st);
   }
   // conv4 1x1 (X3 -> X4)
   {
     DenseRows fa{a.X[2], 64, n * G::OH3 * G::OW3};
     DenseRows fb{P + L.l[3].w, 64, 32};
     EpiBiasAct ep{a.X[3], 32, P + L.l[3].b, 1};
-    launch_gemm<64, 32, 32, 4, 1>(fa, fb, ep, fa.M, 32, 64, st);
+    launch_gemm_x6<128, 32, 32, 4, 1>(fa, fb, ep, fa.M, 32, 64, st);
   }
   // conv_merge Linear (X4 flattened NHWC -> X5)
   {
     DenseRows fa{a.X[3], G::FCIN, n};
     DenseRows fb{P + L.l[4].w, G::FCIN, 512};
     EpiBiasAct ep{a.X[4], 512, P + L.l[4].b, 1};
-    launch_gemm<64, 64, 32, 2, 2>(fa, fb, ep, n, 512, G::FCIN, st);
+    launch_gemm_x6<64, 64, 32, 2, 2>(fa, fb, ep, n, 512, G::FCIN, st);
   }
   // heads (X5 -> out[n][8]: logits, value); out == NULL runs the trunk only (recurrent policy)
   if (out) {
@@ -578,10 +585,10 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
     DenseRows fb{T(4), 512, G::FCIN};  // WT [FCIN][512]
     if (dx4_extra) {  // + the aux heads' gradient w.r.t. X4, under the same ReLU mask
       EpiMaskAdd ep{w.dz4, a.X[3], G::FCIN, dx4_extra};
-      launch_gemm<64, 64, 32, 2, 2>(fa, fb, ep, n, G::FCIN, 512, st);
+      launch_gemm_x6<64, 64, 32, 2, 2>(fa, fb, ep, n, G::FCIN, 512, st);
     } else {
       EpiMask ep{w.dz4, a.X[3], G::FCIN};
-      launch_gemm<64, 64, 32, 2, 2>(fa, fb, ep, n, G::FCIN, 512, st);
+      launch_gemm_x6<64, 64, 32, 2, 2>(fa, fb, ep, n, G::FCIN, 512, st);
     }
     Im2colT<DenseRows> fbw{DenseRows{a.X[3], G::FCIN, n}, G::FCIN};
     launch_wgrad<64, 64, 2, 2>(dz5, 512, 512, fbw, G::FCIN, n, w.slab, w.slab_cap, Gr + L.l[4].w, Gr + L.l[4].b,
@@ -592,7 +599,7 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
     DenseRows fa{w.dz4, 32, n9};
     DenseRows fb{T(3), 32, 64};  // WT [64][32]
     EpiMask ep{w.dz3, a.X[2], 64};
-    launch_gemm<64, 64, 32, 2, 2>(fa, fb, ep, n9, 64, 32, st);
+    launch_gemm_x6<64, 64, 32, 2, 2>(fa, fb, ep, n9, 64, 32, st);
     Im2colT<DenseRows> fbw{DenseRows{a.X[2], 64, n9}, 64};
     launch_wgrad<32, 64, 2, 2>(w.dz4, 32, 32, fbw, 64, n9, w.slab, w.slab_cap, Gr + L.l[3].w, Gr + L.l[3].b, st);
   }
@@ -685,7 +692,7 @@ inline int lstm_forward_step(const PolicyLayout& L, const float* P, int E, const
     DenseRows fa{xc, L.xcat, E};
     DenseRows fb{P + L.lw, L.xcat, 2048};
     EpiBias2 ep{gates, 2048, P + L.lbih, P + L.lbhh};
-    launch_gemm<128, 128, 16, 2, 2>(fa, fb, ep, E, 2048, L.xcat, st);
+    launch_gemm_x6<128, 128, 32, 2, 2>(fa, fb, ep, E, 2048, L.xcat, st);
   }
   const int64_t nc = (int64_t)E * 512;
   hipLaunchKernelGGL(lstm_cell_kernel, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, st, E, gates, c_prev, mask,
@@ -774,7 +781,7 @@ inline int lstm_backward(const PolicyLayout& L, const float* P, int T, int E, co
     DenseRows fa{dg, 2048, E};
     DenseRows fb{w.wcat_t, 2048, L.xcat};
     EpiLstmDx ep{dz5 + (int64_t)t * e512, x5_all + (int64_t)t * e512, w.dh[cur], mask, L.xoff};
-    launch_gemm<64, 64, 32, 2, 2>(fa, fb, ep, E, L.xcat, 2048, st);
+    launch_gemm_x6<64, 64, 32, 2, 2>(fa, fb, ep, E, L.xcat, 2048, st);
   }
   {  // dW_cat = dgates^T x xcat over all T*E rows; b_ih and b_hh share the bias gradient
     Im2colT<DenseRows> fbw{DenseRows{xcat_all, L.xcat, N}, L.xcat};
@@ -798,7 +805,7 @@ inline void deconv_class(const float* in, const float* WT, float* out, const flo
   DgradB<CIN, 4, 2, COUT> fb{WT, COUT, 0, PY, PX};
   EpiDeconv<OH, OW, PY, PX, HYC, WXC> ep{out, COUT, bias, relu};
   if constexpr (COUT >= 32)
-    launch_gemm<64, 32, 32, 4, 1>(fa, fb, ep, M, COUT, 4 * CIN, st);
+    launch_gemm_x6<64, 64, 32, 2, 2>(fa, fb, ep, M, COUT, 4 * CIN, st);
   else
     launch_gemm<64, 16, 32, 4, 1>(fa, fb, ep, M, COUT, 4 * CIN, st);
 }
@@ -880,7 +887,7 @@ int aux_backward_impl(const PolicyLayout& L, const float* P, const float* X4, in
   {  // dA1 = conv(dP, W2) masked by the ReLU of A1, in place
     DenseRows fb{P + L.aw2, 16 * kAuxC2, kAuxC1};
     EpiMask ep{A1, A1, kAuxC1};
-    launch_gemm<64, 32, 32, 4, 1>(Im2{dP, P1}, fb, ep, P1, kAuxC1, 16 * kAuxC2, st);
+    launch_gemm_x6<64, 64, 32, 2, 2>(Im2{dP, P1}, fb, ep, P1, kAuxC1, 16 * kAuxC2, st);
   }
   colsum(A1, (int64_t)P1, kAuxC1, w.colsum, Gr + L.ab1, st);
   // first layer: dW1 = X4^T x im2col(dA1); dX4 = conv(dA1, W1)
@@ -889,7 +896,7 @@ int aux_backward_impl(const PolicyLayout& L, const float* P, const float* X4, in
   {
     DenseRows fb{P + L.aw1, 16 * kAuxC1, 32};
     EpiStore ep{dX4, 32};
-    launch_gemm<64, 32, 32, 4, 1>(Im1{A1, P0}, fb, ep, P0, 32, 16 * kAuxC1, st);
+    launch_gemm_x6<128, 32, 32, 4, 1>(Im1{A1, P0}, fb, ep, P0, 32, 16 * kAuxC1, st);
   }
   VN_HIP(hipGetLastError());
   return VN_OK;

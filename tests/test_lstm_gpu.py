@@ -185,9 +185,11 @@ def test_recurrent_trainer_learns_on_small_scene():
     frames = synth_frames(3, np.arange(len(graph)), (84, 84, 3))
     scene = vnav.scene_from_arrays(graph, spd, frames)
     env = vnav.VectorEnv([scene], 256, seed=1, max_episode_steps=60, tasks=[(0, 5)])
-    tr = vnav.A2CTrainer(env, num_steps=20, seed=0, max_time_steps=1e9, recurrent=True)
+    # the LSTM policy learns this task slowly at the reference's 7e-4: a larger step keeps the
+    # check short
+    tr = vnav.A2CTrainer(env, num_steps=20, seed=0, max_time_steps=1e9, recurrent=True, learning_rate=2e-3)
     lengths = []
-    for u in range(400):  # the LSTM policy needs more updates than the feed-forward one
+    for u in range(400):
         m = tr.step(sync=(u < 20 or u >= 390))
         if "raw" not in m:
             lengths.append(m["episode_length"])

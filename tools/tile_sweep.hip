@@ -118,6 +118,44 @@ int main(int argc, char** argv) {
       WGL(128, 128, 2, 2)
       WGL(64, 128, 2, 2)
     }
+#define DENSEX6(BM, BN, BK, WM, WN)                                                                          \
+    {                                                                                                        \
+      DenseRows fa{xc, XC, E};                                                                               \
+      DenseRows fb{wc, XC, 2048};                                                                            \
+      EpiBias2 ep{gt2, 2048, b0, b0};                                                                        \
+      float ms = timeit([&] { launch_gemm_x6<BM, BN, BK, WM, WN>(fa, fb, ep, E, 2048, XC, st); });           \
+      hipMemcpy(h2.data(), gt2, h2.size() * 4, hipMemcpyDeviceToHost);                                       \
+      double md = 0, mx = 0;                                                                                 \
+      for (size_t q = 0; q < h2.size(); ++q) { md = std::max(md, (double)fabsf(h2[q] - h1[q])); mx = std::max(mx, (double)fabsf(h1[q])); } \
+      double e6 = 0, e1 = 0;                                                                                 \
+      for (int q = 0; q < 2048; ++q) {                                                                       \
+        const int rr = (q * 7919) % E, cc = (q * 104729) % 2048;                                             \
+        double ex = 2.0 * hb[cc];                                                                            \
+        for (int kx = 0; kx < XC; ++kx) ex += (double)hx[(size_t)rr * XC + kx] * (double)hw[(size_t)cc * XC + kx]; \
+        e6 = std::max(e6, fabs(h2[(size_t)rr * 2048 + cc] - ex));                                            \
+        e1 = std::max(e1, fabs(h1[(size_t)rr * 2048 + cc] - ex));                                            \
+      }                                                                                                      \
+      printf("lstm gatesX6<%3d,%3d,%2d,%d,%d> %8.3f ms %7.1f TF  max|x6-f32|/max %.2e  fp64 err x6 %.2e f32 %.2e\n", BM, BN, BK, WM, WN, ms, fl / ms / 1e9, md / mx, e6 / mx, e1 / mx); \
+    }
+    std::vector<float> h1((size_t)E * 2048), h2((size_t)E * 2048), hx((size_t)E * XC), hw(2048ll * XC);
+    hipMemcpy(hx.data(), xc, hx.size() * 4, hipMemcpyDeviceToHost);
+    hipMemcpy(hw.data(), wc, hw.size() * 4, hipMemcpyDeviceToHost);
+    std::vector<float> hb(2048);
+    hipMemcpy(hb.data(), b0, hb.size() * 4, hipMemcpyDeviceToHost);
+    float* gt2 = dalloc((int64_t)E * 2048, 30, 0.f);
+    {
+      DenseRows fa{xc, XC, E};
+      DenseRows fb{wc, XC, 2048};
+      EpiBias2 ep{gt, 2048, b0, b0};
+      launch_gemm<64, 64, 32, 2, 2>(fa, fb, ep, E, 2048, XC, st);
+      hipMemcpy(h1.data(), gt, h1.size() * 4, hipMemcpyDeviceToHost);
+    }
+    DENSEX6(64, 64, 32, 2, 2)
+    DENSEX6(128, 128, 32, 2, 2)
+    DENSEX6(128, 128, 16, 2, 2)
+    DENSEX6(128, 64, 32, 2, 2)
+    DENSEX6(64, 128, 32, 2, 2)
+    DENSEX6(256, 128, 16, 2, 2)
     DENSE32(64, 64, 32, 2, 2)
     DENSE32(128, 128, 32, 2, 2)
     DENSE32(128, 128, 16, 2, 2)
