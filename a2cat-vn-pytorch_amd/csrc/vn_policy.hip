@@ -98,6 +98,47 @@ struct NhwcIm2col {
   VN_ROWS_LOADER
 };
 
+// BigHouseModel conv1 (Conv2d(3, 32, k8, s4), bignet.py:29) im2col over the image frame
+// only: row m = (sample, oy, ox), k = (ky*8 + kx)*3 + c, K = 192; u8 frames as x/255
+// (ScaledFloatFrame) or dense float NCHW frames.
+template <int H, int W, int OH, int OW>
+struct FramesIm2colK8 {
+  FrameSrc src;
+  int M;  // samples * OH * OW
+  __device__ __forceinline__ f4 load4(int m, int k, int kend) const {
+    f4 v = f4zero();
+    if (m >= M) return v;
+    const int smp = m / (OH * OW);
+    const int r = m - smp * (OH * OW);
+    const int oy = r / OW, ox = r - (r / OW) * OW;
+    const int lim = min(kend, 192);
+    if (src.f32[0]) {
+      const float* fr = src.f32[0] + (int64_t)smp * 3 * H * W;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int kk = k + j;
+        if (kk < lim) {
+          const int ky = kk / 24, kx = (kk / 3) % 8, c = kk % 3;
+          v[j] = fr[((int64_t)c * H + oy * 4 + ky) * W + ox * 4 + kx];
+        }
+      }
+    } else {
+      const int64_t row = src.rows[0] ? (int64_t)src.rows[0][smp] : (int64_t)smp;
+      const uint8_t* fr = src.base[0] + row * src.stride;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int kk = k + j;
+        if (kk < lim) {
+          const int ky = kk / 24, kx = (kk / 3) % 8, c = kk % 3;
+          v[j] = (float)fr[((oy * 4 + ky) * W + ox * 4 + kx) * 3 + c] / 255.0f;
+        }
+      }
+    }
+    return v;
+  }
+  VN_ROWS_LOADER
+};
+
 // Dense row-major matrix [rows][ld] (ld % 4 == 0, 16-B aligned).
 struct DenseRows {
   const float* A;
@@ -257,6 +298,7 @@ struct LayerOff {
 };
 
 struct PolicyLayout {
+  int arch;  // 0: BigGoalHouseModel (goal.py), 1: BigHouseModel (bignet.py: image only, Nature-CNN trunk)
   int H, W, A, OH1, OW1, OH2, OW2, OH3, OW3, FCIN;
   LayerOff l[6];  // conv1, conv2, conv3, conv4, fc, head
   int64_t n_params;
@@ -272,20 +314,34 @@ struct PolicyLayout {
   int64_t aw1, ab1, aw2, ab2;
 };
 
-inline PolicyLayout make_layout(int H, int W, int A, int lstm = 0, int aux = 0) {
+inline PolicyLayout make_layout(int H, int W, int A, int lstm = 0, int aux = 0, int arch = 0) {
   PolicyLayout L{};
+  L.arch = arch;
   L.H = H;
   L.W = W;
   L.A = A;
-  L.OH1 = (H - 7) / 4 + 1;
-  L.OW1 = (W - 7) / 4 + 1;
-  L.OH2 = (L.OH1 - 4) / 2 + 1;
-  L.OW2 = (L.OW1 - 4) / 2 + 1;
-  L.OH3 = (L.OH2 - 4) / 2 + 1;
-  L.OW3 = (L.OW2 - 4) / 2 + 1;
+  if (arch == 1) {  // bignet.py:28-41: Conv(3,32,k8,s4), Conv(32,64,k4,s2), Conv(64,32,k3), Linear(32*7*7)
+    L.OH1 = (H - 8) / 4 + 1;
+    L.OW1 = (W - 8) / 4 + 1;
+    L.OH2 = (L.OH1 - 4) / 2 + 1;
+    L.OW2 = (L.OW1 - 4) / 2 + 1;
+    L.OH3 = L.OH2 - 2;
+    L.OW3 = L.OW2 - 2;
+  } else {
+    L.OH1 = (H - 7) / 4 + 1;
+    L.OW1 = (W - 7) / 4 + 1;
+    L.OH2 = (L.OH1 - 4) / 2 + 1;
+    L.OW2 = (L.OW1 - 4) / 2 + 1;
+    L.OH3 = (L.OH2 - 4) / 2 + 1;
+    L.OW3 = (L.OW2 - 4) / 2 + 1;
+  }
   L.FCIN = 32 * L.OH3 * L.OW3;
-  const int couts[6] = {32, 32, 64, 32, 512, A + 1};
-  const int ks[6] = {148, 16 * 32, 16 * 64, 64, L.FCIN, 512};
+  const int couts_g[6] = {32, 32, 64, 32, 512, A + 1};
+  const int ks_g[6] = {148, 16 * 32, 16 * 64, 64, L.FCIN, 512};
+  const int couts_b[6] = {32, 64, 32, 0, 512, A + 1};  // layer 3 (conv4) absent
+  const int ks_b[6] = {192, 16 * 32, 9 * 64, 0, L.FCIN, 512};
+  const int* couts = arch == 1 ? couts_b : couts_g;
+  const int* ks = arch == 1 ? ks_b : ks_g;
   int64_t off = 0, wt = 0;
   for (int i = 0; i < 6; ++i) {
     L.l[i].cout = couts[i];
@@ -326,6 +382,15 @@ inline PolicyLayout make_layout(int H, int W, int A, int lstm = 0, int aux = 0) 
   }
   L.n_params = off;
   L.wt_total = wt;
+  if (arch == 1) {  // X1 (one frame per sample), X2, X3, no X4, X5; no ReLU bitmask
+    L.sz[0] = (int64_t)L.OH1 * L.OW1 * 32;
+    L.sz[1] = (int64_t)L.OH2 * L.OW2 * 64;
+    L.sz[2] = (int64_t)L.OH3 * L.OW3 * 32;
+    L.sz[3] = 0;
+    L.sz[4] = 512;
+    L.msz = 0;
+    return L;
+  }
   L.sz[0] = 2ll * L.OH1 * L.OW1 * 32;
   L.sz[1] = 2ll * L.OH2 * L.OW2 * 32;
   L.sz[2] = (int64_t)L.OH3 * L.OW3 * 64;
@@ -566,6 +631,7 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
   // transposed weights for the dgrad products
   for (int i = 1; i < 6; ++i) {
     const int rows = L.l[i].cout, cols = L.l[i].kp;
+    if (rows * cols == 0) continue;
     hipLaunchKernelGGL(transpose_kernel, dim3((rows * cols + 255) / 256), dim3(256), 0, st, P + L.l[i].w, rows, cols,
                        T(i));
   }
@@ -676,6 +742,108 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
                        a.X[0], w.slab);
     hipLaunchKernelGGL(conv1_wgrad_reduce_kernel, dim3((32 * 160 + 255) / 256), dim3(256), 0, st, w.slab, blocks * 4,
                        Gr + L.l[0].w, Gr + L.l[0].b);
+  }
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
+
+// ---- BigHouseModel trunk (models/bignet.py:26-41,70-75): image only ---------------------
+template <int H0, int W0>
+int forward_bignet(const PolicyLayout& L, const float* P, const FrameSrc& src, int n, const Acts& a, float* out,
+                   hipStream_t st) {
+  constexpr int OH1 = (H0 - 8) / 4 + 1, OW1 = (W0 - 8) / 4 + 1;
+  constexpr int OH2 = (OH1 - 4) / 2 + 1, OW2 = (OW1 - 4) / 2 + 1;
+  constexpr int OH3 = OH2 - 2, OW3 = OW2 - 2, FCIN = 32 * OH3 * OW3;
+  {  // conv1 3 -> 32, k8 s4 (X1 [n][OH1][OW1][32])
+    FramesIm2colK8<H0, W0, OH1, OW1> fa{src, n * OH1 * OW1};
+    DenseRows fb{P + L.l[0].w, 192, 32};
+    EpiBiasAct ep{a.X[0], 32, P + L.l[0].b, 1};
+    launch_gemm_x6<128, 32, 32, 4, 1>(fa, fb, ep, fa.M, 32, 192, st);
+  }
+  {  // conv2 32 -> 64, k4 s2
+    NhwcIm2col<32, 4, 4, 2, OH1, OW1, OH2, OW2, 1> fa{a.X[0], n * OH2 * OW2};
+    DenseRows fb{P + L.l[1].w, 512, 64};
+    EpiBiasAct ep{a.X[1], 64, P + L.l[1].b, 1};
+    launch_gemm_x6<64, 64, 32, 2, 2>(fa, fb, ep, fa.M, 64, 512, st);
+  }
+  {  // conv3 64 -> 32, k3 s1
+    NhwcIm2col<64, 3, 3, 1, OH2, OW2, OH3, OW3, 1> fa{a.X[1], n * OH3 * OW3};
+    DenseRows fb{P + L.l[2].w, 576, 32};
+    EpiBiasAct ep{a.X[2], 32, P + L.l[2].b, 1};
+    launch_gemm_x6<128, 32, 32, 4, 1>(fa, fb, ep, fa.M, 32, 576, st);
+  }
+  {  // conv_merge Linear(32*7*7 -> 512) + ReLU (X5)
+    DenseRows fa{a.X[2], FCIN, n};
+    DenseRows fb{P + L.l[4].w, FCIN, 512};
+    EpiBiasAct ep{a.X[4], 512, P + L.l[4].b, 1};
+    launch_gemm_x6<64, 64, 32, 2, 2>(fa, fb, ep, n, 512, FCIN, st);
+  }
+  if (out) {
+    DenseRows fa{a.X[4], 512, n};
+    DenseRows fb{P + L.l[5].w, 512, L.A + 1};
+    EpiBiasAct ep{out, OUT_LD, P + L.l[5].b, 0};
+    launch_gemm<64, 16, 32, 4, 1>(fa, fb, ep, n, L.A + 1, 512, st);
+  }
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
+
+template <int H0, int W0>
+int backward_bignet(const PolicyLayout& L, const float* P, const FrameSrc& src, int n, const Acts& a,
+                    const float* dout, const float* dz5_in, float* Gr, const BwdWork& w, hipStream_t st) {
+  constexpr int OH1 = (H0 - 8) / 4 + 1, OW1 = (W0 - 8) / 4 + 1;
+  constexpr int OH2 = (OH1 - 4) / 2 + 1, OW2 = (OW1 - 4) / 2 + 1;
+  constexpr int OH3 = OH2 - 2, OW3 = OW2 - 2, FCIN = 32 * OH3 * OW3;
+  const int A1 = L.A + 1;
+  auto T = [&](int i) { return w.wt + L.wt_off[i]; };
+  for (int i = 1; i < 6; ++i) {
+    const int rows = L.l[i].cout, cols = L.l[i].kp;
+    if (rows * cols == 0) continue;
+    hipLaunchKernelGGL(transpose_kernel, dim3((rows * cols + 255) / 256), dim3(256), 0, st, P + L.l[i].w, rows, cols,
+                       T(i));
+  }
+  const float* dz5 = dz5_in ? dz5_in : w.dz5;
+  if (!dz5_in) {  // heads
+    DenseRows fa{dout, OUT_LD, n};
+    DenseRows fb{T(5), A1, 512};
+    EpiMask ep{w.dz5, a.X[4], 512};
+    launch_gemm<64, 64, 32, 2, 2>(fa, fb, ep, n, 512, A1, st);
+    Im2colT<DenseRows> fbw{DenseRows{a.X[4], 512, n}, 512};
+    launch_wgrad<32, 64, 2, 2>(dout, OUT_LD, A1, fbw, 512, n, w.slab, w.slab_cap, Gr + L.l[5].w, Gr + L.l[5].b, st);
+  }
+  float* dz3 = w.dz4;  // [n][FCIN]
+  float* dz2 = w.dz2;  // [n][OH2*OW2*64]
+  {  // conv_merge: dX3 = dz5 x Wfc masked by X3 ; dWfc
+    DenseRows fa{dz5, 512, n};
+    DenseRows fb{T(4), 512, FCIN};
+    EpiMask ep{dz3, a.X[2], FCIN};
+    launch_gemm_x6<64, 64, 32, 2, 2>(fa, fb, ep, n, FCIN, 512, st);
+    Im2colT<DenseRows> fbw{DenseRows{a.X[2], FCIN, n}, FCIN};
+    launch_wgrad<64, 64, 2, 2>(dz5, 512, 512, fbw, FCIN, n, w.slab, w.slab_cap, Gr + L.l[4].w, Gr + L.l[4].b, st);
+  }
+  {  // conv3 (k3 s1): wgrad, then the single-class dgrad into dz2 masked by X2
+    using Im = NhwcIm2col<64, 3, 3, 1, OH2, OW2, OH3, OW3, 1>;
+    const int P3 = n * OH3 * OW3;
+    launch_wgrad<32, 64, 2, 2>(dz3, 32, 32, Im2colT<Im>{Im{a.X[1], P3}, 576}, 576, P3, w.slab, w.slab_cap,
+                               Gr + L.l[2].w, Gr + L.l[2].b, st);
+    const int M = n * OH2 * OW2;
+    DgradA<32, 3, 1, OH3, OW3, OH2, OW2> fa{dz3, M};
+    DgradB<32, 3, 1, 64> fb{T(2), 64, 0, 0, 0};
+    EpiMaskParity<OH2, OW2, 1, 0, 0, OH2, OW2> ep{dz2, a.X[1], 0, 1, 64};
+    launch_gemm_x6<64, 64, 32, 2, 2>(fa, fb, ep, M, 64, 9 * 32, st);
+  }
+  {  // conv2 (k4 s2): wgrad, then parity-class dgrad over X1 in place
+    using Im = NhwcIm2col<32, 4, 4, 2, OH1, OW1, OH2, OW2, 1>;
+    const int P2 = n * OH2 * OW2;
+    launch_wgrad<64, 64, 2, 2>(dz2, 64, 64, Im2colT<Im>{Im{a.X[0], P2}, 512}, 512, P2, w.slab, w.slab_cap,
+                               Gr + L.l[1].w, Gr + L.l[1].b, st);
+    dgrad_all_classes<64, 32, OH1, OW1, OH2, OW2>(dz2, T(1), a.X[0], a.X[0], n, 0, 1, 32, st);
+  }
+  {  // conv1 wgrad from dX1 (in X1's storage) and the frames
+    using Im = FramesIm2colK8<H0, W0, OH1, OW1>;
+    const int P1 = n * OH1 * OW1;
+    launch_wgrad<32, 64, 2, 2>(a.X[0], 32, 32, Im2colT<Im>{Im{src, P1}, 192}, 192, P1, w.slab, w.slab_cap,
+                               Gr + L.l[0].w, Gr + L.l[0].b, st);
   }
   VN_HIP(hipGetLastError());
   return VN_OK;
@@ -950,14 +1118,18 @@ int vn_policy_create(int frame_h, int frame_w, int num_actions, vn_policy** out)
 
 int vn_policy_create_ex(int frame_h, int frame_w, int num_actions, int flags, vn_policy** out) {
   if (!out) return fail(VN_EINVAL, "vn_policy_create: out is NULL");
-  if (flags & ~(VN_POLICY_LSTM | VN_POLICY_AUX)) return fail(VN_EINVAL, "vn_policy_create: unknown flags");
+  if (flags & ~(VN_POLICY_LSTM | VN_POLICY_AUX | VN_POLICY_BIGHOUSE))
+    return fail(VN_EINVAL, "vn_policy_create: unknown flags");
+  if ((flags & VN_POLICY_BIGHOUSE) && (frame_h != 84 || frame_w != 84 || (flags & VN_POLICY_AUX)))
+    return fail(VN_EINVAL, "vn_policy_create: BigHouseModel takes 84x84 frames (Linear(7*7*32)) and no aux heads");
   *out = nullptr;
   if (!supported(frame_h, frame_w))
     return fail(VN_EINVAL, "vn_policy_create: frame size must be 84x84, 174x174 or 300x400");
   if (num_actions < 1 || num_actions + 1 > OUT_LD) return fail(VN_EINVAL, "vn_policy_create: 1..7 actions");
   vn_policy* p = new (std::nothrow) vn_policy();
   if (!p) return fail(VN_ENOMEM, "vn_policy_create: host allocation");
-  p->L = make_layout(frame_h, frame_w, num_actions, (flags & VN_POLICY_LSTM) ? 1 : 0, (flags & VN_POLICY_AUX) ? 1 : 0);
+  p->L = make_layout(frame_h, frame_w, num_actions, (flags & VN_POLICY_LSTM) ? 1 : 0, (flags & VN_POLICY_AUX) ? 1 : 0,
+                     (flags & VN_POLICY_BIGHOUSE) ? 1 : 0);
   *out = p;
   return VN_OK;
 }
@@ -1000,6 +1172,7 @@ int vn_policy_forward(vn_policy* p, const float* params, const vn_frames* frames
     return fail(VN_EINVAL, "vn_policy_forward: missing frames");
   const Acts a = acts_at(p->L, acts, act_capacity, act_offset);
   hipStream_t st = (hipStream_t)stream;
+  if (p->L.arch == 1) return forward_bignet<84, 84>(p->L, params, src, n, a, out, st);
   return dispatch_geo(p->L, [&](auto g) {
     return forward_impl<decltype(g)::H, decltype(g)::W>(p->L, params, src, n, a, out, st);
   });
@@ -1016,6 +1189,10 @@ int vn_policy_backward_ex(vn_policy* p, const float* params, const vn_frames* fr
   const BwdWork w = carve(p->L, workspace, n);
   hipStream_t st = (hipStream_t)stream;
   const float* d = dz5 ? nullptr : dout;
+  if (p->L.arch == 1) {
+    if (dx4_extra) return fail(VN_EINVAL, "vn_policy_backward: BigHouseModel has no aux heads");
+    return backward_bignet<84, 84>(p->L, params, src, n, a, d, dz5, grads, w, st);
+  }
   return dispatch_geo(p->L, [&](auto g) {
     return backward_impl<decltype(g)::H, decltype(g)::W>(p->L, params, src, n, a, d, dz5, dx4_extra, grads, w, st);
   });

@@ -40,7 +40,7 @@ class A2CTrainer:
     def __init__(self, env, net=None, params=None, num_steps=20, gamma=0.99, learning_rate=7e-4,
                  max_time_steps=2e6, rms_alpha=0.99, rms_epsilon=1e-5, max_gradient_norm=0.5,
                  value_coefficient=0.5, entropy_coefficient=0.01, seed=0, process_group=None, recurrent=False,
-                 aux_weight=0.0):
+                 aux_weight=0.0, arch="goal"):
         self.env = env
         self.lib = _lib.load()
         self.device = env.device
@@ -58,7 +58,7 @@ class A2CTrainer:
         self.world, self.rank = vdist.world_of(process_group)
         self.aux_weight = float(aux_weight)
         self.net = net if net is not None else PolicyNet(env.frame_shape[:2], env.num_actions, self.device,
-                                                         recurrent=recurrent, aux=self.aux_weight > 0)
+                                                         recurrent=recurrent, aux=self.aux_weight > 0, arch=arch)
         self.recurrent = self.net.recurrent
         if self.aux_weight > 0 and (not self.net.aux or getattr(env, "aux_arena", None) is None):
             raise ValueError("aux_weight > 0 needs an aux policy (aux=True) and scenes with depth + segmentation")

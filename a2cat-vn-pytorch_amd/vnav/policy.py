@@ -71,8 +71,13 @@ AUX_HEADS = (("deconv_depth", 1, 0), ("deconv_mask", 3, 1), ("deconv_mask_goal",
 class PolicyNet:
     """Handle on a vn_policy: flat parameter layout, forward/backward launches."""
 
-    def __init__(self, frame_hw=(84, 84), num_actions=4, device=None, recurrent=False, aux=False):
+    def __init__(self, frame_hw=(84, 84), num_actions=4, device=None, recurrent=False, aux=False, arch="goal"):
+        """arch "goal": BigGoalHouseModel (models/goal.py); "bighouse": BigHouseModel
+        (models/bignet.py, image only, 84x84)."""
         self.lib = _lib.load()
+        if arch not in ("goal", "bighouse"):
+            raise ValueError("arch must be 'goal' or 'bighouse'")
+        self.arch = arch
         self.recurrent = bool(recurrent)
         self.aux = bool(aux)
         self.frame_hw = tuple(frame_hw)
@@ -80,7 +85,8 @@ class PolicyNet:
         self.device = torch.device("cuda", torch.cuda.current_device() if device is None else
                                    torch.device(device).index or 0)
         h = ctypes.c_void_p()
-        flags = (1 if recurrent else 0) | (2 if aux else 0)  # VN_POLICY_LSTM | VN_POLICY_AUX
+        # VN_POLICY_LSTM | VN_POLICY_AUX | VN_POLICY_BIGHOUSE
+        flags = (1 if recurrent else 0) | (2 if aux else 0) | (4 if arch == "bighouse" else 0)
         _lib.check(self.lib.vn_policy_create_ex(frame_hw[0], frame_hw[1], num_actions, flags, ctypes.byref(h)),
                    "vn_policy_create_ex")
         self._h = h
@@ -90,10 +96,18 @@ class PolicyNet:
         self.n_params = n.value
         self.act_floats = a.value
         self.offsets = {name: (lay[2 * i], lay[2 * i + 1]) for i, name in enumerate(LAYERS)}
-        _, _, o3 = trunk_sizes(*frame_hw)
-        self.fc_in = 32 * o3[0] * o3[1]
-        self.shapes = {"conv1": (32, 148), "conv2": (32, 512), "conv3": (64, 1024), "conv4": (32, 64),
-                       "fc": (512, self.fc_in), "head": (num_actions + 1, 512)}
+        if arch == "bighouse":
+            self.o3 = (7, 7)
+            self.fc_in = 32 * 7 * 7
+            self.shapes = {"conv1": (32, 192), "conv2": (64, 512), "conv3": (32, 576), "conv4": (0, 0),
+                           "fc": (512, self.fc_in), "head": (num_actions + 1, 512)}
+            self.fan_in = {"conv1": 192, "conv2": 512, "conv3": 576, "conv4": 1, "fc": self.fc_in, "head": 512}
+        else:
+            _, _, self.o3 = trunk_sizes(*frame_hw)
+            self.fc_in = 32 * self.o3[0] * self.o3[1]
+            self.shapes = {"conv1": (32, 148), "conv2": (32, 512), "conv3": (64, 1024), "conv4": (32, 64),
+                           "fc": (512, self.fc_in), "head": (num_actions + 1, 512)}
+            self.fan_in = {"conv1": 147, "conv2": 512, "conv3": 1024, "conv4": 64, "fc": self.fc_in, "head": 512}
         self.lstm = None
         if self.recurrent:
             info = (ctypes.c_int64 * 8)()
@@ -137,15 +151,16 @@ class PolicyNet:
         return torch.zeros(self.n_params, dtype=torch.float32, device=self.device)
 
     def init_params(self, seed=0):
-        """BigGoalHouseModel.init_weights (goal.py:26-30): bias 0, W ~ U(+-1/sqrt(fan_in))."""
+        """init_weights (goal.py:26-30, bignet.py:17-21): bias 0, W ~ U(+-1/sqrt(fan_in))."""
         g = torch.Generator(device="cpu").manual_seed(seed)
         flat = torch.zeros(self.n_params, dtype=torch.float32)
-        fan_in = {"conv1": 147, "conv2": 512, "conv3": 1024, "conv4": 64, "fc": self.fc_in, "head": 512}
         v = self.views(flat)
         for name in LAYERS:
             w, _ = v[name]
-            d = 1.0 / math.sqrt(fan_in[name])
-            k = 147 if name == "conv1" else w.shape[1]
+            if w.numel() == 0:
+                continue
+            d = 1.0 / math.sqrt(self.fan_in[name])
+            k = 147 if (name == "conv1" and self.arch == "goal") else w.shape[1]
             w[:, :k].uniform_(-d, d, generator=g)
         if self.lstm:  # goal.py:17-24: xavier_uniform W_ih, orthogonal W_hh, zero biases
             L = self.lstm
@@ -170,19 +185,25 @@ class PolicyNet:
         v = self.views(flat)
         pick = _ReferenceNames(sd)
         t = lambda x: torch.as_tensor(np.asarray(x), dtype=torch.float32)  # noqa: E731
-        w, b = v["conv1"]
-        w[:, :147] = t(pick("shared_base", 0, "weight")).permute(0, 2, 3, 1).reshape(32, 147)
-        b[:] = t(pick("shared_base", 0, "bias"))
-        w, b = v["conv2"]
-        w[:] = t(pick("shared_base", 1, "weight")).permute(0, 2, 3, 1).reshape(32, 512)
-        b[:] = t(pick("shared_base", 1, "bias"))
-        w, b = v["conv3"]
-        w[:] = t(pick("conv_base", 0, "weight")).permute(0, 2, 3, 1).reshape(64, 1024)
-        b[:] = t(pick("conv_base", 0, "bias"))
-        w, b = v["conv4"]
-        w[:] = t(pick("conv_base", 1, "weight")).reshape(32, 64)
-        b[:] = t(pick("conv_base", 1, "bias"))
-        _, _, o3 = trunk_sizes(*self.frame_hw)
+        o3 = self.o3
+        if self.arch == "bighouse":  # bignet.py:28-41: conv_base = Conv k8s4, k4s2, k3; conv_merge Linear
+            for i, (name, k, co) in enumerate((("conv1", 192, 32), ("conv2", 512, 64), ("conv3", 576, 32))):
+                w, b = v[name]
+                w[:] = t(pick("conv_base", i, "weight")).permute(0, 2, 3, 1).reshape(co, k)
+                b[:] = t(pick("conv_base", i, "bias"))
+        else:
+            w, b = v["conv1"]
+            w[:, :147] = t(pick("shared_base", 0, "weight")).permute(0, 2, 3, 1).reshape(32, 147)
+            b[:] = t(pick("shared_base", 0, "bias"))
+            w, b = v["conv2"]
+            w[:] = t(pick("shared_base", 1, "weight")).permute(0, 2, 3, 1).reshape(32, 512)
+            b[:] = t(pick("shared_base", 1, "bias"))
+            w, b = v["conv3"]
+            w[:] = t(pick("conv_base", 0, "weight")).permute(0, 2, 3, 1).reshape(64, 1024)
+            b[:] = t(pick("conv_base", 0, "bias"))
+            w, b = v["conv4"]
+            w[:] = t(pick("conv_base", 1, "weight")).reshape(32, 64)
+            b[:] = t(pick("conv_base", 1, "bias"))
         w, b = v["fc"]
         w[:] = t(pick("conv_merge", 0, "weight")).view(512, 32, o3[0], o3[1]).permute(0, 2, 3, 1).reshape(512, -1)
         b[:] = t(pick("conv_merge", 0, "bias"))
@@ -211,21 +232,27 @@ class PolicyNet:
     def to_reference(self, flat):
         """Flat params (or grads) -> dict in the reference's tensor shapes."""
         v = self.views(flat.detach().float().cpu())
-        _, _, o3 = trunk_sizes(*self.frame_hw)
+        o3 = self.o3
         A = self.num_actions
         out = {}
-        w, b = v["conv1"]
-        out["shared_base.0.0.weight"] = w[:, :147].reshape(32, 7, 7, 3).permute(0, 3, 1, 2).contiguous()
-        out["shared_base.0.0.bias"] = b.clone()
-        w, b = v["conv2"]
-        out["shared_base.0.2.weight"] = w.reshape(32, 4, 4, 32).permute(0, 3, 1, 2).contiguous()
-        out["shared_base.0.2.bias"] = b.clone()
-        w, b = v["conv3"]
-        out["conv_base.0.0.weight"] = w.reshape(64, 4, 4, 64).permute(0, 3, 1, 2).contiguous()
-        out["conv_base.0.0.bias"] = b.clone()
-        w, b = v["conv4"]
-        out["conv_base.0.2.weight"] = w.reshape(32, 64, 1, 1).clone()
-        out["conv_base.0.2.bias"] = b.clone()
+        if self.arch == "bighouse":
+            for i, (name, kk, ci, co) in enumerate((("conv1", 8, 3, 32), ("conv2", 4, 32, 64), ("conv3", 3, 64, 32))):
+                w, b = v[name]
+                out["conv_base.0.%d.weight" % (2 * i)] = w.reshape(co, kk, kk, ci).permute(0, 3, 1, 2).contiguous()
+                out["conv_base.0.%d.bias" % (2 * i)] = b.clone()
+        else:
+            w, b = v["conv1"]
+            out["shared_base.0.0.weight"] = w[:, :147].reshape(32, 7, 7, 3).permute(0, 3, 1, 2).contiguous()
+            out["shared_base.0.0.bias"] = b.clone()
+            w, b = v["conv2"]
+            out["shared_base.0.2.weight"] = w.reshape(32, 4, 4, 32).permute(0, 3, 1, 2).contiguous()
+            out["shared_base.0.2.bias"] = b.clone()
+            w, b = v["conv3"]
+            out["conv_base.0.0.weight"] = w.reshape(64, 4, 4, 64).permute(0, 3, 1, 2).contiguous()
+            out["conv_base.0.0.bias"] = b.clone()
+            w, b = v["conv4"]
+            out["conv_base.0.2.weight"] = w.reshape(32, 64, 1, 1).clone()
+            out["conv_base.0.2.bias"] = b.clone()
         w, b = v["fc"]
         out["conv_merge.0.1.weight"] = w.reshape(512, o3[0], o3[1], 32).permute(0, 3, 1, 2).reshape(512, -1).contiguous()
         out["conv_merge.0.1.bias"] = b.clone()
@@ -498,12 +525,14 @@ class _AuxDeconvFunction(torch.autograd.Function):
 class GoalNavPolicy(torch.nn.Module):
     """Drop-in for BigGoalHouseModel's trunk + heads (see module docstring)."""
 
+    _ARCH = "goal"
+
     def __init__(self, num_inputs=3, num_outputs=4, frame_hw=(84, 84), device=None, seed=0, recurrent=False,
                  aux=False):
         super().__init__()
         if num_inputs != 3:
             raise ValueError("frames are RGB (num_inputs=3)")
-        self.net = PolicyNet(frame_hw, num_outputs, device, recurrent=recurrent, aux=aux)
+        self.net = PolicyNet(frame_hw, num_outputs, device, recurrent=recurrent, aux=aux, arch=self._ARCH)
         self.deconv_cell_size = 4  # goal.py:70,148
         self.params = torch.nn.Parameter(self.net.init_params(seed))
         self.lstm_layers, self.lstm_hidden_size = 1, 512  # goal.py:61-62 (state shape contract)
@@ -587,3 +616,24 @@ class GoalNavPolicy(torch.nn.Module):
         h, w = p.shape[-2:]
         heads = tuple(p[:, o:o + c].reshape(*lead, c, h, w) for _, c, o in AUX_HEADS)
         return heads, states
+
+
+class BigHousePolicy(GoalNavPolicy):
+    """Drop-in for BigHouseModel (models/bignet.py:26-75): ``forward(inputs, masks, states)``
+    with ``inputs = (observations, last_reward_action)`` and observations ONE image tensor
+    ([B,T,84,84,3] uint8 or [B,T,3,84,84] float), Nature-CNN trunk (Conv k8s4 -> k4s2 -> k3,
+    Linear(7*7*32, 512)) on the HIP kernels, then the heads (recurrent=True: the LSTM core)."""
+
+    _ARCH = "bighouse"
+
+    def __init__(self, num_inputs=3, num_outputs=4, device=None, seed=0, recurrent=True):
+        super().__init__(num_inputs, num_outputs, (84, 84), device, seed, recurrent=recurrent)
+
+    def forward(self, inputs, masks=None, states=None):
+        observations, last_reward_action = inputs if isinstance(inputs, tuple) and len(inputs) == 2 \
+            else (inputs, None)
+        # the image feeds both frame slots; the BigHouse kernels read only the first
+        return super().forward(((observations, observations), last_reward_action), masks, states)
+
+    def forward_deconv(self, inputs, masks=None, states=None):
+        raise NotImplementedError("BigHouseModel has no deconv heads (bignet.py)")

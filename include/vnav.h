@@ -245,6 +245,12 @@ int vn_policy_backward_trunk(vn_policy* p, const float* params, const vn_frames*
  * AH, AW = first deconv map, PH, PW = prediction map). Heads read conv_base's output (X4)
  * from the activation store of vn_policy_forward; a1 [n][AH][AW][48], pred [n][PH][PW][8]. */
 #define VN_POLICY_AUX 2
+/* BigHouseModel (models/bignet.py:26-75) instead of BigGoalHouseModel: image only (the goal
+ * frames are ignored), Conv(3,32,k8,s4) ReLU, Conv(32,64,k4,s2) ReLU, Conv(64,32,k3) ReLU,
+ * Linear(7*7*32, 512) ReLU (84x84 frames only, as the reference's Linear fixes), then the same
+ * heads / recurrent core. Layer slots: conv1 [32][8][8][3], conv2 [64][4][4][32],
+ * conv3 [32][3][3][64], (conv4 slot empty), conv_merge, head. */
+#define VN_POLICY_BIGHOUSE 4
 typedef struct vn_aux_targets {
   const float* table;           /* [rows][PH][PW][4] from vn_aux_target_table */
   const int32_t* image_rows;    /* [n] row of each sample's state (vn_frames.image_rows) */

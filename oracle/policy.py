@@ -140,6 +140,85 @@ def aux_loss(predictions, targets):
     return sum(F.mse_loss(p, t) for p, t in zip(predictions, targets))
 
 
+class BigHouseOracle(nn.Module):
+    """BigHouseModel (models/bignet.py:26-75): conv_base Conv(3,32,k8,s4) ReLU, Conv(32,64,k4,s2)
+    ReLU, Conv(64,32,k3) ReLU; conv_merge Linear(7*7*32, 512) ReLU; heads; the recurrent core
+    as RecurrentGoalNetOracle (MaskedRNN convention unpinned). Image only."""
+
+    def __init__(self, num_outputs=4):
+        super().__init__()
+        self.conv1 = nn.Conv2d(3, 32, 8, stride=4)
+        self.conv2 = nn.Conv2d(32, 64, 4, stride=2)
+        self.conv3 = nn.Conv2d(64, 32, 3)
+        self.fc = nn.Linear(7 * 7 * 32, 512)
+        self.policy_logits = nn.Linear(512, num_outputs)
+        self.critic = nn.Linear(512, 1)
+        self.lstm = nn.LSTM(512 + num_outputs + 1, 512, num_layers=1, batch_first=True)
+
+    def features(self, image):
+        x = F.relu(self.conv3(F.relu(self.conv2(F.relu(self.conv1(image))))))
+        return F.relu(self.fc(x.flatten(1)))
+
+    def forward(self, image):
+        f = self.features(image)
+        return self.policy_logits(f), self.critic(f)
+
+    def forward_seq(self, image, last_reward_action, masks, states):
+        B, T = image.shape[:2]
+        x = torch.cat((self.features(image.flatten(0, 1)).view(B, T, 512), last_reward_action), 2)
+        h, c = states[0].transpose(0, 1), states[1].transpose(0, 1)
+        outs = []
+        for t in range(T):
+            m = masks[:, t].reshape(1, B, 1)
+            o, (h, c) = self.lstm(x[:, t:t + 1], (h * m, c * m))
+            outs.append(o)
+        y = torch.cat(outs, 1)
+        return self.policy_logits(y), self.critic(y), (h.transpose(0, 1), c.transpose(0, 1))
+
+    def load_reference(self, sd):
+        m = {"conv_base.0.0": self.conv1, "conv_base.0.2": self.conv2, "conv_base.0.4": self.conv3,
+             "conv_merge.0.1": self.fc, "policy_logits.0": self.policy_logits, "critic.0": self.critic}
+        for k, mod in m.items():
+            mod.weight.data.copy_(torch.as_tensor(sd[k + ".weight"]))
+            mod.bias.data.copy_(torch.as_tensor(sd[k + ".bias"]))
+        for name in ("weight_ih_l0", "weight_hh_l0", "bias_ih_l0", "bias_hh_l0"):
+            keys = [k for k in sd if k.endswith(name)]
+            if keys:
+                getattr(self.lstm, name).data.copy_(torch.as_tensor(sd[keys[0]]))
+        return self
+
+
+BIGHOUSE_PARAM_ORDER = (  # BigHouseModel.named_parameters() order for the trunk + heads
+    "conv_base.0.0.weight", "conv_base.0.0.bias", "conv_base.0.2.weight", "conv_base.0.2.bias",
+    "conv_base.0.4.weight", "conv_base.0.4.bias", "conv_merge.0.1.weight", "conv_merge.0.1.bias",
+    "critic.0.weight", "critic.0.bias", "policy_logits.0.weight", "policy_logits.0.bias",
+)
+BIGHOUSE_SHAPES = {
+    "conv_base.0.0.weight": (32, 3, 8, 8), "conv_base.0.0.bias": (32,),
+    "conv_base.0.2.weight": (64, 32, 4, 4), "conv_base.0.2.bias": (64,),
+    "conv_base.0.4.weight": (32, 64, 3, 3), "conv_base.0.4.bias": (32,),
+    "conv_merge.0.1.weight": (512, 1568), "conv_merge.0.1.bias": (512,),
+    "critic.0.weight": (1, 512), "critic.0.bias": (1,),
+    "policy_logits.0.weight": (4, 512), "policy_logits.0.bias": (4,),
+}
+
+
+def seeded_bighouse_state(seed):
+    """tests/golden/gen_model_goldens.py:seeded_weights over BigHouseModel's trunk + heads."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    out = {}
+    for name in BIGHOUSE_PARAM_ORDER:
+        shape = BIGHOUSE_SHAPES[name]
+        if name.endswith("bias"):
+            v = rng.uniform(-0.05, 0.05, size=shape)
+        else:
+            d = 1.0 / np.sqrt(int(np.prod(shape[1:])))
+            v = rng.uniform(-d, d, size=shape)
+        out[name] = v.astype(np.float32)
+    return out
+
+
 def frames_to_float(u8):
     """uint8 [...,H,W,C] -> float32 [...,C,H,W] / 255 (TransposeImage + ScaledFloatFrame)."""
     x = torch.as_tensor(u8)

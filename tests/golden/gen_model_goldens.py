@@ -26,6 +26,7 @@ REPO = os.path.dirname(os.path.dirname(HERE))
 sys.path[:0] = [os.path.join(HERE, "stubs"), "/root/reference", REPO]
 
 from models.goal import AuxiliaryBigGoalHouseModel, BigGoalHouseModel  # noqa: E402  (the reference modules)
+from models.bignet import BigHouseModel  # noqa: E402
 
 from oracle import a2c  # noqa: E402
 
@@ -146,10 +147,42 @@ def aux_case(frame, B, T, seed):
     return out
 
 
+BIG_USED = ("conv_base", "conv_merge", "policy_logits", "critic")
+
+
+def bighouse_case(B, T, seed):
+    """BigHouseModel (models/bignet.py:26-75, unmodified: its Linear(7*7*32) fits 84x84):
+    conv_base + conv_merge features and the heads on them (the LSTM's MaskedRNN semantics are
+    unpinned), weights from the seed (PCG64). Stores the inputs, features, logits, value and
+    the engine's A2C loss gradients of the conv and head parameters."""
+    torch.manual_seed(seed)
+    model = BigHouseModel(3, 4)
+    seeded_weights(model, seed, BIG_USED)
+    rng = np.random.RandomState(seed)
+    image = torch.as_tensor(rng.randint(0, 256, size=(B, T, 84, 84, 3)).astype(np.uint8))
+    img = (image.permute(0, 1, 4, 2, 3).float() / 255.0).contiguous()
+    feats = model.conv_merge(model.conv_base(img))
+    logits, value = model.policy_logits(feats), model.critic(feats)
+    N = B * T
+    actions = torch.as_tensor(rng.randint(0, 4, size=N))
+    rets = torch.as_tensor(rng.randn(N).astype(np.float32))
+    loss, _ = a2c.loss(logits.reshape(N, 4), value.reshape(N), actions, rets)
+    model.zero_grad()
+    loss.backward()
+    out = {"image": image.numpy(), "features": feats.detach().numpy(), "logits": logits.detach().numpy(),
+           "value": value.detach().numpy(), "actions": actions.numpy().astype(np.int32), "returns": rets.numpy(),
+           "loss": np.array([loss.item()], dtype=np.float32), "seed": np.array([seed])}
+    for name, p in model.named_parameters():
+        if name.split(".")[0] in ("conv_base", "policy_logits", "critic"):
+            out["g:" + name] = p.grad.numpy()
+    return out
+
+
 def main():
     np.savez_compressed(os.path.join(HERE, "policy84.npz"), **case(84, 3, 2, 11))
     np.savez_compressed(os.path.join(HERE, "policy174.npz"), **case(174, 2, 1, 12, store_weights=False))
     np.savez_compressed(os.path.join(HERE, "aux174.npz"), **aux_case(174, 2, 1, 13))
+    np.savez_compressed(os.path.join(HERE, "bighouse84.npz"), **bighouse_case(2, 2, 14))
     n_params = sum(p.numel() for n, p in build(84, 0).named_parameters() if n.split(".")[0] in USED)
     print("84x84 trunk+heads parameters:", n_params)
 

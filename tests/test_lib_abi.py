@@ -58,7 +58,7 @@ def test_recurrent_policy_layout(built_lib):
     assert lib.vn_policy_info(h, ctypes.byref(n), None, None) == 0
     assert n.value == base + 2048 * xcat + 4096
     lib.vn_policy_destroy(h)
-    assert lib.vn_policy_create_ex(84, 84, 4, 4, ctypes.byref(h)) != 0  # unknown flag
+    assert lib.vn_policy_create_ex(84, 84, 4, 8, ctypes.byref(h)) != 0  # unknown flag
 
 
 def test_aux_policy_layout(built_lib):
@@ -83,3 +83,24 @@ def test_aux_policy_layout(built_lib):
         assert lib.vn_policy_info(h, ctypes.byref(n), None, None) == 0
         assert n.value == plain + 24576 + 48 + 6144 + 8
         lib.vn_policy_destroy(h)
+
+
+def test_bighouse_policy_layout(built_lib):
+    """VN_POLICY_BIGHOUSE: BigHouseModel's trunk (bignet.py:28-41) + heads = 863365 parameters
+    (the count of the reference module's conv_base/conv_merge/critic/policy_logits), the LSTM
+    appended as for the goal net; 84x84 only, no aux heads."""
+    from vnav import _lib
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    n = ctypes.c_int64()
+    assert lib.vn_policy_create_ex(84, 84, 4, 4, ctypes.byref(h)) == 0
+    assert lib.vn_policy_info(h, ctypes.byref(n), None, None) == 0
+    assert n.value == 863365
+    lib.vn_policy_destroy(h)
+    assert lib.vn_policy_create_ex(84, 84, 4, 5, ctypes.byref(h)) == 0
+    info = (ctypes.c_int64 * 8)()
+    assert lib.vn_policy_lstm_info(h, info) == 0
+    assert info[0] == 863365 and info[5] == 512 + 4 + 1
+    lib.vn_policy_destroy(h)
+    assert lib.vn_policy_create_ex(174, 174, 4, 4, ctypes.byref(h)) != 0  # Linear(7*7*32) fixes 84x84
+    assert lib.vn_policy_create_ex(84, 84, 4, 6, ctypes.byref(h)) != 0    # no aux heads on BigHouse
