@@ -16,6 +16,8 @@
 //            deterministic reduce sums (and scales by 1/255).
 #pragma once
 
+#include "vn_conv1_lanes.h"
+
 namespace vn {
 
 typedef float f16v __attribute__((ext_vector_type(16)));
@@ -132,7 +134,7 @@ __device__ __forceinline__ void split3_bf16(float w, uint16_t& hi, uint16_t& mid
 }
 
 template <int H, int W, int OH, int OW>
-__global__ __launch_bounds__(256) void conv1_fwd_x3_kernel(FrameSrc src, int n_frames, const float* __restrict__ Wt,
+__global__ __launch_bounds__(256, 2) void conv1_fwd_x3_kernel(FrameSrc src, int n_frames, const float* __restrict__ Wt,
                                                            const float* __restrict__ bias, float* __restrict__ Y,
                                                            uint32_t* __restrict__ mask) {
   constexpr int RB = W * 3;                 // frame row bytes
@@ -308,6 +310,211 @@ __global__ void conv1_wgrad_reduce_kernel(const float* __restrict__ slab, int ns
     dW[co * 148 + k] = k < 147 ? s * (1.0f / 255.0f) : 0.0f;
   else
     db[co] = s;
+}
+
+// ---- weight gradient on bf16 MFMA with split dZ ----------------------------------
+// D[co 32][tap 32] += A[co][pixel 16] * B[pixel 16][tap] on v_mfma_f32_32x32x16_bf16, five
+// tap tiles (147 taps + bias column): dZ is split by truncation into three bf16 terms
+// (exact, as the forward's weights), the frame bytes are exact in bf16, so every product is
+// exact and the fp32 accumulation sees the same terms as the f32 kernel.
+//   A: read straight from dZ in its MFMA layout — lane (co, h) takes the 8 pixels of group
+//      g = 2s + h (one output row's pixels 8(g % 3) .. +7, the last group of a row half
+//      padding with dZ = 0): eight loads of one 128-B pixel row each, two steps ahead.
+//   B: the frame is staged per workgroup as Q[y][x & 3][c][x >> 2] (bf16, strides 24 / 72 /
+//      296 elements), so the 8 pixels of a group at one tap (ky, kx, c) are 8 consecutive
+//      elements: one ds_read_b128 per tile (taps kx >= 4 sit in tiles 3-4 and take one more
+//      element and a 16-bit funnel shift). The tap -> lane tables (vn_conv1_lanes.h) put
+//      the 16 lanes of every b128 pass group on distinct bank quads.
+// Wave w takes the steps s = w (mod 4) of every frame; the four wave sums are folded through
+// LDS into one slab per workgroup, slot tile*32 + c32 (kConv1WgradCol maps it to dW).
+constexpr int kQPC = 24, kQPX = 72, kQRS = 296;  // Q strides (bf16 elements): c row, x & 3 plane, image row
+
+template <int H, int W>
+constexpr bool conv1_wgrad_x3_fits() {
+  return H == 84 && W == 84;  // the lane tables are laid out for this frame (20x20 map)
+}
+
+template <int H, int W, int OH, int OW>
+__global__ __launch_bounds__(256) void conv1_wgrad_x3_kernel(FrameSrc src, int n_frames, const float* __restrict__ dZ,
+                                                             float* __restrict__ slab) {
+  static_assert(H == 84 && W == 84 && OH == 20 && OW == 20, "Q layout and lane tables for 84x84 frames");
+  constexpr int RB = W * 3;
+  constexpr int NPIX = OH * OW;
+  constexpr int GPR = (OW + 7) / 8;       // 8-pixel groups per output row
+  constexpr int KS = (OH * GPR + 1) / 2;  // 16-pixel steps: two groups (one per lane half)
+  constexpr int PAIRS = (W / 4 + 1) / 2;  // x>>2 pairs per image row (the last one half)
+  constexpr int TASKS = H * PAIRS;        // (row, pair) staging tasks per frame
+  constexpr int NT = (TASKS + 255) / 256;
+  static_assert(kQRS >= 4 * kQPX + 8 && kQPX == 3 * kQPC && kQPC >= 2 * PAIRS + 2, "Q strides");
+  __shared__ __attribute__((aligned(16))) uint16_t Q[H * kQRS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, c32 = lane & 31;
+  {  // never-written Q entries (x >> 2 >= 22, row tails) are read by padding pixels: zero
+    uint4* q4 = reinterpret_cast<uint4*>(Q);
+    for (int i = tid; i < H * kQRS / 8; i += 256) q4[i] = uint4{0u, 0u, 0u, 0u};
+  }
+  int loff[5];
+#pragma unroll
+  for (int nt = 0; nt < 5; ++nt) {
+    const int t = kConv1WgradRead[nt][c32], ky = t / 21, kx = (t / 3) % 7, c = t % 3;
+    loff[nt] = ky * kQRS + (kx & 3) * kQPX + c * kQPC;
+  }
+  const int col2 = kConv1WgradCol[2][c32];  // tile 2 carries the bias column and pad lanes
+  const uint32_t keep2 = col2 >= 0 && col2 < 147 ? 0xffffffffu : 0u;
+  const uint32_t add2 = col2 == 148 ? 0x3f803f80u : 0u;
+  const uint32_t keep4 = kConv1WgradCol[4][c32] >= 0 ? 0xffffffffu : 0u;
+  f16v acc[5];
+#pragma unroll
+  for (int nt = 0; nt < 5; ++nt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[nt][r] = 0.0f;
+  // staging task (row y, pair m): pixels 8m .. 8m+7 of row y = 24 frame bytes (12 in the
+  // last, half pair), prefetched into registers one frame ahead. vmcnt retires loads in
+  // issue order, so the next frame's tasks are issued one per step between the dZ loads
+  // (a whole-frame prefetch would stall the first dZ use behind it).
+  uint32_t pre[NT][6];
+  auto load_task = [&](int r, int f) {
+    const int t = tid + r * 256;
+    if (t < TASKS) {
+      const int y = t / PAIRS, m = t - (t / PAIRS) * PAIRS;
+      const uint32_t* s4 = reinterpret_cast<const uint32_t*>(frame_ptr(src, f) + y * RB + m * 24);
+      const bool full = 8 * m + 8 <= W;
+#pragma unroll
+      for (int q = 0; q < 6; ++q) pre[r][q] = (q < 3 || full) ? s4[q] : 0u;
+    }
+  };
+  static_assert(NT <= (KS / 4) - 1, "every wave has a step per staging task");
+  auto stage_frame_q = [&]() {
+#pragma unroll
+    for (int r = 0; r < NT; ++r) {
+      const int t = tid + r * 256;
+      if (t < TASKS) {
+        const int y = t / PAIRS, m = t - (t / PAIRS) * PAIRS;
+        uint32_t* qrow = reinterpret_cast<uint32_t*>(Q + y * kQRS + 2 * m);
+#pragma unroll
+        for (int rx = 0; rx < 4; ++rx)
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            const int b0 = 3 * rx + c, b1 = b0 + 12;  // pixel rx and rx + 4 of the 8
+            const float lo = (float)((pre[r][b0 >> 2] >> (8 * (b0 & 3))) & 0xffu);
+            const float hi = (float)((pre[r][b1 >> 2] >> (8 * (b1 & 3))) & 0xffu);
+            qrow[(rx * kQPX + c * kQPC) / 2] = __builtin_amdgcn_perm(__float_as_uint(hi), __float_as_uint(lo), 0x07060302u);
+          }
+      }
+    }
+  };
+  float zc[8], zn[8];  // steps s and s + 4 in flight
+  auto load_z = [&](float (&z)[8], int f, int s) {
+    const int g = 2 * s + h, oy = g / GPR, ox0 = 8 * (g - (g / GPR) * GPR);
+    const float* zf = dZ + ((int64_t)f * NPIX + oy * OW + ox0) * 32 + c32;
+    const int nv = g < OH * GPR ? min(8, OW - ox0) : 0;
+    if (nv == 8) {  // whole group: eight loads off one address
+#pragma unroll
+      for (int j = 0; j < 8; ++j) z[j] = zf[j * 32];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) z[j] = j < nv ? zf[j * 32] : 0.0f;
+    }
+  };
+  if ((int)blockIdx.x < n_frames)
+#pragma unroll
+    for (int r = 0; r < NT; ++r) load_task(r, blockIdx.x);
+  for (int f = blockIdx.x; f < n_frames; f += gridDim.x) {
+    stage_frame_q();
+    if (wave < KS) load_z(zc, f, wave);
+    if (wave + 4 < KS) load_z(zn, f, wave + 4);
+    __syncthreads();
+    const int fnext = f + (int)gridDim.x;
+    // one 16-pixel step (the wave's i-th) from the dZ values in z, which then takes step
+    // s + 8 (the two buffers alternate, no copies)
+    auto step = [&](int s, int i, float (&z)[8]) {
+      union { uint16_t u[8]; bf16x8 v; } a0, a1, a2;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) split3_bf16(z[j], a0.u[j], a1.u[j], a2.u[j]);
+#pragma unroll
+      for (int r = 0; r < NT; ++r)
+        if (i == r && fnext < n_frames) load_task(r, fnext);
+      if (s + 8 < KS) load_z(z, f, s + 8);
+      const int g = min(2 * s + h, OH * GPR - 1);
+      const int oy = g / GPR, ox0 = 8 * (g - (g / GPR) * GPR);
+      const uint16_t* gb = Q + oy * 4 * kQRS + ox0;
+      union { bf16x8 v; uint4 q; uint32_t d[4]; } b[5];
+      uint32_t e[2];
+#pragma unroll
+      for (int nt = 0; nt < 5; ++nt) b[nt].q = *reinterpret_cast<const uint4*>(gb + loff[nt]);
+#pragma unroll
+      for (int nt = 3; nt < 5; ++nt) e[nt - 3] = gb[loff[nt] + 8];
+#pragma unroll
+      for (int nt = 3; nt < 5; ++nt) {  // taps kx >= 4 read pixel x >> 2 one further
+        const uint32_t d0 = b[nt].d[0], d1 = b[nt].d[1], d2 = b[nt].d[2], d3 = b[nt].d[3];
+        b[nt].d[0] = __builtin_amdgcn_alignbit(d1, d0, 16);
+        b[nt].d[1] = __builtin_amdgcn_alignbit(d2, d1, 16);
+        b[nt].d[2] = __builtin_amdgcn_alignbit(d3, d2, 16);
+        b[nt].d[3] = __builtin_amdgcn_alignbit(e[nt - 3], d3, 16);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        b[2].d[q] = (b[2].d[q] & keep2) | add2;
+        b[4].d[q] &= keep4;
+      }
+#pragma unroll
+      for (int nt = 0; nt < 5; ++nt) acc[nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0.v, b[nt].v, acc[nt], 0, 0, 0);
+#pragma unroll
+      for (int nt = 0; nt < 5; ++nt) acc[nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1.v, b[nt].v, acc[nt], 0, 0, 0);
+#pragma unroll
+      for (int nt = 0; nt < 5; ++nt) acc[nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2.v, b[nt].v, acc[nt], 0, 0, 0);
+    };
+    for (int s = wave, i = 0; s < KS; s += 8, i += 2) {
+      step(s, i, zc);
+      if (s + 4 < KS) step(s + 4, i + 1, zn);
+    }
+    __syncthreads();
+  }
+  // fold the four wave sums in LDS (fixed order), one slab per workgroup: D[co][slot]
+  float* red = reinterpret_cast<float*>(Q);
+  for (int w = 0; w < 4; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int nt = 0; nt < 5; ++nt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int co = (r & 3) + 8 * (r >> 2) + 4 * h;
+          const int i = co * 160 + nt * 32 + c32;
+          red[i] = w == 0 ? acc[nt][r] : red[i] + acc[nt][r];
+        }
+    }
+    __syncthreads();
+  }
+  float* out = slab + (int64_t)blockIdx.x * (32 * 160);
+  for (int i = tid; i < 32 * 160 / 4; i += 256)
+    reinterpret_cast<f4*>(out)[i] = reinterpret_cast<const f4*>(red)[i];
+}
+
+// dW / db from the slot-ordered partial sums of conv1_wgrad_x3_kernel (kConv1WgradCol).
+__global__ void conv1_wgrad_x3_finish_kernel(const float* __restrict__ part, int nparts, float* dW, float* db) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;  // co*160 + slot
+  if (idx >= 32 * 160) return;
+  const int co = idx / 160, slot = idx - (idx / 160) * 160;
+  const int col = kConv1WgradCol[slot >> 5][slot & 31];
+  if (col < 0) return;
+  float s = 0.0f;
+  for (int z = 0; z < nparts; ++z) s += part[(int64_t)z * 32 * 160 + idx];
+  if (col < 147)
+    dW[co * 148 + col] = s * (1.0f / 255.0f);
+  else
+    db[co] = s;
+  if (col == 148) dW[co * 148 + 147] = 0.0f;  // k = 147 is padding
+}
+
+// Deterministic two-stage sum of nslab slabs of n floats: stage 1 sums the slabs z = y
+// (mod gridDim.y) per column into partial[y]; stage 2 (conv1_wgrad_finish_kernel or
+// sum_slabs_kernel) sums the partials in order.
+__global__ void slab_partial_kernel(const float* __restrict__ slab, int nslab, int64_t n, float* __restrict__ partial) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float s = 0.0f;
+  for (int z = blockIdx.y; z < nslab; z += gridDim.y) s += slab[(int64_t)z * n + i];
+  partial[(int64_t)blockIdx.y * n + i] = s;
 }
 
 // ---- conv2 weight gradient ----------------------------------------------------

@@ -15,6 +15,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <mutex>
 #include <new>
 #include <unordered_map>
@@ -24,16 +26,7 @@
 #include "vn_lstm.h"
 #include "vn_aux.h"
 
-namespace vn {
-
-struct FrameSrc {
-  const uint8_t* base[2];
-  const int32_t* rows[2];
-  int64_t stride;
-  const float* f32[2];  // optional dense float NCHW frames (TransposeImage+ScaledFloatFrame output)
-};
-
-}  // namespace vn
+#include "vn_frames.h"
 #include "vn_conv1.h"
 namespace vn {
 
@@ -415,6 +408,12 @@ inline int resident_blocks(const void* kernel, int threads, size_t lds) {
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, threads, lds) != hipSuccess || per < 1) per = 1;
+  if (getenv("VN_DEBUG_OCC")) {
+    hipFuncAttributes fa{};
+    (void)hipFuncGetAttributes(&fa, kernel);
+    fprintf(stderr, "[vn occ] kernel %p threads %d lds %zu: %d blocks/CU (numRegs %d, static lds %zu)\n", kernel,
+            threads, lds, per, fa.numRegs, (size_t)fa.sharedSizeBytes);
+  }
   const int blocks = std::max(1, per * std::max(cus, 1));
   cache[kernel] = blocks;
   return blocks;
@@ -726,6 +725,18 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
     const int P1 = 2 * n * G::OH1 * G::OW1;
     Im2colT<Im> fbw{Im{src, P1}, 148};
     launch_wgrad<32, 64, 2, 2>(a.X[0], 32, 32, fbw, 148, P1, w.slab, w.slab_cap, Gr + L.l[0].w, Gr + L.l[0].b, st);
+  } else if constexpr (conv1_wgrad_x3_fits<H0, W0>()) {
+    const int frames = 2 * n;
+    const void* kfn = (const void*)conv1_wgrad_x3_kernel<H0, W0, G::OH1, G::OW1>;
+    const int blocks = std::min(frames, resident_blocks(kfn, 256, 0));
+    hipLaunchKernelGGL((conv1_wgrad_x3_kernel<H0, W0, G::OH1, G::OW1>), dim3(blocks), dim3(256), 0, st, src, frames,
+                       a.X[0], w.slab);
+    constexpr int kParts = 32;
+    float* part = w.slab + (int64_t)blocks * 32 * 160;
+    hipLaunchKernelGGL(slab_partial_kernel, dim3((32 * 160 + 255) / 256, kParts), dim3(256), 0, st, w.slab, blocks,
+                       (int64_t)32 * 160, part);
+    hipLaunchKernelGGL(conv1_wgrad_x3_finish_kernel, dim3((32 * 160 + 255) / 256), dim3(256), 0, st, part, kParts,
+                       Gr + L.l[0].w, Gr + L.l[0].b);
   } else if constexpr (kConv1Lds) {
     const int frames = 2 * n;
     constexpr int CP = (G::OH1 * G::OW1 <= 400) ? (G::OH1 * G::OW1 + 7) / 8 * 8 : 448;
