@@ -1,7 +1,7 @@
 #!/bin/bash
 # rocprofv3 --pmc passes (one per ';'-separated counter set, no tracing) over the training
 # bench for the kernels matching REGEX. Usage on the GPU box:
-#   PMC_SETS="A B;C D" bash tools/pmc_sets.sh REGEX  -> gpurun_out/pmcs_k*/ CSVs
+#   PMC_SETS="A B;C D" bash tools/pmc_sets.sh REGEX  -> gpurun_out/pmcs_k*/ CSVs; summary: tools/pmc_sets_summary.py
 set -o pipefail
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 export TMPDIR=/tmp

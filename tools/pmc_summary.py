@@ -1,16 +1,52 @@
-"""Per-dispatch averages of the counters in gpurun_out/pmcs_k*/ (tools/pmc_sets.sh)."""
-import collections
+"""Summarise tools/pmc_traffic.sh output into per-launch HBM bytes for vn_step.
+
+Correction (MI355X_MICROARCH.md §HBM): on gfx950 FETCH_SIZE reports exactly half of the
+bytes of a wide coalesced streaming read (16 B/lane, as vn_step's frame gather issues),
+so read bytes = 2 * FETCH_SIZE * 1024; WRITE_SIZE is exact for 16-B/lane stores.
+"""
 import csv
 import glob
+import json
+import os
 import sys
 
-root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
-for d in sorted(glob.glob(root + "/pmcs_k*/")):
-    for f in glob.glob(d + "**/*counter_collection.csv", recursive=True):
-        rows = list(csv.DictReader(open(f)))
-        agg = collections.defaultdict(float)
-        for r in rows:
-            agg[r["Counter_Name"]] += float(r["Counter_Value"])
-        disp = len({r["Dispatch_Id"] for r in rows}) or 1
-        for k, v in agg.items():
-            print("%-40s %.4g" % (k, v / disp))
+
+def per_dispatch(pattern, counter):
+    vals = []
+    for path in glob.glob(pattern, recursive=True):
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                if row.get("Counter_Name") == counter and "env_kernel<0" in row.get("Kernel_Name", ""):
+                    vals.append(float(row["Counter_Value"]))
+    return vals
+
+
+def main(out_dir, dest):
+    fetch = per_dispatch(os.path.join(out_dir, "pmc_fetch", "**", "*counter_collection.csv"), "FETCH_SIZE")
+    write = per_dispatch(os.path.join(out_dir, "pmc_write", "**", "*counter_collection.csv"), "WRITE_SIZE")
+    if not fetch or not write:
+        raise SystemExit("no env_kernel<MODE_STEP> counter rows found")
+    f_kb = sorted(fetch)[len(fetch) // 2]
+    w_kb = sorted(write)[len(write) // 2]
+    envs, fb = 4096, 84 * 84 * 3
+    alg = envs * (4 * fb + 32)
+    res = {
+        "kernel": "vn::env_kernel<0, 16> (vn_step)",
+        "config": "bench.py default: 4096 envs, 20 synthetic scenes, 84x84x3",
+        "dispatches": [len(fetch), len(write)],
+        "fetch_size_kb_median": f_kb,
+        "write_size_kb_median": w_kb,
+        "read_bytes": 2 * f_kb * 1024,
+        "write_bytes": w_kb * 1024,
+        "traffic_bytes_per_launch": 2 * f_kb * 1024 + w_kb * 1024,
+        "algorithmic_bytes_per_launch": alg,
+        "traffic_over_algorithmic": (2 * f_kb * 1024 + w_kb * 1024) / alg,
+        "correction": "read = 2 x FETCH_SIZE (gfx950 half-count for 16-B/lane streaming reads), write = WRITE_SIZE",
+    }
+    with open(dest, "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out", sys.argv[2] if len(sys.argv) > 2 else "vn_step_pmc.json")
