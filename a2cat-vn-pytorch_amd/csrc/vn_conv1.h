@@ -689,6 +689,159 @@ __global__ __launch_bounds__(256) void conv2_dgrad_kernel(const float* __restric
   }
 }
 
+// ---- conv2 input gradient on bf16 MFMA (split operands) ---------------------------
+// The same product as conv2_dgrad_kernel with both fp32 operands split by truncation into
+// three exact bf16 terms and the six terms of magnitude >= 2^-16 summed on
+// v_mfma_f32_16x16x32_bf16 (gemm_x6_kernel's scheme: dropped terms are below fp32 rounding).
+// Wave w owns parity class (py, px) = (w >> 1, w & 1); K step t = tap t (32 co), so an A
+// fragment (lane: class pixel i16, co 8q..8q+7 of one tap) is one 16-B read of a split dZ2
+// plane; dZ2_f is split once when it is staged (three planes, rows padded to 40 bf16 so 16
+// consecutive pixel rows fall on distinct bank quads; row NP is the zero row of
+// out-of-range taps). The split weights (4 taps x 2 ci tiles x 3 terms) stay in
+// registers; two 16-pixel tiles run together (four independent accumulators).
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+
+template <int IH, int IW, int OH, int OW>
+constexpr size_t conv2_dgrad_x6_lds() {
+  return (size_t)3 * (OH * OW + 1) * 40 * 2;
+}
+
+template <int IH, int IW, int OH, int OW>
+constexpr bool conv2_dgrad_x6_fits() {
+  return IH % 2 == 0 && IW % 2 == 0 && conv2_dgrad_x6_lds<IH, IW, OH, OW>() <= 64 * 1024;
+}
+
+__device__ __forceinline__ void split3_pack(const f4& v, uint2& t0, uint2& t1, uint2& t2) {
+  uint16_t h[4], m[4], l[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) split3_bf16(v[e], h[e], m[e], l[e]);
+  t0 = uint2{h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16)};
+  t1 = uint2{m[0] | ((uint32_t)m[1] << 16), m[2] | ((uint32_t)m[3] << 16)};
+  t2 = uint2{l[0] | ((uint32_t)l[1] << 16), l[2] | ((uint32_t)l[3] << 16)};
+}
+
+// The epilogue stores each tile straight from the accumulators under the conv1 ReLU
+// bitmask (staging the frame's result in LDS for 16-B stores measured slower: the extra
+// 58 KB of LDS cost a resident workgroup and the store phase did not overlap compute).
+template <int IH, int IW, int OH, int OW>
+__global__ __launch_bounds__(256, 2) void conv2_dgrad_x6_kernel(const float* __restrict__ dZ2,
+                                                                const float* __restrict__ WT,
+                                                                const uint32_t* __restrict__ mask,
+                                                                float* __restrict__ dX1, int n_frames) {
+  constexpr int NP = OH * OW;
+  constexpr int HYC = IH / 2, WXC = IW / 2, NPC = HYC * WXC;
+  constexpr int TILES = (NPC + 15) / 16;
+  constexpr int PS = 40;                 // plane row stride (bf16)
+  constexpr int PL = (NP + 1) * PS;      // plane size
+  static_assert(IH % 2 == 0 && IW % 2 == 0, "even conv1 maps");
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem_dg[];
+  uint16_t* zs = reinterpret_cast<uint16_t*>(smem_dg);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int py = wave >> 1, px = wave & 1;
+  const int i16 = lane & 15, q = lane >> 4;
+  bf16x8_t bw[4][2][3];  // [tap][ci tile][term]: B[k = co 8q + j][ci]
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int ky = py + 2 * (t >> 1), kx = px + 2 * (t & 1);
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      union { uint16_t u[8]; bf16x8_t v; } b0, b1, b2;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        split3_bf16(WT[((ky * 4 + kx) * 32 + nt * 16 + i16) * 32 + 8 * q + j], b0.u[j], b1.u[j], b2.u[j]);
+      bw[t][nt][0] = b0.v;
+      bw[t][nt][1] = b1.v;
+      bw[t][nt][2] = b2.v;
+    }
+  }
+  for (int i = tid; i < 3 * PS / 2; i += 256) {  // zero rows
+    const int pl = i / (PS / 2), e = i - pl * (PS / 2);
+    reinterpret_cast<uint32_t*>(zs + pl * PL + NP * PS)[e] = 0u;
+  }
+  constexpr int NZ = (NP * 8 + 255) / 256;
+  f4 zr[NZ];
+  auto load_z = [&](int f) {
+    const f4* z4 = reinterpret_cast<const f4*>(dZ2 + (int64_t)f * NP * 32);
+#pragma unroll
+    for (int j = 0; j < NZ; ++j) {
+      const int i = tid + j * 256;
+      if (i < NP * 8) zr[j] = z4[i];
+    }
+  };
+  if ((int)blockIdx.x < n_frames) load_z(blockIdx.x);
+  for (int f = blockIdx.x; f < n_frames; f += gridDim.x) {
+#pragma unroll
+    for (int j = 0; j < NZ; ++j) {
+      const int i = tid + j * 256;
+      if (i < NP * 8) {
+        uint2 t0, t1, t2;
+        split3_pack(zr[j], t0, t1, t2);
+        uint16_t* d = zs + (i >> 3) * PS + 4 * (i & 7);
+        *reinterpret_cast<uint2*>(d) = t0;
+        *reinterpret_cast<uint2*>(d + PL) = t1;
+        *reinterpret_cast<uint2*>(d + 2 * PL) = t2;
+      }
+    }
+    __syncthreads();
+    if (f + (int)gridDim.x < n_frames) load_z(f + gridDim.x);
+#pragma unroll 1
+    for (int t0 = 0; t0 < TILES; t0 += 2) {
+      int off[2][4];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int pc = (t0 + u) * 16 + i16;  // this lane's class pixel (A row)
+        const int yy = pc / WXC, xx = pc - (pc / WXC) * WXC;
+#pragma unroll
+        for (int tap = 0; tap < 4; ++tap) {
+          const int oy = yy - (tap >> 1), ox = xx - (tap & 1);
+          const bool ok = pc < NPC && oy >= 0 && oy < OH && ox >= 0 && ox < OW;
+          off[u][tap] = (ok ? (oy * OW + ox) : NP) * PS + 8 * q;
+        }
+      }
+      f4 acc[2][2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) acc[u][nt] = f4zero();
+#pragma unroll
+      for (int tap = 0; tap < 4; ++tap) {
+        bf16x8_t a[2][3];
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int tm = 0; tm < 3; ++tm) a[u][tm] = *reinterpret_cast<const bf16x8_t*>(zs + tm * PL + off[u][tap]);
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) {  // small terms first
+            f4 c = acc[u][nt];
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u][2], bw[tap][nt][0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u][0], bw[tap][nt][2], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u][1], bw[tap][nt][1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u][1], bw[tap][nt][0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u][0], bw[tap][nt][1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u][0], bw[tap][nt][0], c, 0, 0, 0);
+            acc[u][nt] = c;
+          }
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int pr = (t0 + u) * 16 + q * 4 + r;
+          if (pr < NPC) {
+            const int y = (pr / WXC) * 2 + py, x = (pr % WXC) * 2 + px;
+            const int64_t pix = ((int64_t)f * IH + y) * IW + x;
+            const uint32_t mw = mask[pix];
+            dX1[pix * 32 + i16] = (mw >> i16) & 1u ? acc[u][0][r] : 0.0f;
+            dX1[pix * 32 + 16 + i16] = (mw >> (i16 + 16)) & 1u ? acc[u][1][r] : 0.0f;
+          }
+        }
+    }
+    __syncthreads();
+  }
+}
+
 template <int IH, int IW, int OH, int OW>
 constexpr size_t conv2_wgrad_lds() {
   return ((size_t)IH * IW * 32 + (size_t)(OH * OW + 1) / 2 * 2 * 32) * 4;

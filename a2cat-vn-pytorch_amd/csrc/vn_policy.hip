@@ -703,7 +703,24 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
     if constexpr (G::OH1 % 2 == 0 && G::OW1 % 2 == 0) {
       // the u8 conv1 kernel left X1's ReLU as a bitmask: read 4 B per pixel instead of X1
       const bool bits = kConv1LdsFrame<H0, W0> && !(src.f32[0] || src.f32[1]);
-      if (bits) {
+      bool done = false;
+      if constexpr (conv2_dgrad_x6_fits<G::OH1, G::OW1, G::OH2, G::OW2>()) {
+        if (bits) {
+          const void* kfn = (const void*)conv2_dgrad_x6_kernel<G::OH1, G::OW1, G::OH2, G::OW2>;
+          constexpr size_t lds = conv2_dgrad_x6_lds<G::OH1, G::OW1, G::OH2, G::OW2>();
+          static bool attr = false;  // > 64 KiB of dynamic LDS needs the opt-in attribute
+          if (!attr) {
+            VN_HIP(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            attr = true;
+          }
+          const int blocks = std::min(frames, resident_blocks(kfn, 256, lds));
+          hipLaunchKernelGGL((conv2_dgrad_x6_kernel<G::OH1, G::OW1, G::OH2, G::OW2>), dim3(blocks), dim3(256), lds, st,
+                             w.dz2, T(1), a.M1, a.X[0], frames);
+          done = true;
+        }
+      }
+      if (done) {
+      } else if (bits) {
         const int blocks = std::min(
             frames, resident_blocks((const void*)conv2_dgrad_kernel<G::OH1, G::OW1, G::OH2, G::OW2, true>, 256, 0));
         hipLaunchKernelGGL((conv2_dgrad_kernel<G::OH1, G::OW1, G::OH2, G::OW2, true>), dim3(blocks), dim3(256), 0, st,

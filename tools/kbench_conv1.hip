@@ -40,8 +40,26 @@ int main(int argc, char** argv) {
   FrameSrc src{{ar, ar}, {ri, rg}, fb, {nullptr, nullptr}};
   hipEvent_t a, b;
   CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+  const char* which = argc > 2 ? argv[2] : "wgrad";
+  float *dz2, *wt, *dx1; uint32_t* msk;
+  CK(hipMalloc(&dz2, (size_t)frames * 81 * 32 * 4));
+  CK(hipMalloc(&wt, 16 * 32 * 32 * 4));
+  CK(hipMalloc(&msk, (size_t)frames * 400 * 4));
+  dx1 = dz;  // reuse: frames x 400 x 32
+  hipLaunchKernelGGL(fill_f, dim3(((size_t)frames * 81 * 32 + 255) / 256), dim3(256), 0, 0, dz2, (size_t)frames * 81 * 32);
+  hipLaunchKernelGGL(fill_f, dim3((16 * 32 * 32 + 255) / 256), dim3(256), 0, 0, wt, (size_t)16 * 32 * 32);
+  hipLaunchKernelGGL(fill_f, dim3(((size_t)frames * 400 + 255) / 256), dim3(256), 0, 0, (float*)msk, (size_t)frames * 400);
+  constexpr size_t dlds = conv2_dgrad_x6_lds<20, 20, 9, 9>();
+  CK(hipFuncSetAttribute((const void*)conv2_dgrad_x6_kernel<20, 20, 9, 9>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dlds));
   for (int grid : {512, 768, 1024}) {
-    auto run = [&]() { hipLaunchKernelGGL((conv1_wgrad_x3_kernel<84, 84, 20, 20>), dim3(grid), dim3(256), 0, 0, src, frames, dz, slab); };
+    auto run = [&]() {
+      if (which[0] == 'w')
+        hipLaunchKernelGGL((conv1_wgrad_x3_kernel<84, 84, 20, 20>), dim3(grid), dim3(256), 0, 0, src, frames, dz, slab);
+      else if (which[0] == 'd')
+        hipLaunchKernelGGL((conv2_dgrad_x6_kernel<20, 20, 9, 9>), dim3(grid), dim3(256), dlds, 0, dz2, wt, msk, dx1, frames);
+      else
+        hipLaunchKernelGGL((conv2_dgrad_kernel<20, 20, 9, 9, true>), dim3(grid), dim3(256), 0, 0, dz2, wt, dx1, msk, dx1, frames);
+    };
     run();
     CK(hipDeviceSynchronize());
     CK(hipEventRecord(a));
@@ -49,7 +67,7 @@ int main(int argc, char** argv) {
     CK(hipEventRecord(b));
     CK(hipEventSynchronize(b));
     float ms; CK(hipEventElapsedTime(&ms, a, b));
-    printf("conv1_wgrad_x3 grid %d: %.3f ms\n", grid, ms / 5);
+    printf("%s grid %d: %.3f ms\n", which, grid, ms / 5);
   }
   return 0;
 }
