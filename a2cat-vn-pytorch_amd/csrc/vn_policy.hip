@@ -151,6 +151,30 @@ struct DenseRows {
   VN_ROWS_LOADER
 };
 
+// Row-major rows [0, M) of A plus a ones row at m == M (k < kend): the transposed input
+// of a row-fill wgrad, whose ones row gives the bias gradient column.
+struct RowsOnes {
+  const float* A;
+  int64_t ld;
+  int M;
+  __device__ __forceinline__ f4 load4_fast(int m, int k) const {
+    return *reinterpret_cast<const f4*>(A + (int64_t)m * ld + k);
+  }
+  __device__ __forceinline__ f4 load4(int m, int k, int kend) const {
+    if (m > M || k >= kend) return f4zero();
+    f4 v = f4zero();
+    if (m == M) {
+      for (int j = 0; j < 4 && k + j < kend; ++j) v[j] = 1.0f;
+      return v;
+    }
+    const float* p = A + (int64_t)m * ld + k;
+    if (k + 3 < kend) return *reinterpret_cast<const f4*>(p);
+    for (int j = 0; j < 4 && k + j < kend; ++j) v[j] = p[j];
+    return v;
+  }
+  VN_ROWS_LOADER
+};
+
 // wgrad A operand: dZ [P][ld] read as rows r..r+3 (output channels) at pixel p.
 struct DenseT {
   const float* A;
@@ -282,6 +306,32 @@ __global__ void transpose_kernel(const float* __restrict__ W, int rows, int cols
   if (idx >= rows * cols) return;
   const int r = idx / cols, c = idx - (idx / cols) * cols;
   WT[(int64_t)c * rows + r] = W[idx];
+}
+
+// dst[c][r] = src[r][c] for a rows x cols block (row strides lds / ldd), 64 x 64 tiles
+// through LDS: both the reads and the writes are row-contiguous.
+__global__ __launch_bounds__(256) void tile_transpose_kernel(const float* __restrict__ src, int rows, int cols,
+                                                             int64_t lds, float* __restrict__ dst, int64_t ldd) {
+  __shared__ float t[64][65];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int r = r0 + ty + 4 * i, c = c0 + tx;
+    if (r < rows && c < cols) t[ty + 4 * i][tx] = src[(int64_t)r * lds + c];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int c = c0 + ty + 4 * i, r = r0 + tx;
+    if (r < rows && c < cols) dst[(int64_t)c * ldd + r] = t[tx][ty + 4 * i];
+  }
+}
+
+inline void tile_transpose(const float* src, int rows, int cols, int64_t lds, float* dst, int64_t ldd,
+                           hipStream_t st) {
+  hipLaunchKernelGGL(tile_transpose_kernel, dim3((cols + 63) / 64, (rows + 63) / 64), dim3(256), 0, st, src, rows, cols,
+                     lds, dst, ldd);
 }
 
 // ---- geometry & layout ------------------------------------------------------------
@@ -465,6 +515,29 @@ inline void launch_wgrad(const float* dZ, int64_t ldz, int M, FB fb, int KP, int
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, slab, splits, M, N, dW, db);
 }
 
+// Split-K wgrad on the x6 core from transposed operands: dZT [M][P] (rows = output
+// channels, k = samples) and XT [KP][P] (+ the ones row), both row-fill. The producers'
+// [P][*] tensors are transposed once (tile_transpose) so the reduction runs k-contiguous.
+template <int BM, int BN, int WM, int WN>
+inline void launch_wgrad_x6(const float* dZT, int M, const float* XT, int KP, int P, int64_t ldt, float* slab,
+                            int64_t slab_cap, float* dW, float* db, hipStream_t st) {
+  constexpr int BK = 32;
+  const int N = KP + 1;
+  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  int splits = std::max(1, std::min((2048 + tiles - 1) / tiles, (P + 255) / 256));
+  while ((int64_t)splits * M * N > slab_cap && splits > 1) splits /= 2;
+  int kchunk = (P + splits - 1) / splits;
+  kchunk = (kchunk + BK - 1) / BK * BK;
+  splits = (P + kchunk - 1) / kchunk;
+  DenseRows fa{dZT, ldt, M};
+  RowsOnes fb{XT, ldt, KP};
+  EpiSlab ep{slab, M, N};
+  hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, BK, WM, WN, DenseRows, RowsOnes, EpiSlab>), grid_for(M, N, BM, BN, splits),
+                     dim3(256), 0, st, fa, fb, ep, M, N, P, kchunk);
+  const int total = M * N;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, slab, splits, M, N, dW, db);
+}
+
 // dgrad of one (group, parity) class of a k4 s2 conv: input pixels (y, x) with
 // y % 2 == PY, x % 2 == PX of nimg images, masked by the ReLU of their producer.
 template <int COUT, int CINF, int H, int W, int OH, int OW, int PY, int PX>
@@ -593,7 +666,7 @@ struct BwdWork {
 };
 
 inline int64_t slab_floats(const PolicyLayout& L) {
-  return 12ll << 20;  // split-K slab capacity (launch_wgrad halves the split count to fit)
+  return 24ll << 20;  // split-K slab capacity (launch_wgrad halves the split count to fit)
 }
 
 inline int64_t workspace_floats(const PolicyLayout& L, int64_t n) {
@@ -911,6 +984,8 @@ struct LstmWork {
   float* head_t;   // [512][A+1]
   float* dh_heads; // [T*E][512]
   float* dgates;   // [T*E][2048]
+  float* dgates_t; // [2048][T*E]
+  float* xcat_t;   // [xcat][T*E]
   float* dh[2];    // [E][512]
   float* dc[2];    // [E][512]
   float* slab;
@@ -918,7 +993,8 @@ struct LstmWork {
 
 inline int64_t lstm_workspace_floats(const PolicyLayout& L, int64_t T, int64_t E) {
   const int64_t n = T * E;
-  return 2048ll * L.xcat + 512ll * 8 + n * 512 + n * 2048 + 4 * E * 512 + slab_floats(L) + 64;
+  const int64_t nt = (n + 3) / 4 * 4;  // row stride of the transposed copies
+  return 2048ll * L.xcat + 512ll * 8 + n * 512 + n * 2048 + nt * (2048 + L.xcat) + 4 * E * 512 + slab_floats(L) + 64;
 }
 
 inline LstmWork lstm_carve(const PolicyLayout& L, float* ws, int64_t T, int64_t E) {
@@ -932,6 +1008,11 @@ inline LstmWork lstm_carve(const PolicyLayout& L, float* ws, int64_t T, int64_t 
   p += T * E * 512;
   w.dgates = p;
   p += T * E * 2048;
+  const int64_t nt = (T * E + 3) / 4 * 4;
+  w.dgates_t = p;
+  p += nt * 2048;
+  w.xcat_t = p;
+  p += nt * L.xcat;
   for (int i = 0; i < 2; ++i) {
     w.dh[i] = p;
     p += E * 512;
@@ -979,10 +1060,13 @@ inline int lstm_backward(const PolicyLayout& L, const float* P, int T, int E, co
     EpiLstmDx ep{dz5 + (int64_t)t * e512, x5_all + (int64_t)t * e512, w.dh[cur], mask, L.xoff};
     launch_gemm_x6<64, 64, 32, 2, 2>(fa, fb, ep, E, L.xcat, 2048, st);
   }
-  {  // dW_cat = dgates^T x xcat over all T*E rows; b_ih and b_hh share the bias gradient
-    Im2colT<DenseRows> fbw{DenseRows{xcat_all, L.xcat, N}, L.xcat};
-    launch_wgrad<128, 64, 2, 2>(w.dgates, 2048, 2048, fbw, L.xcat, N, w.slab, slab_floats(L), Gr + L.lw, Gr + L.lbih,
-                                st);
+  {  // dW_cat = dgates^T x xcat over all T*E rows (x6 core on transposed copies, k = rows
+     // contiguous); b_ih and b_hh share the bias gradient
+    const int64_t nt = ((int64_t)N + 3) / 4 * 4;
+    tile_transpose(w.dgates, N, 2048, 2048, w.dgates_t, nt, st);
+    tile_transpose(xcat_all, N, L.xcat, L.xcat, w.xcat_t, nt, st);
+    launch_wgrad_x6<128, 128, 2, 2>(w.dgates_t, 2048, w.xcat_t, L.xcat, N, nt, w.slab, slab_floats(L), Gr + L.lw,
+                                   Gr + L.lbih, st);
     VN_HIP(hipMemcpyAsync(Gr + L.lbhh, Gr + L.lbih, 2048 * sizeof(float), hipMemcpyDeviceToDevice, st));
   }
   VN_HIP(hipGetLastError());
