@@ -112,15 +112,37 @@ __global__ __launch_bounds__(320) void conv1_fwd_kernel(FrameSrc src, int n_fram
 // f32 kernel). Three accumulators (one per term) keep three independent MFMA chains.
 // K is relaid k' = ky*24 + kr (kr = kx*3 + c < 21, 21..23 and ky = 7 zero-weighted) so
 // the 8 k' of a lane's fragment are 8 consecutive frame bytes of one image row: the
-// frame is staged once per workgroup into LDS as bf16 rows of RS elements and a fragment
-// is two aligned 8-byte LDS reads; the split weights sit in LDS as per-lane fragments
-// (one ds_read_b128 each), and the next frame is prefetched into registers. Frames whose
-// row bytes are not a multiple of 4 or whose bf16 image does not fit use the f32 kernel.
+// frame is staged into LDS as bf16 rows of RS elements and a fragment is two aligned
+// 8-byte LDS reads; the split weights sit in LDS as per-lane fragments (one ds_read_b128
+// each), and the next work item's bytes are prefetched into registers.
+// Work item = (frame, band of BR output rows): a band stages the 4*BR + 4 image rows its
+// taps read (row 4*BR + 3 is the zero-weighted ky = 7 of the band's last row). BR is the
+// whole map when the bf16 frame fits next to the weights in half the LDS (84x84: one
+// band, two workgroups per CU), else the map is cut into equal bands that do (174x174:
+// 9,9,9,9,6 rows). Frame rows of an odd byte count take the f32 kernel.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int kConv1X3WeightLds = 11 * 3 * 64 * 16;  // split weight fragments [slice][term][lane]
+
+template <int H, int W>
+struct Conv1X3Band {
+  static constexpr int RB = W * 3, RS = (RB + 3) / 4 * 4;  // row bytes; LDS row stride (bf16)
+  static constexpr int OH = (H - 7) / 4 + 1;
+  static constexpr int rows_of(int br) { return 4 * br + 4 < H ? 4 * br + 4 : H; }
+  static constexpr size_t lds_of(int br) { return (size_t)rows_of(br) * RS * 2 + kConv1X3WeightLds; }
+  static constexpr int br_max() {
+    int br = OH;
+    while (br > 1 && lds_of(br) > 80 * 1024) --br;
+    return br;
+  }
+  static constexpr int NB = (OH + br_max() - 1) / br_max();  // bands per frame
+  static constexpr int BR = (OH + NB - 1) / NB;               // output rows per band
+  static constexpr int BRI = rows_of(BR);                     // image rows staged per band
+};
 
 template <int H, int W>
 constexpr bool conv1_x3_fits() {
-  return (W * 3) % 4 == 0 && (size_t)H * ((W * 3 + 3) / 4 * 4) * 2 + 11 * 3 * 64 * 16 <= 80 * 1024;
+  return (W * 3) % 2 == 0 && (size_t)H * W * 3 % 4 == 0 && Conv1X3Band<H, W>::lds_of(Conv1X3Band<H, W>::BR) <= 80 * 1024;
 }
 
 __device__ __forceinline__ void split3_bf16(float w, uint16_t& hi, uint16_t& mid, uint16_t& lo) {
@@ -133,20 +155,24 @@ __device__ __forceinline__ void split3_bf16(float w, uint16_t& hi, uint16_t& mid
   lo = (uint16_t)(__float_as_uint(r2) >> 16);
 }
 
+__device__ __forceinline__ uint32_t u8x2_bf16(uint32_t v) {  // two low bytes -> two bf16
+  return (__float_as_uint((float)(v & 0xffu)) >> 16) | (__float_as_uint((float)((v >> 8) & 0xffu)) & 0xffff0000u);
+}
+
 template <int H, int W, int OH, int OW>
 __global__ __launch_bounds__(256, 2) void conv1_fwd_x3_kernel(FrameSrc src, int n_frames, const float* __restrict__ Wt,
                                                            const float* __restrict__ bias, float* __restrict__ Y,
                                                            uint32_t* __restrict__ mask) {
-  constexpr int RB = W * 3;                 // frame row bytes
-  constexpr int RS = (RB + 3) / 4 * 4;      // LDS row stride (bf16 elements)
+  using B = Conv1X3Band<H, W>;
+  constexpr int RB = B::RB, RS = B::RS, BR = B::BR, NB = B::NB, BRI = B::BRI;
   constexpr int NPIX = OH * OW;
-  constexpr int TILES = (NPIX + 31) / 32;
-  constexpr int NS = 11;                    // k' slices of 16 (k' < 176)
-  constexpr int ND = H * RB / 4;            // frame dwords
-  constexpr int NPF = (ND + 255) / 256;     // prefetched dwords per thread
-  static_assert(RB % 4 == 0, "frame rows of whole dwords");
-  // LDS: the bf16 frame image, then the split weights as per-lane 16-B fragments [s][term][lane]
-  __shared__ __attribute__((aligned(16))) uint16_t img[H * RS];
+  constexpr int TILES = (BR * OW + 31) / 32;  // tiles of a full band
+  constexpr int NS = 11;                      // k' slices of 16 (k' < 176)
+  constexpr int ND = BRI * RB / 4;            // dwords of a full band
+  constexpr int NPF = (ND + 255) / 256;       // prefetched dwords per thread
+  static_assert(RB % 2 == 0 && (BRI * RB) % 4 == 0, "band rows of whole dwords");
+  // LDS: the band's bf16 image rows, then the split weights as per-lane 16-B fragments [s][term][lane]
+  __shared__ __attribute__((aligned(16))) uint16_t img[BRI * RS];
   __shared__ __attribute__((aligned(16))) bf16x8 bw[NS * 3 * 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, c32 = lane & 31;
@@ -164,36 +190,51 @@ __global__ __launch_bounds__(256, 2) void conv1_fwd_x3_kernel(FrameSrc src, int 
     bw[(sl * 3 + 2) * 64 + ln] = t2.v;
   }
   const float bs = bias[c32];
-  uint32_t pre[NPF];  // next frame's bytes, in flight while the current frame computes
-  auto load_frame = [&](int f) {
-    const uint32_t* s4 = reinterpret_cast<const uint32_t*>(frame_ptr(src, f));
+  const int n_items = n_frames * NB;
+  // dwords of item it's band: rows 4*BR*band .. (clamped to the frame)
+  auto band_dwords = [&](int band) { return min(BRI, H - 4 * BR * band) * RB / 4; };
+  uint32_t pre[NPF];  // next item's bytes, in flight while the current item computes
+  auto load_item = [&](int it) {
+    const int f = it / NB, band = it - (it / NB) * NB;
+    const uint32_t* s4 = reinterpret_cast<const uint32_t*>(frame_ptr(src, f) + (int64_t)4 * BR * band * RB);
+    const int nd = band_dwords(band);
 #pragma unroll
     for (int j = 0; j < NPF; ++j) {
       const int i = tid + j * 256;
-      if (i < ND) pre[j] = s4[i];
+      if (i < nd) pre[j] = s4[i];
     }
   };
-  if ((int)blockIdx.x < n_frames) load_frame(blockIdx.x);
-  for (int f = blockIdx.x; f < n_frames; f += gridDim.x) {
+  if ((int)blockIdx.x < n_items) load_item(blockIdx.x);
+  for (int it = blockIdx.x; it < n_items; it += gridDim.x) {
+    const int f = it / NB, band = it - (it / NB) * NB;
+    const int oy0 = BR * band, nr = min(BR, OH - oy0), npb = nr * OW;
+    const int nd = band_dwords(band);
 #pragma unroll
-    for (int j = 0; j < NPF; ++j) {  // u8 -> bf16 rows (a dword never straddles a row)
+    for (int j = 0; j < NPF; ++j) {  // u8 -> bf16 rows
       const int i = tid + j * 256;
-      if (i < ND) {
+      if (i < nd) {
         const uint32_t v = pre[j];
         const int e = i * 4, row = e / RB, col = e - row * RB;
-        const uint32_t b0 = __float_as_uint((float)(v & 0xffu)) >> 16;
-        const uint32_t b1 = __float_as_uint((float)((v >> 8) & 0xffu)) >> 16;
-        const uint32_t b2 = __float_as_uint((float)((v >> 16) & 0xffu)) >> 16;
-        const uint32_t b3 = __float_as_uint((float)(v >> 24)) >> 16;
-        *reinterpret_cast<uint2*>(img + row * RS + col) = uint2{b0 | (b1 << 16), b2 | (b3 << 16)};
+        if constexpr (RB % 4 == 0) {  // a dword never straddles a row
+          *reinterpret_cast<uint2*>(img + row * RS + col) = uint2{u8x2_bf16(v), u8x2_bf16(v >> 16)};
+        } else {  // byte pairs never straddle (RB even)
+          *reinterpret_cast<uint32_t*>(img + row * RS + col) = u8x2_bf16(v);
+          const bool wrap = col + 2 == RB;
+          *reinterpret_cast<uint32_t*>(img + (row + wrap) * RS + (wrap ? 0 : col + 2)) = u8x2_bf16(v >> 16);
+        }
       }
     }
     __syncthreads();
-    if (f + (int)gridDim.x < n_frames) load_frame(f + gridDim.x);
-    for (int t = wave; t < TILES; t += 4) {
-      const int px = min(t * 32 + c32, NPIX - 1);
+    if (it + (int)gridDim.x < n_items) load_item(it + gridDim.x);
+    const int tiles = (npb + 31) / 32;
+    for (int t = wave; t < tiles; t += 4) {
+      const int px = min(t * 32 + c32, npb - 1);
       const int oy = px / OW, ox = px - (px / OW) * OW;
       const uint16_t* base = img + (oy * 4) * RS + ox * 12;
+      // opaque per tile: keeps the 33 weight-fragment reads inside the tile loop (hoisted,
+      // they would hold 132 VGPRs across it and spill)
+      int wl = lane;
+      asm volatile("" : "+v"(wl));
       f16v acc[3];
 #pragma unroll
       for (int p = 0; p < 3; ++p)
@@ -208,22 +249,24 @@ __global__ __launch_bounds__(256, 2) void conv1_fwd_x3_kernel(FrameSrc src, int 
         a.u[1] = q[1];
 #pragma unroll
         for (int p = 0; p < 3; ++p)
-          acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.v, bw[(sl * 3 + p) * 64 + lane], acc[p], 0, 0, 0);
+          acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.v, bw[(sl * 3 + p) * 64 + wl], acc[p], 0, 0, 0);
       }
+      const int64_t pix0 = (int64_t)f * NPIX + oy0 * OW;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int rr = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         const float sum = (acc[2][r] + acc[1][r]) + acc[0][r];
         const float y = fmaxf(sum * (1.0f / 255.0f) + bs, 0.0f);
         const uint64_t bal = __ballot(y > 0.0f);
-        if (rr < NPIX) {
-          Y[((int64_t)f * NPIX + rr) * 32 + c32] = y;
-          if (c32 == 0) mask[(int64_t)f * NPIX + rr] = (uint32_t)(bal >> (32 * h));
+        if (rr < npb) {
+          Y[(pix0 + rr) * 32 + c32] = y;
+          if (c32 == 0) mask[pix0 + rr] = (uint32_t)(bal >> (32 * h));
         }
       }
     }
     __syncthreads();
   }
+  (void)TILES;
 }
 
 // ---- weight gradient ----------------------------------------------------------
@@ -693,7 +736,8 @@ __global__ __launch_bounds__(256) void conv2_dgrad_kernel(const float* __restric
 // The same product as conv2_dgrad_kernel with both fp32 operands split by truncation into
 // three exact bf16 terms and the six terms of magnitude >= 2^-16 summed on
 // v_mfma_f32_16x16x32_bf16 (gemm_x6_kernel's scheme: dropped terms are below fp32 rounding).
-// Wave w owns parity class (py, px) = (w >> 1, w & 1); K step t = tap t (32 co), so an A
+// Wave w owns parity class (py, px) = ((w & 3) >> 1, w & 1) (with 8 waves, waves w and w + 4
+// take alternate tile pairs of the class); K step t = tap t (32 co), so an A
 // fragment (lane: class pixel i16, co 8q..8q+7 of one tap) is one 16-B read of a split dZ2
 // plane; dZ2_f is split once when it is staged (three planes, rows padded to 40 bf16 so 16
 // consecutive pixel rows fall on distinct bank quads; row NP is the zero row of
@@ -708,7 +752,16 @@ constexpr size_t conv2_dgrad_x6_lds() {
 
 template <int IH, int IW, int OH, int OW>
 constexpr bool conv2_dgrad_x6_fits() {
-  return IH % 2 == 0 && IW % 2 == 0 && conv2_dgrad_x6_lds<IH, IW, OH, OW>() <= 64 * 1024;
+  return IH % 2 == 0 && IW % 2 == 0 && conv2_dgrad_x6_lds<IH, IW, OH, OW>() <= 160 * 1024;
+}
+
+// Waves per workgroup: 4 (one per parity class) while two workgroups share a CU's LDS
+// (84x84: 20x20 conv1 map, 24 KB of planes); 8 (two per class, alternate tile pairs) when
+// the planes take more than half the LDS (174x174: 42x42 map, 96 KB) — the same 2 waves
+// per SIMD from one workgroup.
+template <int IH, int IW, int OH, int OW>
+constexpr int conv2_dgrad_x6_waves() {
+  return conv2_dgrad_x6_lds<IH, IW, OH, OW>() <= 64 * 1024 ? 4 : 8;
 }
 
 __device__ __forceinline__ void split3_pack(const f4& v, uint2& t0, uint2& t1, uint2& t2) {
@@ -723,8 +776,8 @@ __device__ __forceinline__ void split3_pack(const f4& v, uint2& t0, uint2& t1, u
 // The epilogue stores each tile straight from the accumulators under the conv1 ReLU
 // bitmask (staging the frame's result in LDS for 16-B stores measured slower: the extra
 // 58 KB of LDS cost a resident workgroup and the store phase did not overlap compute).
-template <int IH, int IW, int OH, int OW>
-__global__ __launch_bounds__(256, 2) void conv2_dgrad_x6_kernel(const float* __restrict__ dZ2,
+template <int IH, int IW, int OH, int OW, int NW>
+__global__ __launch_bounds__(NW * 64, 2) void conv2_dgrad_x6_kernel(const float* __restrict__ dZ2,
                                                                 const float* __restrict__ WT,
                                                                 const uint32_t* __restrict__ mask,
                                                                 float* __restrict__ dX1, int n_frames) {
@@ -737,7 +790,8 @@ __global__ __launch_bounds__(256, 2) void conv2_dgrad_x6_kernel(const float* __r
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_dg[];
   uint16_t* zs = reinterpret_cast<uint16_t*>(smem_dg);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int py = wave >> 1, px = wave & 1;
+  constexpr int NT = NW * 64;
+  const int cls = wave & 3, py = cls >> 1, px = cls & 1;
   const int i16 = lane & 15, q = lane >> 4;
   bf16x8_t bw[4][2][3];  // [tap][ci tile][term]: B[k = co 8q + j][ci]
 #pragma unroll
@@ -754,17 +808,17 @@ __global__ __launch_bounds__(256, 2) void conv2_dgrad_x6_kernel(const float* __r
       bw[t][nt][2] = b2.v;
     }
   }
-  for (int i = tid; i < 3 * PS / 2; i += 256) {  // zero rows
+  for (int i = tid; i < 3 * PS / 2; i += NT) {  // zero rows
     const int pl = i / (PS / 2), e = i - pl * (PS / 2);
     reinterpret_cast<uint32_t*>(zs + pl * PL + NP * PS)[e] = 0u;
   }
-  constexpr int NZ = (NP * 8 + 255) / 256;
+  constexpr int NZ = (NP * 8 + NT - 1) / NT;
   f4 zr[NZ];
   auto load_z = [&](int f) {
     const f4* z4 = reinterpret_cast<const f4*>(dZ2 + (int64_t)f * NP * 32);
 #pragma unroll
     for (int j = 0; j < NZ; ++j) {
-      const int i = tid + j * 256;
+      const int i = tid + j * NT;
       if (i < NP * 8) zr[j] = z4[i];
     }
   };
@@ -772,7 +826,7 @@ __global__ __launch_bounds__(256, 2) void conv2_dgrad_x6_kernel(const float* __r
   for (int f = blockIdx.x; f < n_frames; f += gridDim.x) {
 #pragma unroll
     for (int j = 0; j < NZ; ++j) {
-      const int i = tid + j * 256;
+      const int i = tid + j * NT;
       if (i < NP * 8) {
         uint2 t0, t1, t2;
         split3_pack(zr[j], t0, t1, t2);
@@ -785,7 +839,7 @@ __global__ __launch_bounds__(256, 2) void conv2_dgrad_x6_kernel(const float* __r
     __syncthreads();
     if (f + (int)gridDim.x < n_frames) load_z(f + gridDim.x);
 #pragma unroll 1
-    for (int t0 = 0; t0 < TILES; t0 += 2) {
+    for (int t0 = 2 * (wave >> 2); t0 < TILES; t0 += 2 * (NW / 4)) {
       int off[2][4];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {

@@ -595,26 +595,37 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
                  hipStream_t st) {
   using G = Geo<H0, W0>;
   const int A1 = L.A + 1;
-  // conv1 (frames -> X1), 2n frames. The specialised kernel stages whole u8 frames in LDS;
-  // dense float frames and frames too large for LDS (300x400) take the generic im2col path.
-  constexpr bool kConv1Lds = kConv1LdsFrame<H0, W0>;
-  if (!kConv1Lds || src.f32[0] || src.f32[1]) {
+  // conv1 (frames -> X1), 2n frames. u8 frames take the split-bf16 kernel (bands of
+  // output rows staged in LDS), else the f32 LDS-frame kernel; dense float frames take the
+  // generic im2col path.
+  constexpr bool kX3 = conv1_x3_fits<H0, W0>(), kConv1Lds = kConv1LdsFrame<H0, W0>;
+  const bool f32in = src.f32[0] || src.f32[1];
+  const int frames = 2 * n;
+  bool conv1_done = false;
+  if constexpr (kX3) {
+    if (!f32in) {  // bf16 MFMA on split weights (exact products)
+      using B = Conv1X3Band<H0, W0>;
+      const int blocks =
+          std::min(frames * B::NB, resident_blocks((const void*)conv1_fwd_x3_kernel<H0, W0, G::OH1, G::OW1>, 256, 0));
+      hipLaunchKernelGGL((conv1_fwd_x3_kernel<H0, W0, G::OH1, G::OW1>), dim3(blocks), dim3(256), 0, st, src, frames,
+                         P + L.l[0].w, P + L.l[0].b, a.X[0], a.M1);
+      conv1_done = true;
+    }
+  } else if constexpr (kConv1Lds) {
+    if (!f32in) {
+      constexpr int NF = (2 * H0 * W0 * 3 <= 64 * 1024) ? 2 : 1;
+      const int blocks = std::min((frames + NF - 1) / NF,
+                                  resident_blocks((const void*)conv1_fwd_kernel<H0, W0, G::OH1, G::OW1, NF>, 320, 0));
+      hipLaunchKernelGGL((conv1_fwd_kernel<H0, W0, G::OH1, G::OW1, NF>), dim3(blocks), dim3(320), 0, st, src, frames,
+                         P + L.l[0].w, P + L.l[0].b, a.X[0], a.M1);
+      conv1_done = true;
+    }
+  }
+  if (!conv1_done) {
     FramesIm2col<H0, W0, G::OH1, G::OW1> fa{src, 2 * n * G::OH1 * G::OW1};
     DenseRows fb{P + L.l[0].w, 148, 32};
     EpiBiasAct ep{a.X[0], 32, P + L.l[0].b, 1};
     launch_gemm_x6<128, 32, 32, 4, 1>(fa, fb, ep, fa.M, 32, 148, st);
-  } else if constexpr (conv1_x3_fits<H0, W0>()) {  // bf16 MFMA on split weights (exact products)
-    const int frames = 2 * n;
-    const int blocks = std::min(frames, resident_blocks((const void*)conv1_fwd_x3_kernel<H0, W0, G::OH1, G::OW1>, 256, 0));
-    hipLaunchKernelGGL((conv1_fwd_x3_kernel<H0, W0, G::OH1, G::OW1>), dim3(blocks), dim3(256), 0, st, src, frames,
-                       P + L.l[0].w, P + L.l[0].b, a.X[0], a.M1);
-  } else if constexpr (kConv1Lds) {
-    constexpr int NF = (2 * H0 * W0 * 3 <= 64 * 1024) ? 2 : 1;
-    const int frames = 2 * n;
-    const int blocks =
-        std::min((frames + NF - 1) / NF, resident_blocks((const void*)conv1_fwd_kernel<H0, W0, G::OH1, G::OW1, NF>, 320, 0));
-    hipLaunchKernelGGL((conv1_fwd_kernel<H0, W0, G::OH1, G::OW1, NF>), dim3(blocks), dim3(320), 0, st, src, frames,
-                       P + L.l[0].w, P + L.l[0].b, a.X[0], a.M1);
   }
   // conv2 (X1 -> X2)
   {
@@ -775,20 +786,21 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
     }
     if constexpr (G::OH1 % 2 == 0 && G::OW1 % 2 == 0) {
       // the u8 conv1 kernel left X1's ReLU as a bitmask: read 4 B per pixel instead of X1
-      const bool bits = kConv1LdsFrame<H0, W0> && !(src.f32[0] || src.f32[1]);
+      const bool bits = (conv1_x3_fits<H0, W0>() || kConv1LdsFrame<H0, W0>) && !(src.f32[0] || src.f32[1]);
       bool done = false;
       if constexpr (conv2_dgrad_x6_fits<G::OH1, G::OW1, G::OH2, G::OW2>()) {
         if (bits) {
-          const void* kfn = (const void*)conv2_dgrad_x6_kernel<G::OH1, G::OW1, G::OH2, G::OW2>;
+          constexpr int NW = conv2_dgrad_x6_waves<G::OH1, G::OW1, G::OH2, G::OW2>();
+          const void* kfn = (const void*)conv2_dgrad_x6_kernel<G::OH1, G::OW1, G::OH2, G::OW2, NW>;
           constexpr size_t lds = conv2_dgrad_x6_lds<G::OH1, G::OW1, G::OH2, G::OW2>();
           static bool attr = false;  // > 64 KiB of dynamic LDS needs the opt-in attribute
           if (!attr) {
             VN_HIP(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
             attr = true;
           }
-          const int blocks = std::min(frames, resident_blocks(kfn, 256, lds));
-          hipLaunchKernelGGL((conv2_dgrad_x6_kernel<G::OH1, G::OW1, G::OH2, G::OW2>), dim3(blocks), dim3(256), lds, st,
-                             w.dz2, T(1), a.M1, a.X[0], frames);
+          const int blocks = std::min(frames, resident_blocks(kfn, NW * 64, lds));
+          hipLaunchKernelGGL((conv2_dgrad_x6_kernel<G::OH1, G::OW1, G::OH2, G::OW2, NW>), dim3(blocks), dim3(NW * 64), lds,
+                             st, w.dz2, T(1), a.M1, a.X[0], frames);
           done = true;
         }
       }

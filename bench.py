@@ -52,6 +52,7 @@ def parse():
     p.add_argument("--train-steps", type=int, default=6, help="timed A2C updates (0 = skip the train leg)")
     p.add_argument("--train-warmup", type=int, default=2)
     p.add_argument("--no-train-ff", action="store_true", help="skip the feed-forward (no LSTM) train leg")
+    p.add_argument("--no-train-84", action="store_true", help="skip the 84x84 LSTM train leg")
     p.add_argument("--no-train-ref", action="store_true",
                    help="skip the 174x174 LSTM + aux-deconv train leg (the reference's logged experiment shape)")
     p.add_argument("--c5", action="store_true", help="add the 300x400 + goal + aux-depth train leg (config C5)")
@@ -310,8 +311,9 @@ def main():
     train = train_ff = train_ref = train_c5 = None
     if args.train_steps > 0:
         torch.cuda.empty_cache()
-        train = bench_train(args, scenes, dev, world, rank, recurrent=True)
-        torch.cuda.empty_cache()
+        if not args.no_train_84:
+            train = bench_train(args, scenes, dev, world, rank, recurrent=True)
+            torch.cuda.empty_cache()
         if not args.no_train_ff:
             train_ff = bench_train(args, scenes, dev, world, rank, recurrent=False)
             torch.cuda.empty_cache()

@@ -144,6 +144,96 @@ def test_autograd_policy_vs_torch_oracle():
     _close(lf.detach().cpu(), logits.detach().cpu(), 1e-5, "f32 input logits")
 
 
+def _policy_174(seed):
+    from vnav.policy import GoalNavPolicy
+    torch.manual_seed(seed)
+    pol = GoalNavPolicy(3, 4, (174, 174))
+    with torch.no_grad():
+        pol.params.add_(torch.randn_like(pol.params) * 0.01)
+    return pol
+
+
+def _grads_174(pol, img, gl, actions, rets):
+    pol.params.grad = None
+    logits, value, _ = pol(((img.cuda(), gl.cuda()), None), None, None)
+    loss, _ = oa2c.loss(logits.reshape(-1, 4), value.reshape(-1), actions.cuda(), rets.cuda())
+    loss.backward()
+    return logits.detach().cpu().reshape(-1, 4), value.detach().cpu().reshape(-1), pol.params.grad.clone()
+
+
+def test_autograd_policy_174_vs_torch_oracle():
+    """The reference's unmodified 174x174 topology (42x42 -> 20x20 -> 9x9, Linear(2592)):
+    forward and every parameter gradient vs the float64 CPU oracle. Inputs are chosen with
+    no conv1/conv2 pre-activation within 5e-7 of zero: a ReLU tie flipped by fp32 rounding
+    moves its conv gradient by ~1e-3 of the scale (the gradients are sums with heavy
+    cancellation), a tie rather than an error (test_policy_174_large_batch_consistency
+    covers large batches against the GPU's own small-batch gradients)."""
+    import torch.nn.functional as F
+    pol = _policy_174(3)
+    ref = GoalNetOracle((174, 174)).load_reference(pol.reference_state_dict()).double()
+    n = 4
+    for seed in range(4, 400):
+        rng = np.random.RandomState(seed)
+        img = torch.as_tensor(rng.randint(0, 256, size=(n, 1, 174, 174, 3)).astype(np.uint8))
+        gl = torch.as_tensor(rng.randint(0, 256, size=(n, 1, 174, 174, 3)).astype(np.uint8))
+        fi = frames_to_float(img.reshape(-1, 174, 174, 3)).double()
+        fg = frames_to_float(gl.reshape(-1, 174, 174, 3)).double()
+        with torch.no_grad():
+            z1 = [ref.conv1(v) for v in (fi, fg)]
+            z2 = [ref.conv2(F.relu(z)) for z in z1]
+            margin = min(float(z.abs().min()) for z in z1 + z2)
+        if margin > 5e-7:
+            break
+    assert margin > 5e-7
+    actions = torch.as_tensor(rng.randint(0, 4, size=n))
+    rets = torch.as_tensor(rng.randn(n).astype(np.float32))
+    logits, value, grad = _grads_174(pol, img, gl, actions, rets)
+    rl, rv = ref(fi, fg)
+    _close(logits, rl.detach(), 1e-5, "logits")
+    _close(value, rv.detach().view(-1), 1e-5, "value")
+    rloss, _ = oa2c.loss(rl, rv.view(-1), actions, rets.double())
+    rloss.backward()
+    mine = pol.net.to_reference(grad)
+    names = {"shared_base.0.0": ref.conv1, "shared_base.0.2": ref.conv2, "conv_base.0.0": ref.conv3,
+             "conv_base.0.2": ref.conv4, "conv_merge.0.1": ref.fc, "policy_logits.0": ref.policy_logits,
+             "critic.0": ref.critic}
+    errs = {}
+    for k, mod in names.items():
+        for kind in ("weight", "bias"):
+            b = getattr(mod, kind).grad.numpy()
+            errs[k + "." + kind] = np.abs(mine[k + "." + kind].numpy() - b).max() / max(np.abs(b).max(), 1e-30)
+    bad = {k: "%.3g" % e for k, e in errs.items() if e > 1e-4}
+    assert not bad, bad
+
+
+def test_policy_174_large_batch_consistency():
+    """128 samples at 174x174 in one batch — the banded conv1 kernels (5 bands per frame)
+    and the 8-wave conv2 input gradient wrap their persistent grids — against the same
+    samples in 32 batches of 4 (no grid wraps): per-sample outputs agree, and the batch
+    gradient equals the mean of the small-batch gradients (identical ReLU masks: every
+    forward kernel computes a sample independently of the batch)."""
+    pol = _policy_174(5)
+    B = 128
+    rng = np.random.RandomState(7)
+    img = torch.as_tensor(rng.randint(0, 256, size=(B, 1, 174, 174, 3)).astype(np.uint8))
+    gl = torch.as_tensor(rng.randint(0, 256, size=(B, 1, 174, 174, 3)).astype(np.uint8))
+    actions = torch.as_tensor(rng.randint(0, 4, size=B))
+    rets = torch.as_tensor(rng.randn(B).astype(np.float32))
+    logits, value, grad = _grads_174(pol, img, gl, actions, rets)
+    parts = [_grads_174(pol, img[k:k + 4], gl[k:k + 4], actions[k:k + 4], rets[k:k + 4]) for k in range(0, B, 4)]
+    _close(logits, torch.cat([p[0] for p in parts]), 1e-6, "logits")
+    _close(value, torch.cat([p[1] for p in parts]), 1e-6, "value")
+    gmean = sum(p[2].double() for p in parts) / len(parts)
+    mine, ref = pol.net.to_reference(grad), pol.net.to_reference(gmean.float())
+    bad = {}
+    for k in ref:
+        b = ref[k].numpy().astype(np.float64)
+        e = np.abs(mine[k].numpy() - b).max() / max(np.abs(b).max(), 1e-30)
+        if e > 1e-5:
+            bad[k] = "%.3g" % e
+    assert not bad, bad
+
+
 def test_row_gather_equals_dense_batch():
     import vnav
     from vnav.policy import PolicyNet, frames_from_batch, frames_from_rows

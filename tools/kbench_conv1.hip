@@ -50,13 +50,13 @@ int main(int argc, char** argv) {
   hipLaunchKernelGGL(fill_f, dim3((16 * 32 * 32 + 255) / 256), dim3(256), 0, 0, wt, (size_t)16 * 32 * 32);
   hipLaunchKernelGGL(fill_f, dim3(((size_t)frames * 400 + 255) / 256), dim3(256), 0, 0, (float*)msk, (size_t)frames * 400);
   constexpr size_t dlds = conv2_dgrad_x6_lds<20, 20, 9, 9>();
-  CK(hipFuncSetAttribute((const void*)conv2_dgrad_x6_kernel<20, 20, 9, 9>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dlds));
+  CK(hipFuncSetAttribute((const void*)conv2_dgrad_x6_kernel<20, 20, 9, 9, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dlds));
   for (int grid : {512, 768, 1024}) {
     auto run = [&]() {
       if (which[0] == 'w')
         hipLaunchKernelGGL((conv1_wgrad_x3_kernel<84, 84, 20, 20>), dim3(grid), dim3(256), 0, 0, src, frames, dz, slab);
       else if (which[0] == 'd')
-        hipLaunchKernelGGL((conv2_dgrad_x6_kernel<20, 20, 9, 9>), dim3(grid), dim3(256), dlds, 0, dz2, wt, msk, dx1, frames);
+        hipLaunchKernelGGL((conv2_dgrad_x6_kernel<20, 20, 9, 9, 4>), dim3(grid), dim3(256), dlds, 0, dz2, wt, msk, dx1, frames);
       else
         hipLaunchKernelGGL((conv2_dgrad_kernel<20, 20, 9, 9, true>), dim3(grid), dim3(256), 0, 0, dz2, wt, dx1, msk, dx1, frames);
     };
