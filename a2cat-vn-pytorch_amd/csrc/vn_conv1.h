@@ -361,96 +361,151 @@ __global__ void conv1_wgrad_reduce_kernel(const float* __restrict__ slab, int ns
 // (exact, as the forward's weights), the frame bytes are exact in bf16, so every product is
 // exact and the fp32 accumulation sees the same terms as the f32 kernel.
 //   A: read straight from dZ in its MFMA layout — lane (co, h) takes the 8 pixels of group
-//      g = 2s + h (one output row's pixels 8(g % 3) .. +7, the last group of a row half
+//      g = 2s + h (one output row's pixels 8(g % GPR) .. +7, the last group of a row
 //      padding with dZ = 0): eight loads of one 128-B pixel row each, two steps ahead.
-//   B: the frame is staged per workgroup as Q[y][x & 3][c][x >> 2] (bf16, strides 24 / 72 /
-//      296 elements), so the 8 pixels of a group at one tap (ky, kx, c) are 8 consecutive
+//   B: the frame is staged as Q[y][x & 3][c][x >> 2] (bf16, strides PC / PX / RSQ elements
+//      of the layout), so the 8 pixels of a group at one tap (ky, kx, c) are 8 consecutive
 //      elements: one ds_read_b128 per tile (taps kx >= 4 sit in tiles 3-4 and take one more
-//      element and a 16-bit funnel shift). The tap -> lane tables (vn_conv1_lanes.h) put
-//      the 16 lanes of every b128 pass group on distinct bank quads.
-// Wave w takes the steps s = w (mod 4) of every frame; the four wave sums are folded through
+//      element and a 16-bit funnel shift). The tap -> lane tables (vn_conv1_lanes.h, one per
+//      layout) put the 16 lanes of every b128 pass group on distinct bank quads.
+// Work item = (frame, band of BR output rows); a band stages the 4*BR + 3 image rows its taps
+// read (84x84: the whole frame in one band; 174x174: 6 bands of 7 rows; 300x400: 19 of 4).
+// Wave w takes the steps s = w (mod 4) of every band; the four wave sums are folded through
 // LDS into one slab per workgroup, slot tile*32 + c32 (kConv1WgradCol maps it to dW).
-constexpr int kQPC = 24, kQPX = 72, kQRS = 296;  // Q strides (bf16 elements): c row, x & 3 plane, image row
+template <int H, int W>
+struct Conv1WgQ;  // Q strides (bf16 elements) and the lane-table layout id
+template <>
+struct Conv1WgQ<84, 84> {
+  static constexpr int PC = 24, PX = 72, RSQ = 296, ID = 0;
+};
+template <>
+struct Conv1WgQ<174, 174> {
+  static constexpr int PC = 72, PX = 216, RSQ = 888, ID = 1;
+};
+template <>
+struct Conv1WgQ<300, 400> {
+  static constexpr int PC = 120, PX = 360, RSQ = 1464, ID = 2;
+};
+
+template <int H, int W>
+struct Conv1WgBand {
+  using Q = Conv1WgQ<H, W>;
+  static constexpr int OH = (H - 7) / 4 + 1, OW = (W - 7) / 4 + 1;
+  static constexpr int GPR = (OW + 7) / 8;  // 8-pixel groups per output row
+  static constexpr int rows_of(int br) { return 4 * br + 3 < H ? 4 * br + 3 : H; }
+  static constexpr size_t lds_of(int br) { return (size_t)rows_of(br) * Q::RSQ * 2; }
+  static constexpr int br_max() {
+    int br = OH;
+    while (br > 1 && lds_of(br) > 56 * 1024) --br;
+    return br;
+  }
+  static constexpr int NB = (OH + br_max() - 1) / br_max();
+  static constexpr int BR = (OH + NB - 1) / NB;
+  static constexpr int BRI = rows_of(BR);
+  static constexpr size_t LDS = lds_of(BR) > 32 * 160 * 4 ? lds_of(BR) : 32 * 160 * 4;  // + the final fold
+};
 
 template <int H, int W>
 constexpr bool conv1_wgrad_x3_fits() {
-  return H == 84 && W == 84;  // the lane tables are laid out for this frame (20x20 map)
+  return (H == 84 && W == 84) || (H == 174 && W == 174) || (H == 300 && W == 400);
 }
 
 template <int H, int W, int OH, int OW>
 __global__ __launch_bounds__(256) void conv1_wgrad_x3_kernel(FrameSrc src, int n_frames, const float* __restrict__ dZ,
                                                              float* __restrict__ slab) {
-  static_assert(H == 84 && W == 84 && OH == 20 && OW == 20, "Q layout and lane tables for 84x84 frames");
+  using Bd = Conv1WgBand<H, W>;
+  using QL = typename Bd::Q;
+  constexpr int PC = QL::PC, PX = QL::PX, RSQ = QL::RSQ;
   constexpr int RB = W * 3;
   constexpr int NPIX = OH * OW;
-  constexpr int GPR = (OW + 7) / 8;       // 8-pixel groups per output row
-  constexpr int KS = (OH * GPR + 1) / 2;  // 16-pixel steps: two groups (one per lane half)
-  constexpr int PAIRS = (W / 4 + 1) / 2;  // x>>2 pairs per image row (the last one half)
-  constexpr int TASKS = H * PAIRS;        // (row, pair) staging tasks per frame
-  constexpr int NT = (TASKS + 255) / 256;
-  static_assert(kQRS >= 4 * kQPX + 8 && kQPX == 3 * kQPC && kQPC >= 2 * PAIRS + 2, "Q strides");
-  __shared__ __attribute__((aligned(16))) uint16_t Q[H * kQRS];
+  constexpr int GPR = Bd::GPR, BR = Bd::BR, NB = Bd::NB, BRI = Bd::BRI;
+  constexpr int PAIRS = (W + 7) / 8;  // 8-pixel (x) staging pairs per image row (the last one partial)
+  constexpr int NT = (BRI * PAIRS + 255) / 256;
+  constexpr int NDW = RB % 4 == 0 ? 6 : 7;  // dwords per staging task (7: rows start at 2 mod 4)
+  static_assert(OH == Bd::OH && OW == Bd::OW, "geometry");
+  // staged pairs never overlap; every window read (padding pixels included) stays inside its
+  // image row and sees written or zeroed (finite) entries
+  static_assert(PX >= 3 * PC && PC >= 2 * PAIRS && 3 * PX + 2 * PC + 8 * GPR < RSQ, "Q strides");
+  static_assert(RB % 2 == 0, "even row bytes");
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem_wg[];
+  uint16_t* Q = reinterpret_cast<uint16_t*>(smem_wg);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, c32 = lane & 31;
-  {  // never-written Q entries (x >> 2 >= 22, row tails) are read by padding pixels: zero
+  {  // never-written Q entries (x >> 2 >= 2 * PAIRS, row tails) are read by padding pixels: zero
     uint4* q4 = reinterpret_cast<uint4*>(Q);
-    for (int i = tid; i < H * kQRS / 8; i += 256) q4[i] = uint4{0u, 0u, 0u, 0u};
+    for (int i = tid; i < BRI * RSQ / 8; i += 256) q4[i] = uint4{0u, 0u, 0u, 0u};
   }
   int loff[5];
 #pragma unroll
   for (int nt = 0; nt < 5; ++nt) {
-    const int t = kConv1WgradRead[nt][c32], ky = t / 21, kx = (t / 3) % 7, c = t % 3;
-    loff[nt] = ky * kQRS + (kx & 3) * kQPX + c * kQPC;
+    const int t = kConv1WgradRead[QL::ID][nt][c32], ky = t / 21, kx = (t / 3) % 7, c = t % 3;
+    loff[nt] = ky * RSQ + (kx & 3) * PX + c * PC;
   }
-  const int col2 = kConv1WgradCol[2][c32];  // tile 2 carries the bias column and pad lanes
+  const int col2 = kConv1WgradCol[QL::ID][2][c32];  // tile 2 carries the bias column and pad lanes
   const uint32_t keep2 = col2 >= 0 && col2 < 147 ? 0xffffffffu : 0u;
   const uint32_t add2 = col2 == 148 ? 0x3f803f80u : 0u;
-  const uint32_t keep4 = kConv1WgradCol[4][c32] >= 0 ? 0xffffffffu : 0u;
+  const uint32_t keep4 = kConv1WgradCol[QL::ID][4][c32] >= 0 ? 0xffffffffu : 0u;
   f16v acc[5];
 #pragma unroll
   for (int nt = 0; nt < 5; ++nt)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[nt][r] = 0.0f;
-  // staging task (row y, pair m): pixels 8m .. 8m+7 of row y = 24 frame bytes (12 in the
-  // last, half pair), prefetched into registers one frame ahead. vmcnt retires loads in
-  // issue order, so the next frame's tasks are issued one per step between the dZ loads
-  // (a whole-frame prefetch would stall the first dZ use behind it).
-  uint32_t pre[NT][6];
-  auto load_task = [&](int r, int f) {
+  const int n_items = n_frames * NB;
+  auto band_rows = [&](int band) { return min(BRI, H - 4 * BR * band); };
+  // staging task (band row y, pair m): pixels 8m .. 8m+7 of the row = 24 frame bytes (fewer
+  // in the last pair), prefetched into registers one item ahead as NDW aligned dwords.
+  // vmcnt retires loads in issue order, so the next item's tasks are issued one per step
+  // between the dZ loads (a whole-frame prefetch would stall the first dZ use behind it).
+  uint32_t pre[NT][NDW];
+  auto load_task = [&](int r, int it) {
     const int t = tid + r * 256;
-    if (t < TASKS) {
+    const int band = it - (it / NB) * NB;
+    if (t < band_rows(band) * PAIRS) {
       const int y = t / PAIRS, m = t - (t / PAIRS) * PAIRS;
-      const uint32_t* s4 = reinterpret_cast<const uint32_t*>(frame_ptr(src, f) + y * RB + m * 24);
-      const bool full = 8 * m + 8 <= W;
+      const int64_t off = (int64_t)(4 * BR * band + y) * RB + m * 24;
+      const uint32_t* s4 = reinterpret_cast<const uint32_t*>(frame_ptr(src, it / NB) + (off & ~(int64_t)3));
+      const int nbytes = (int)(off & 3) + min(24, RB - m * 24);  // bytes of the aligned window
 #pragma unroll
-      for (int q = 0; q < 6; ++q) pre[r][q] = (q < 3 || full) ? s4[q] : 0u;
+      for (int q = 0; q < NDW; ++q) pre[r][q] = 4 * q < nbytes ? s4[q] : 0u;
     }
   };
-  static_assert(NT <= (KS / 4) - 1, "every wave has a step per staging task");
-  auto stage_frame_q = [&]() {
+  auto stage_q = [&](int band) {
 #pragma unroll
     for (int r = 0; r < NT; ++r) {
       const int t = tid + r * 256;
-      if (t < TASKS) {
+      if (t < band_rows(band) * PAIRS) {
         const int y = t / PAIRS, m = t - (t / PAIRS) * PAIRS;
-        uint32_t* qrow = reinterpret_cast<uint32_t*>(Q + y * kQRS + 2 * m);
+        uint32_t d[6];
+        if constexpr (NDW == 6) {
+#pragma unroll
+          for (int q = 0; q < 6; ++q) d[q] = pre[r][q];
+        } else {
+          const int sh = (int)((((int64_t)(4 * BR * band + y) * RB) & 3) * 8);  // 0 or 16
+#pragma unroll
+          for (int q = 0; q < 6; ++q) d[q] = __builtin_amdgcn_alignbit(pre[r][q + 1], pre[r][q], sh);
+        }
+        const int nv = min(24, RB - m * 24);  // valid bytes of the pair
+#pragma unroll
+        for (int q = 0; q < 6; ++q)
+          if (4 * q + 4 > nv) d[q] = 4 * q >= nv ? 0u : d[q] & (0xffffffffu >> (8 * (4 * q + 4 - nv)));
+        uint32_t* qrow = reinterpret_cast<uint32_t*>(Q + y * RSQ + 2 * m);
 #pragma unroll
         for (int rx = 0; rx < 4; ++rx)
 #pragma unroll
           for (int c = 0; c < 3; ++c) {
             const int b0 = 3 * rx + c, b1 = b0 + 12;  // pixel rx and rx + 4 of the 8
-            const float lo = (float)((pre[r][b0 >> 2] >> (8 * (b0 & 3))) & 0xffu);
-            const float hi = (float)((pre[r][b1 >> 2] >> (8 * (b1 & 3))) & 0xffu);
-            qrow[(rx * kQPX + c * kQPC) / 2] = __builtin_amdgcn_perm(__float_as_uint(hi), __float_as_uint(lo), 0x07060302u);
+            const float lo = (float)((d[b0 >> 2] >> (8 * (b0 & 3))) & 0xffu);
+            const float hi = (float)((d[b1 >> 2] >> (8 * (b1 & 3))) & 0xffu);
+            qrow[(rx * PX + c * PC) / 2] = __builtin_amdgcn_perm(__float_as_uint(hi), __float_as_uint(lo), 0x07060302u);
           }
       }
     }
   };
   float zc[8], zn[8];  // steps s and s + 4 in flight
-  auto load_z = [&](float (&z)[8], int f, int s) {
-    const int g = 2 * s + h, oy = g / GPR, ox0 = 8 * (g - (g / GPR) * GPR);
+  auto load_z = [&](float (&z)[8], int f, int oy0, int ng, int s) {
+    const int g = 2 * s + h, oy = oy0 + g / GPR, ox0 = 8 * (g - (g / GPR) * GPR);
     const float* zf = dZ + ((int64_t)f * NPIX + oy * OW + ox0) * 32 + c32;
-    const int nv = g < OH * GPR ? min(8, OW - ox0) : 0;
+    const int nv = g < ng ? min(8, OW - ox0) : 0;
     if (nv == 8) {  // whole group: eight loads off one address
 #pragma unroll
       for (int j = 0; j < 8; ++j) z[j] = zf[j * 32];
@@ -459,28 +514,33 @@ __global__ __launch_bounds__(256) void conv1_wgrad_x3_kernel(FrameSrc src, int n
       for (int j = 0; j < 8; ++j) z[j] = j < nv ? zf[j * 32] : 0.0f;
     }
   };
-  if ((int)blockIdx.x < n_frames)
+  if ((int)blockIdx.x < n_items)
 #pragma unroll
     for (int r = 0; r < NT; ++r) load_task(r, blockIdx.x);
-  for (int f = blockIdx.x; f < n_frames; f += gridDim.x) {
-    stage_frame_q();
-    if (wave < KS) load_z(zc, f, wave);
-    if (wave + 4 < KS) load_z(zn, f, wave + 4);
+  for (int it = blockIdx.x; it < n_items; it += gridDim.x) {
+    const int f = it / NB, band = it - (it / NB) * NB;
+    const int oy0 = BR * band, nr = min(BR, OH - oy0);
+    const int ng = nr * GPR, KS = (ng + 1) / 2;  // groups, 16-pixel steps of the band
+    stage_q(band);
+    if (wave < KS) load_z(zc, f, oy0, ng, wave);
+    if (wave + 4 < KS) load_z(zn, f, oy0, ng, wave + 4);
     __syncthreads();
-    const int fnext = f + (int)gridDim.x;
+    const int inext = it + (int)gridDim.x;
     // one 16-pixel step (the wave's i-th) from the dZ values in z, which then takes step
     // s + 8 (the two buffers alternate, no copies)
-    auto step = [&](int s, int i, float (&z)[8]) {
+    int ns = 0;  // steps this wave has run in the item
+    auto step = [&](int s, float (&z)[8]) {
       union { uint16_t u[8]; bf16x8 v; } a0, a1, a2;
 #pragma unroll
       for (int j = 0; j < 8; ++j) split3_bf16(z[j], a0.u[j], a1.u[j], a2.u[j]);
 #pragma unroll
       for (int r = 0; r < NT; ++r)
-        if (i == r && fnext < n_frames) load_task(r, fnext);
-      if (s + 8 < KS) load_z(z, f, s + 8);
-      const int g = min(2 * s + h, OH * GPR - 1);
+        if (ns == r && inext < n_items) load_task(r, inext);
+      ++ns;
+      if (s + 8 < KS) load_z(z, f, oy0, ng, s + 8);
+      const int g = min(2 * s + h, ng - 1);
       const int oy = g / GPR, ox0 = 8 * (g - (g / GPR) * GPR);
-      const uint16_t* gb = Q + oy * 4 * kQRS + ox0;
+      const uint16_t* gb = Q + oy * 4 * RSQ + ox0;
       union { bf16x8 v; uint4 q; uint32_t d[4]; } b[5];
       uint32_t e[2];
 #pragma unroll
@@ -507,10 +567,14 @@ __global__ __launch_bounds__(256) void conv1_wgrad_x3_kernel(FrameSrc src, int n
 #pragma unroll
       for (int nt = 0; nt < 5; ++nt) acc[nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2.v, b[nt].v, acc[nt], 0, 0, 0);
     };
-    for (int s = wave, i = 0; s < KS; s += 8, i += 2) {
-      step(s, i, zc);
-      if (s + 4 < KS) step(s + 4, i + 1, zn);
+    for (int s = wave; s < KS; s += 8) {
+      step(s, zc);
+      if (s + 4 < KS) step(s + 4, zn);
     }
+    // staging tasks of the next item not issued inside the steps (short bands)
+#pragma unroll
+    for (int r = 0; r < NT; ++r)
+      if (r >= ns && inext < n_items) load_task(r, inext);
     __syncthreads();
   }
   // fold the four wave sums in LDS (fixed order), one slab per workgroup: D[co][slot]
@@ -522,23 +586,25 @@ __global__ __launch_bounds__(256) void conv1_wgrad_x3_kernel(FrameSrc src, int n
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int co = (r & 3) + 8 * (r >> 2) + 4 * h;
-          const int i = co * 160 + nt * 32 + c32;
-          red[i] = w == 0 ? acc[nt][r] : red[i] + acc[nt][r];
+          const int ix = co * 160 + nt * 32 + c32;
+          red[ix] = w == 0 ? acc[nt][r] : red[ix] + acc[nt][r];
         }
     }
     __syncthreads();
   }
   float* out = slab + (int64_t)blockIdx.x * (32 * 160);
-  for (int i = tid; i < 32 * 160 / 4; i += 256)
-    reinterpret_cast<f4*>(out)[i] = reinterpret_cast<const f4*>(red)[i];
+  for (int ix = tid; ix < 32 * 160 / 4; ix += 256)
+    reinterpret_cast<f4*>(out)[ix] = reinterpret_cast<const f4*>(red)[ix];
 }
 
-// dW / db from the slot-ordered partial sums of conv1_wgrad_x3_kernel (kConv1WgradCol).
-__global__ void conv1_wgrad_x3_finish_kernel(const float* __restrict__ part, int nparts, float* dW, float* db) {
+// dW / db from the slot-ordered partial sums of conv1_wgrad_x3_kernel (kConv1WgradCol of
+// layout `layout`).
+__global__ void conv1_wgrad_x3_finish_kernel(const float* __restrict__ part, int nparts, int layout, float* dW,
+                                             float* db) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;  // co*160 + slot
   if (idx >= 32 * 160) return;
   const int co = idx / 160, slot = idx - (idx / 160) * 160;
-  const int col = kConv1WgradCol[slot >> 5][slot & 31];
+  const int col = kConv1WgradCol[layout][slot >> 5][slot & 31];
   if (col < 0) return;
   float s = 0.0f;
   for (int z = 0; z < nparts; ++z) s += part[(int64_t)z * 32 * 160 + idx];

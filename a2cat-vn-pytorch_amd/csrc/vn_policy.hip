@@ -822,39 +822,49 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
   }
   // ---- conv1: wgrad from dz1 (in X1's storage) and the frames
   constexpr bool kConv1Lds = kConv1LdsFrame<H0, W0>;
-  if (!kConv1Lds || src.f32[0] || src.f32[1]) {
+  const bool f32in = src.f32[0] || src.f32[1];
+  bool wg_done = false;
+  if constexpr (conv1_wgrad_x3_fits<H0, W0>()) {
+    if (!f32in) {
+      const int frames = 2 * n;
+      using Bd = Conv1WgBand<H0, W0>;
+      const void* kfn = (const void*)conv1_wgrad_x3_kernel<H0, W0, G::OH1, G::OW1>;
+      const int blocks = std::min(frames * Bd::NB, resident_blocks(kfn, 256, Bd::LDS));
+      hipLaunchKernelGGL((conv1_wgrad_x3_kernel<H0, W0, G::OH1, G::OW1>), dim3(blocks), dim3(256), Bd::LDS, st, src,
+                         frames, a.X[0], w.slab);
+      constexpr int kParts = 32;
+      float* part = w.slab + (int64_t)blocks * 32 * 160;
+      hipLaunchKernelGGL(slab_partial_kernel, dim3((32 * 160 + 255) / 256, kParts), dim3(256), 0, st, w.slab, blocks,
+                         (int64_t)32 * 160, part);
+      hipLaunchKernelGGL(conv1_wgrad_x3_finish_kernel, dim3((32 * 160 + 255) / 256), dim3(256), 0, st, part, kParts,
+                         (int)Bd::Q::ID, Gr + L.l[0].w, Gr + L.l[0].b);
+      wg_done = true;
+    }
+  } else if constexpr (kConv1Lds) {
+    if (!f32in) {
+      const int frames = 2 * n;
+      constexpr int CP = (G::OH1 * G::OW1 <= 400) ? (G::OH1 * G::OW1 + 7) / 8 * 8 : 448;
+      constexpr size_t lds = conv1_wgrad_lds<H0, W0, CP>();
+      static bool attr = false;  // > 64 KiB of dynamic LDS needs the opt-in attribute
+      if (!attr) {
+        VN_HIP(hipFuncSetAttribute((const void*)conv1_wgrad_kernel<H0, W0, G::OH1, G::OW1, CP>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        attr = true;
+      }
+      const int blocks = std::min({frames, kConv1WgradBlocks,
+                                   resident_blocks((const void*)conv1_wgrad_kernel<H0, W0, G::OH1, G::OW1, CP>, 256, lds)});
+      hipLaunchKernelGGL((conv1_wgrad_kernel<H0, W0, G::OH1, G::OW1, CP>), dim3(blocks), dim3(256), lds, st, src, frames,
+                         a.X[0], w.slab);
+      hipLaunchKernelGGL(conv1_wgrad_reduce_kernel, dim3((32 * 160 + 255) / 256), dim3(256), 0, st, w.slab, blocks * 4,
+                         Gr + L.l[0].w, Gr + L.l[0].b);
+      wg_done = true;
+    }
+  }
+  if (!wg_done) {
     using Im = FramesIm2col<H0, W0, G::OH1, G::OW1>;
     const int P1 = 2 * n * G::OH1 * G::OW1;
     Im2colT<Im> fbw{Im{src, P1}, 148};
     launch_wgrad<32, 64, 2, 2>(a.X[0], 32, 32, fbw, 148, P1, w.slab, w.slab_cap, Gr + L.l[0].w, Gr + L.l[0].b, st);
-  } else if constexpr (conv1_wgrad_x3_fits<H0, W0>()) {
-    const int frames = 2 * n;
-    const void* kfn = (const void*)conv1_wgrad_x3_kernel<H0, W0, G::OH1, G::OW1>;
-    const int blocks = std::min(frames, resident_blocks(kfn, 256, 0));
-    hipLaunchKernelGGL((conv1_wgrad_x3_kernel<H0, W0, G::OH1, G::OW1>), dim3(blocks), dim3(256), 0, st, src, frames,
-                       a.X[0], w.slab);
-    constexpr int kParts = 32;
-    float* part = w.slab + (int64_t)blocks * 32 * 160;
-    hipLaunchKernelGGL(slab_partial_kernel, dim3((32 * 160 + 255) / 256, kParts), dim3(256), 0, st, w.slab, blocks,
-                       (int64_t)32 * 160, part);
-    hipLaunchKernelGGL(conv1_wgrad_x3_finish_kernel, dim3((32 * 160 + 255) / 256), dim3(256), 0, st, part, kParts,
-                       Gr + L.l[0].w, Gr + L.l[0].b);
-  } else if constexpr (kConv1Lds) {
-    const int frames = 2 * n;
-    constexpr int CP = (G::OH1 * G::OW1 <= 400) ? (G::OH1 * G::OW1 + 7) / 8 * 8 : 448;
-    constexpr size_t lds = conv1_wgrad_lds<H0, W0, CP>();
-    static bool attr = false;  // > 64 KiB of dynamic LDS needs the opt-in attribute
-    if (!attr) {
-      VN_HIP(hipFuncSetAttribute((const void*)conv1_wgrad_kernel<H0, W0, G::OH1, G::OW1, CP>,
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      attr = true;
-    }
-    const int blocks = std::min(
-        {frames, kConv1WgradBlocks, resident_blocks((const void*)conv1_wgrad_kernel<H0, W0, G::OH1, G::OW1, CP>, 256, lds)});
-    hipLaunchKernelGGL((conv1_wgrad_kernel<H0, W0, G::OH1, G::OW1, CP>), dim3(blocks), dim3(256), lds, st, src, frames,
-                       a.X[0], w.slab);
-    hipLaunchKernelGGL(conv1_wgrad_reduce_kernel, dim3((32 * 160 + 255) / 256), dim3(256), 0, st, w.slab, blocks * 4,
-                       Gr + L.l[0].w, Gr + L.l[0].b);
   }
   VN_HIP(hipGetLastError());
   return VN_OK;
