@@ -628,14 +628,39 @@ __global__ void slab_partial_kernel(const float* __restrict__ slab, int nslab, i
 
 // ---- conv2 weight gradient ----------------------------------------------------
 // dW2[co][(ky*4+kx)*32 + ci] = sum over frames and output pixels p of
-// dZ2[f][p][co] * X1[f][(2oy+ky)*IW + 2ox+kx][ci]. One frame per workgroup iteration:
-// X1_f (IH*IW*32 fp32) and dZ2_f are staged in LDS; wave w owns taps 4w..4w+3 (four
-// 32x32 accumulators: co x ci), two output pixels per MFMA step. Bias gradient: colsum.
+// dZ2[f][p][co] * X1[f][(2oy+ky)*IW + 2ox+kx][ci]. Work item = (frame, band of BR output
+// rows): the band's X1 rows (2*BR + 2 of them) and dZ2 rows are staged in LDS; wave w owns
+// taps 4w..4w+3 (four 32x32 accumulators: co x ci), two output pixels per MFMA step.
+// 84x84 (20x20 conv1 map) stages the whole frame in one band; 174x174 (42x42) bands of 5
+// rows keep two workgroups per CU. Bias gradient: column sums of dZ2 (wave 0).
+template <int IH, int IW, int OH, int OW>
+struct Conv2WgBand {
+  static constexpr int rows_of(int br) { return 2 * br + 2 < IH ? 2 * br + 2 : IH; }
+  static constexpr size_t lds_of(int br) {
+    return ((size_t)rows_of(br) * IW * 32 + (size_t)(br * OW + 1) / 2 * 2 * 32) * 4;
+  }
+  static constexpr int br_max() {
+    int br = OH;
+    while (br > 1 && lds_of(br) > 80 * 1024) --br;
+    return br;
+  }
+  static constexpr int NB = (OH + br_max() - 1) / br_max();
+  static constexpr int BR = (OH + NB - 1) / NB;
+  static constexpr size_t LDS = lds_of(BR);
+};
+
+template <int IH, int IW, int OH, int OW>
+constexpr size_t conv2_wgrad_lds() {
+  return Conv2WgBand<IH, IW, OH, OW>::LDS;
+}
+
 template <int IH, int IW, int OH, int OW>
 __global__ __launch_bounds__(256) void conv2_wgrad_kernel(const float* __restrict__ X1, const float* __restrict__ dZ2,
                                                           int n_frames, float* __restrict__ slab,
                                                           float* __restrict__ bias_slab) {
-  constexpr int NX = IH * IW * 32, NP = OH * OW, NPE = (NP + 1) / 2 * 2;
+  using Bd = Conv2WgBand<IH, IW, OH, OW>;
+  constexpr int BR = Bd::BR, NB = Bd::NB;
+  constexpr int NX = Bd::rows_of(BR) * IW * 32, NP = OH * OW;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   float* xs = reinterpret_cast<float*>(smem);
   float* ds = xs + NX;
@@ -647,23 +672,27 @@ __global__ __launch_bounds__(256) void conv2_wgrad_kernel(const float* __restric
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[j][r] = 0.0f;
   float bacc = 0.0f;  // bias gradient: column sums of dZ2 (wave 0 only)
-  for (int f = blockIdx.x; f < n_frames; f += gridDim.x) {
+  const int n_items = n_frames * NB;
+  for (int it = blockIdx.x; it < n_items; it += gridDim.x) {
+    const int f = it / NB, band = it - (it / NB) * NB;
+    const int oy0 = BR * band, nr = min(BR, OH - oy0), npb = nr * OW, npe = (npb + 1) / 2 * 2;
+    const int y0 = 2 * oy0, nx = min(2 * nr + 2, IH - y0) * IW * 32;
     {
-      const f4* s4 = reinterpret_cast<const f4*>(X1 + (int64_t)f * NX);
+      const f4* s4 = reinterpret_cast<const f4*>(X1 + ((int64_t)f * IH + y0) * IW * 32);
       f4* d4 = reinterpret_cast<f4*>(xs);
 #pragma unroll 4
-      for (int i = tid; i < NX / 4; i += 256) d4[i] = s4[i];
-      const f4* z4 = reinterpret_cast<const f4*>(dZ2 + (int64_t)f * NP * 32);
+      for (int i = tid; i < nx / 4; i += 256) d4[i] = s4[i];
+      const f4* z4 = reinterpret_cast<const f4*>(dZ2 + ((int64_t)f * NP + oy0 * OW) * 32);
       f4* e4 = reinterpret_cast<f4*>(ds);
-      for (int i = tid; i < NPE * 8; i += 256) e4[i] = i < NP * 8 ? z4[i] : f4zero();
+      for (int i = tid; i < npe * 8; i += 256) e4[i] = i < npb * 8 ? z4[i] : f4zero();
     }
     __syncthreads();
 #pragma unroll 3
-    for (int s = 0; s < NPE / 2; ++s) {
+    for (int s = 0; s < npe / 2; ++s) {
       const int p = 2 * s + h;
       const float a = ds[p * 32 + c32];
       if (wave == 0) bacc += a;
-      const int pp = p < NP ? p : 0;
+      const int pp = p < npb ? p : 0;
       const int oy = pp / OW, ox = pp - (pp / OW) * OW;
       const float* xb = xs + ((2 * oy) * IW + 2 * ox) * 32 + c32;
 #pragma unroll
@@ -960,11 +989,6 @@ __global__ __launch_bounds__(NW * 64, 2) void conv2_dgrad_x6_kernel(const float*
     }
     __syncthreads();
   }
-}
-
-template <int IH, int IW, int OH, int OW>
-constexpr size_t conv2_wgrad_lds() {
-  return ((size_t)IH * IW * 32 + (size_t)(OH * OW + 1) / 2 * 2 * 32) * 4;
 }
 
 // Deterministic column sums of a [rows][32] matrix: per-block partials, then one block.

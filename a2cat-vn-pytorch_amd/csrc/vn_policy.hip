@@ -763,9 +763,10 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
   // ---- conv2 (k4 s2): wgrad (needs X1), then dgrad into dz1 written over X1
   {
     const int frames = 2 * n;
-    const int blocks = std::min(frames, kConv2WgradBlocks);
+    using Bd2 = Conv2WgBand<G::OH1, G::OW1, G::OH2, G::OW2>;
+    const int blocks = std::min(frames * Bd2::NB, kConv2WgradBlocks);
     constexpr size_t lds = conv2_wgrad_lds<G::OH1, G::OW1, G::OH2, G::OW2>();
-    if constexpr (lds <= 160 * 1024) {
+    if constexpr (lds <= 80 * 1024) {  // two workgroups per CU (bands of output rows)
       static bool attr = false;
       if (!attr) {
         VN_HIP(hipFuncSetAttribute((const void*)conv2_wgrad_kernel<G::OH1, G::OW1, G::OH2, G::OW2>,
@@ -778,7 +779,7 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
       hipLaunchKernelGGL(sum_slabs_kernel, dim3((32 * 512 + 255) / 256), dim3(256), 0, st, w.slab, blocks,
                          (int64_t)32 * 512, Gr + L.l[1].w);
       hipLaunchKernelGGL(sum_slabs_kernel, dim3(1), dim3(32), 0, st, bias_slab, blocks, (int64_t)32, Gr + L.l[1].b);
-    } else {  // frames whose conv1 map does not fit the LDS (174x174): generic split-K path
+    } else {  // a conv1 map row too wide for a band in half the LDS: generic split-K path
       using Im = NhwcIm2col<32, 4, 4, 2, G::OH1, G::OW1, G::OH2, G::OW2, 1>;
       const int P2 = 2 * n * G::OH2 * G::OW2;
       Im2colT<Im> fbw{Im{a.X[0], P2}, 512};
