@@ -189,7 +189,9 @@ __global__ __launch_bounds__(256, 2) void conv1_fwd_x3_kernel(FrameSrc src, int 
     bw[(sl * 3 + 1) * 64 + ln] = t1.v;
     bw[(sl * 3 + 2) * 64 + ln] = t2.v;
   }
-  const float bs = bias[c32];
+  f4 bs[4];  // the transposed tile's lane holds channels 8j + 4h .. +3 (j = 0..3) of pixel c32
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bs[j] = *reinterpret_cast<const f4*>(bias + 8 * j + 4 * h);
   const int n_items = n_frames * NB;
   // dwords of item it's band: rows 4*BR*band .. (clamped to the frame)
   auto band_dwords = [&](int band) { return min(BRI, H - 4 * BR * band) * RB / 4; };
@@ -248,20 +250,29 @@ __global__ __launch_bounds__(256, 2) void conv1_fwd_x3_kernel(FrameSrc src, int 
         a.u[0] = q[0];
         a.u[1] = q[1];
 #pragma unroll
-        for (int p = 0; p < 3; ++p)
-          acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.v, bw[(sl * 3 + p) * 64 + wl], acc[p], 0, 0, 0);
+        for (int p = 0; p < 3; ++p)  // D^T = W^T A^T: rows = channels, columns = pixels
+          acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bw[(sl * 3 + p) * 64 + wl], a.v, acc[p], 0, 0, 0);
       }
-      const int64_t pix0 = (int64_t)f * NPIX + oy0 * OW;
+      // lane (pixel c32, h) holds channels 8j + 4h + (0..3): four 16-B stores per lane; the
+      // ReLU bits of the other 16 channels come from the partner lane (c32, 1 - h)
+      const int rr = t * 32 + c32;
+      const int64_t pix = (int64_t)f * NPIX + oy0 * OW + rr;
+      uint32_t bits = 0;
+      f4 y[4];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int rr = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const float sum = (acc[2][r] + acc[1][r]) + acc[0][r];
-        const float y = fmaxf(sum * (1.0f / 255.0f) + bs, 0.0f);
-        const uint64_t bal = __ballot(y > 0.0f);
-        if (rr < npb) {
-          Y[(pix0 + rr) * 32 + c32] = y;
-          if (c32 == 0) mask[pix0 + rr] = (uint32_t)(bal >> (32 * h));
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = 4 * j + r;
+          const float sum = (acc[2][i] + acc[1][i]) + acc[0][i];
+          y[j][r] = fmaxf(sum * (1.0f / 255.0f) + bs[j][r], 0.0f);
+          bits |= (y[j][r] > 0.0f ? 1u : 0u) << (8 * j + 4 * h + r);
         }
+      bits |= (uint32_t)__shfl_xor((int)bits, 32);
+      if (rr < npb) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) *reinterpret_cast<f4*>(Y + pix * 32 + 8 * j + 4 * h) = y[j];
+        if (h == 0) mask[pix] = bits;
       }
     }
     __syncthreads();
@@ -868,9 +879,11 @@ __device__ __forceinline__ void split3_pack(const f4& v, uint2& t0, uint2& t1, u
   t2 = uint2{l[0] | ((uint32_t)l[1] << 16), l[2] | ((uint32_t)l[3] << 16)};
 }
 
-// The epilogue stores each tile straight from the accumulators under the conv1 ReLU
-// bitmask (staging the frame's result in LDS for 16-B stores measured slower: the extra
-// 58 KB of LDS cost a resident workgroup and the store phase did not overlap compute).
+// The product is computed transposed (MFMA rows = ci, columns = pixels), so the epilogue
+// stores 4 consecutive channels of a pixel per lane straight from the accumulators (16-B
+// stores under 4 bits of the conv1 ReLU bitmask: 4x fewer store instructions than the
+// pixel-row layout's dword stores, which left the kernel store-issue bound; staging the
+// result in LDS instead cost a resident workgroup and measured slower).
 template <int IH, int IW, int OH, int OW, int NW>
 __global__ __launch_bounds__(NW * 64, 2) void conv2_dgrad_x6_kernel(const float* __restrict__ dZ2,
                                                                 const float* __restrict__ WT,
@@ -962,30 +975,36 @@ __global__ __launch_bounds__(NW * 64, 2) void conv2_dgrad_x6_kernel(const float*
 #pragma unroll
         for (int u = 0; u < 2; ++u)
 #pragma unroll
-          for (int nt = 0; nt < 2; ++nt) {  // small terms first
+          for (int nt = 0; nt < 2; ++nt) {  // small terms first; D^T = W^T dZ2^T: rows = ci, cols = pixels
             f4 c = acc[u][nt];
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u][2], bw[tap][nt][0], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u][0], bw[tap][nt][2], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u][1], bw[tap][nt][1], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u][1], bw[tap][nt][0], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u][0], bw[tap][nt][1], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u][0], bw[tap][nt][0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[tap][nt][0], a[u][2], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[tap][nt][2], a[u][0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[tap][nt][1], a[u][1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[tap][nt][0], a[u][1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[tap][nt][1], a[u][0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[tap][nt][0], a[u][0], c, 0, 0, 0);
             acc[u][nt] = c;
           }
       }
+      // the transposed product leaves lane (pixel i16, q) holding channels nt*16 + 4q .. +3 of
+      // its pixel: one 16-B store per (tile, ci tile) under 4 bits of the ReLU mask
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < 2; ++u) {
+        const int pr = (t0 + u) * 16 + i16;
+        if (pr < NPC) {
+          const int y = (pr / WXC) * 2 + py, x = (pr % WXC) * 2 + px;
+          const int64_t pix = ((int64_t)f * IH + y) * IW + x;
+          const uint32_t mw = mask[pix];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int pr = (t0 + u) * 16 + q * 4 + r;
-          if (pr < NPC) {
-            const int y = (pr / WXC) * 2 + py, x = (pr % WXC) * 2 + px;
-            const int64_t pix = ((int64_t)f * IH + y) * IW + x;
-            const uint32_t mw = mask[pix];
-            dX1[pix * 32 + i16] = (mw >> i16) & 1u ? acc[u][0][r] : 0.0f;
-            dX1[pix * 32 + 16 + i16] = (mw >> (i16 + 16)) & 1u ? acc[u][1][r] : 0.0f;
+          for (int nt = 0; nt < 2; ++nt) {
+            const uint32_t m4 = mw >> (nt * 16 + 4 * q);
+            f4 v = acc[u][nt];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = (m4 >> r) & 1u ? v[r] : 0.0f;
+            *reinterpret_cast<f4*>(dX1 + pix * 32 + nt * 16 + 4 * q) = v;
           }
         }
+      }
     }
     __syncthreads();
   }
