@@ -1010,6 +1010,154 @@ __global__ __launch_bounds__(NW * 64, 2) void conv2_dgrad_x6_kernel(const float*
   }
 }
 
+// ---- conv2 forward on bf16 MFMA (split operands) -----------------------------------
+// X2[f][oy][ox][co] = relu(b[co] + sum over taps (ky, kx) and ci of
+// X1[f][2oy+ky][2ox+kx][ci] * W2[co][ky][kx][ci])  (k4 s2, 32 -> 32 channels).
+// Work item = (frame, band of BR output rows); 8 waves: wave w owns kernel row ky = w & 3
+// (taps (ky, 0..3), their split weights — 4 taps x 2 co tiles x 3 terms — in registers) and
+// the pixel tiles t = w >> 2 (mod 2) of the band. The band's X1 rows are split once when they
+// are staged, into three bf16 planes laid out [row][x & 1][x >> 1][ci] (pixel stride 40:
+// the 16 pixels of a B fragment — consecutive ox, stride-2 x — fall on distinct bank quads),
+// so each x6 product reads its operands with one ds_read_b128 per term instead of gathering
+// and splitting an im2col tile per K step from L2 (the generic path's VALU-bound split).
+// Each wave's product is D[co][pixel] over its 4 taps (K = 128) on
+// v_mfma_f32_16x16x32_bf16; the four kernel-row partials go to LDS and are summed in a
+// fixed order with the bias and ReLU, 16 B per thread.
+template <int IH, int IW, int OH, int OW>
+struct Conv2FwdBand {
+  static constexpr int WH = (IW + 1) / 2;  // x >> 1 columns per parity
+  static constexpr int PSX = 40;           // pixel stride in a plane (bf16)
+  static constexpr int RSP = 2 * WH * PSX; // plane row stride (bf16)
+  static constexpr int rows_of(int br) { return 2 * br + 2 < IH ? 2 * br + 2 : IH; }
+  static constexpr int tiles_of(int br) { return (br * OW + 15) / 16; }
+  static constexpr size_t planes_of(int br) { return (size_t)3 * rows_of(br) * RSP * 2; }
+  static constexpr size_t lds_of(int br) { return planes_of(br) + (size_t)4 * tiles_of(br) * 16 * 32 * 4; }
+  static constexpr int br_max() {
+    int br = OH;
+    while (br > 1 && lds_of(br) > 160 * 1024) --br;
+    return br;
+  }
+  static constexpr int NB = (OH + br_max() - 1) / br_max();
+  static constexpr int BR = (OH + NB - 1) / NB;
+  static constexpr size_t LDS = lds_of(BR);
+};
+
+// Whole frames only: banded maps (174x174, 300x400) re-stage overlapping X1 rows and, at one
+// workgroup per CU, measured slower than the generic im2col GEMM (1.09 vs 0.97 ms per 174x174
+// rollout step); the 20x20 map of 84x84 frames runs 179 vs 212 us.
+template <int IH, int IW, int OH, int OW>
+constexpr bool conv2_fwd_x6_fits() {
+  return Conv2FwdBand<IH, IW, OH, OW>::NB == 1 && Conv2FwdBand<IH, IW, OH, OW>::LDS <= 160 * 1024;
+}
+
+template <int IH, int IW, int OH, int OW>
+__global__ __launch_bounds__(512, 2) void conv2_fwd_x6_kernel(const float* __restrict__ X1,
+                                                              const float* __restrict__ W2,
+                                                              const float* __restrict__ bias,
+                                                              float* __restrict__ X2, int n_frames) {
+  using Bd = Conv2FwdBand<IH, IW, OH, OW>;
+  constexpr int BR = Bd::BR, NB = Bd::NB, WH = Bd::WH, PSX = Bd::PSX, RSP = Bd::RSP;
+  constexpr int BRI = Bd::rows_of(BR), TP = Bd::tiles_of(BR) * 16;  // staged rows, padded band pixels
+  constexpr int PL = BRI * RSP;                                        // plane size (bf16)
+  constexpr int NP = OH * OW;
+  constexpr int NV = (BRI * IW * 8 + 511) / 512;                       // prefetched f4 per thread
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem_c2[];
+  uint16_t* xs = reinterpret_cast<uint16_t*>(smem_c2);
+  float* part = reinterpret_cast<float*>(smem_c2 + (size_t)3 * PL * 2);  // [4][TP][32]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ky = wave & 3, ph = wave >> 2;
+  const int i16 = lane & 15, q = lane >> 4;
+  bf16x8_t wf[4][2][3];  // [kx][co tile][term]: A[co = nt*16 + i16][k = ci 8q .. 8q+7]
+#pragma unroll
+  for (int kx = 0; kx < 4; ++kx)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      union { uint16_t u[8]; bf16x8_t v; } t0, t1, t2;
+      const float* wp = W2 + (nt * 16 + i16) * 512 + (ky * 4 + kx) * 32 + 8 * q;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) split3_bf16(wp[j], t0.u[j], t1.u[j], t2.u[j]);
+      wf[kx][nt][0] = t0.v;
+      wf[kx][nt][1] = t1.v;
+      wf[kx][nt][2] = t2.v;
+    }
+  const int n_items = n_frames * NB;
+  auto band_f4 = [&](int band) { return min(BRI, IH - 2 * BR * band) * IW * 8; };
+  f4 pre[NV];
+  auto load_item = [&](int it) {
+    const int f = it / NB, band = it - (it / NB) * NB;
+    const f4* s4 = reinterpret_cast<const f4*>(X1 + ((int64_t)f * IH + 2 * BR * band) * IW * 32);
+    const int nv = band_f4(band);
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int i = tid + j * 512;
+      if (i < nv) pre[j] = s4[i];
+    }
+  };
+  if ((int)blockIdx.x < n_items) load_item(blockIdx.x);
+  for (int it = blockIdx.x; it < n_items; it += gridDim.x) {
+    const int f = it / NB, band = it - (it / NB) * NB;
+    const int oy0 = BR * band, nr = min(BR, OH - oy0), npb = nr * OW;
+    {  // split the band's X1 rows into the three planes
+      const int nv = band_f4(band);
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        const int i = tid + j * 512;
+        if (i < nv) {
+          const int c4 = i & 7, px = i >> 3, y = px / IW, x = px - (px / IW) * IW;
+          uint2 t0, t1, t2;
+          split3_pack(pre[j], t0, t1, t2);
+          uint16_t* d = xs + y * RSP + ((x & 1) * WH + (x >> 1)) * PSX + 4 * c4;
+          *reinterpret_cast<uint2*>(d) = t0;
+          *reinterpret_cast<uint2*>(d + PL) = t1;
+          *reinterpret_cast<uint2*>(d + 2 * PL) = t2;
+        }
+      }
+    }
+    __syncthreads();
+    if (it + (int)gridDim.x < n_items) load_item(it + gridDim.x);
+    const int tiles = (npb + 15) / 16;
+    for (int t = ph; t < tiles; t += 2) {
+      const int p = min(t * 16 + i16, npb - 1);  // this lane's band pixel (B column)
+      const int oy = p / OW, ox = p - (p / OW) * OW;
+      const uint16_t* xb = xs + (2 * oy + ky) * RSP + ox * PSX + 8 * q;
+      f4 acc[2] = {f4zero(), f4zero()};
+#pragma unroll
+      for (int kx = 0; kx < 4; ++kx) {
+        const uint16_t* xp = xb + ((kx & 1) * WH + (kx >> 1)) * PSX;
+        bf16x8_t b[3];
+#pragma unroll
+        for (int tm = 0; tm < 3; ++tm) b[tm] = *reinterpret_cast<const bf16x8_t*>(xp + tm * PL);
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {  // small terms first
+          f4 c = acc[nt];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[kx][nt][2], b[0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[kx][nt][0], b[2], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[kx][nt][1], b[1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[kx][nt][1], b[0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[kx][nt][0], b[1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[kx][nt][0], b[0], c, 0, 0, 0);
+          acc[nt] = c;
+        }
+      }
+      // lane (pixel i16, q) holds co nt*16 + 4q .. +3 of its pixel
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+        *reinterpret_cast<f4*>(part + ((ky * TP + t * 16 + i16) * 32 + nt * 16 + 4 * q)) = acc[nt];
+    }
+    __syncthreads();
+    const int64_t out0 = ((int64_t)f * NP + oy0 * OW) * 32;
+    for (int i = tid; i < npb * 8; i += 512) {  // (pixel, co quad): fixed-order sum of the 4 rows
+      const int p = i >> 3, c4 = i & 7;
+      const f4* pp = reinterpret_cast<const f4*>(part) + p * 8 + c4;
+      f4 v = ((pp[0] + pp[TP * 8]) + pp[2 * TP * 8]) + pp[3 * TP * 8];
+      const f4 b4 = *reinterpret_cast<const f4*>(bias + 4 * c4);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r] + b4[r], 0.0f);
+      *reinterpret_cast<f4*>(X2 + out0 + (int64_t)i * 4) = v;
+    }
+  }
+}
+
 // Deterministic column sums of a [rows][32] matrix: per-block partials, then one block.
 __global__ __launch_bounds__(256) void colsum32_partial_kernel(const float* __restrict__ A, int64_t rows,
                                                                float* __restrict__ partial) {

@@ -627,8 +627,19 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
     EpiBiasAct ep{a.X[0], 32, P + L.l[0].b, 1};
     launch_gemm_x6<128, 32, 32, 4, 1>(fa, fb, ep, fa.M, 32, 148, st);
   }
-  // conv2 (X1 -> X2)
-  {
+  // conv2 (X1 -> X2): X1 bands split once into LDS planes (conv2_fwd_x6_kernel)
+  if constexpr (conv2_fwd_x6_fits<G::OH1, G::OW1, G::OH2, G::OW2>()) {
+    using Bd = Conv2FwdBand<G::OH1, G::OW1, G::OH2, G::OW2>;
+    const void* kfn = (const void*)conv2_fwd_x6_kernel<G::OH1, G::OW1, G::OH2, G::OW2>;
+    static bool attr = false;  // > 64 KiB of dynamic LDS needs the opt-in attribute
+    if (!attr) {
+      VN_HIP(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)Bd::LDS));
+      attr = true;
+    }
+    const int blocks = std::min(frames * Bd::NB, resident_blocks(kfn, 512, Bd::LDS));
+    hipLaunchKernelGGL((conv2_fwd_x6_kernel<G::OH1, G::OW1, G::OH2, G::OW2>), dim3(blocks), dim3(512), Bd::LDS, st,
+                       a.X[0], P + L.l[1].w, P + L.l[1].b, a.X[1], frames);
+  } else {
     NhwcIm2col<32, 4, 4, 2, G::OH1, G::OW1, G::OH2, G::OW2, 1> fa{a.X[0], 2 * n * G::OH2 * G::OW2};
     DenseRows fb{P + L.l[1].w, 512, 32};
     EpiBiasAct ep{a.X[1], 32, P + L.l[1].b, 1};
