@@ -174,6 +174,59 @@ __global__ __launch_bounds__(256) void rmsprop_kernel(float* __restrict__ params
   }
 }
 
+// Per-env-step bookkeeping of the rollout, one workgroup: the next step's recurrent inputs
+// (last action / last reward of UnrealEnvBaseWrapper, models/goal.py:63-64, and the episode
+// mask m = 1 - done) and the finished-episode statistics of deep_rl's RewardCollector
+// (experiments/thor_cached_auxiliary.py:59-64: count, return sum, length sum) summed in a
+// fixed order — replaces ~20 small framework kernels per step.
+constexpr int kPostThreads = 1024;
+__global__ __launch_bounds__(kPostThreads) void step_post_kernel(const int32_t* __restrict__ actions,
+                                                                 const float* __restrict__ rewards,
+                                                                 const uint8_t* __restrict__ dones,
+                                                                 const float* __restrict__ ep_return,
+                                                                 const int32_t* __restrict__ ep_length, int E, int A,
+                                                                 int64_t* prev_action, float* prev_reward,
+                                                                 float* prev_mask, float* lra, float* mask_out,
+                                                                 float* stats3) {
+  float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f;
+  for (int e = threadIdx.x; e < E; e += kPostThreads) {
+    const bool d = dones[e] != 0;
+    const int a = actions[e];
+    const float r = rewards[e], m = d ? 0.0f : 1.0f;
+    if (prev_action) prev_action[e] = a;
+    if (prev_reward) prev_reward[e] = r;
+    if (prev_mask) prev_mask[e] = m;
+    if (mask_out) mask_out[e] = m;
+    if (lra) {
+      for (int j = 0; j < A; ++j) lra[(int64_t)e * (A + 1) + j] = j == a ? m : 0.0f;
+      lra[(int64_t)e * (A + 1) + A] = r * m;
+    }
+    if (d) {
+      s0 += 1.0f;
+      s1 += ep_return[e];
+      s2 += (float)ep_length[e];
+    }
+  }
+  __shared__ float red[3][kPostThreads / 64];
+  for (int o = 32; o > 0; o >>= 1) {
+    s0 += __shfl_xor(s0, o);
+    s1 += __shfl_xor(s1, o);
+    s2 += __shfl_xor(s2, o);
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[0][w] = s0;
+    red[1][w] = s1;
+    red[2][w] = s2;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    float t = 0.0f;
+    for (int i = 0; i < kPostThreads / 64; ++i) t += red[threadIdx.x][i];
+    stats3[threadIdx.x] += t;
+  }
+}
+
 }  // namespace vn
 
 using namespace vn;
@@ -237,6 +290,18 @@ int vn_rmsprop_step(float* params, const float* grads, float* square_avg, int64_
   const int blocks = (int)std::min<int64_t>((n + 255) / 256, 2048);
   hipLaunchKernelGGL(rmsprop_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, params, grads, square_avg, n,
                      scale, scalars2, lr, alpha, eps);
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
+
+int vn_a2c_step_post(const int32_t* actions, const float* rewards, const uint8_t* dones, const float* ep_return,
+                     const int32_t* ep_length, int E, int num_actions, int64_t* prev_action, float* prev_reward,
+                     float* prev_mask, float* lra_next, float* mask_next, float* episode_stats3, vn_stream_t stream) {
+  if (!actions || !rewards || !dones || !ep_return || !ep_length || !episode_stats3 || E <= 0 || num_actions < 1)
+    return fail(VN_EINVAL, "vn_a2c_step_post: bad args");
+  hipLaunchKernelGGL(step_post_kernel, dim3(1), dim3(kPostThreads), 0, (hipStream_t)stream, actions, rewards, dones,
+                     ep_return, ep_length, E, num_actions, prev_action, prev_reward, prev_mask, lra_next, mask_next,
+                     episode_stats3);
   VN_HIP(hipGetLastError());
   return VN_OK;
 }

@@ -110,6 +110,8 @@ SIGNATURES.update({
     "vn_a2c_loss_grad": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int,
                                         c_float, c_float, c_void_p, c_void_p,
                                         c_void_p]),
+    "vn_a2c_step_post": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                                 c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "vn_grad_norm": (c_int, [c_void_p, c_int64, c_float, c_float, c_void_p,
                                     c_void_p, c_void_p]),
     "vn_rmsprop_step": (c_int, [c_void_p, c_void_p, c_void_p, c_int64,

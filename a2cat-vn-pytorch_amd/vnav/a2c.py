@@ -162,8 +162,9 @@ class A2CTrainer:
             net.forward(self.params, frames, E, self.acts, N, t * E, self.out[sl])
             return
         net.forward(self.params, frames, E, self.acts, N, t * E, None)
-        self.masks[t].copy_(self.prev_mask)
-        self._last_reward_action(self.lra[t], self.masks[t])
+        if t == 0:  # later steps' inputs were written by vn_a2c_step_post after the previous env step
+            self.masks[0].copy_(self.prev_mask)
+            self._last_reward_action(self.lra[0], self.masks[0])
         hp = self.h0 if t == 0 else self.h_all[(t - 1) * E:t * E]
         cp = self.c0 if t == 0 else self.c_all[(t - 1) * E:t * E]
         net.lstm_step(self.params, E, net.x5(self.acts, N)[sl], self.lra[t], self.masks[t], hp, cp, self.xcat[sl],
@@ -177,8 +178,6 @@ class A2CTrainer:
             return
         T = self.num_steps
         net.forward(self.params, frames, E, self.boot_acts, E, 0, None)
-        self.boot_mask.copy_(self.prev_mask)
-        self._last_reward_action(self.boot_lra, self.boot_mask)
         last = slice((T - 1) * E, T * E)
         net.lstm_step(self.params, E, net.x5(self.boot_acts, E), self.boot_lra, self.boot_mask, self.h_all[last],
                       self.c_all[last], self.boot_xcat, self.gates, self.boot_la, self.boot_c, self.boot_h)
@@ -201,14 +200,17 @@ class A2CTrainer:
                                             self._stream()), "vn_policy_sample")
             env.step(self.actions[sl], out=dict(reward=self.rewards[t], done=self.dones[t], state=self.states),
                      gather=False)
-            d = self.dones[t].to(torch.float32)
-            if self.recurrent:
-                self.prev_action.copy_(self.actions[sl])
-                self.prev_reward.copy_(self.rewards[t])
-                torch.sub(1.0, d, out=self.prev_mask)
-            self.episode_stats[0] += d.sum()
-            self.episode_stats[1] += (info["ep_return"] * d).sum()
-            self.episode_stats[2] += (info["ep_length"].to(torch.float32) * d).sum()
+            # next step's (last action, last reward) * mask and mask (bootstrap slots after the
+            # last step), the prev_* carries, and the finished-episode statistics: one kernel
+            rec = self.recurrent
+            lra_n = (self.lra[t + 1] if t + 1 < T else self.boot_lra) if rec else None
+            mask_n = (self.masks[t + 1] if t + 1 < T else self.boot_mask) if rec else None
+            _lib.check(lib.vn_a2c_step_post(
+                _lib.ptr(self.actions[sl]), _lib.ptr(self.rewards[t]), _lib.ptr(self.dones[t]),
+                _lib.ptr(info["ep_return"]), _lib.ptr(info["ep_length"]), E, A,
+                _lib.ptr(self.prev_action) if rec else None, _lib.ptr(self.prev_reward) if rec else None,
+                _lib.ptr(self.prev_mask) if rec else None, _lib.ptr(lra_n), _lib.ptr(mask_n),
+                _lib.ptr(self.episode_stats), self._stream()), "vn_a2c_step_post")
         # bootstrap value of the final observation
         self._bootstrap(self._frames(info["img_row"], info["goal_row"]))
 

@@ -290,6 +290,17 @@ int vn_a2c_returns(const float* rewards, const uint8_t* dones, const float* boot
 int vn_a2c_loss_grad(const float* out, const int32_t* actions, const float* returns, int n,
                      int num_actions, float value_coef, float entropy_coef, float* dout,
                      float* stats4, vn_stream_t stream);
+/* Rollout bookkeeping after env step t (one launch): the next step's recurrent inputs —
+ * last action one-hot and last reward times the episode mask m = 1 - done, and m itself
+ * (UnrealEnvBaseWrapper's extra input, models/goal.py:63-64; mask rule of MaskedRNN,
+ * unpinned) into lra_next [E][A+1] / mask_next [E] — prev_* carries, and the finished
+ * episodes' (count, return sum, length sum) added to episode_stats3 in a fixed order
+ * (deep_rl RewardCollector, experiments/thor_cached_auxiliary.py:59-64). Pointers other
+ * than the inputs and episode_stats3 may be NULL. */
+int vn_a2c_step_post(const int32_t* actions, const float* rewards, const uint8_t* dones,
+                     const float* ep_return, const int32_t* ep_length, int E, int num_actions,
+                     int64_t* prev_action, float* prev_reward, float* prev_mask, float* lra_next,
+                     float* mask_next, float* episode_stats3, vn_stream_t stream);
 /* scalars2 = (total norm of scale*grads, clip coefficient) computed on the device. */
 int vn_grad_norm(const float* grads, int64_t n, float scale, float max_norm, double* partial_512,
                  float* scalars2, vn_stream_t stream);
