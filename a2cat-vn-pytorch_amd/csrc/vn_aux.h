@@ -171,4 +171,171 @@ __global__ __launch_bounds__(256) void aux_loss_grad_kernel(int n, int PH, int P
   }
 }
 
+// Second head layer (48 -> 8 transposed conv, k4 s2, block-diagonal weights) as a direct
+// kernel, optionally fused with the loss: SPI samples' A1 maps are staged in LDS (pixel
+// stride 52 floats: 16 consecutive pixels on distinct bank quads, one zero pixel for the
+// taps outside the map); every wave works on one parity class at a time so the weights of
+// its taps are wave-uniform (scalar loads); a thread computes the 7 real outputs of one
+// pixel from the 2x2 taps that reach it (4 x (16 + 48 + 48) = 448 FMAs, only the head's
+// own 16 input channels per output — the GEMM form multiplied the 2/3 structural zeros and
+// padded N = 8 to 16). !LOSS: writes pred [n][PH][PW][8]. LOSS: the per-head MSE gradient
+// against the target table goes straight to dpred (pred is never written) and the squared
+// errors to stats[0..2] (aux_loss_grad_kernel's contract).
+constexpr int kAux2Threads = 512;
+constexpr int kAux2Pst = 52;
+
+template <int AH, int AW>
+constexpr int aux2_spi() {
+  constexpr int per = (AH * AW + 1) * kAux2Pst * 4;
+  return per * 2 <= 96 * 1024 ? (96 * 1024 / per < 8 ? 96 * 1024 / per : 8) : 1;
+}
+constexpr int kAux2Wfl = 4 * 4 * kAuxC1 * kAuxC2;  // weights [class][tap][ci][8] in LDS
+template <int AH, int AW>
+constexpr size_t aux2_lds() {
+  return (size_t)aux2_spi<AH, AW>() * (AH * AW + 1) * kAux2Pst * 4 + kAux2Wfl * 4;
+}
+template <int AH, int AW>
+constexpr bool aux2_fits() {
+  return aux2_lds<AH, AW>() <= 160 * 1024;
+}
+
+template <int AH, int AW, int PH, int PW, bool LOSS>
+__global__ __launch_bounds__(kAux2Threads) void aux_deconv2_kernel(const float* __restrict__ A1, int n,
+                                                                    const float* __restrict__ W2,
+                                                                    const float* __restrict__ b2,
+                                                                    float* __restrict__ pred,
+                                                                    const f4* __restrict__ table,
+                                                                    const int32_t* __restrict__ img_rows,
+                                                                    const int32_t* __restrict__ goal_rows,
+                                                                    float weight, float* __restrict__ dpred,
+                                                                    float* __restrict__ stats) {
+  constexpr int SPI = aux2_spi<AH, AW>();
+  constexpr int NPX = AH * AW, SST = (NPX + 1) * kAux2Pst;  // pixels, per-sample LDS stride
+  constexpr int HYC = PH / 2, WXC = PW / 2, NPC = HYC * WXC;
+  static_assert(PH == 2 * AH + 2 && PW == 2 * AW + 2, "k4 s2 transposed conv geometry");
+  extern __shared__ __attribute__((aligned(16))) float as_aux[];
+  float* ws_aux = as_aux + SPI * SST;  // [cls][tap = 2a + b][ci][8]
+  const int tid = threadIdx.x;
+  for (int i = tid; i < SPI * 48; i += kAux2Threads) as_aux[(i / 48) * SST + NPX * kAux2Pst + i % 48] = 0.0f;
+  for (int i = tid; i < kAux2Wfl; i += kAux2Threads) {
+    const int c = i & 7, ci = (i >> 3) % kAuxC1, tap = (i / (8 * kAuxC1)) & 3, cls = i / (32 * kAuxC1);
+    const int ky = (cls >> 1) + 2 * (tap >> 1), kx = (cls & 1) + 2 * (tap & 1);
+    ws_aux[i] = W2[(ci * 4 + ky) * 32 + kx * 8 + c];
+  }
+  float bias[7];
+#pragma unroll
+  for (int c = 0; c < 7; ++c) bias[c] = b2[c];
+  const float inv[3] = {2.0f * weight / ((float)n * PH * PW), 2.0f * weight / (3.0f * n * PH * PW),
+                        2.0f * weight / (3.0f * n * PH * PW)};
+  float sq[3] = {0.0f, 0.0f, 0.0f};
+  // the next item's A1 maps are loaded into registers while this one computes
+  constexpr int NV = (SPI * NPX * 12 + kAux2Threads - 1) / kAux2Threads;
+  f4 pre[NV];
+  auto load_item = [&](int s0) {
+    const int nv = min(SPI, n - s0) * NPX * 12;
+    const f4* src = reinterpret_cast<const f4*>(A1 + (int64_t)s0 * NPX * 48);
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int i = tid + j * kAux2Threads;
+      if (i < nv) pre[j] = src[i];
+    }
+  };
+  if ((int)blockIdx.x * SPI < n) load_item(blockIdx.x * SPI);
+  for (int s0 = blockIdx.x * SPI; s0 < n; s0 += gridDim.x * SPI) {
+    const int ns = min(SPI, n - s0);
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int i = tid + j * kAux2Threads;
+      if (i < ns * NPX * 12) {
+        const int sp = i / (NPX * 12), r = i - sp * (NPX * 12), px = r / 12, c4 = r - (r / 12) * 12;
+        *reinterpret_cast<f4*>(as_aux + sp * SST + px * kAux2Pst + 4 * c4) = pre[j];
+      }
+    }
+    __syncthreads();
+    if (s0 + (int)gridDim.x * SPI < n) load_item(s0 + gridDim.x * SPI);
+    for (int cls = 0; cls < 4; ++cls) {  // wave-uniform parity class -> broadcast weight reads
+      const int py = cls >> 1, px = cls & 1;
+      for (int q = tid; q < ns * NPC; q += kAux2Threads) {
+        const int sp = q / NPC, p = q - sp * NPC, yy = p / WXC, xx = p - (p / WXC) * WXC;
+        const int Y = 2 * yy + py, X = 2 * xx + px, s = s0 + sp;
+        f4 ti, tg;  // targets issued before the products
+        if constexpr (LOSS) {
+          ti = table[(int64_t)img_rows[s] * PH * PW + Y * PW + X];
+          tg = table[(int64_t)goal_rows[s] * PH * PW + Y * PW + X];
+        }
+        float o[7];
+#pragma unroll
+        for (int c = 0; c < 7; ++c) o[c] = bias[c];
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int b = 0; b < 2; ++b) {
+            const int iy = yy - a, ix = xx - b;
+            const bool ok = iy >= 0 && iy < AH && ix >= 0 && ix < AW;
+            const float* ap = as_aux + sp * SST + (ok ? iy * AW + ix : NPX) * kAux2Pst;
+            const float* wp = ws_aux + ((cls * 4 + 2 * a + b) * kAuxC1) * 8;
+#pragma unroll
+            for (int hd = 0; hd < 3; ++hd)  // head hd reads input channels 16hd .. 16hd + 15
+#pragma unroll 2
+              for (int kq = 0; kq < 4; ++kq) {
+                const int k = 4 * hd + kq;
+                const f4 av = *reinterpret_cast<const f4*>(ap + 4 * k);
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                  const f4 wv = reinterpret_cast<const f4*>(wp + (4 * k + jj) * 8)[hd < 2 ? 0 : 1];
+                  if (hd == 0) {
+                    o[0] = fmaf(av[jj], wv[0], o[0]);
+                  } else if (hd == 1) {
+                    o[1] = fmaf(av[jj], wv[1], o[1]);
+                    o[2] = fmaf(av[jj], wv[2], o[2]);
+                    o[3] = fmaf(av[jj], wv[3], o[3]);
+                  } else {
+                    o[4] = fmaf(av[jj], wv[0], o[4]);
+                    o[5] = fmaf(av[jj], wv[1], o[5]);
+                    o[6] = fmaf(av[jj], wv[2], o[6]);
+                  }
+                }
+              }
+          }
+        const int64_t pix = (int64_t)s * PH * PW + Y * PW + X;
+        if constexpr (!LOSS) {
+          *reinterpret_cast<f4*>(pred + pix * kAuxC2) = f4{o[0], o[1], o[2], o[3]};
+          *reinterpret_cast<f4*>(pred + pix * kAuxC2 + 4) = f4{o[4], o[5], o[6], 0.0f};
+        } else {
+          const float t[7] = {ti[0], ti[1], ti[2], ti[3], tg[1], tg[2], tg[3]};
+          float g[8];
+#pragma unroll
+          for (int c = 0; c < 7; ++c) {
+            const float d = o[c] - t[c];
+            const int h = c == 0 ? 0 : (c <= 3 ? 1 : 2);
+            sq[h] += d * d;
+            g[c] = d * inv[h];
+          }
+          g[7] = 0.0f;
+          *reinterpret_cast<f4*>(dpred + pix * kAuxC2) = f4{g[0], g[1], g[2], g[3]};
+          *reinterpret_cast<f4*>(dpred + pix * kAuxC2 + 4) = f4{g[4], g[5], g[6], g[7]};
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if constexpr (LOSS) {  // per-workgroup statistics (the staging area is free after the last barrier)
+    float* red = as_aux;   // [3][waves]
+    constexpr int NWV = kAux2Threads / 64;
+    const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+    for (int h = 0; h < 3; ++h) {
+      float v = sq[h];
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+      if (lane == 0) red[h * NWV + wave] = v;
+    }
+    __syncthreads();
+    if (tid < 3) {
+      float v = 0.0f;
+      for (int w = 0; w < NWV; ++w) v += red[tid * NWV + w];
+      if (v != 0.0f) atomicAdd(stats + tid, v);
+    }
+  }
+}
+
 }  // namespace vn

@@ -1169,6 +1169,23 @@ inline void colsum(const float* src, int64_t rows, int cols, float* partial, flo
   hipLaunchKernelGGL(colsum_final_kernel, dim3(1), dim3(64), 0, st, partial, blocks, cols, out);
 }
 
+template <int AH, int AW, int PH, int PW, bool LOSS>
+inline void launch_aux2(const float* A1, int n, const float* W2, const float* b2, float* pred,
+                        const vn_aux_targets* tg, float weight, float* dpred, float* stats, hipStream_t st) {
+  constexpr size_t lds = aux2_lds<AH, AW>();
+  const void* kfn = (const void*)aux_deconv2_kernel<AH, AW, PH, PW, LOSS>;
+  static bool attr = false;  // > 64 KiB of dynamic LDS needs the opt-in attribute
+  if (!attr) {
+    (void)hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  constexpr int SPI = aux2_spi<AH, AW>();
+  const int blocks = std::min((n + SPI - 1) / SPI, resident_blocks(kfn, kAux2Threads, lds));
+  hipLaunchKernelGGL((aux_deconv2_kernel<AH, AW, PH, PW, LOSS>), dim3(blocks), dim3(kAux2Threads), lds, st, A1, n, W2,
+                     b2, pred, tg ? reinterpret_cast<const f4*>(tg->table) : nullptr, tg ? tg->image_rows : nullptr,
+                     tg ? tg->goal_rows : nullptr, weight, dpred, stats);
+}
+
 template <int H0, int W0>
 int aux_forward_impl(const PolicyLayout& L, const float* P, const float* X4, int n, float* A1, float* Pout,
                      const AuxWork& w, hipStream_t st) {
@@ -1177,7 +1194,34 @@ int aux_forward_impl(const PolicyLayout& L, const float* P, const float* X4, int
   hipLaunchKernelGGL(transpose_kernel, dim3((32 * 768 + 255) / 256), dim3(256), 0, st, P + L.aw1, 32, 768, w.w1t);
   hipLaunchKernelGGL(transpose_kernel, dim3((48 * 128 + 255) / 256), dim3(256), 0, st, P + L.aw2, 48, 128, w.w2t);
   deconv_all<32, kAuxC1, IH, IW, AH, AW>(X4, w.w1t, A1, P + L.ab1, 1, n, st);
-  deconv_all<kAuxC1, kAuxC2, AH, AW, PH, PW>(A1, w.w2t, Pout, P + L.ab2, 0, n, st);
+  if constexpr (aux2_fits<AH, AW>()) {
+    launch_aux2<AH, AW, PH, PW, false>(A1, n, P + L.aw2, P + L.ab2, Pout, nullptr, 0.0f, nullptr, nullptr, st);
+  } else {
+    deconv_all<kAuxC1, kAuxC2, AH, AW, PH, PW>(A1, w.w2t, Pout, P + L.ab2, 0, n, st);
+  }
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
+
+// Forward of both head layers with the loss fused into the second: dpred and stats as
+// vn_aux_loss_grad, the prediction itself is not written (maps whose A1 does not fit the
+// direct kernel's LDS run forward + loss separately into `pred`).
+template <int H0, int W0>
+int aux_forward_loss_impl(const PolicyLayout& L, const float* P, const float* X4, int n, float* A1, float* pred,
+                          const vn_aux_targets* tg, float weight, float* dpred, float* stats, const AuxWork& w,
+                          hipStream_t st) {
+  using G = Geo<H0, W0>;
+  constexpr int IH = G::OH3, IW = G::OW3, AH = 2 * IH + 2, AW = 2 * IW + 2, PH = 2 * AH + 2, PW = 2 * AW + 2;
+  if constexpr (aux2_fits<AH, AW>()) {
+    hipLaunchKernelGGL(transpose_kernel, dim3((32 * 768 + 255) / 256), dim3(256), 0, st, P + L.aw1, 32, 768, w.w1t);
+    deconv_all<32, kAuxC1, IH, IW, AH, AW>(X4, w.w1t, A1, P + L.ab1, 1, n, st);
+    launch_aux2<AH, AW, PH, PW, true>(A1, n, P + L.aw2, P + L.ab2, nullptr, tg, weight, dpred, stats, st);
+  } else {
+    const int rc = aux_forward_impl<H0, W0>(L, P, X4, n, A1, pred, w, st);
+    if (rc != VN_OK) return rc;
+    hipLaunchKernelGGL(aux_loss_grad_kernel, dim3(kAuxLossBlocks), dim3(256), 0, st, n, PH, PW, pred,
+                       reinterpret_cast<const f4*>(tg->table), tg->image_rows, tg->goal_rows, weight, dpred, stats);
+  }
   VN_HIP(hipGetLastError());
   return VN_OK;
 }
@@ -1415,6 +1459,20 @@ int vn_aux_loss_grad(vn_policy* p, const float* pred, int n, const vn_aux_target
                      targets->goal_rows, weight, dpred, stats4);
   VN_HIP(hipGetLastError());
   return VN_OK;
+}
+
+int vn_aux_forward_loss_grad(vn_policy* p, const float* params, float* acts, int64_t act_capacity, int n, float* a1,
+                             float* pred, const vn_aux_targets* targets, float weight, float* dpred, float* stats4,
+                             float* workspace, vn_stream_t stream) {
+  if (!p || !p->L.aux || !params || !acts || !a1 || !pred || !targets || !targets->table || !targets->image_rows ||
+      !targets->goal_rows || !dpred || !stats4 || !workspace || n <= 0 || n > act_capacity)
+    return fail(VN_EINVAL, "vn_aux_forward_loss_grad: bad args");
+  const Acts a = acts_at(p->L, acts, act_capacity, 0);
+  const AuxWork w = aux_carve(p->L, workspace);
+  return dispatch_geo(p->L, [&](auto g) {
+    return aux_forward_loss_impl<decltype(g)::H, decltype(g)::W>(p->L, params, a.X[3], n, a1, pred, targets, weight,
+                                                                  dpred, stats4, w, (hipStream_t)stream);
+  });
 }
 
 int vn_aux_backward(vn_policy* p, const float* params, float* acts, int64_t act_capacity, int n, float* a1,

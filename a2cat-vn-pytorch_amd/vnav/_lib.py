@@ -96,6 +96,8 @@ SIGNATURES.update({
                                c_void_p]),
     "vn_aux_target_table": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int64, c_void_p, c_void_p]),
     "vn_aux_loss_grad": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_float, c_void_p, c_void_p, c_void_p]),
+    "vn_aux_forward_loss_grad": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p,
+                                         c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
     "vn_aux_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p,
                                 c_void_p, c_void_p, c_void_p]),
     "vn_policy_backward_ex": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int64, c_void_p, c_void_p,

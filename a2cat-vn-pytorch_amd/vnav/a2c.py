@@ -228,8 +228,8 @@ class A2CTrainer:
         dx4 = None
         if self.aux_weight > 0:  # deconv heads: forward, loss gradient, backward -> dL/dX4
             self.aux_stats.zero_()
-            net.aux_forward(self.params, self.acts, N, N, self.a1, self.pred, self.aux_ws)
-            net.aux_loss_grad(self.pred, N, self._aux_targets, self.aux_weight, self.dpred, self.aux_stats)
+            net.aux_forward_loss_grad(self.params, self.acts, N, N, self.a1, self.pred, self._aux_targets,
+                                      self.aux_weight, self.dpred, self.aux_stats, self.aux_ws)
             net.aux_backward(self.params, self.acts, N, N, self.a1, self.dpred, self.grads, self.dx4, self.aux_ws)
             dx4 = self.dx4
         frames = self._frames(self.rows_img, self.rows_goal)

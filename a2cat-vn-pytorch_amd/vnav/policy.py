@@ -340,6 +340,15 @@ class PolicyNet:
         _lib.check(self.lib.vn_aux_loss_grad(self._h, P(pred), int(n), ctypes.byref(targets), ctypes.c_float(weight),
                                              P(dpred), P(stats), _lib.stream_ptr(self.device)), "vn_aux_loss_grad")
 
+    def aux_forward_loss_grad(self, params, acts, capacity, n, a1, pred, targets, weight, dpred, stats, workspace):
+        """aux_forward + aux_loss_grad with the loss fused into the second head layer (pred is
+        scratch: written only for maps too large for the fused kernel)."""
+        P = _lib.ptr
+        _lib.check(self.lib.vn_aux_forward_loss_grad(self._h, P(params), P(acts), int(capacity), int(n), P(a1),
+                                                     P(pred), ctypes.byref(targets), ctypes.c_float(weight), P(dpred),
+                                                     P(stats), P(workspace), _lib.stream_ptr(self.device)),
+                   "vn_aux_forward_loss_grad")
+
     def aux_backward(self, params, acts, capacity, n, a1, dpred, grads, dx4, workspace):
         P = _lib.ptr
         _lib.check(self.lib.vn_aux_backward(self._h, P(params), P(acts), int(capacity), int(n), P(a1), P(dpred),

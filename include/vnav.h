@@ -270,6 +270,12 @@ int vn_aux_target_table(vn_policy* p, const uint8_t* depth, const uint8_t* segme
  * goal row's seg targets; stats4[0..2] += per-head sums of squared errors. */
 int vn_aux_loss_grad(vn_policy* p, const float* pred, int n, const vn_aux_targets* targets, float weight,
                      float* dpred, float* stats4, vn_stream_t stream);
+/* vn_aux_forward + vn_aux_loss_grad in one pass: the second head layer computes each
+ * prediction pixel and its loss gradient together (the trainer's path: the prediction is
+ * never stored; pred is scratch, written only for maps too large for the fused kernel). */
+int vn_aux_forward_loss_grad(vn_policy* p, const float* params, float* acts, int64_t act_capacity, int n,
+                             float* a1, float* pred, const vn_aux_targets* targets, float weight,
+                             float* dpred, float* stats4, float* workspace, vn_stream_t stream);
 /* Head gradients into grads and dL/dX4 [n][h3][w3][32] (before conv_base's ReLU mask) into
  * dx4; consumes a1. */
 int vn_aux_backward(vn_policy* p, const float* params, float* acts, int64_t act_capacity, int n, float* a1,

@@ -138,6 +138,48 @@ def test_aux_loss_kernel_vs_oracle():
     _close(stats[:3].cpu().numpy() / numel, np.array([x.item() for x in losses]), 1e-5, "per-head MSE")
 
 
+@pytest.mark.parametrize("hw", [(84, 84), (174, 174)])
+def test_fused_aux_forward_loss_matches_unfused(hw):
+    """The trainer's fused path (second head layer as a direct kernel computing each
+    prediction pixel's loss gradient in place, vn_aux_forward_loss_grad) against the
+    module path (vn_aux_forward: prediction stored, then vn_aux_loss_grad): dpred and the
+    per-head squared-error sums agree to fp32 reassociation; the direct second layer
+    itself is pinned by test_aux_heads_match_reference_174 (module path)."""
+    import vnav
+    from vnav.policy import AuxTargets, GoalNavPolicy
+    frame = hw + (3,)
+    env = vnav.VectorEnv([_aux_scene(0, frame), _aux_scene(1, frame)], 96, seed=3)
+    pol = GoalNavPolicy(3, 4, hw, aux=True)
+    torch.manual_seed(4)
+    with torch.no_grad():
+        pol.params.add_(torch.randn_like(pol.params) * 0.02)
+    net, n = pol.net, 96
+    env.observe(gather=False)
+    rows_i, rows_g = env._info["img_row"].clone(), env._info["goal_row"].clone()
+    from vnav.policy import frames_from_rows
+    arena, fb, _, _ = env.frame_arena()
+    frames = frames_from_rows(arena, fb, rows_i, rows_g)
+    acts = net.new_acts(n)
+    out = torch.zeros((n, 8), device="cuda")
+    net.forward(pol.params.data, frames, n, acts, n, 0, out)
+    depth, seg = env.aux_arena
+    table = net.aux_target_table(depth, seg)
+    tg = AuxTargets(table.data_ptr(), rows_i.data_ptr(), rows_g.data_ptr())
+    ph, pw = net.aux_layout["p_hw"]
+    ah, aw = net.aux_layout["a_hw"]
+    ws = torch.empty(net.aux_workspace_floats(), device="cuda")
+    a1 = torch.empty((n, ah, aw, 48), device="cuda")
+    pred = torch.empty((n, ph, pw, 8), device="cuda")
+    d_ref, d_fused = torch.empty_like(pred), torch.empty_like(pred)
+    s_ref, s_fused = torch.zeros(4, device="cuda"), torch.zeros(4, device="cuda")
+    net.aux_forward(pol.params.data, acts, n, n, a1, pred, ws)
+    net.aux_loss_grad(pred, n, tg, 0.05, d_ref, s_ref)
+    net.aux_forward_loss_grad(pol.params.data, acts, n, n, a1, pred, tg, 0.05, d_fused, s_fused, ws)
+    torch.cuda.synchronize()
+    _close(d_fused.cpu().numpy(), d_ref.cpu().numpy(), 1e-5, "dpred")
+    _close(s_fused[:3].cpu().numpy(), s_ref[:3].cpu().numpy(), 1e-5, "stats")
+
+
 def test_auxiliary_graph_five_tuple_observation():
     """AuxiliaryGraph-v0 (GoalGymGraphAuxiliaryEnv.observe, environments/gym_graph/graph.py:
     115-120): (rgb, goal rgb, depth, segmentation, goal segmentation) by state / goal row."""
