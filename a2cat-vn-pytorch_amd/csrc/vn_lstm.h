@@ -6,8 +6,9 @@
 // PyTorch gate order (i, f, g, o); c_t = f (c_{t-1} m_t) + i g, h_t = o tanh(c_t).
 // m_t = 0 where an episode starts at t (the MaskedRNN reset; its exact deep_rl semantics
 // are not in the reference tree: parity unpinned). BPTT runs inside one rollout
-// (states entering the rollout are constants); the weight gradient of all T steps is one
-// split-K GEMM over T*E rows of [dgates | xcat].
+// (states entering the rollout are constants). Only dh_{t-1} = m_t (dgates_t x W_hh) is
+// sequential; the trunk's input gradient of all T steps (dgates x W_ih, features part) and
+// the weight gradient (one split-K GEMM over T*E rows of [dgates | xcat]) run after the loop.
 #pragma once
 
 namespace vn {
@@ -76,21 +77,12 @@ __global__ void lstm_cell_bwd_kernel(int n, const float* __restrict__ dh_heads, 
   dc_prev_out[idx] = dc * f * m;
 }
 
-// Epilogue of the per-step dgrad product dxcat = dgates x W_cat: feature columns feed the
-// trunk (masked by conv_merge's ReLU), h columns become the previous step's dh (times m_t).
-struct EpiLstmDx {
-  float* dz5;
-  const float* x5;
+// Epilogue of the per-step recurrent product dh_{t-1} = m_t (dgates_t x W_hh).
+struct EpiLstmDh {
   float* dh_prev;
   const float* mask;
-  int xoff;
   __device__ __forceinline__ void operator()(int row, int col, float v, int) const {
-    if (col < 512) {
-      const int64_t i = (int64_t)row * 512 + col;
-      dz5[i] = x5[i] > 0.0f ? v : 0.0f;
-    } else if (col >= xoff) {
-      dh_prev[(int64_t)row * 512 + (col - xoff)] = v * (mask ? mask[row] : 1.0f);
-    }
+    dh_prev[(int64_t)row * 512 + col] = v * (mask ? mask[row] : 1.0f);
   }
 };
 

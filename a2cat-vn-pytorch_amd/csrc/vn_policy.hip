@@ -1089,10 +1089,17 @@ inline int lstm_backward(const PolicyLayout& L, const float* P, int T, int E, co
     hipLaunchKernelGGL(lstm_cell_bwd_kernel, dim3(cb), dim3(256), 0, st, E, w.dh_heads + (int64_t)t * e512,
                        last ? nullptr : w.dh[cur ^ 1], last ? nullptr : w.dc[cur ^ 1], acts_all + (int64_t)t * E * 2048,
                        c_all + (int64_t)t * e512, cprev, mask, dg, w.dc[cur]);
+    // only the recurrent part is sequential: dh_{t-1} = m_t (dgates_t x W_hh)
     DenseRows fa{dg, 2048, E};
-    DenseRows fb{w.wcat_t, 2048, L.xcat};
-    EpiLstmDx ep{dz5 + (int64_t)t * e512, x5_all + (int64_t)t * e512, w.dh[cur], mask, L.xoff};
-    launch_gemm_x6<64, 64, 32, 2, 2>(fa, fb, ep, E, L.xcat, 2048, st);
+    DenseRows fb{w.wcat_t + (int64_t)L.xoff * 2048, 2048, 512};
+    EpiLstmDh ep{w.dh[cur], mask};
+    launch_gemm_x6<64, 64, 32, 2, 2>(fa, fb, ep, E, 512, 2048, st);
+  }
+  {  // the trunk's input gradient of all T steps in one product: dz5 = relu'(x5) (dgates x W_ih[:, :512])
+    DenseRows fa{w.dgates, 2048, N};
+    DenseRows fb{w.wcat_t, 2048, 512};
+    EpiMask ep{dz5, x5_all, 512};
+    launch_gemm_x6<128, 128, 32, 2, 2>(fa, fb, ep, N, 512, 2048, st);
   }
   {  // dW_cat = dgates^T x xcat over all T*E rows (x6 core on transposed copies, k = rows
      // contiguous); b_ih and b_hh share the bias gradient
