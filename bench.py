@@ -107,6 +107,54 @@ def pmc_traffic(envs, scenes):
                                        "source": "live rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes"}
 
 
+def pmc_train_mfma(envs, scenes):
+    """Measured matrix-core utilisation of one 84x84 LSTM training update (rollout + update):
+    a rocprofv3 --pmc pass (SQ_VALU_MFMA_BUSY_CYCLES summed over the SIMDs, GRBM_GUI_ACTIVE
+    summed over the 8 XCDs; no tracing) over a child bench run. Busy fraction =
+    sum(MFMA busy) / (SIMDs x sum(GRBM) / 8) over every dispatch of the run. The split-bf16
+    products issue 3-6 bf16 MFMAs per fp32 product, so this is pipe occupancy, not the
+    algorithmic fraction reported next to it."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    if shutil.which("rocprofv3") is None:
+        return None
+    d = tempfile.mkdtemp(prefix="vnav_pmc_mfma_", dir="/tmp")
+    cmd = ["rocprofv3", "--pmc", "SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE", "--output-format", "csv", "-d", d,
+           "-o", "run", "--", sys.executable, os.path.abspath(__file__), "--steps", "2", "--warmup", "1",
+           "--no-cpu-baseline", "--no-pmc", "--no-train-ff", "--no-train-ref", "--train-steps", "1",
+           "--train-warmup", "0", "--envs", str(envs), "--scenes", str(scenes)]
+    env = dict(os.environ, TMPDIR="/tmp")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    try:
+        r = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                           timeout=300)
+    except Exception:
+        return None
+    if r.returncode != 0:
+        return None
+    mfma = grbm = 0.0
+    disp = set()
+    for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                name = row.get("Kernel_Name", "")
+                if "env_kernel" in name or "random_actions" in name or "synth_frames" in name:
+                    continue  # the env-only warmup steps and scene synthesis of the child run
+                disp.add(row["Dispatch_Id"])
+                if row["Counter_Name"] == "SQ_VALU_MFMA_BUSY_CYCLES":
+                    mfma += float(row["Counter_Value"])
+                elif row["Counter_Name"] == "GRBM_GUI_ACTIVE":
+                    grbm += float(row["Counter_Value"])
+    if grbm <= 0:
+        return None
+    return {"mfma_busy_cycles": mfma, "grbm_gui_active": grbm, "dispatches": len(disp),
+            "source": "live rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE, one LSTM update"}
+
+
 def aux_flops_per_sample(o3):
     """Algorithmic FLOPs of the deconv heads per sample (forward + both gradients): first
     layer 32 -> 3x16 over 2x2 taps per output pixel, second layer 16 -> (1, 3, 3) per head."""
@@ -254,8 +302,11 @@ def main():
         workers = max(1, min(16, len(os.sched_getaffinity(0))))
         cpu = cpu_baseline(scenes, args.cpu_seconds, workers)
     traffic, traffic_info = None, None
+    mfma_pmc = None
     if rank == 0 and world == 1 and not args.no_pmc:  # child rocprofv3 runs, before this process touches the GPU
         traffic, traffic_info = pmc_traffic(args.envs, args.scenes)
+        if args.train_steps > 0 and not args.no_train_84:
+            mfma_pmc = pmc_train_mfma(args.envs, args.scenes)
 
     ndev = torch.cuda.device_count()
     dev = torch.device("cuda", local % max(ndev, 1))
@@ -331,6 +382,11 @@ def main():
                                    model="AuxiliaryBigGoalHouseModel (LSTM + deconv heads), 300x400 (config C5)")
             torch.cuda.empty_cache()
     if rank == 0:
+        if train is not None and mfma_pmc is not None:
+            simds = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
+            mfma_pmc["simds"] = simds
+            mfma_pmc["busy_frac"] = mfma_pmc["mfma_busy_cycles"] / (simds * mfma_pmc["grbm_gui_active"] / 8.0)
+            train["roofline"]["mfma_busy_measured"] = mfma_pmc
         env_steps = E * K * world
         value = env_steps / elapsed
         bpe = alg_bytes_per_env_step(fb)
