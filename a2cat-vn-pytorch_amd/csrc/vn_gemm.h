@@ -207,11 +207,44 @@ __device__ __forceinline__ void commit_rows_x6(const f4* r, uint16_t* s, int tid
   }
 }
 
+// Transposing source (wgrad: both operands gathered along the reduction index, fetch_trans
+// slots): the 4 rows of slot i at k = kk are split and written as 16-bit elements of the
+// three k-contiguous planes the MFMA loop reads.
+template <int ROWS, int BK, int LDK>
+__device__ __forceinline__ void commit_trans_x6(const f4* r, uint16_t* s, int tid) {
+  constexpr int R4 = ROWS / 4, T = R4 * BK, NS = (T + 255) / 256, PLANE = ROWS * LDK;
+#pragma unroll
+  for (int j = 0; j < NS; ++j) {
+    const int i = tid + j * 256;
+    if (T % 256 == 0 || i < T) {
+      const int kk = (i >> 1) % BK, rq = (i & 1) + 2 * (i / (2 * BK));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float r1, r2, r3;
+        const uint32_t t0 = bf16_split_bits(r[j][e], r1);
+        const uint32_t t1 = bf16_split_bits(r1, r2);
+        const uint32_t t2 = bf16_split_bits(r2, r3);
+        uint16_t* d = s + (4 * rq + e) * LDK + kk;
+        d[0] = (uint16_t)t0;
+        d[PLANE] = (uint16_t)t1;
+        d[2 * PLANE] = (uint16_t)t2;
+      }
+    }
+  }
+}
+
+template <int ROWS, int BK, int LDK, class L>
+__device__ __forceinline__ void commit_x6(const f4* r, uint16_t* s, int tid) {
+  if constexpr (L::kTrans)
+    commit_trans_x6<ROWS, BK, LDK>(r, s, tid);
+  else
+    commit_rows_x6<ROWS, BK, LDK>(r, s, tid);
+}
+
 template <int BM, int BN, int BK, int WM, int WN, class FA, class FB, class EP>
 __global__ __launch_bounds__(256) void gemm_x6_kernel(FA fa, FB fb, EP ep, int M, int N, int K, int kchunk) {
   static_assert(WM * WN == 4, "4 waves per workgroup");
   static_assert(BK % 16 == 0, "BK multiple of 16");
-  static_assert(!FA::kTrans && !FB::kTrans, "row-fill loaders only");
   constexpr int LDK = BK + 8;
   constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
   static_assert(TM >= 1 && TN >= 1, "tile too small for the wave layout");
@@ -240,8 +273,8 @@ __global__ __launch_bounds__(256) void gemm_x6_kernel(FA fa, FB fb, EP ep, int M
     fb.template fetch<BN, BK>(pb, n0, kb, ke, tid);
   }
   for (int k0 = kb; k0 < ke; k0 += BK) {
-    commit_rows_x6<BM, BK, LDK>(pa, As, tid);
-    commit_rows_x6<BN, BK, LDK>(pb, Bs, tid);
+    commit_x6<BM, BK, LDK, FA>(pa, As, tid);
+    commit_x6<BN, BK, LDK, FB>(pb, Bs, tid);
     __syncthreads();
     if (k0 + BK < ke) {
       fa.template fetch<BM, BK>(pa, m0, k0 + BK, ke, tid);

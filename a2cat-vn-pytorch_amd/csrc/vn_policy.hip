@@ -515,6 +515,27 @@ inline void launch_wgrad(const float* dZ, int64_t ldz, int M, FB fb, int KP, int
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, slab, splits, M, N, dW, db);
 }
 
+// The same split-K wgrad on the x6 core: both operands gathered along the reduction index
+// (DenseT dZ, Im2colT im2col) and split into bf16 planes as they are staged.
+template <int BM, int BN, int WM, int WN, class FB>
+inline void launch_wgrad6(const float* dZ, int64_t ldz, int M, FB fb, int KP, int P, float* slab, int64_t slab_cap,
+                          float* dW, float* db, hipStream_t st) {
+  constexpr int BK = 32;
+  const int N = KP + 1;
+  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  int splits = std::max(1, std::min((2048 + tiles - 1) / tiles, (P + 255) / 256));
+  while ((int64_t)splits * M * N > slab_cap && splits > 1) splits /= 2;
+  int kchunk = (P + splits - 1) / splits;
+  kchunk = (kchunk + BK - 1) / BK * BK;
+  splits = (P + kchunk - 1) / kchunk;
+  DenseT fa{dZ, ldz, M};
+  EpiSlab ep{slab, M, N};
+  hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, BK, WM, WN, DenseT, FB, EpiSlab>), grid_for(M, N, BM, BN, splits),
+                     dim3(256), 0, st, fa, fb, ep, M, N, P, kchunk);
+  const int total = M * N;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, slab, splits, M, N, dW, db);
+}
+
 // Split-K wgrad on the x6 core from transposed operands: dZT [M][P] (rows = output
 // channels, k = samples) and XT [KP][P] (+ the ones row), both row-fill. The producers'
 // [P][*] tensors are transposed once (tile_transpose) so the reduction runs k-contiguous.
@@ -751,8 +772,8 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
       launch_gemm_x6<64, 64, 32, 2, 2>(fa, fb, ep, n, G::FCIN, 512, st);
     }
     Im2colT<DenseRows> fbw{DenseRows{a.X[3], G::FCIN, n}, G::FCIN};
-    launch_wgrad<64, 64, 2, 2>(dz5, 512, 512, fbw, G::FCIN, n, w.slab, w.slab_cap, Gr + L.l[4].w, Gr + L.l[4].b,
-                               st);
+    launch_wgrad6<128, 128, 2, 2>(dz5, 512, 512, fbw, G::FCIN, n, w.slab, w.slab_cap, Gr + L.l[4].w, Gr + L.l[4].b,
+                                  st);
   }
   // ---- conv4 (1x1): dX3 = dz4 x W4 masked by X3 ; dW4 = dz4^T x X3
   {
@@ -767,7 +788,7 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
   {
     using Im = NhwcIm2col<32, 4, 4, 2, G::OH2, G::OW2, G::OH3, G::OW3, 2>;
     Im2colT<Im> fbw{Im{a.X[1], n9}, 1024};
-    launch_wgrad<64, 64, 2, 2>(w.dz3, 64, 64, fbw, 1024, n9, w.slab, w.slab_cap, Gr + L.l[2].w, Gr + L.l[2].b, st);
+    launch_wgrad6<64, 128, 2, 2>(w.dz3, 64, 64, fbw, 1024, n9, w.slab, w.slab_cap, Gr + L.l[2].w, Gr + L.l[2].b, st);
     for (int g = 0; g < 2; ++g)
       dgrad_all_classes<64, 64, G::OH2, G::OW2, G::OH3, G::OW3>(w.dz3, T(2), w.dz2, a.X[1], n, g, 2, 32, st);
   }
@@ -954,7 +975,7 @@ int backward_bignet(const PolicyLayout& L, const float* P, const FrameSrc& src, 
     EpiMask ep{dz3, a.X[2], FCIN};
     launch_gemm_x6<64, 64, 32, 2, 2>(fa, fb, ep, n, FCIN, 512, st);
     Im2colT<DenseRows> fbw{DenseRows{a.X[2], FCIN, n}, FCIN};
-    launch_wgrad<64, 64, 2, 2>(dz5, 512, 512, fbw, FCIN, n, w.slab, w.slab_cap, Gr + L.l[4].w, Gr + L.l[4].b, st);
+    launch_wgrad6<128, 128, 2, 2>(dz5, 512, 512, fbw, FCIN, n, w.slab, w.slab_cap, Gr + L.l[4].w, Gr + L.l[4].b, st);
   }
   {  // conv3 (k3 s1): wgrad, then the single-class dgrad into dz2 masked by X2
     using Im = NhwcIm2col<64, 3, 3, 1, OH2, OW2, OH3, OW3, 1>;
@@ -970,7 +991,7 @@ int backward_bignet(const PolicyLayout& L, const float* P, const FrameSrc& src, 
   {  // conv2 (k4 s2): wgrad, then parity-class dgrad over X1 in place
     using Im = NhwcIm2col<32, 4, 4, 2, OH1, OW1, OH2, OW2, 1>;
     const int P2 = n * OH2 * OW2;
-    launch_wgrad<64, 64, 2, 2>(dz2, 64, 64, Im2colT<Im>{Im{a.X[0], P2}, 512}, 512, P2, w.slab, w.slab_cap,
+    launch_wgrad6<64, 128, 2, 2>(dz2, 64, 64, Im2colT<Im>{Im{a.X[0], P2}, 512}, 512, P2, w.slab, w.slab_cap,
                                Gr + L.l[1].w, Gr + L.l[1].b, st);
     dgrad_all_classes<64, 32, OH1, OW1, OH2, OW2>(dz2, T(1), a.X[0], a.X[0], n, 0, 1, 32, st);
   }
@@ -1256,8 +1277,8 @@ int aux_backward_impl(const PolicyLayout& L, const float* P, const float* X4, in
   }
   colsum(A1, (int64_t)P1, kAuxC1, w.colsum, Gr + L.ab1, st);
   // first layer: dW1 = X4^T x im2col(dA1); dX4 = conv(dA1, W1)
-  launch_wgrad<32, 64, 2, 2>(X4, 32, 32, Im2colT<Im1>{Im1{A1, P0}, 16 * kAuxC1}, 16 * kAuxC1, P0, w.slab,
-                             slab_floats(L), Gr + L.aw1, w.db, st);
+  launch_wgrad6<32, 128, 1, 4>(X4, 32, 32, Im2colT<Im1>{Im1{A1, P0}, 16 * kAuxC1}, 16 * kAuxC1, P0, w.slab,
+                               slab_floats(L), Gr + L.aw1, w.db, st);
   {
     DenseRows fb{P + L.aw1, 16 * kAuxC1, 32};
     EpiStore ep{dX4, 32};
