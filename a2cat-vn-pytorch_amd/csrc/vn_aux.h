@@ -28,12 +28,13 @@ struct EpiDeconv {
   int C;
   const float* bias;
   int relu;
-  __device__ __forceinline__ void operator()(int row, int col, float v, int) const {
+  __device__ __forceinline__ float pre_col(int col) const { return bias[col]; }
+  __device__ __forceinline__ void post(int row, int col, float v, float b, int) const {
     constexpr int per = HYC * WXC;
     const int n = row / per;
     const int r = row - n * per;
     const int y = (r / WXC) * 2 + PY, x = (r % WXC) * 2 + PX;
-    v += bias[col];
+    v += b;
     Y[(((int64_t)n * OH + y) * OW + x) * C + col] = relu ? fmaxf(v, 0.0f) : v;
   }
 };
@@ -45,9 +46,12 @@ struct EpiMaskAdd {
   const float* X;
   int64_t ld;
   const float* extra;
-  __device__ __forceinline__ void operator()(int row, int col, float v, int) const {
+  __device__ __forceinline__ float2 pre(int row, int col) const {
     const int64_t i = (int64_t)row * ld + col;
-    out[i] = X[i] > 0.0f ? v + extra[i] : 0.0f;
+    return float2{X[i], extra[i]};
+  }
+  __device__ __forceinline__ void post(int row, int col, float v, float2 xe, int) const {
+    out[(int64_t)row * ld + col] = xe.x > 0.0f ? v + xe.y : 0.0f;
   }
 };
 

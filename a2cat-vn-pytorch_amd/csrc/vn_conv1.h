@@ -852,8 +852,8 @@ __global__ __launch_bounds__(256) void conv2_dgrad_kernel(const float* __restric
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 
 template <int IH, int IW, int OH, int OW>
-constexpr size_t conv2_dgrad_x6_lds() {
-  return (size_t)3 * (OH * OW + 1) * 40 * 2;
+constexpr size_t conv2_dgrad_x6_lds() {  // three dZ2 planes + the frame's conv1 ReLU words
+  return (size_t)3 * (OH * OW + 1) * 40 * 2 + (size_t)IH * IW * 4;
 }
 
 template <int IH, int IW, int OH, int OW>
@@ -897,6 +897,9 @@ __global__ __launch_bounds__(NW * 64, 2) void conv2_dgrad_x6_kernel(const float*
   static_assert(IH % 2 == 0 && IW % 2 == 0, "even conv1 maps");
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_dg[];
   uint16_t* zs = reinterpret_cast<uint16_t*>(smem_dg);
+  // the frame's ReLU words, staged with dZ2: a global load in the epilogue made every tile
+  // wait (vmcnt counts stores too) for its previous tile's stores
+  uint32_t* ms = reinterpret_cast<uint32_t*>(smem_dg + (size_t)3 * (NP + 1) * 40 * 2);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   constexpr int NT = NW * 64;
   const int cls = wave & 3, py = cls >> 1, px = cls & 1;
@@ -920,14 +923,20 @@ __global__ __launch_bounds__(NW * 64, 2) void conv2_dgrad_x6_kernel(const float*
     const int pl = i / (PS / 2), e = i - pl * (PS / 2);
     reinterpret_cast<uint32_t*>(zs + pl * PL + NP * PS)[e] = 0u;
   }
-  constexpr int NZ = (NP * 8 + NT - 1) / NT;
+  constexpr int NZ = (NP * 8 + NT - 1) / NT, NM = (IH * IW + NT - 1) / NT;
   f4 zr[NZ];
-  auto load_z = [&](int f) {
+  uint32_t mr[NM];
+  auto load_z = [&](int f) {  // dZ2 and the ReLU words of frame f, into registers
     const f4* z4 = reinterpret_cast<const f4*>(dZ2 + (int64_t)f * NP * 32);
 #pragma unroll
     for (int j = 0; j < NZ; ++j) {
       const int i = tid + j * NT;
       if (i < NP * 8) zr[j] = z4[i];
+    }
+#pragma unroll
+    for (int j = 0; j < NM; ++j) {
+      const int i = tid + j * NT;
+      if (i < IH * IW) mr[j] = mask[(int64_t)f * IH * IW + i];
     }
   };
   if ((int)blockIdx.x < n_frames) load_z(blockIdx.x);
@@ -943,6 +952,11 @@ __global__ __launch_bounds__(NW * 64, 2) void conv2_dgrad_x6_kernel(const float*
         *reinterpret_cast<uint2*>(d + PL) = t1;
         *reinterpret_cast<uint2*>(d + 2 * PL) = t2;
       }
+    }
+#pragma unroll
+    for (int j = 0; j < NM; ++j) {
+      const int i = tid + j * NT;
+      if (i < IH * IW) ms[i] = mr[j];
     }
     __syncthreads();
     if (f + (int)gridDim.x < n_frames) load_z(f + gridDim.x);
@@ -994,7 +1008,7 @@ __global__ __launch_bounds__(NW * 64, 2) void conv2_dgrad_x6_kernel(const float*
         if (pr < NPC) {
           const int y = (pr / WXC) * 2 + py, x = (pr % WXC) * 2 + px;
           const int64_t pix = ((int64_t)f * IH + y) * IW + x;
-          const uint32_t mw = mask[pix];
+          const uint32_t mw = ms[y * IW + x];
 #pragma unroll
           for (int nt = 0; nt < 2; ++nt) {
             const uint32_t m4 = mw >> (nt * 16 + 4 * q);

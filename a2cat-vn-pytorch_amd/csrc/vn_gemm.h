@@ -26,6 +26,106 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ f4 f4zero() { return f4{0.f, 0.f, 0.f, 0.f}; }
 
+// Two-phase epilogues: a functor's side inputs (bias, the producing activation of a ReLU
+// mask, ...) are all loaded before the stores that use them, then post(row, col, v, side,
+// split) stores. With one load per element inside the store loop, every load waited on
+// vmcnt, which on gfx950 also counts the tile's earlier stores: the epilogue ran one memory
+// round trip per element. A functor says what its side input depends on: pre_col(col) (one
+// value per tile column: loaded once per j), pre_row(row) (once per row), or pre(row, col)
+// (per element: loaded one i-slice of the tile at a time to bound the registers held).
+template <class E, class = void>
+struct has_pre : std::false_type {};
+template <class E>
+struct has_pre<E, std::void_t<decltype(&E::pre)>> : std::true_type {};
+template <class E, class = void>
+struct has_pre_col : std::false_type {};
+template <class E>
+struct has_pre_col<E, std::void_t<decltype(&E::pre_col)>> : std::true_type {};
+template <class E, class = void>
+struct has_pre_row : std::false_type {};
+template <class E>
+struct has_pre_row<E, std::void_t<decltype(&E::pre_row)>> : std::true_type {};
+
+// Epilogue over an accumulator tile: NR values per (i, j) whose (row, col) come from rc; the
+// column of a value depends on j (and the lane) only, its row on i and r only.
+template <int TM, int TN, int NR, class EP, class ACC, class RC>
+__device__ __forceinline__ void run_epilogue(const EP& ep, const ACC& acc, int M, int N, int z, RC rc) {
+  if constexpr (has_pre_col<EP>::value) {
+    using PT = decltype(ep.pre_col(0));
+    PT pv[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      int row, col;
+      rc(0, j, 0, row, col);
+      if (col < N) pv[j] = ep.pre_col(col);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+          int row, col;
+          rc(i, j, r, row, col);
+          if (row < M && col < N) ep.post(row, col, acc[i][j][r], pv[j], z);
+        }
+  } else if constexpr (has_pre_row<EP>::value) {
+    using PT = decltype(ep.pre_row(0));
+    PT pv[TM][NR];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        int row, col;
+        rc(i, 0, r, row, col);
+        if (row < M) pv[i][r] = ep.pre_row(row);
+      }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+          int row, col;
+          rc(i, j, r, row, col);
+          if (row < M && col < N) ep.post(row, col, acc[i][j][r], pv[i][r], z);
+        }
+  } else if constexpr (has_pre<EP>::value) {
+    using PT = decltype(ep.pre(0, 0));
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      PT pv[TN][NR];
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+          int row, col;
+          rc(i, j, r, row, col);
+          if (row < M && col < N) pv[j][r] = ep.pre(row, col);
+        }
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+          int row, col;
+          rc(i, j, r, row, col);
+          if (row < M && col < N) ep.post(row, col, acc[i][j][r], pv[j][r], z);
+        }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+          int row, col;
+          rc(i, j, r, row, col);
+          if (row < M && col < N) ep(row, col, acc[i][j][r], z);
+        }
+  }
+}
+
 template <int BM, int BN, int BK, int WM, int WN, class FA, class FB, class EP>
 __global__ __launch_bounds__(256) void gemm_kernel(FA fa, FB fb, EP ep, int M, int N, int K, int kchunk) {
   static_assert(WM * WN == 4, "4 waves per workgroup");
@@ -82,16 +182,10 @@ __global__ __launch_bounds__(256) void gemm_kernel(FA fa, FB fb, EP ep, int M, i
     }
     __syncthreads();
   }
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wm * TM * 16 + i * 16 + (lane >> 4) * 4 + r;
-        const int col = n0 + wn * TN * 16 + j * 16 + (lane & 15);
-        if (row < M && col < N) ep(row, col, acc[i][j][r], (int)blockIdx.z);
-      }
+  run_epilogue<TM, TN, 4>(ep, acc, M, N, (int)blockIdx.z, [&](int i, int j, int r, int& row, int& col) {
+    row = m0 + wm * TM * 16 + i * 16 + (lane >> 4) * 4 + r;
+    col = n0 + wn * TN * 16 + j * 16 + (lane & 15);
+  });
 }
 
 // Same core on v_mfma_f32_32x32x2_f32 (64-cycle issue = 64-cycle latency: one accumulator
@@ -155,16 +249,10 @@ __global__ __launch_bounds__(256) void gemm32_kernel(FA fa, FB fb, EP ep, int M,
     }
     __syncthreads();
   }
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        const int col = n0 + wn * TN * 32 + j * 32 + (lane & 31);
-        if (row < M && col < N) ep(row, col, acc[i][j][r], (int)blockIdx.z);
-      }
+  run_epilogue<TM, TN, 16>(ep, acc, M, N, (int)blockIdx.z, [&](int i, int j, int r, int& row, int& col) {
+    row = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    col = n0 + wn * TN * 32 + j * 32 + (lane & 31);
+  });
 }
 
 // ---- fp32 GEMM on bf16 MFMA with split operands ("x6") ---------------------------
@@ -306,16 +394,10 @@ __global__ __launch_bounds__(256) void gemm_x6_kernel(FA fa, FB fb, EP ep, int M
     }
     __syncthreads();
   }
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        const int col = n0 + wn * TN * 32 + j * 32 + (lane & 31);
-        if (row < M && col < N) ep(row, col, acc[i][j][r], (int)blockIdx.z);
-      }
+  run_epilogue<TM, TN, 16>(ep, acc, M, N, (int)blockIdx.z, [&](int i, int j, int r, int& row, int& col) {
+    row = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    col = n0 + wn * TN * 32 + j * 32 + (lane & 31);
+  });
 }
 
 // ---- fill helpers: fetch (global -> registers) then commit (registers -> LDS) ----

@@ -81,8 +81,9 @@ __global__ void lstm_cell_bwd_kernel(int n, const float* __restrict__ dh_heads, 
 struct EpiLstmDh {
   float* dh_prev;
   const float* mask;
-  __device__ __forceinline__ void operator()(int row, int col, float v, int) const {
-    dh_prev[(int64_t)row * 512 + col] = v * (mask ? mask[row] : 1.0f);
+  __device__ __forceinline__ float pre_row(int row) const { return mask ? mask[row] : 1.0f; }
+  __device__ __forceinline__ void post(int row, int col, float v, float m, int) const {
+    dh_prev[(int64_t)row * 512 + col] = v * m;
   }
 };
 
@@ -91,8 +92,9 @@ struct EpiBias2 {
   int64_t ld;
   const float* b0;
   const float* b1;
-  __device__ __forceinline__ void operator()(int row, int col, float v, int) const {
-    Y[(int64_t)row * ld + col] = v + b0[col] + b1[col];
+  __device__ __forceinline__ float2 pre_col(int col) const { return float2{b0[col], b1[col]}; }
+  __device__ __forceinline__ void post(int row, int col, float v, float2 b, int) const {
+    Y[(int64_t)row * ld + col] = v + b.x + b.y;
   }
 };
 

@@ -249,8 +249,9 @@ struct EpiBiasAct {
   int64_t ld;
   const float* bias;
   int relu;
-  __device__ __forceinline__ void operator()(int row, int col, float v, int) const {
-    v += bias[col];
+  __device__ __forceinline__ float pre_col(int col) const { return bias[col]; }
+  __device__ __forceinline__ void post(int row, int col, float v, float b, int) const {
+    v += b;
     Y[(int64_t)row * ld + col] = relu ? fmaxf(v, 0.0f) : v;
   }
 };
@@ -260,9 +261,9 @@ struct EpiMask {
   float* out;
   const float* X;
   int64_t ld;
-  __device__ __forceinline__ void operator()(int row, int col, float v, int) const {
-    const int64_t i = (int64_t)row * ld + col;
-    out[i] = X[i] > 0.0f ? v : 0.0f;
+  __device__ __forceinline__ float pre(int row, int col) const { return X[(int64_t)row * ld + col]; }
+  __device__ __forceinline__ void post(int row, int col, float v, float x, int) const {
+    out[(int64_t)row * ld + col] = x > 0.0f ? v : 0.0f;
   }
 };
 
@@ -271,13 +272,16 @@ struct EpiMaskParity {
   float* out;
   const float* X;
   int g, G, cin;
-  __device__ __forceinline__ void operator()(int row, int col, float v, int) const {
+  __device__ __forceinline__ int64_t index(int row, int col) const {
     constexpr int per = HYC * WXC;
     const int n = row / per;
     const int r = row - n * per;
     const int y = (r / WXC) * S + PY, x = (r % WXC) * S + PX;
-    const int64_t i = ((((int64_t)n * G + g) * H + y) * W + x) * cin + col;
-    out[i] = X[i] > 0.0f ? v : 0.0f;
+    return ((((int64_t)n * G + g) * H + y) * W + x) * cin + col;
+  }
+  __device__ __forceinline__ float pre(int row, int col) const { return X[index(row, col)]; }
+  __device__ __forceinline__ void post(int row, int col, float v, float x, int) const {
+    out[index(row, col)] = x > 0.0f ? v : 0.0f;
   }
 };
 
