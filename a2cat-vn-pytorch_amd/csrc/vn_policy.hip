@@ -293,14 +293,16 @@ struct EpiSlab {
   }
 };
 
-__global__ void wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int M, int N, float* dW, float* db) {
+// Split-K slab [splits][M][N] -> dW [M][KP] and, when N == KP + 1, the bias column db [M].
+__global__ void wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int M, int N, int KP, float* dW,
+                                    float* db) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= M * N) return;
   const int row = idx / N, col = idx - (idx / N) * N;
   float s = 0.0f;
   for (int z = 0; z < splits; ++z) s += slab[((int64_t)z * M + row) * N + col];
-  if (col < N - 1)
-    dW[(int64_t)row * (N - 1) + col] = s;
+  if (col < KP)
+    dW[(int64_t)row * KP + col] = s;
   else
     db[row] = s;
 }
@@ -505,7 +507,7 @@ template <int BM, int BN, int WM, int WN, class FB>
 inline void launch_wgrad(const float* dZ, int64_t ldz, int M, FB fb, int KP, int P, float* slab, int64_t slab_cap,
                          float* dW, float* db, hipStream_t st) {
   constexpr int BK = 32;
-  const int N = KP + 1;
+  const int N = KP + (db ? 1 : 0);  // db == nullptr: no bias column
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   int splits = std::max(1, std::min((2048 + tiles - 1) / tiles, (P + 255) / 256));
   while ((int64_t)splits * M * N > slab_cap && splits > 1) splits /= 2;
@@ -516,7 +518,7 @@ inline void launch_wgrad(const float* dZ, int64_t ldz, int M, FB fb, int KP, int
   EpiSlab ep{slab, M, N};
   launch_gemm<BM, BN, BK, WM, WN>(fa, fb, ep, M, N, P, st, splits, kchunk);
   const int total = M * N;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, slab, splits, M, N, dW, db);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, slab, splits, M, N, KP, dW, db);
 }
 
 // The same split-K wgrad on the x6 core: both operands gathered along the reduction index
@@ -525,7 +527,7 @@ template <int BM, int BN, int WM, int WN, class FB>
 inline void launch_wgrad6(const float* dZ, int64_t ldz, int M, FB fb, int KP, int P, float* slab, int64_t slab_cap,
                           float* dW, float* db, hipStream_t st) {
   constexpr int BK = 32;
-  const int N = KP + 1;
+  const int N = KP + (db ? 1 : 0);  // db == nullptr: no bias column
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   int splits = std::max(1, std::min((2048 + tiles - 1) / tiles, (P + 255) / 256));
   while ((int64_t)splits * M * N > slab_cap && splits > 1) splits /= 2;
@@ -537,7 +539,7 @@ inline void launch_wgrad6(const float* dZ, int64_t ldz, int M, FB fb, int KP, in
   hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, BK, WM, WN, DenseT, FB, EpiSlab>), grid_for(M, N, BM, BN, splits),
                      dim3(256), 0, st, fa, fb, ep, M, N, P, kchunk);
   const int total = M * N;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, slab, splits, M, N, dW, db);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, slab, splits, M, N, KP, dW, db);
 }
 
 // Split-K wgrad on the x6 core from transposed operands: dZT [M][P] (rows = output
@@ -547,7 +549,7 @@ template <int BM, int BN, int WM, int WN>
 inline void launch_wgrad_x6(const float* dZT, int M, const float* XT, int KP, int P, int64_t ldt, float* slab,
                             int64_t slab_cap, float* dW, float* db, hipStream_t st) {
   constexpr int BK = 32;
-  const int N = KP + 1;
+  const int N = KP + (db ? 1 : 0);  // db == nullptr: no bias column
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   int splits = std::max(1, std::min((2048 + tiles - 1) / tiles, (P + 255) / 256));
   while ((int64_t)splits * M * N > slab_cap && splits > 1) splits /= 2;
@@ -560,7 +562,7 @@ inline void launch_wgrad_x6(const float* dZT, int M, const float* XT, int KP, in
   hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, BK, WM, WN, DenseRows, RowsOnes, EpiSlab>), grid_for(M, N, BM, BN, splits),
                      dim3(256), 0, st, fa, fb, ep, M, N, P, kchunk);
   const int total = M * N;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, slab, splits, M, N, dW, db);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, slab, splits, M, N, KP, dW, db);
 }
 
 // dgrad of one (group, parity) class of a k4 s2 conv: input pixels (y, x) with
@@ -1268,9 +1270,10 @@ int aux_backward_impl(const PolicyLayout& L, const float* P, const float* X4, in
   const int P1 = n * AH * AW, P0 = n * IH * IW;
   using Im2 = NhwcIm2col<kAuxC2, 4, 4, 2, PH, PW, AH, AW, 1>;  // dP windows per A1 pixel
   using Im1 = NhwcIm2col<kAuxC1, 4, 4, 2, AH, AW, IH, IW, 1>;  // dA1 windows per X4 pixel
-  // second layer: dW2 = A1^T x im2col(dP) (block-diagonal mask), db2 = column sums of dP
-  launch_wgrad<32, 64, 2, 2>(A1, kAuxC1, kAuxC1, Im2colT<Im2>{Im2{dP, P1}, 16 * kAuxC2}, 16 * kAuxC2, P1, w.slab,
-                             slab_floats(L), Gr + L.aw2, w.db, st);
+  // second layer: dW2 = A1^T x im2col(dP) (block-diagonal mask), db2 = column sums of dP (the
+  // head biases come from colsum, so the weight GEMMs carry no ones column)
+  launch_wgrad6<64, 128, 2, 2>(A1, kAuxC1, kAuxC1, Im2colT<Im2>{Im2{dP, P1}, 16 * kAuxC2}, 16 * kAuxC2, P1, w.slab,
+                               slab_floats(L), Gr + L.aw2, nullptr, st);
   hipLaunchKernelGGL(aux_blockdiag_mask_kernel, dim3((kAuxC1 * 16 * kAuxC2 + 255) / 256), dim3(256), 0, st,
                      Gr + L.aw2);
   colsum(dP, (int64_t)n * PH * PW, kAuxC2, w.colsum, Gr + L.ab2, st);
@@ -1282,7 +1285,7 @@ int aux_backward_impl(const PolicyLayout& L, const float* P, const float* X4, in
   colsum(A1, (int64_t)P1, kAuxC1, w.colsum, Gr + L.ab1, st);
   // first layer: dW1 = X4^T x im2col(dA1); dX4 = conv(dA1, W1)
   launch_wgrad6<32, 128, 1, 4>(X4, 32, 32, Im2colT<Im1>{Im1{A1, P0}, 16 * kAuxC1}, 16 * kAuxC1, P0, w.slab,
-                               slab_floats(L), Gr + L.aw1, w.db, st);
+                               slab_floats(L), Gr + L.aw1, nullptr, st);
   {
     DenseRows fb{P + L.aw1, 16 * kAuxC1, 32};
     EpiStore ep{dX4, 32};
