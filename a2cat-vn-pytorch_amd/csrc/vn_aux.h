@@ -342,4 +342,217 @@ __global__ __launch_bounds__(kAux2Threads) void aux_deconv2_kernel(const float* 
   }
 }
 
+// ---- fused second-layer backward ------------------------------------------------------
+// One pass over (A1, dP) per sample replaces four launches (dW2 product, dA1 product with
+// its ReLU mask, and the two bias column sums), and keeps the block-diagonal structure the
+// GEMM forms multiplied as zeros: head h's 16 input channels only meet its own output
+// channels (1, 3, 3), so dW2 has 16 x 16 x 7 live entries (of 48 x 128) and dA1 a K of
+// 16 x nco per head. Work per workgroup: one sample at a time, its dP map staged in LDS
+// (pixel stride 9 floats: 16 pixels two apart land on distinct banks); each wave takes
+// 16-pixel tiles of the A1 map and runs, on v_mfma_f32_16x16x4f32,
+//   dW2 (per head, C[ci][tap,co] += A1[px][ci] * dP[2y+ky][2x+kx][co] over the tile's 16
+//        pixels; 7 accumulator tiles held across all the workgroup's samples), and
+//   dA1 (C[px][ci] = sum_{tap,co} dP[2y+ky][2x+kx][co] * W2[ci][tap][co], weights in
+//        registers), masked by A1 > 0 and written over A1 in place (the tile's A1 is read
+//        by the same wave before it is overwritten);
+// db1 (column sums of dA1) and db2 (of dP) ride along. Per-workgroup partials
+// [7][4][64] + 48 + 8 are reduced in a fixed order (deterministic) by the finish kernel.
+constexpr int kAuxBThreads = 512;
+constexpr int kAuxBDs = 9;                                  // LDS floats per dP pixel
+constexpr int kAuxBPart = 7 * 4 * 64 + kAuxC1 + kAuxC2;     // floats per workgroup partial
+template <int PH, int PW>
+constexpr size_t auxb_lds() {
+  return (size_t)PH * PW * kAuxBDs * 4;
+}
+template <int AH, int AW, int PH, int PW>
+constexpr bool auxb_fits() {
+  return (AH * AW) % 16 == 0 && auxb_lds<PH, PW>() <= 80 * 1024 && auxb_lds<PH, PW>() >= 7 * 4 * 64 * 4 + 64 * 4;
+}
+
+// LDS offset (pixel stride kAuxBDs) of (tap, output channel) relative to a window corner.
+template <int PW>
+__device__ __forceinline__ int auxb_tap_off(int tap, int co) {
+  return ((tap >> 2) * PW + (tap & 3)) * kAuxBDs + co;
+}
+
+template <int AH, int AW, int PH, int PW>
+__global__ __launch_bounds__(kAuxBThreads, 4) void aux_backward2_kernel(float* __restrict__ A1,
+                                                                        const float* __restrict__ dP, int n,
+                                                                        const float* __restrict__ W2,
+                                                                        float* __restrict__ part) {
+  constexpr int NPX = AH * AW, NT = NPX / 16, NPP = PH * PW;
+  static_assert(PH == 2 * AH + 2 && PW == 2 * AW + 2 && NPX % 16 == 0, "k4 s2 transposed conv geometry");
+  extern __shared__ __attribute__((aligned(16))) float dps[];  // [NPP][kAuxBDs]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l16 = lane & 15, lq = lane >> 4;
+  // dA1 operands: step u of K (4 + 12 + 12 over the heads), lane k = 4u' + lq. The LDS
+  // offsets of heads 1 and 2 repeat every 3 steps one window row down (k = 12j + 4v + lq:
+  // tap = 4j + (4v + lq) / 3), so three per lane are kept.
+  float wb[28];
+#pragma unroll
+  for (int u = 0; u < 28; ++u) {
+    const int h = u < 4 ? 0 : (u < 16 ? 1 : 2);
+    const int k = 4 * (u < 4 ? u : (u < 16 ? u - 4 : u - 16)) + lq;
+    const int tap = h == 0 ? k : k / 3;
+    const int co = h == 0 ? 0 : (h == 1 ? 1 : 4) + k % 3;
+    wb[u] = W2[(16 * h + l16) * 128 + tap * 8 + co];
+  }
+  int coff[3];
+#pragma unroll
+  for (int v = 0; v < 3; ++v) coff[v] = auxb_tap_off<PW>((4 * v + lq) / 3, 1 + (4 * v + lq) % 3);
+  // dW2 operand B: column l16 of accumulator tile q (head 0: tap; heads 1, 2: 3 taps x co)
+  int boff[7];
+#pragma unroll
+  for (int q = 0; q < 7; ++q) {
+    if (q == 0) {
+      boff[q] = auxb_tap_off<PW>(l16, 0);
+    } else {
+      const int col = 16 * ((q - 1) % 3) + l16;
+      boff[q] = auxb_tap_off<PW>(col / 3, (q <= 3 ? 1 : 4) + col % 3);
+    }
+  }
+  f4 accw[7];
+#pragma unroll
+  for (int q = 0; q < 7; ++q) accw[q] = f4zero();
+  float db1[3] = {0.0f, 0.0f, 0.0f};
+  f4 db2 = f4zero();
+  for (int s = blockIdx.x; s < n; s += gridDim.x) {
+    const f4* src = reinterpret_cast<const f4*>(dP + (int64_t)s * NPP * kAuxC2);
+    for (int i = tid; i < NPP * 2; i += kAuxBThreads) {
+      const f4 v = src[i];
+      float* d = dps + (i >> 1) * kAuxBDs + (i & 1) * 4;
+      d[0] = v[0];
+      d[1] = v[1];
+      d[2] = v[2];
+      d[3] = v[3];
+      db2 += v;
+    }
+    __syncthreads();
+    float* a1 = A1 + (int64_t)s * NPX * kAuxC1;
+    for (int t = wave; t < NT; t += kAuxBThreads / 64) {
+#pragma unroll 2
+      for (int ks = 0; ks < 4; ++ks) {  // dW2 over the tile's pixels, 4 per MFMA
+        const int px = 16 * t + 4 * ks + lq;
+        const int base = (2 * (px / AW) * PW + 2 * (px % AW)) * kAuxBDs;
+        const float* ap = a1 + px * kAuxC1 + l16;
+        const float x0 = ap[0], x1 = ap[16], x2 = ap[32];
+        float b[7];
+#pragma unroll
+        for (int q = 0; q < 7; ++q) b[q] = dps[base + boff[q]];
+        accw[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(x0, b[0], accw[0], 0, 0, 0);
+#pragma unroll
+        for (int q = 1; q < 4; ++q) accw[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(x1, b[q], accw[q], 0, 0, 0);
+#pragma unroll
+        for (int q = 4; q < 7; ++q) accw[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(x2, b[q], accw[q], 0, 0, 0);
+      }
+      // dA1 of the tile: rows = pixels 16t + l16 (operand A), C rows 16t + 4 lq + r
+      const int pa = 16 * t + l16;
+      const int abase = (2 * (pa / AW) * PW + 2 * (pa % AW)) * kAuxBDs;
+      f4 acc[3] = {f4zero(), f4zero(), f4zero()};
+#pragma unroll
+      for (int u = 0; u < 4; ++u)  // head 0: tap = 4u + lq (ky = u, kx = lq), channel 0
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(dps[abase + (u * PW + lq) * kAuxBDs], wb[u], acc[0], 0, 0, 0);
+#pragma unroll
+      for (int u = 4; u < 28; ++u) {
+        const int h = u < 16 ? 1 : 2, up = u - (h == 1 ? 4 : 16);
+        const float a = dps[abase + coff[up % 3] + (up / 3) * PW * kAuxBDs + (h == 2 ? 3 : 0)];
+        acc[h] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, wb[u], acc[h], 0, 0, 0);
+      }
+      float* op = a1 + (16 * t + 4 * lq) * kAuxC1 + l16;
+      float m[3][4];
+#pragma unroll
+      for (int h = 0; h < 3; ++h)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) m[h][r] = op[r * kAuxC1 + 16 * h];
+#pragma unroll
+      for (int h = 0; h < 3; ++h)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = m[h][r] > 0.0f ? acc[h][r] : 0.0f;
+          db1[h] += v;
+          op[r * kAuxC1 + 16 * h] = v;
+        }
+    }
+    __syncthreads();
+  }
+  // workgroup reduction in a fixed order: wave by wave into LDS (the staging area is free)
+  float* red = dps;  // [7][4][64] dW2, [48] db1, [8] db2
+#pragma unroll
+  for (int h = 0; h < 3; ++h) {
+    db1[h] += __shfl_xor(db1[h], 16);
+    db1[h] += __shfl_xor(db1[h], 32);
+  }
+#pragma unroll
+  for (int o = 2; o < 64; o <<= 1)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) db2[c] += __shfl_xor(db2[c], o);
+  for (int w = 0; w < kAuxBThreads / 64; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int q = 0; q < 7; ++q)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float* d = red + (q * 4 + r) * 64 + lane;
+          *d = (w == 0 ? 0.0f : *d) + accw[q][r];
+        }
+      if (lane < 16) {
+#pragma unroll
+        for (int h = 0; h < 3; ++h) {
+          float* d = red + 7 * 4 * 64 + 16 * h + lane;
+          *d = (w == 0 ? 0.0f : *d) + db1[h];
+        }
+      }
+      if (lane < 2) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          float* d = red + 7 * 4 * 64 + kAuxC1 + 4 * lane + c;
+          *d = (w == 0 ? 0.0f : *d) + db2[c];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  for (int i = tid; i < kAuxBPart; i += kAuxBThreads) part[(int64_t)blockIdx.x * kAuxBPart + i] = red[i];
+}
+
+// dW2 [48][16][8] (zeros off the head blocks), db1 [48], db2 [8] from the partials: one
+// wave per output, lane-strided over the workgroups and a fixed shuffle tree.
+__global__ void aux_backward2_finish_kernel(const float* __restrict__ part, int nblk, float* __restrict__ dW2,
+                                            float* __restrict__ db1, float* __restrict__ db2) {
+  const int idx = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64, lane = threadIdx.x & 63;
+  constexpr int NW = kAuxC1 * 16 * kAuxC2;
+  if (idx >= NW + kAuxC1 + kAuxC2) return;
+  int src;
+  if (idx < NW) {
+    const int ci = idx / 128, tap = (idx / 8) % 16, co = idx % 8, h = ci / 16;
+    if (aux_head_of_out(co) != h) {
+      if (lane == 0) dW2[idx] = 0.0f;
+      return;
+    }
+    int q, col;
+    if (h == 0) {
+      q = 0;
+      col = tap;
+    } else {
+      const int c3 = tap * 3 + co - (h == 1 ? 1 : 4);
+      q = 1 + 3 * (h - 1) + c3 / 16;
+      col = c3 % 16;
+    }
+    const int cl = ci % 16;
+    src = (q * 4 + (cl & 3)) * 64 + 16 * (cl >> 2) + col;
+  } else {
+    src = 7 * 4 * 64 + (idx - NW);
+  }
+  float s = 0.0f;
+  for (int b = lane; b < nblk; b += 64) s += part[(int64_t)b * kAuxBPart + src];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (lane != 0) return;
+  if (idx < NW)
+    dW2[idx] = s;
+  else if (idx < NW + kAuxC1)
+    db1[idx - NW] = s;
+  else
+    db2[idx - NW - kAuxC1] = s;
+}
+
 }  // namespace vn

@@ -1260,6 +1260,28 @@ int aux_forward_loss_impl(const PolicyLayout& L, const float* P, const float* X4
   return VN_OK;
 }
 
+// Second head layer backward as products (maps whose dP does not fit aux_backward2_kernel's
+// LDS): dW2 = A1^T x im2col(dP) (block-diagonal mask), db2 = column sums of dP (the head
+// biases come from column sums, so the weight products carry no ones column), dA1 =
+// conv(dP, W2) masked by the ReLU of A1 in place, db1 = column sums of dA1.
+template <int AH, int AW, int PH, int PW>
+void aux_backward_layer2_gemm(const PolicyLayout& L, const float* P, int n, float* A1, const float* dP, float* Gr,
+                              const AuxWork& w, hipStream_t st) {
+  const int P1 = n * AH * AW;
+  using Im2 = NhwcIm2col<kAuxC2, 4, 4, 2, PH, PW, AH, AW, 1>;  // dP windows per A1 pixel
+  launch_wgrad6<64, 128, 2, 2>(A1, kAuxC1, kAuxC1, Im2colT<Im2>{Im2{dP, P1}, 16 * kAuxC2}, 16 * kAuxC2, P1, w.slab,
+                               slab_floats(L), Gr + L.aw2, nullptr, st);
+  hipLaunchKernelGGL(aux_blockdiag_mask_kernel, dim3((kAuxC1 * 16 * kAuxC2 + 255) / 256), dim3(256), 0, st,
+                     Gr + L.aw2);
+  colsum(dP, (int64_t)n * PH * PW, kAuxC2, w.colsum, Gr + L.ab2, st);
+  {
+    DenseRows fb{P + L.aw2, 16 * kAuxC2, kAuxC1};
+    EpiMask ep{A1, A1, kAuxC1};
+    launch_gemm_x6<64, 64, 32, 2, 2>(Im2{dP, P1}, fb, ep, P1, kAuxC1, 16 * kAuxC2, st);
+  }
+  colsum(A1, (int64_t)P1, kAuxC1, w.colsum, Gr + L.ab1, st);
+}
+
 // Gradients of the heads' parameters and dX4 [n][IH][IW][32] (unmasked) from dP; A1 is
 // overwritten by its own gradient.
 template <int H0, int W0>
@@ -1267,22 +1289,25 @@ int aux_backward_impl(const PolicyLayout& L, const float* P, const float* X4, in
                       float* Gr, float* dX4, const AuxWork& w, hipStream_t st) {
   using G = Geo<H0, W0>;
   constexpr int IH = G::OH3, IW = G::OW3, AH = 2 * IH + 2, AW = 2 * IW + 2, PH = 2 * AH + 2, PW = 2 * AW + 2;
-  const int P1 = n * AH * AW, P0 = n * IH * IW;
-  using Im2 = NhwcIm2col<kAuxC2, 4, 4, 2, PH, PW, AH, AW, 1>;  // dP windows per A1 pixel
+  const int P0 = n * IH * IW;
   using Im1 = NhwcIm2col<kAuxC1, 4, 4, 2, AH, AW, IH, IW, 1>;  // dA1 windows per X4 pixel
-  // second layer: dW2 = A1^T x im2col(dP) (block-diagonal mask), db2 = column sums of dP (the
-  // head biases come from colsum, so the weight GEMMs carry no ones column)
-  launch_wgrad6<64, 128, 2, 2>(A1, kAuxC1, kAuxC1, Im2colT<Im2>{Im2{dP, P1}, 16 * kAuxC2}, 16 * kAuxC2, P1, w.slab,
-                               slab_floats(L), Gr + L.aw2, nullptr, st);
-  hipLaunchKernelGGL(aux_blockdiag_mask_kernel, dim3((kAuxC1 * 16 * kAuxC2 + 255) / 256), dim3(256), 0, st,
-                     Gr + L.aw2);
-  colsum(dP, (int64_t)n * PH * PW, kAuxC2, w.colsum, Gr + L.ab2, st);
-  {  // dA1 = conv(dP, W2) masked by the ReLU of A1, in place
-    DenseRows fb{P + L.aw2, 16 * kAuxC2, kAuxC1};
-    EpiMask ep{A1, A1, kAuxC1};
-    launch_gemm_x6<64, 64, 32, 2, 2>(Im2{dP, P1}, fb, ep, P1, kAuxC1, 16 * kAuxC2, st);
+  if constexpr (auxb_fits<AH, AW, PH, PW>()) {
+    // second layer in one pass: dW2, db2, dA1 (masked, over A1) and db1
+    const void* kfn = (const void*)aux_backward2_kernel<AH, AW, PH, PW>;
+    constexpr size_t lds = auxb_lds<PH, PW>();
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      attr = true;
+    }
+    const int blocks = std::min(n, std::min(resident_blocks(kfn, kAuxBThreads, lds), kColsumBlocks));
+    hipLaunchKernelGGL((aux_backward2_kernel<AH, AW, PH, PW>), dim3(blocks), dim3(kAuxBThreads), lds, st, A1, dP, n,
+                       P + L.aw2, w.slab);
+    hipLaunchKernelGGL(aux_backward2_finish_kernel, dim3((kAuxC1 * 16 * kAuxC2 + kAuxC1 + kAuxC2 + 3) / 4),
+                       dim3(256), 0, st, w.slab, blocks, Gr + L.aw2, Gr + L.ab1, Gr + L.ab2);
+  } else {
+    aux_backward_layer2_gemm<AH, AW, PH, PW>(L, P, n, A1, dP, Gr, w, st);
   }
-  colsum(A1, (int64_t)P1, kAuxC1, w.colsum, Gr + L.ab1, st);
   // first layer: dW1 = X4^T x im2col(dA1); dX4 = conv(dA1, W1)
   launch_wgrad6<32, 128, 1, 4>(X4, 32, 32, Im2colT<Im1>{Im1{A1, P0}, 16 * kAuxC1}, 16 * kAuxC1, P0, w.slab,
                                slab_floats(L), Gr + L.aw1, nullptr, st);

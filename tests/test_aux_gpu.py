@@ -93,6 +93,45 @@ def test_aux_grads_reach_trunk_vs_oracle_84():
     assert float(mine["conv_merge.0.1.weight"].abs().max()) == 0.0
 
 
+def test_aux_grads_large_batch_consistency_174():
+    """1040 samples at 174x174 in one batch — the fused head backward
+    (aux_backward2_kernel) then runs more samples than workgroups, so each accumulates
+    several samples' dW2/db partials — against the same samples in 26 batches of 40: the
+    batch gradient of the head MSE equals the mean of the small-batch gradients."""
+    from vnav.policy import GoalNavPolicy
+    torch.manual_seed(1)
+    pol = GoalNavPolicy(3, 4, (174, 174), aux=True)
+    with torch.no_grad():
+        pol.params.add_(torch.randn_like(pol.params) * 0.01)
+    B, C = 1040, 40
+    rng = np.random.RandomState(9)
+    img = torch.as_tensor(rng.randint(0, 256, size=(B, 1, 174, 174, 3)).astype(np.uint8)).cuda()
+    gl = torch.as_tensor(rng.randint(0, 256, size=(B, 1, 174, 174, 3)).astype(np.uint8)).cuda()
+    shapes = [p.shape[2:] for p in pol.forward_deconv(((img[:1], gl[:1]), None))[0]]
+    targets = [torch.as_tensor(rng.rand(B, 1, *sh).astype(np.float32)).cuda() for sh in shapes]
+
+    def grads(lo, hi):
+        pol.params.grad = None
+        preds, _ = pol.forward_deconv(((img[lo:hi], gl[lo:hi]), None))
+        loss = sum(torch.nn.functional.mse_loss(p, t[lo:hi]) for p, t in zip(preds, targets))
+        loss.backward()
+        return pol.params.grad.detach().clone()
+
+    full = grads(0, B)
+    gmean = sum(grads(k, k + C).double() for k in range(0, B, C)) / (B // C)
+    mine, ref = pol.net.to_reference(full), pol.net.to_reference(gmean.float())
+    bad = {}
+    for k in ref:
+        b = ref[k].numpy().astype(np.float64)
+        if np.abs(b).max() == 0.0:
+            continue
+        e = np.abs(mine[k].numpy() - b).max() / np.abs(b).max()
+        if e > 1e-5:
+            bad[k] = "%.3g" % e
+    assert not bad, bad
+    assert any(k.startswith("deconv_mask_goal") for k in ref)
+
+
 def _aux_scene(k, frame=(84, 84, 3)):
     import vnav
     sc = vnav.synthetic_scene(k, frame_shape=frame)
