@@ -684,20 +684,48 @@ __global__ __launch_bounds__(256) void conv2_wgrad_kernel(const float* __restric
     for (int r = 0; r < 16; ++r) acc[j][r] = 0.0f;
   float bacc = 0.0f;  // bias gradient: column sums of dZ2 (wave 0 only)
   const int n_items = n_frames * NB;
-  for (int it = blockIdx.x; it < n_items; it += gridDim.x) {
+  // The next item's band is loaded into registers while this one computes (the load and
+  // the MFMA phases of the two workgroups on a CU otherwise ran in lockstep, unoverlapped).
+  constexpr int NVX = (NX / 4 + 255) / 256, NVD = ((BR * OW + 1) / 2 * 2 * 8 + 255) / 256;
+  f4 px4[NVX], pd4[NVD];
+  auto load_item = [&](int it) {
     const int f = it / NB, band = it - (it / NB) * NB;
     const int oy0 = BR * band, nr = min(BR, OH - oy0), npb = nr * OW, npe = (npb + 1) / 2 * 2;
     const int y0 = 2 * oy0, nx = min(2 * nr + 2, IH - y0) * IW * 32;
+    const f4* s4 = reinterpret_cast<const f4*>(X1 + ((int64_t)f * IH + y0) * IW * 32);
+#pragma unroll
+    for (int j = 0; j < NVX; ++j) {
+      const int i = tid + 256 * j;
+      if (i < nx / 4) px4[j] = s4[i];
+    }
+    const f4* z4 = reinterpret_cast<const f4*>(dZ2 + ((int64_t)f * NP + oy0 * OW) * 32);
+#pragma unroll
+    for (int j = 0; j < NVD; ++j) {
+      const int i = tid + 256 * j;
+      if (i < npe * 8) pd4[j] = i < npb * 8 ? z4[i] : f4zero();
+    }
+  };
+  if ((int)blockIdx.x < n_items) load_item(blockIdx.x);
+  for (int it = blockIdx.x; it < n_items; it += gridDim.x) {
+    const int band = it - (it / NB) * NB;
+    const int oy0 = BR * band, nr = min(BR, OH - oy0), npb = nr * OW, npe = (npb + 1) / 2 * 2;
+    const int y0 = 2 * oy0, nx = min(2 * nr + 2, IH - y0) * IW * 32;
     {
-      const f4* s4 = reinterpret_cast<const f4*>(X1 + ((int64_t)f * IH + y0) * IW * 32);
       f4* d4 = reinterpret_cast<f4*>(xs);
-#pragma unroll 4
-      for (int i = tid; i < nx / 4; i += 256) d4[i] = s4[i];
-      const f4* z4 = reinterpret_cast<const f4*>(dZ2 + ((int64_t)f * NP + oy0 * OW) * 32);
+#pragma unroll
+      for (int j = 0; j < NVX; ++j) {
+        const int i = tid + 256 * j;
+        if (i < nx / 4) d4[i] = px4[j];
+      }
       f4* e4 = reinterpret_cast<f4*>(ds);
-      for (int i = tid; i < npe * 8; i += 256) e4[i] = i < npb * 8 ? z4[i] : f4zero();
+#pragma unroll
+      for (int j = 0; j < NVD; ++j) {
+        const int i = tid + 256 * j;
+        if (i < npe * 8) e4[i] = pd4[j];
+      }
     }
     __syncthreads();
+    if (it + (int)gridDim.x < n_items) load_item(it + gridDim.x);
 #pragma unroll 3
     for (int s = 0; s < npe / 2; ++s) {
       const int p = 2 * s + h;
