@@ -340,19 +340,23 @@ def main():
             torch.distributed.barrier()
 
     K = args.steps
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    # one HIP event pair around the K launches (vn_step runs on torch's current stream): the
+    # per-launch duration is the region's device time / K, inter-kernel gaps included. Event
+    # records between every launch cost ~5 us of device time each step and slowed the
+    # region itself by that much.
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    ev0.record()
     for k in range(K):
-        ev[k][0].record()
         env.step(actions[step], out=out)
-        ev[k][1].record()
         step += 1
+    ev1.record()
     torch.cuda.synchronize(dev)
     barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    kern_ms = ev0.elapsed_time(ev1) / K
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
