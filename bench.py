@@ -43,8 +43,8 @@ def alg_bytes_per_env_step(frame_bytes):
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=200)
-    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--steps", type=int, default=1000)
+    p.add_argument("--warmup", type=int, default=500)
     p.add_argument("--envs", type=int, default=4096, help="envs per GPU")
     p.add_argument("--scenes", type=int, default=20)
     p.add_argument("--cpu-seconds", type=float, default=10.0)
