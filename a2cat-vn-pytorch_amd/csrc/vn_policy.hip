@@ -285,6 +285,26 @@ struct EpiMaskParity {
   }
 };
 
+// EpiMaskParity over all G channel groups at once: column c of the product is channel
+// c % CIN of group c / CIN (input layout [n][G][H][W][CIN]).
+template <int H, int W, int S, int PY, int PX, int HYC, int WXC, int CIN>
+struct EpiMaskParityG {
+  float* out;
+  const float* X;
+  int G;
+  __device__ __forceinline__ int64_t index(int row, int col) const {
+    constexpr int per = HYC * WXC;
+    const int n = row / per;
+    const int r = row - n * per;
+    const int y = (r / WXC) * S + PY, x = (r % WXC) * S + PX;
+    return ((((int64_t)n * G + col / CIN) * H + y) * W + x) * CIN + col % CIN;
+  }
+  __device__ __forceinline__ float pre(int row, int col) const { return X[index(row, col)]; }
+  __device__ __forceinline__ void post(int row, int col, float v, float x, int) const {
+    out[index(row, col)] = x > 0.0f ? v : 0.0f;
+  }
+};
+
 struct EpiSlab {
   float* slab;
   int M, N;
@@ -578,6 +598,29 @@ inline void dgrad_class(const float* dz, const float* WT, float* out, const floa
   launch_gemm_x6<128, 32, 32, 4, 1>(fa, fb, ep, M, cin, 4 * COUT, st);
 }
 
+// All G input-channel groups of a class in one product (N = G * cin): the gathered and
+// split dZ operand serves twice the columns.
+template <int COUT, int CIN, int H, int W, int OH, int OW, int PY, int PX>
+inline void dgrad_class_groups(const float* dz, const float* WT, float* out, const float* X, int nimg, int G,
+                               hipStream_t st) {
+  constexpr int HYC = (H - PY + 1) / 2, WXC = (W - PX + 1) / 2;
+  const int M = nimg * HYC * WXC;
+  DgradA<COUT, 4, 2, OH, OW, HYC, WXC> fa{dz, M};
+  static_assert(CIN == 32, "conv3: two groups of 32 channels (W^T rows of 64)");
+  DgradB<COUT, 4, 2, 2 * CIN> fb{WT, G * CIN, 0, PY, PX};
+  EpiMaskParityG<H, W, 2, PY, PX, HYC, WXC, CIN> ep{out, X, G};
+  launch_gemm_x6<128, 64, 32, 2, 2>(fa, fb, ep, M, G * CIN, 4 * COUT, st);
+}
+
+template <int COUT, int CIN, int H, int W, int OH, int OW>
+inline void dgrad_all_classes_groups(const float* dz, const float* WT, float* out, const float* X, int nimg, int G,
+                                     hipStream_t st) {
+  dgrad_class_groups<COUT, CIN, H, W, OH, OW, 0, 0>(dz, WT, out, X, nimg, G, st);
+  dgrad_class_groups<COUT, CIN, H, W, OH, OW, 0, 1>(dz, WT, out, X, nimg, G, st);
+  dgrad_class_groups<COUT, CIN, H, W, OH, OW, 1, 0>(dz, WT, out, X, nimg, G, st);
+  dgrad_class_groups<COUT, CIN, H, W, OH, OW, 1, 1>(dz, WT, out, X, nimg, G, st);
+}
+
 template <int COUT, int CINF, int H, int W, int OH, int OW>
 inline void dgrad_all_classes(const float* dz, const float* WT, float* out, const float* X, int nimg, int g, int G,
                               int cin, hipStream_t st) {
@@ -795,8 +838,7 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
     using Im = NhwcIm2col<32, 4, 4, 2, G::OH2, G::OW2, G::OH3, G::OW3, 2>;
     Im2colT<Im> fbw{Im{a.X[1], n9}, 1024};
     launch_wgrad6<64, 128, 2, 2>(w.dz3, 64, 64, fbw, 1024, n9, w.slab, w.slab_cap, Gr + L.l[2].w, Gr + L.l[2].b, st);
-    for (int g = 0; g < 2; ++g)
-      dgrad_all_classes<64, 64, G::OH2, G::OW2, G::OH3, G::OW3>(w.dz3, T(2), w.dz2, a.X[1], n, g, 2, 32, st);
+    dgrad_all_classes_groups<64, 32, G::OH2, G::OW2, G::OH3, G::OW3>(w.dz3, T(2), w.dz2, a.X[1], n, 2, st);
   }
   // ---- conv2 (k4 s2): wgrad (needs X1), then dgrad into dz1 written over X1
   {
