@@ -720,7 +720,10 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
     NhwcIm2col<32, 4, 4, 2, G::OH2, G::OW2, G::OH3, G::OW3, 2> fa{a.X[1], n * G::OH3 * G::OW3};
     DenseRows fb{P + L.l[2].w, 1024, 64};
     EpiBiasAct ep{a.X[2], 64, P + L.l[2].b, 1};
-    launch_gemm_x6<64, 64, 32, 2, 2>(fa, fb, ep, fa.M, 64, 1024, st);
+    if constexpr (G::OH3 * G::OW3 >= 64)  // 174x174, 300x400: 128-row tiles (A split over more MFMAs)
+      launch_gemm_x6<128, 64, 32, 2, 2>(fa, fb, ep, fa.M, 64, 1024, st);
+    else  // 84x84: 3x3 maps, 64-row tiles keep >= 2 tiles per CU
+      launch_gemm_x6<64, 64, 32, 2, 2>(fa, fb, ep, fa.M, 64, 1024, st);
   }
   // conv4 1x1 (X3 -> X4)
   {
