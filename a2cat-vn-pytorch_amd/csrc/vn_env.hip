@@ -791,6 +791,20 @@ int vn_set_state(vn_ctx* c, const int32_t* src, vn_stream_t stream) {
   return VN_OK;
 }
 
+int vn_get_episode_returns(vn_ctx* c, float* dst, vn_stream_t stream) {
+  if (!c || !dst) return fail(VN_EINVAL, "vn_get_episode_returns: NULL argument");
+  DeviceGuard guard(c->device);
+  VN_HIP(hipMemcpyAsync(dst, c->ep_ret, (size_t)c->n_envs * 4, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return VN_OK;
+}
+
+int vn_set_episode_returns(vn_ctx* c, const float* src, vn_stream_t stream) {
+  if (!c || !src) return fail(VN_EINVAL, "vn_set_episode_returns: NULL argument");
+  DeviceGuard guard(c->device);
+  VN_HIP(hipMemcpyAsync(c->ep_ret, src, (size_t)c->n_envs * 4, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return VN_OK;
+}
+
 int vn_frame_arena(vn_ctx* c, const uint8_t** arena, int64_t* frame_bytes, int64_t* n_rows) {
   if (!c) return fail(VN_EINVAL, "vn_frame_arena: NULL ctx");
   if (arena) *arena = c->arena;

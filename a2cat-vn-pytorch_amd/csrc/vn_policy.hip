@@ -19,6 +19,8 @@
 #include <cstdlib>
 #include <mutex>
 #include <new>
+#include <map>
+#include <tuple>
 #include <unordered_map>
 
 #include "vn_common.h"
@@ -473,15 +475,17 @@ constexpr int OUT_LD = 8;  // [n][8]: logits 0..A-1, value at A
 constexpr int kConv1WgradBlocks = 512;  // x 4 wave slabs x 32 x 160 floats (fits the slab)
 constexpr int kConv2WgradBlocks = 512;  // x (32 x 512 + 32) floats (fits the slab)
 
-// Resident workgroups of a persistent kernel on the current device (cached per kernel).
+// Resident workgroups of a persistent kernel on the current device, cached per (device,
+// kernel, threads, LDS bytes): a process may drive policies on several devices.
 inline int resident_blocks(const void* kernel, int threads, size_t lds) {
   static std::mutex mu;
-  static std::unordered_map<const void*, int> cache;
-  std::lock_guard<std::mutex> lock(mu);
-  auto it = cache.find(kernel);
-  if (it != cache.end()) return it->second;
+  static std::map<std::tuple<int, const void*, int, size_t>, int> cache;
   int dev = 0, cus = 0, per = 0;
   (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lock(mu);
+  const auto key = std::make_tuple(dev, kernel, threads, lds);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, threads, lds) != hipSuccess || per < 1) per = 1;
   if (getenv("VN_DEBUG_OCC")) {
@@ -491,8 +495,23 @@ inline int resident_blocks(const void* kernel, int threads, size_t lds) {
             threads, lds, per, fa.numRegs, (size_t)fa.sharedSizeBytes);
   }
   const int blocks = std::max(1, per * std::max(cus, 1));
-  cache[kernel] = blocks;
+  cache[key] = blocks;
   return blocks;
+}
+
+// Opt-in to `lds` bytes of dynamic LDS for `kernel` on the current device, once per (device,
+// kernel) and again only if a larger size is asked for (the attribute is per device).
+inline hipError_t ensure_dyn_lds(const void* kernel, size_t lds) {
+  static std::mutex mu;
+  static std::map<std::pair<int, const void*>, size_t> done;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lock(mu);
+  size_t& have = done[std::make_pair(dev, kernel)];
+  if (have >= lds) return hipSuccess;
+  const hipError_t e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e == hipSuccess) have = lds;
+  return e;
 }
 
 inline dim3 grid_for(int M, int N, int BM, int BN, int splits = 1) {
@@ -701,11 +720,7 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
   if constexpr (conv2_fwd_x6_fits<G::OH1, G::OW1, G::OH2, G::OW2>()) {
     using Bd = Conv2FwdBand<G::OH1, G::OW1, G::OH2, G::OW2>;
     const void* kfn = (const void*)conv2_fwd_x6_kernel<G::OH1, G::OW1, G::OH2, G::OW2>;
-    static bool attr = false;  // > 64 KiB of dynamic LDS needs the opt-in attribute
-    if (!attr) {
-      VN_HIP(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)Bd::LDS));
-      attr = true;
-    }
+    VN_HIP(ensure_dyn_lds(kfn, Bd::LDS));  // > 64 KiB dynamic LDS: opt-in
     const int blocks = std::min(frames * Bd::NB, resident_blocks(kfn, 512, Bd::LDS));
     hipLaunchKernelGGL((conv2_fwd_x6_kernel<G::OH1, G::OW1, G::OH2, G::OW2>), dim3(blocks), dim3(512), Bd::LDS, st,
                        a.X[0], P + L.l[1].w, P + L.l[1].b, a.X[1], frames);
@@ -850,12 +865,7 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
     const int blocks = std::min(frames * Bd2::NB, kConv2WgradBlocks);
     constexpr size_t lds = conv2_wgrad_lds<G::OH1, G::OW1, G::OH2, G::OW2>();
     if constexpr (lds <= 80 * 1024) {  // two workgroups per CU (bands of output rows)
-      static bool attr = false;
-      if (!attr) {
-        VN_HIP(hipFuncSetAttribute((const void*)conv2_wgrad_kernel<G::OH1, G::OW1, G::OH2, G::OW2>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        attr = true;
-      }
+      VN_HIP(ensure_dyn_lds((const void*)conv2_wgrad_kernel<G::OH1, G::OW1, G::OH2, G::OW2>, lds));  // > 64 KiB dynamic LDS: opt-in
       float* bias_slab = w.slab + (int64_t)blocks * 32 * 512;
       hipLaunchKernelGGL((conv2_wgrad_kernel<G::OH1, G::OW1, G::OH2, G::OW2>), dim3(blocks), dim3(256), lds, st,
                          a.X[0], w.dz2, frames, w.slab, bias_slab);
@@ -877,11 +887,7 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
           constexpr int NW = conv2_dgrad_x6_waves<G::OH1, G::OW1, G::OH2, G::OW2>();
           const void* kfn = (const void*)conv2_dgrad_x6_kernel<G::OH1, G::OW1, G::OH2, G::OW2, NW>;
           constexpr size_t lds = conv2_dgrad_x6_lds<G::OH1, G::OW1, G::OH2, G::OW2>();
-          static bool attr = false;  // > 64 KiB of dynamic LDS needs the opt-in attribute
-          if (!attr) {
-            VN_HIP(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-            attr = true;
-          }
+          VN_HIP(ensure_dyn_lds(kfn, lds));  // > 64 KiB dynamic LDS: opt-in
           const int blocks = std::min(frames, resident_blocks(kfn, NW * 64, lds));
           hipLaunchKernelGGL((conv2_dgrad_x6_kernel<G::OH1, G::OW1, G::OH2, G::OW2, NW>), dim3(blocks), dim3(NW * 64), lds,
                              st, w.dz2, T(1), a.M1, a.X[0], frames);
@@ -929,12 +935,7 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
       const int frames = 2 * n;
       constexpr int CP = (G::OH1 * G::OW1 <= 400) ? (G::OH1 * G::OW1 + 7) / 8 * 8 : 448;
       constexpr size_t lds = conv1_wgrad_lds<H0, W0, CP>();
-      static bool attr = false;  // > 64 KiB of dynamic LDS needs the opt-in attribute
-      if (!attr) {
-        VN_HIP(hipFuncSetAttribute((const void*)conv1_wgrad_kernel<H0, W0, G::OH1, G::OW1, CP>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        attr = true;
-      }
+      VN_HIP(ensure_dyn_lds((const void*)conv1_wgrad_kernel<H0, W0, G::OH1, G::OW1, CP>, lds));  // > 64 KiB dynamic LDS: opt-in
       const int blocks = std::min({frames, kConv1WgradBlocks,
                                    resident_blocks((const void*)conv1_wgrad_kernel<H0, W0, G::OH1, G::OW1, CP>, 256, lds)});
       hipLaunchKernelGGL((conv1_wgrad_kernel<H0, W0, G::OH1, G::OW1, CP>), dim3(blocks), dim3(256), lds, st, src, frames,
@@ -1253,11 +1254,7 @@ inline void launch_aux2(const float* A1, int n, const float* W2, const float* b2
                         const vn_aux_targets* tg, float weight, float* dpred, float* stats, hipStream_t st) {
   constexpr size_t lds = aux2_lds<AH, AW>();
   const void* kfn = (const void*)aux_deconv2_kernel<AH, AW, PH, PW, LOSS>;
-  static bool attr = false;  // > 64 KiB of dynamic LDS needs the opt-in attribute
-  if (!attr) {
-    (void)hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr = true;
-  }
+  (void)ensure_dyn_lds(kfn, lds);  // > 64 KiB dynamic LDS: opt-in (a failure surfaces at the launch check)
   constexpr int SPI = aux2_spi<AH, AW>();
   const int blocks = std::min((n + SPI - 1) / SPI, resident_blocks(kfn, kAux2Threads, lds));
   hipLaunchKernelGGL((aux_deconv2_kernel<AH, AW, PH, PW, LOSS>), dim3(blocks), dim3(kAux2Threads), lds, st, A1, n, W2,
@@ -1340,11 +1337,7 @@ int aux_backward_impl(const PolicyLayout& L, const float* P, const float* X4, in
     // second layer in one pass: dW2, db2, dA1 (masked, over A1) and db1
     const void* kfn = (const void*)aux_backward2_kernel<AH, AW, PH, PW>;
     constexpr size_t lds = auxb_lds<PH, PW>();
-    static bool attr = false;
-    if (!attr) {
-      (void)hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      attr = true;
-    }
+    VN_HIP(ensure_dyn_lds(kfn, lds));  // > 64 KiB dynamic LDS: opt-in
     const int blocks = std::min(n, std::min(resident_blocks(kfn, kAuxBThreads, lds), kColsumBlocks));
     hipLaunchKernelGGL((aux_backward2_kernel<AH, AW, PH, PW>), dim3(blocks), dim3(kAuxBThreads), lds, st, A1, dP, n,
                        P + L.aw2, w.slab);

@@ -63,6 +63,8 @@ SIGNATURES = {
     "vn_random_actions": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p]),
     "vn_get_state": (c_int, [c_void_p, c_void_p, c_void_p]),
     "vn_set_state": (c_int, [c_void_p, c_void_p, c_void_p]),
+    "vn_get_episode_returns": (c_int, [c_void_p, c_void_p, c_void_p]),
+    "vn_set_episode_returns": (c_int, [c_void_p, c_void_p, c_void_p]),
     "vn_frame_arena": (c_int, [c_void_p, P(c_void_p), P(c_int64), P(c_int64)]),
     "vn_scene_row_base": (c_int, [c_void_p, c_int, P(c_int64)]),
     "vn_error_flags_sync": (c_int, [c_void_p, P(c_uint32), c_int]),

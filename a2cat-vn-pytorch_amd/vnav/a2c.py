@@ -19,8 +19,9 @@ With a recurrent net (``recurrent=True``) each step also runs the LSTM core: the
 zeroed where an episode starts (mask m_t = 1 - done_{t-1}); the update back-propagates
 through the T steps of the rollout (truncated BPTT) and (h, c) carry on to the next.
 
-With ``aux_weight > 0`` (AuxiliaryTrainer, experiments/ai2_auxiliary/trainer.py:21-55:
-auxiliary_weight 0.05) the update adds the deconv loss of AuxiliaryBigGoalHouseModel's
+With ``aux_weight > 0`` (AuxiliaryTrainer, experiments/ai2_auxiliary/trainer.py:21-55; its
+default auxiliary_weight is 0.05, the logged thor-cached-auxiliary experiment sets 0.1 at
+experiments/thor_cached_auxiliary.py:42) the update adds the deconv loss of AuxiliaryBigGoalHouseModel's
 depth / segmentation / goal-segmentation heads against avg-pooled targets gathered from
 the env's aux arena by row. The reference computes it on a sequence sampled from
 UnrealTrainer's replay buffer (deep_rl, absent); here it uses the on-policy rollout batch
@@ -295,7 +296,8 @@ class A2CTrainer:
 
     def state_dict(self):
         sd = {"params": self.params.detach().cpu(), "square_avg": self.square_avg.cpu(),
-              "env_state": self.env.get_state().cpu(), "num_updates": self.num_updates,
+              "env_state": self.env.get_state().cpu(), "env_ep_return": self.env.get_episode_returns().cpu(),
+              "num_updates": self.num_updates,
               "total_steps": self.total_steps, "seed": self.seed}
         if self.recurrent:
             for k in self._RECURRENT_STATE:
@@ -306,6 +308,7 @@ class A2CTrainer:
         self.params.copy_(sd["params"].to(self.device))
         self.square_avg.copy_(sd["square_avg"].to(self.device))
         self.env.set_state(sd["env_state"])
+        self.env.set_episode_returns(sd["env_ep_return"])
         self.num_updates = int(sd["num_updates"])
         self.total_steps = int(sd["total_steps"])
         if self.recurrent:

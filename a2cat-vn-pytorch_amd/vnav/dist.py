@@ -58,9 +58,12 @@ def reduce_metrics_(m, n_mean, group=None):
 
 
 def broadcast_params_(flat, src=0, group=None):
+    """Broadcast from the group's rank `src` (a rank WITHIN `group`, translated to the global
+    rank torch.distributed.broadcast expects, so subgroups without global rank 0 work)."""
     world, _ = world_of(group)
     if world > 1:
-        dist.broadcast(flat, src=src, group=group)
+        gsrc = src if group is None else dist.get_global_rank(group, src)
+        dist.broadcast(flat, src=gsrc, group=group)
     return flat
 
 

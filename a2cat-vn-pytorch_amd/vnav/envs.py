@@ -245,6 +245,18 @@ class VectorEnv:
         buf = buf.to(device=self.device, dtype=torch.int32).contiguous()
         _lib.check(self.lib.vn_set_state(self._ctx, _lib.ptr(buf), self._stream()), "vn_set_state")
 
+    def get_episode_returns(self):
+        """Running return of every env's unfinished episode ([E] f32, device)."""
+        buf = torch.empty(self.num_envs, dtype=torch.float32, device=self.device)
+        _lib.check(self.lib.vn_get_episode_returns(self._ctx, _lib.ptr(buf), self._stream()),
+                   "vn_get_episode_returns")
+        return buf
+
+    def set_episode_returns(self, buf):
+        buf = buf.to(device=self.device, dtype=torch.float32).contiguous()
+        _lib.check(self.lib.vn_set_episode_returns(self._ctx, _lib.ptr(buf), self._stream()),
+                   "vn_set_episode_returns")
+
     def frame_arena(self):
         """(arena uint8 tensor view [rows, H, W, C] over the scene cache, row bases per scene)."""
         p, fb, rows = ctypes.c_void_p(), ctypes.c_int64(), ctypes.c_int64()

@@ -33,6 +33,9 @@ FP32_MFMA_PEAK_TFLOPS = 157.3  # dense f32 MFMA = f32 vector peak (MI355X_MICROA
 # the reference's only throughput record: deep_rl fps of thor-cached-auxiliary (174x174, LSTM +
 # aux deconv, 4 envs, 1 GPU), steady-state median, BASELINE.md §2 / outputs/output.txt
 REFERENCE_LOG_FPS = 106.0
+# auxiliary_weight of the logged experiment (experiments/thor_cached_auxiliary.py:42; 0.05 is only
+# AuxiliaryTrainer's default, experiments/ai2_auxiliary/trainer.py:25)
+AUX_WEIGHT_LOGGED = 0.1
 
 
 def alg_bytes_per_env_step(frame_bytes):
@@ -374,15 +377,16 @@ def main():
             torch.cuda.empty_cache()
         if not args.no_train_ref:
             # thor-cached-auxiliary as logged (outputs/output.txt): 174x174 scenes, LSTM policy,
-            # aux deconv loss (weight 0.05, ai2_auxiliary/trainer.py:25), 4 scenes
+            # aux deconv loss with the experiment's weight 0.1 (experiments/thor_cached_auxiliary.py:42
+            # overrides AuxiliaryTrainer's 0.05 default, ai2_auxiliary/trainer.py:25), 4 scenes
             train_ref = bench_train(args, aux_scenes(4, (174, 174, 3)), dev, world, rank, recurrent=True,
-                                    aux_weight=0.05, updates=3, warmup=1,
+                                    aux_weight=AUX_WEIGHT_LOGGED, updates=3, warmup=1,
                                     model="AuxiliaryBigGoalHouseModel (LSTM + deconv heads), 174x174")
             train_ref["reference_log_fps"] = REFERENCE_LOG_FPS
             torch.cuda.empty_cache()
         if args.c5:
             train_c5 = bench_train(args, aux_scenes(4, (300, 400, 3)), dev, world, rank, recurrent=True,
-                                   aux_weight=0.05, envs=512, updates=3, warmup=1,
+                                   aux_weight=AUX_WEIGHT_LOGGED, envs=512, updates=3, warmup=1,
                                    model="AuxiliaryBigGoalHouseModel (LSTM + deconv heads), 300x400 (config C5)")
             torch.cuda.empty_cache()
     if rank == 0:

@@ -156,6 +156,12 @@ int vn_gather_rows(const uint8_t* src_dev, int64_t row_bytes, const int32_t* row
  * Order: scene, state, goal, obs_state, elapsed, episode(reset count), sched_pos. */
 int vn_get_state(vn_ctx* ctx, int32_t* dst_dev_7xE, vn_stream_t stream);
 int vn_set_state(vn_ctx* ctx, const int32_t* src_dev_7xE, vn_stream_t stream);
+/* Running (unfinished) episode return per env, [n_envs] f32 on the device: the rest of the
+ * per-env state a checkpoint needs (the finished-episode return RewardCollector reports,
+ * A18, is this sum at done). Tasks, scene assignment and curriculum are configuration and
+ * are re-applied by the caller. */
+int vn_get_episode_returns(vn_ctx* ctx, float* dst_dev_E, vn_stream_t stream);
+int vn_set_episode_returns(vn_ctx* ctx, const float* src_dev_E, vn_stream_t stream);
 
 /* Scene-cache arena: all scenes' frames back to back, row = frame. */
 int vn_frame_arena(vn_ctx* ctx, const uint8_t** arena_dev, int64_t* frame_bytes,

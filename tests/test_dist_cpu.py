@@ -99,3 +99,42 @@ def test_shard_covers_all_envs():
         assert spans[0][0] == 0 and sum(c for _, c in spans) == n
         for (s0, c0), (s1, _) in zip(spans, spans[1:]):
             assert s0 + c0 == s1
+
+
+def _bcast_worker(rank, world, port, q):
+    import sys
+    for p in (REPO, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+    from vnav import dist as vdist
+    vdist.init_distributed(backend="gloo")
+    sub = dist.new_group([1, 2])  # a subgroup without global rank 0: every rank must call new_group
+    flat = torch.full((16,), float(rank))
+    if rank in (1, 2):
+        vdist.broadcast_params_(flat, group=sub)  # src = the subgroup's rank 0 = global rank 1
+        trainer_world = vdist.world_of(sub)
+    else:
+        trainer_world = None
+    q.put((rank, flat.numpy(), trainer_world))
+    dist.destroy_process_group()
+
+
+def test_gloo_subgroup_broadcast_uses_group_rank():
+    """broadcast_params_(group=g) sends from g's first member, not from global rank 0."""
+    world = 3
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_bcast_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert np.all(res[0][1] == 0.0)            # rank 0 is not in the group: untouched
+    assert np.all(res[1][1] == 1.0) and np.all(res[2][1] == 1.0)
+    assert res[1][2] == (2, 0) and res[2][2] == (2, 1)

@@ -1,5 +1,5 @@
-"""A2CTrainer: one full update on the GPU vs the same update restated on the CPU oracle
-(torch fp32 model + oracle A2C) from the rollout the GPU produced."""
+"""A2CTrainer: a full update on the GPU vs the same update restated on the CPU oracle
+(torch fp32 model + oracle A2C) from the rollout the GPU produced, and checkpoint/resume."""
 import numpy as np
 import pytest
 import torch
@@ -18,7 +18,13 @@ def test_update_matches_cpu_oracle():
         s.observations = synth_frames(s.synth_id, np.arange(s.n_states), s.frame_shape)
     env = vnav.VectorEnv(sc, 12, seed=21, max_episode_steps=6)
     tr = vnav.A2CTrainer(env, num_steps=5, seed=3, max_time_steps=1e6)
+    # compare the SECOND update: its RMSprop step divides by the square_avg carried from the
+    # first, so the step size depends on the gradient's magnitude (the first step from
+    # square_avg = 0 is ~10*lr*sign(g) and would only check signs)
+    tr.step(sync=True)
     p0 = tr.params.detach().clone()
+    sq0 = tr.square_avg.detach().clone()
+    assert sq0.abs().max().item() > 0
     tr.rollout()
     rows_img = tr.rows_img.cpu().numpy()
     rows_goal = tr.rows_goal.cpu().numpy()
@@ -47,16 +53,18 @@ def test_update_matches_cpu_oracle():
     params = [m.weight for m in (ref.conv1, ref.conv2, ref.conv3, ref.conv4, ref.fc, ref.policy_logits, ref.critic)]
     params += [m.bias for m in (ref.conv1, ref.conv2, ref.conv3, ref.conv4, ref.fc, ref.policy_logits, ref.critic)]
     grads = [p.grad.clone() for p in params]
-    sq = [torch.zeros_like(p) for p in params]
-    with torch.no_grad():
-        oa2c.clip_and_rmsprop([p.data for p in params], grads, sq, lr)
-    new = tr.net.to_reference(tr.params)
     names = ["shared_base.0.0", "shared_base.0.2", "conv_base.0.0", "conv_base.0.2", "conv_merge.0.1",
              "policy_logits.0", "critic.0"]
     keys = [n + ".weight" for n in names] + [n + ".bias" for n in names]
-    for k, p, p_old in zip(keys, params, [tr.net.to_reference(p0)[k] for k in keys]):
+    sq_old = tr.net.to_reference(sq0)
+    sq = [sq_old[k].clone().view_as(p) for k, p in zip(keys, params)]
+    with torch.no_grad():
+        oa2c.clip_and_rmsprop([p.data for p in params], grads, sq, lr)
+    new = tr.net.to_reference(tr.params)
+    old = tr.net.to_reference(p0)
+    for k, p, p_old in zip(keys, params, [old[k].view_as(p) for k in keys]):
         step_ref = (p.data - p_old)
-        step_gpu = (new[k] - p_old)
+        step_gpu = (new[k].view_as(p) - p_old)
         scale = step_ref.abs().max().item()
         assert (step_gpu - step_ref).abs().max().item() <= 2e-3 * scale + 1e-9, k
 
@@ -82,3 +90,37 @@ def test_trainer_learns_on_small_scene():
     early = np.nanmean(lengths[5:20])
     late = np.nanmean(lengths[-10:])
     assert np.isfinite(late) and late < 0.8 * early, (early, late)
+
+
+@pytest.mark.parametrize("recurrent", [False, True])
+def test_checkpoint_resume_is_exact(recurrent):
+    """state_dict after K updates, restored into a fresh env + trainer, continues exactly as
+    the uninterrupted run: parameters, optimiser state and the logged metrics (episode
+    count / return / length, which need the running per-env returns) match bit for bit."""
+    import dataclasses
+    import vnav
+    # a step penalty and a collision penalty, so the running returns of in-flight episodes
+    # are non-zero (with the cached reward table (1, -0, 0) they are 0 until the goal)
+    sc = [dataclasses.replace(vnav.synthetic_scene(k), rewards=(1.0, -0.01, -0.1)) for k in range(2)]
+
+    def make():
+        env = vnav.VectorEnv(sc, 64, seed=5, max_episode_steps=12)
+        return vnav.A2CTrainer(env, num_steps=5, seed=9, max_time_steps=1e6, recurrent=recurrent)
+
+    keys = ("value_loss", "action_loss", "entropy", "episodes", "reward", "episode_length", "grad_norm")
+    a = make()
+    for _ in range(3):
+        a.step(sync=True)
+    sd = {k: (v.clone() if torch.is_tensor(v) else v) for k, v in a.state_dict().items()}
+    assert sd["env_ep_return"].abs().sum().item() > 0  # some episodes are in flight with reward
+    ma = [a.step(sync=True) for _ in range(3)]
+    pa, sqa = a.params.detach().cpu(), a.square_avg.cpu()
+    del a
+    b = make()
+    b.load_state_dict(sd)
+    mb = [b.step(sync=True) for _ in range(3)]
+    assert torch.equal(pa, b.params.detach().cpu())
+    assert torch.equal(sqa, b.square_avg.cpu())
+    for x, y in zip(ma, mb):
+        for k in keys:
+            assert (x[k] == y[k]) or (np.isnan(x[k]) and np.isnan(y[k])), (k, x[k], y[k])
