@@ -62,7 +62,7 @@ def test_update_matches_cpu_oracle():
         oa2c.clip_and_rmsprop([p.data for p in params], grads, sq, lr)
     new = tr.net.to_reference(tr.params)
     old = tr.net.to_reference(p0)
-    for k, p, p_old in zip(keys, params, [old[k].view_as(p) for k in keys]):
+    for k, p, p_old in zip(keys, params, [old[k].view_as(q) for k, q in zip(keys, params)]):
         step_ref = (p.data - p_old)
         step_gpu = (new[k].view_as(p) - p_old)
         scale = step_ref.abs().max().item()
