@@ -115,6 +115,60 @@ __global__ __launch_bounds__(256) void k_wave_env_nt(Args a) {
   }
 }
 
+// K1b: per-stream policy, CV bits: 1/2 = nt store image/goal output, 4/8 = nt load image/goal
+template <bool NT>
+__device__ __forceinline__ uint4 ldp(const uint4* p) {
+  if constexpr (NT) {
+    uint4 v;
+    v.x = __builtin_nontemporal_load(&p->x);
+    v.y = __builtin_nontemporal_load(&p->y);
+    v.z = __builtin_nontemporal_load(&p->z);
+    v.w = __builtin_nontemporal_load(&p->w);
+    return v;
+  } else {
+    return *p;
+  }
+}
+template <bool NT>
+__device__ __forceinline__ void stp(uint4* p, uint4 v) {
+  if constexpr (NT) {
+    __builtin_nontemporal_store(v.x, &p->x);
+    __builtin_nontemporal_store(v.y, &p->y);
+    __builtin_nontemporal_store(v.z, &p->z);
+    __builtin_nontemporal_store(v.w, &p->w);
+  } else {
+    *p = v;
+  }
+}
+template <int CV>
+__global__ __launch_bounds__(256) void k_policy(Args a) {
+  constexpr int U = 4;
+  const int lane = threadIdx.x & 63;
+  const int e = uni(blockIdx.x * 4 + (threadIdx.x >> 6));
+  const int64_t ir = a.img_rows[a.set * E + e], gr = a.goal_rows[e];
+  const uint4* s1 = reinterpret_cast<const uint4*>(a.arena + ir * F);
+  const uint4* s2 = reinterpret_cast<const uint4*>(a.arena + gr * F);
+  uint4* d1 = reinterpret_cast<uint4*>(a.obs + (int64_t)e * F);
+  uint4* d2 = reinterpret_cast<uint4*>(a.goal + (int64_t)e * F);
+  int i = lane;
+  for (; i + 64 * (U - 1) < NV; i += 64 * U) {
+    uint4 x[U], y[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) x[u] = ldp<(CV & 4) != 0>(s1 + i + 64 * u);
+#pragma unroll
+    for (int u = 0; u < U; ++u) y[u] = ldp<(CV & 8) != 0>(s2 + i + 64 * u);
+#pragma unroll
+    for (int u = 0; u < U; ++u) stp<(CV & 1) != 0>(d1 + i + 64 * u, x[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) stp<(CV & 2) != 0>(d2 + i + 64 * u, y[u]);
+  }
+  for (; i < NV; i += 64) {
+    const uint4 x = ldp<(CV & 4) != 0>(s1 + i), y = ldp<(CV & 8) != 0>(s2 + i);
+    stp<(CV & 1) != 0>(d1 + i, x);
+    stp<(CV & 2) != 0>(d2 + i, y);
+  }
+}
+
 // K2: one wave per frame (2 waves per env), WG = 4 waves = 2 envs
 template <int U>
 __global__ __launch_bounds__(256) void k_wave_frame(Args a) {
@@ -162,6 +216,39 @@ __global__ __launch_bounds__(256) void k_wg_env(Args a) {
     d1[i] = x;
     d2[i] = y;
   }
+}
+
+// K6: traffic split probes (same geometry as K0, nt image loads): MODE 0 = read both frames,
+// write image output only; 1 = read image only, write both outputs; 2 = write both outputs
+// only (no reads); 3 = read both only (xor into one dword per lane)
+template <int MODE>
+__global__ __launch_bounds__(256) void k_probe(Args a) {
+  const int lane = threadIdx.x & 63;
+  const int e = uni(blockIdx.x * 4 + (threadIdx.x >> 6));
+  const int64_t ir = a.img_rows[a.set * E + e], gr = a.goal_rows[e];
+  const uint4* s1 = reinterpret_cast<const uint4*>(a.arena + ir * F);
+  const uint4* s2 = reinterpret_cast<const uint4*>(a.arena + gr * F);
+  uint4* d1 = reinterpret_cast<uint4*>(a.obs + (int64_t)e * F);
+  uint4* d2 = reinterpret_cast<uint4*>(a.goal + (int64_t)e * F);
+  uint32_t acc = 0;
+  for (int i = lane; i < NV; i += 64) {
+    if constexpr (MODE == 0) {
+      const uint4 x = s1[i], y = s2[i];
+      d1[i] = make_uint4(x.x ^ y.x, x.y ^ y.y, x.z ^ y.z, x.w ^ y.w);
+    } else if constexpr (MODE == 1) {
+      const uint4 x = s1[i];
+      d1[i] = x;
+      d2[i] = x;
+    } else if constexpr (MODE == 2) {
+      const uint4 x = make_uint4(i, e, 0, 0);
+      d1[i] = x;
+      d2[i] = x;
+    } else {
+      const uint4 x = s1[i], y = s2[i];
+      acc ^= x.x ^ y.y ^ x.z ^ y.w;
+    }
+  }
+  if constexpr (MODE == 3) if (acc == 0x12345678u) d1[lane] = make_uint4(acc, 0, 0, 0);
 }
 
 // K4: flat float4 copy of the same byte count (2 x E x F read, same written), grid-stride
@@ -228,6 +315,16 @@ int main(int argc, char** argv) {
       hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, b);
     };
   };
+  {
+    char nm[64];
+#define POL(cv)                                                         \
+  snprintf(nm, sizeof nm, "policy cv%-2d (st i%d g%d, nt-ld i%d g%d)", cv, cv & 1, (cv >> 1) & 1, (cv >> 2) & 1, \
+           (cv >> 3) & 1);                                              \
+  rep(nm, time_it(envk(k_policy<cv>, E / 4), reps));
+    for (int round = 0; round < 2; ++round) {
+      POL(0) POL(1) POL(2) POL(3) POL(4) POL(5) POL(6) POL(7) POL(8) POL(9) POL(10) POL(11) POL(12) POL(13) POL(14) POL(15)
+    }
+  }
   rep("wave/env U4 (vn_step)", time_it(envk(k_wave_env<4>, E / 4), reps));
   rep("wave/env U2", time_it(envk(k_wave_env<2>, E / 4), reps));
   rep("wave/env U8", time_it(envk(k_wave_env<8>, E / 4), reps));
@@ -239,6 +336,30 @@ int main(int argc, char** argv) {
   rep("wg/env U2", time_it(envk(k_wg_env<2>, E), reps));
   rep("wg/env U1", time_it(envk(k_wg_env<1>, E), reps));
   rep("wave/env U4 (again)", time_it(envk(k_wave_env<4>, E / 4), reps));
+  {  // traffic probes; bytes column still counts the full 4F per env
+    rep("probe rd2 wr1 (3F)", time_it(envk(k_probe<0>, E / 4), reps));
+    rep("probe rd1 wr2 (3F)", time_it(envk(k_probe<1>, E / 4), reps));
+    rep("probe wr2 only (2F)", time_it(envk(k_probe<2>, E / 4), reps));
+    rep("probe rd2 only (2F)", time_it(envk(k_probe<3>, E / 4), reps));
+    // hot goal rows: every env's goal among 64 rows (L2/MALL resident)
+    std::vector<int> hot(E);
+    for (int i = 0; i < E; ++i) hot[i] = g[i % 64];
+    int* hot_rows;
+    CK(hipMalloc(&hot_rows, (size_t)E * 4));
+    CK(hipMemcpy(hot_rows, hot.data(), hot.size() * 4, hipMemcpyHostToDevice));
+    Args H = A;
+    H.goal_rows = hot_rows;
+    auto hk = [&](auto kern) {
+      return [=](int i) mutable {
+        Args b = H;
+        b.set = i % SETS;
+        hipLaunchKernelGGL(kern, dim3(E / 4), dim3(256), 0, 0, b);
+      };
+    };
+    rep("hot goals U4", time_it(hk(k_wave_env<4>), reps));
+    rep("hot goals U4 nt-store", time_it(hk(k_wave_env_nt<4, false, true>), reps));
+    rep("hot goals U4 nt-load", time_it(hk(k_wave_env_nt<4, true, false>), reps));
+  }
   // flat copies of 2*E*F bytes (src = first rows of the arena; dst = obs..goal contiguous? use obs+goal as one)
   uint8_t* dst;
   CK(hipMalloc(&dst, (size_t)2 * E * F));
