@@ -1,0 +1,323 @@
+// gemm_x6_bench.hip — where the time of the split-bf16 ("x6") GEMM core goes, at the LSTM
+// gates shape (M 4096, N 2048, K 1032; DenseRows x DenseRows). Diagnostic tool, not part of
+// the library. Variants of the core loop (flags of xk below):
+//   LOADS 0: no global loads (LDS filled once: MFMA + LDS-read bound)
+//   SPLIT 0: commit writes only the hi plane (the VALU split and two thirds of the LDS
+//            writes removed; numerically wrong, timing only)
+//   PF 2   : two register stages of global prefetch
+//   PRIO 1 : s_setprio 1 around the MFMA cluster
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/gemm_x6_bench.hip -o tools/gemm_x6_bench
+#include "../a2cat-vn-pytorch_amd/csrc/vn_policy.hip"
+
+#include <cstdio>
+#include <vector>
+
+using namespace vn;
+
+namespace vn {
+int fail(int code, const std::string& msg) {
+  fprintf(stderr, "%s\n", msg.c_str());
+  return code;
+}
+int hip_fail(hipError_t e, const char* what) {
+  fprintf(stderr, "%s: %s\n", what, hipGetErrorString(e));
+  return VN_EHIP;
+}
+}  // namespace vn
+
+__global__ void fill_kernel(float* p, int64_t n, uint32_t seed, float lo) {
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const uint32_t h = frame_hash(seed, (uint32_t)(i >> 32), (uint32_t)i);
+    p[i] = lo + (float)(h >> 8) * (1.0f / 16777216.0f);
+  }
+}
+
+static float* dalloc(int64_t n, uint32_t seed, float lo) {
+  float* p = nullptr;
+  if (hipMalloc(&p, n * 4) != hipSuccess) {
+    printf("alloc failed\n");
+    exit(1);
+  }
+  hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, 0, p, n, seed, lo);
+  return p;
+}
+
+template <class F>
+static float timeit(F f, int reps = 20) {
+  hipEvent_t a, b;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  for (int i = 0; i < 3; ++i) f();
+  hipDeviceSynchronize();
+  hipEventRecord(a, 0);
+  for (int r = 0; r < reps; ++r) f();
+  hipEventRecord(b, 0);
+  hipEventSynchronize(b);
+  float ms;
+  hipEventElapsedTime(&ms, a, b);
+  return ms / reps;
+}
+
+template <int ROWS, int BK, int LDK>
+__device__ __forceinline__ void commit_hi_only(const f4* r, uint16_t* s, int tid) {
+  constexpr int Q = BK / 4, T = ROWS * Q, NS = (T + 255) / 256;
+#pragma unroll
+  for (int j = 0; j < NS; ++j) {
+    const int i = tid + j * 256;
+    if (T % 256 == 0 || i < T) {
+      const int rr = i / Q, q = i - (i / Q) * Q;
+      uint32_t t0[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) t0[e] = __float_as_uint(r[j][e]) >> 16;
+      uint16_t* d = s + rr * LDK + 4 * q;
+      *reinterpret_cast<uint2*>(d) = uint2{t0[0] | (t0[1] << 16), t0[2] | (t0[3] << 16)};
+    }
+  }
+}
+
+template <int BM, int BN, int BK, int WM, int WN, int LOADS, int SPLIT, int PF, int PRIO, class FA, class FB, class EP>
+__global__ __launch_bounds__(256) void xk(FA fa, FB fb, EP ep, int M, int N, int K) {
+  constexpr int LDK = BK + 8;
+  constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
+  constexpr int NA = (FA::template slots<BM, BK>() + 255) / 256;
+  constexpr int NB = (FB::template slots<BN, BK>() + 255) / 256;
+  __shared__ __attribute__((aligned(16))) uint16_t As[3 * BM * LDK];
+  __shared__ __attribute__((aligned(16))) uint16_t Bs[3 * BN * LDK];
+  typedef float f16v_ __attribute__((ext_vector_type(16)));
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WM, wn = wave / WM;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int kb = 0, ke = K;
+  f16v_ acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+  const int ra = (wm * TM * 32 + (lane & 31)) * LDK + 8 * (lane >> 5);
+  const int rb = (wn * TN * 32 + (lane & 31)) * LDK + 8 * (lane >> 5);
+  f4 pa[PF][NA], pb[PF][NB];
+  fa.template fetch<BM, BK>(pa[0], m0, kb, ke, tid);
+  fb.template fetch<BN, BK>(pb[0], n0, kb, ke, tid);
+  if constexpr (PF == 2) {
+    fa.template fetch<BM, BK>(pa[1], m0, kb + BK, ke, tid);
+    fb.template fetch<BN, BK>(pb[1], n0, kb + BK, ke, tid);
+  }
+  if constexpr (LOADS == 0) {
+    commit_x6<BM, BK, LDK, FA>(pa[0], As, tid);
+    commit_x6<BN, BK, LDK, FB>(pb[0], Bs, tid);
+    __syncthreads();
+  }
+  auto tile = [&](auto stage, int k0) {
+    constexpr int S = decltype(stage)::value;
+    if constexpr (LOADS) {
+      if constexpr (SPLIT) {
+        commit_x6<BM, BK, LDK, FA>(pa[S], As, tid);
+        commit_x6<BN, BK, LDK, FB>(pb[S], Bs, tid);
+      } else {
+        commit_hi_only<BM, BK, LDK>(pa[S], As, tid);
+        commit_hi_only<BN, BK, LDK>(pb[S], Bs, tid);
+      }
+      __syncthreads();
+      if (k0 + PF * BK < ke) {
+        fa.template fetch<BM, BK>(pa[S], m0, k0 + PF * BK, ke, tid);
+        fb.template fetch<BN, BK>(pb[S], n0, k0 + PF * BK, ke, tid);
+      }
+    }
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 16) {
+      bf16x8_ a[3][TM], b[3][TN];
+#pragma unroll
+      for (int t = 0; t < 3; ++t) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          a[t][i] = *reinterpret_cast<const bf16x8_*>(&As[t * BM * LDK + ra + i * 32 * LDK + kk]);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          b[t][j] = *reinterpret_cast<const bf16x8_*>(&Bs[t * BN * LDK + rb + j * 32 * LDK + kk]);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][i], b[0][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[2][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[1][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[0][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[1][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[0][j], acc[i][j], 0, 0, 0);
+        }
+    }
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+    if constexpr (LOADS) __syncthreads();
+  };
+  if constexpr (PF == 2) {
+    for (int k0 = kb; k0 < ke; k0 += 2 * BK) {
+      tile(std::integral_constant<int, 0>{}, k0);
+      if (k0 + BK < ke) tile(std::integral_constant<int, 1>{}, k0 + BK);
+    }
+  } else {
+    for (int k0 = kb; k0 < ke; k0 += BK) tile(std::integral_constant<int, 0>{}, k0);
+  }
+  run_epilogue<TM, TN, 16>(ep, acc, M, N, 0, [&](int i, int j, int r, int& row, int& col) {
+    row = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    col = n0 + wn * TN * 32 + j * 32 + (lane & 31);
+  });
+}
+
+// Double-buffered LDS: tile k's MFMAs run while tile k+1 (already in registers) is split
+// into the other buffer and tile k+2's global loads are issued; one barrier per tile.
+// SG: sched_group_barrier interleave pattern (0 = compiler's choice).
+template <int BM, int BN, int BK, int WM, int WN, int SG, class FA, class FB, class EP>
+__global__ __launch_bounds__(256) void xdb(FA fa, FB fb, EP ep, int M, int N, int K) {
+  constexpr int LDK = BK + 8;
+  constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
+  constexpr int NA = (FA::template slots<BM, BK>() + 255) / 256;
+  constexpr int NB = (FB::template slots<BN, BK>() + 255) / 256;
+  constexpr int ASZ = 3 * BM * LDK, BSZ = 3 * BN * LDK;
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem16[];
+  typedef float f16v_ __attribute__((ext_vector_type(16)));
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WM, wn = wave / WM;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int ke = K;
+  f16v_ acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+  const int ra = (wm * TM * 32 + (lane & 31)) * LDK + 8 * (lane >> 5);
+  const int rb = (wn * TN * 32 + (lane & 31)) * LDK + 8 * (lane >> 5);
+  f4 pa[NA], pb[NB];
+  fa.template fetch<BM, BK>(pa, m0, 0, ke, tid);
+  fb.template fetch<BN, BK>(pb, n0, 0, ke, tid);
+  commit_x6<BM, BK, LDK, FA>(pa, smem16, tid);
+  commit_x6<BN, BK, LDK, FB>(pb, smem16 + ASZ, tid);
+  if (BK < ke) {
+    fa.template fetch<BM, BK>(pa, m0, BK, ke, tid);
+    fb.template fetch<BN, BK>(pb, n0, BK, ke, tid);
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int k0 = 0; k0 < ke; k0 += BK) {
+    const uint16_t* As = smem16 + cur * (ASZ + BSZ);
+    const uint16_t* Bs = As + ASZ;
+    uint16_t* An = smem16 + (cur ^ 1) * (ASZ + BSZ);
+    const bool more = k0 + BK < ke;
+    bf16x8_ a[BK / 16][3][TM], b[BK / 16][3][TN];
+#pragma unroll
+    for (int kq = 0; kq < BK / 16; ++kq)
+#pragma unroll
+      for (int t = 0; t < 3; ++t) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          a[kq][t][i] = *reinterpret_cast<const bf16x8_*>(&As[t * BM * LDK + ra + i * 32 * LDK + kq * 16]);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          b[kq][t][j] = *reinterpret_cast<const bf16x8_*>(&Bs[t * BN * LDK + rb + j * 32 * LDK + kq * 16]);
+      }
+    if (more) {
+      commit_x6<BM, BK, LDK, FA>(pa, An, tid);
+      commit_x6<BN, BK, LDK, FB>(pb, An + ASZ, tid);
+    }
+#pragma unroll
+    for (int kq = 0; kq < BK / 16; ++kq)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[kq][2][i], b[kq][0][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[kq][0][i], b[kq][2][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[kq][1][i], b[kq][1][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[kq][1][i], b[kq][0][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[kq][0][i], b[kq][1][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[kq][0][i], b[kq][0][j], acc[i][j], 0, 0, 0);
+        }
+    if constexpr (SG == 1) {
+      // per MFMA: 5 VALU, 1 DS write (the commit), then global loads at the end
+#pragma unroll
+      for (int q = 0; q < (BK / 16) * TM * TN * 6; ++q) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+        __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+      }
+    }
+    if (k0 + 2 * BK < ke) {
+      fa.template fetch<BM, BK>(pa, m0, k0 + 2 * BK, ke, tid);
+      fb.template fetch<BN, BK>(pb, n0, k0 + 2 * BK, ke, tid);
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+  run_epilogue<TM, TN, 16>(ep, acc, M, N, 0, [&](int i, int j, int r, int& row, int& col) {
+    row = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    col = n0 + wn * TN * 32 + j * 32 + (lane & 31);
+  });
+}
+
+int main() {
+  const int E = 4096, XC = 1032, N = 2048;
+  float* xc = dalloc((int64_t)E * XC, 21, -0.5f);
+  float* wc = dalloc((int64_t)N * XC, 22, -0.05f);
+  float* gt = dalloc((int64_t)E * N, 23, 0.f);
+  float* b0 = dalloc(N, 24, 0.f);
+  hipStream_t st = 0;
+  const double fl = 2.0 * E * N * XC;
+  DenseRows fa{xc, XC, E};
+  DenseRows fb{wc, XC, N};
+  EpiBias2 ep{gt, N, b0, b0};
+  auto rep = [&](const char* name, float ms) {
+    printf("%-44s %8.1f us %7.1f TF(f32-equiv) %6.1f%% of x6 peak\n", name, ms * 1e3, fl / ms / 1e9,
+           100.0 * fl * 6 / (ms * 1e-3) / 2.5e15);
+  };
+  rep("library gemm_x6 <128,128,32,2,2>", timeit([&] { launch_gemm_x6<128, 128, 32, 2, 2>(fa, fb, ep, E, N, XC, st); }));
+  rep("library gemm_x6 <64,64,32,2,2>", timeit([&] { launch_gemm_x6<64, 64, 32, 2, 2>(fa, fb, ep, E, N, XC, st); }));
+#define XK(BM, BN, BK, WM, WN, L, S, P, R)                                                                   \
+  rep("xk<" #BM "," #BN "," #BK "> loads" #L " split" #S " pf" #P " prio" #R, timeit([&] {                  \
+        hipLaunchKernelGGL((xk<BM, BN, BK, WM, WN, L, S, P, R, DenseRows, DenseRows, EpiBias2>),             \
+                           grid_for(E, N, BM, BN), dim3(256), 0, st, fa, fb, ep, E, N, XC);                  \
+      }));
+  XK(128, 128, 32, 2, 2, 1, 1, 1, 0)
+  XK(128, 128, 32, 2, 2, 0, 1, 1, 0)
+  XK(128, 128, 32, 2, 2, 1, 0, 1, 0)
+  XK(128, 128, 32, 2, 2, 1, 1, 2, 0)
+  XK(128, 128, 32, 2, 2, 1, 1, 1, 1)
+  XK(128, 128, 64, 2, 2, 1, 1, 1, 0)
+  XK(128, 128, 64, 2, 2, 0, 1, 1, 0)
+  XK(64, 64, 32, 2, 2, 0, 1, 1, 0)
+#define XDB(BM, BN, BK, WM, WN, SG)                                                                       \
+  {                                                                                                        \
+    auto kf = xdb<BM, BN, BK, WM, WN, SG, DenseRows, DenseRows, EpiBias2>;                                 \
+    const int lds = 2 * 3 * (BM + BN) * (BK + 8) * 2;                                                      \
+    hipFuncSetAttribute((const void*)kf, hipFuncAttributeMaxDynamicSharedMemorySize, lds);                \
+    rep("xdb<" #BM "," #BN "," #BK "> sg" #SG, timeit([&] {                                                 \
+          hipLaunchKernelGGL(kf, grid_for(E, N, BM, BN), dim3(256), lds, st, fa, fb, ep, E, N, XC);         \
+        }));                                                                                               \
+    hipError_t e = hipGetLastError();                                                                      \
+    if (e != hipSuccess) printf("  launch error %s\n", hipGetErrorString(e));                              \
+  }
+  XDB(128, 128, 32, 2, 2, 0)
+  XDB(128, 128, 32, 2, 2, 1)
+  XDB(128, 128, 16, 2, 2, 0)
+  XDB(128, 128, 16, 2, 2, 1)
+  XDB(64, 128, 32, 2, 2, 0)
+  XDB(64, 64, 32, 2, 2, 0)
+  // correctness of xdb vs the library kernel (same products, same order per accumulator)
+  {
+    std::vector<float> h1((size_t)E * N), h2((size_t)E * N);
+    launch_gemm_x6<128, 128, 32, 2, 2>(fa, fb, ep, E, N, XC, st);
+    hipMemcpy(h1.data(), gt, h1.size() * 4, hipMemcpyDeviceToHost);
+    auto kf = xdb<128, 128, 32, 2, 2, 0, DenseRows, DenseRows, EpiBias2>;
+    hipLaunchKernelGGL(kf, grid_for(E, N, 128, 128), dim3(256), 2 * 3 * 256 * 40 * 2, st, fa, fb, ep, E, N, XC);
+    hipMemcpy(h2.data(), gt, h2.size() * 4, hipMemcpyDeviceToHost);
+    size_t bad = 0;
+    for (size_t q = 0; q < h1.size(); ++q) bad += (h1[q] != h2[q]);
+    printf("xdb vs library: %zu of %zu differ\n", bad, h1.size());
+  }
+  printf("done\n");
+  return 0;
+}
