@@ -158,19 +158,16 @@ __device__ void reset_env(const EnvArgs& a, int e, int lane, int& sc, int& s, in
 }
 
 // Copy the image frame and goal frame of one env: 16-B lanes, 4 x 2 loads in flight. The
-// image frame is a random arena row read once per step: its loads are nontemporal (`nt`) so
-// it streams past the caches, while the goal frame (re-read every step of the episode) and
-// the output rows (read next by the consumer) keep the default policy. Measured on the bench
-// (4096 envs, 626 MB arena; tools/ab/copy_variants.sh): 57-60 us -> 55 us per launch; nt on
-// both loads, on the stores, or on any mix measured within 1 us of it, nt on all four
-// streams 73 us.
-__device__ __forceinline__ uint4 ld16_nt(const uint4* p) {
-  uint4 v;
-  v.x = __builtin_nontemporal_load(&p->x);
-  v.y = __builtin_nontemporal_load(&p->y);
-  v.z = __builtin_nontemporal_load(&p->z);
-  v.w = __builtin_nontemporal_load(&p->w);
-  return v;
+// output rows are written with nontemporal (`nt`) stores; loads keep the default policy.
+// Measured (tools/copybench.hip cache-policy sweep over the 16 load/store combinations, and
+// the bench, tools/ab/copy_variants.sh): at 4096 envs default stores 57-60 us, any single nt
+// stream 54-56 us; at 32768 envs per GPU nt on both stores 446 us (6.2 TB/s) vs 551 us
+// default and 545-563 us with nt loads; nt on all four streams is the slowest everywhere.
+__device__ __forceinline__ void st16_nt(uint4* p, const uint4 v) {
+  __builtin_nontemporal_store(v.x, &p->x);
+  __builtin_nontemporal_store(v.y, &p->y);
+  __builtin_nontemporal_store(v.z, &p->z);
+  __builtin_nontemporal_store(v.w, &p->w);
 }
 
 template <int VEC>
@@ -188,18 +185,18 @@ __device__ __forceinline__ void copy_two_frames(uint8_t* __restrict__ d1, const 
     for (; i + 64 * (U - 1) < n; i += 64 * U) {
       uint4 va[U], vb[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) va[u] = ld16_nt(a + i + 64 * u);
+      for (int u = 0; u < U; ++u) va[u] = a[i + 64 * u];
 #pragma unroll
       for (int u = 0; u < U; ++u) vb[u] = b[i + 64 * u];
 #pragma unroll
-      for (int u = 0; u < U; ++u) x[i + 64 * u] = va[u];
+      for (int u = 0; u < U; ++u) st16_nt(x + i + 64 * u, va[u]);
 #pragma unroll
-      for (int u = 0; u < U; ++u) y[i + 64 * u] = vb[u];
+      for (int u = 0; u < U; ++u) st16_nt(y + i + 64 * u, vb[u]);
     }
     for (; i < n; i += 64) {
-      const uint4 a0 = ld16_nt(a + i), b0 = b[i];
-      x[i] = a0;
-      y[i] = b0;
+      const uint4 a0 = a[i], b0 = b[i];
+      st16_nt(x + i, a0);
+      st16_nt(y + i, b0);
     }
   } else if constexpr (VEC == 4) {
     const int n = (int)(bytes >> 2);

@@ -368,6 +368,10 @@ __global__ __launch_bounds__(256) void gemm_x6_kernel(FA fa, FB fb, EP ep, int M
       fa.template fetch<BM, BK>(pa, m0, k0 + BK, ke, tid);
       fb.template fetch<BN, BK>(pb, n0, k0 + BK, ke, tid);
     }
+    // the MFMA cluster at raised wave priority: the co-resident workgroup's wave on this SIMD
+    // then runs its commit (VALU split, LDS writes) in this wave's MFMA gaps instead of
+    // delaying its MFMA issue (tools/gemm_x6_bench.hip, LSTM gates shape: 117 -> 102 us)
+    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 16) {
       bf16x8_ a[3][TM], b[3][TN];
@@ -392,6 +396,7 @@ __global__ __launch_bounds__(256) void gemm_x6_kernel(FA fa, FB fb, EP ep, int M
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[0][j], acc[i][j], 0, 0, 0);
         }
     }
+    __builtin_amdgcn_s_setprio(0);
     __syncthreads();
   }
   run_epilogue<TM, TN, 16>(ep, acc, M, N, (int)blockIdx.z, [&](int i, int j, int r, int& row, int& col) {

@@ -18,7 +18,7 @@
     }                                                                             \
   } while (0)
 
-constexpr int E = 4096;
+static int E = 4096;  // envs (argv[2])
 constexpr int F = 21168;  // 84*84*3
 constexpr int NV = F / 16;  // 1323 uint4 per frame
 constexpr int ROWS = 29564;
@@ -31,6 +31,7 @@ struct Args {
   uint8_t* obs;
   uint8_t* goal;
   int set;
+  int n;
 };
 
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -40,7 +41,7 @@ template <int U>
 __global__ __launch_bounds__(256) void k_wave_env(Args a) {
   const int lane = threadIdx.x & 63;
   const int e = uni(blockIdx.x * 4 + (threadIdx.x >> 6));
-  const int64_t ir = a.img_rows[a.set * E + e], gr = a.goal_rows[e];
+  const int64_t ir = a.img_rows[a.set * a.n + e], gr = a.goal_rows[e];
   const uint4* s1 = reinterpret_cast<const uint4*>(a.arena + ir * F);
   const uint4* s2 = reinterpret_cast<const uint4*>(a.arena + gr * F);
   uint4* d1 = reinterpret_cast<uint4*>(a.obs + (int64_t)e * F);
@@ -69,7 +70,7 @@ template <int U, bool NTL, bool NTS>
 __global__ __launch_bounds__(256) void k_wave_env_nt(Args a) {
   const int lane = threadIdx.x & 63;
   const int e = uni(blockIdx.x * 4 + (threadIdx.x >> 6));
-  const int64_t ir = a.img_rows[a.set * E + e], gr = a.goal_rows[e];
+  const int64_t ir = a.img_rows[a.set * a.n + e], gr = a.goal_rows[e];
   const uint4* s1 = reinterpret_cast<const uint4*>(a.arena + ir * F);
   const uint4* s2 = reinterpret_cast<const uint4*>(a.arena + gr * F);
   uint4* d1 = reinterpret_cast<uint4*>(a.obs + (int64_t)e * F);
@@ -145,7 +146,7 @@ __global__ __launch_bounds__(256) void k_policy(Args a) {
   constexpr int U = 4;
   const int lane = threadIdx.x & 63;
   const int e = uni(blockIdx.x * 4 + (threadIdx.x >> 6));
-  const int64_t ir = a.img_rows[a.set * E + e], gr = a.goal_rows[e];
+  const int64_t ir = a.img_rows[a.set * a.n + e], gr = a.goal_rows[e];
   const uint4* s1 = reinterpret_cast<const uint4*>(a.arena + ir * F);
   const uint4* s2 = reinterpret_cast<const uint4*>(a.arena + gr * F);
   uint4* d1 = reinterpret_cast<uint4*>(a.obs + (int64_t)e * F);
@@ -175,7 +176,7 @@ __global__ __launch_bounds__(256) void k_wave_frame(Args a) {
   const int lane = threadIdx.x & 63;
   const int w = uni(blockIdx.x * 4 + (threadIdx.x >> 6));
   const int e = w >> 1, which = w & 1;
-  const int64_t r = which ? a.goal_rows[e] : a.img_rows[a.set * E + e];
+  const int64_t r = which ? a.goal_rows[e] : a.img_rows[a.set * a.n + e];
   const uint4* s = reinterpret_cast<const uint4*>(a.arena + r * F);
   uint4* d = reinterpret_cast<uint4*>((which ? a.goal : a.obs) + (int64_t)e * F);
   int i = lane;
@@ -194,7 +195,7 @@ template <int U>
 __global__ __launch_bounds__(256) void k_wg_env(Args a) {
   const int t = threadIdx.x;
   const int e = blockIdx.x;
-  const int64_t ir = a.img_rows[a.set * E + e], gr = a.goal_rows[e];
+  const int64_t ir = a.img_rows[a.set * a.n + e], gr = a.goal_rows[e];
   const uint4* s1 = reinterpret_cast<const uint4*>(a.arena + ir * F);
   const uint4* s2 = reinterpret_cast<const uint4*>(a.arena + gr * F);
   uint4* d1 = reinterpret_cast<uint4*>(a.obs + (int64_t)e * F);
@@ -225,7 +226,7 @@ template <int MODE>
 __global__ __launch_bounds__(256) void k_probe(Args a) {
   const int lane = threadIdx.x & 63;
   const int e = uni(blockIdx.x * 4 + (threadIdx.x >> 6));
-  const int64_t ir = a.img_rows[a.set * E + e], gr = a.goal_rows[e];
+  const int64_t ir = a.img_rows[a.set * a.n + e], gr = a.goal_rows[e];
   const uint4* s1 = reinterpret_cast<const uint4*>(a.arena + ir * F);
   const uint4* s2 = reinterpret_cast<const uint4*>(a.arena + gr * F);
   uint4* d1 = reinterpret_cast<uint4*>(a.obs + (int64_t)e * F);
@@ -289,6 +290,8 @@ float time_it(L launch, int reps) {
 
 int main(int argc, char** argv) {
   const int reps = argc > 1 ? atoi(argv[1]) : 300;
+  if (argc > 2) E = atoi(argv[2]);
+  const int quick = argc > 3 ? atoi(argv[3]) : 0;
   uint8_t *arena, *obs, *goal;
   int *img_rows, *goal_rows;
   CK(hipMalloc(&arena, (size_t)ROWS * F));
@@ -307,7 +310,8 @@ int main(int argc, char** argv) {
   auto rep = [&](const char* name, float us) {
     printf("%-34s %8.2f us  %7.0f GB/s  frac %.3f\n", name, us, bytes / (us * 1e-6) / 1e9, bytes / (us * 1e-6) / 8e12);
   };
-  Args A{arena, img_rows, goal_rows, obs, goal, 0};
+  Args A{arena, img_rows, goal_rows, obs, goal, 0, E};
+  printf("E = %d envs\n", E);
   auto envk = [&](auto kern, int grid) {
     return [=](int i) mutable {
       Args b = A;
@@ -321,7 +325,7 @@ int main(int argc, char** argv) {
   snprintf(nm, sizeof nm, "policy cv%-2d (st i%d g%d, nt-ld i%d g%d)", cv, cv & 1, (cv >> 1) & 1, (cv >> 2) & 1, \
            (cv >> 3) & 1);                                              \
   rep(nm, time_it(envk(k_policy<cv>, E / 4), reps));
-    for (int round = 0; round < 2; ++round) {
+    for (int round = 0; round < (quick ? 1 : 2); ++round) {
       POL(0) POL(1) POL(2) POL(3) POL(4) POL(5) POL(6) POL(7) POL(8) POL(9) POL(10) POL(11) POL(12) POL(13) POL(14) POL(15)
     }
   }
@@ -336,7 +340,7 @@ int main(int argc, char** argv) {
   rep("wg/env U2", time_it(envk(k_wg_env<2>, E), reps));
   rep("wg/env U1", time_it(envk(k_wg_env<1>, E), reps));
   rep("wave/env U4 (again)", time_it(envk(k_wave_env<4>, E / 4), reps));
-  {  // traffic probes; bytes column still counts the full 4F per env
+  if (!quick) {  // traffic probes; bytes column still counts the full 4F per env
     rep("probe rd2 wr1 (3F)", time_it(envk(k_probe<0>, E / 4), reps));
     rep("probe rd1 wr2 (3F)", time_it(envk(k_probe<1>, E / 4), reps));
     rep("probe wr2 only (2F)", time_it(envk(k_probe<2>, E / 4), reps));
@@ -361,21 +365,24 @@ int main(int argc, char** argv) {
     rep("hot goals U4 nt-load", time_it(hk(k_wave_env_nt<4, true, false>), reps));
   }
   // flat copies of 2*E*F bytes (src = first rows of the arena; dst = obs..goal contiguous? use obs+goal as one)
-  uint8_t* dst;
+  // flat copies of 2*E*F bytes from a source of that size (the arena is smaller at large E)
+  uint8_t *dst, *src;
   CK(hipMalloc(&dst, (size_t)2 * E * F));
+  CK(hipMalloc(&src, (size_t)2 * E * F));
+  CK(hipMemset(src, 3, (size_t)2 * E * F));
   const int64_t n = (int64_t)2 * E * F / 16;
   for (int blocks : {1024, 2048, 4096, 8192}) {
     char nm[64];
     snprintf(nm, sizeof nm, "flat grid-stride %d WGs", blocks);
-    rep(nm, time_it([=](int) { hipLaunchKernelGGL(k_flat, dim3(blocks), dim3(256), 0, 0, (const uint4*)arena, (uint4*)dst, n); }, reps));
+    rep(nm, time_it([=](int) { hipLaunchKernelGGL(k_flat, dim3(blocks), dim3(256), 0, 0, (const uint4*)src, (uint4*)dst, n); }, reps));
   }
   rep("flat exact U4", time_it([=](int) {
-        hipLaunchKernelGGL(k_flat_exact<4>, dim3((n + 1023) / 1024), dim3(256), 0, 0, (const uint4*)arena, (uint4*)dst, n);
+        hipLaunchKernelGGL(k_flat_exact<4>, dim3((n + 1023) / 1024), dim3(256), 0, 0, (const uint4*)src, (uint4*)dst, n);
       }, reps));
   rep("flat exact U8", time_it([=](int) {
-        hipLaunchKernelGGL(k_flat_exact<8>, dim3((n + 2047) / 2048), dim3(256), 0, 0, (const uint4*)arena, (uint4*)dst, n);
+        hipLaunchKernelGGL(k_flat_exact<8>, dim3((n + 2047) / 2048), dim3(256), 0, 0, (const uint4*)src, (uint4*)dst, n);
       }, reps));
-  rep("hipMemcpyAsync D2D", time_it([=](int) { (void)hipMemcpyAsync(dst, arena, (size_t)2 * E * F, hipMemcpyDeviceToDevice, 0); }, reps));
+  rep("hipMemcpyAsync D2D", time_it([=](int) { (void)hipMemcpyAsync(dst, src, (size_t)2 * E * F, hipMemcpyDeviceToDevice, 0); }, reps));
   // flat copy of 8x the bytes: steady-state ceiling without launch ramp
   {
     uint8_t* big;  // copy its first half (4 x the bytes) into its second half
