@@ -29,10 +29,14 @@ __device__ __forceinline__ void softmax_stats(const float* lg, int A, float* p, 
   }
 }
 
+// ctr_dev (optional): the Philox counter is *ctr_dev + ctr (a device-side update counter, so
+// a captured hipGraph of the update samples with a fresh counter on every replay).
 __global__ void sample_kernel(const float* __restrict__ out, int n, int A, uint32_t k0, uint32_t k1, uint64_t ctr,
-                              int32_t* actions, float* logp_out, float* ent_out, float* value_out) {
+                              const int64_t* __restrict__ ctr_dev, int32_t* actions, float* logp_out, float* ent_out,
+                              float* value_out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  if (ctr_dev) ctr += (uint64_t)*ctr_dev;
   float lg[7], p[7], lp[7], H;
   for (int j = 0; j < A; ++j) lg[j] = out[(int64_t)i * OUT_LD_A2C + j];
   softmax_stats(lg, A, p, lp, H);
@@ -163,9 +167,10 @@ __global__ void norm_final_kernel(const double* partial, int nb, float max_norm,
 
 __global__ __launch_bounds__(256) void rmsprop_kernel(float* __restrict__ params, const float* __restrict__ grads,
                                                       float* __restrict__ sq, int64_t n, float scale,
-                                                      const float* __restrict__ scalars, float lr, float alpha,
-                                                      float eps) {
+                                                      const float* __restrict__ scalars, float lr,
+                                                      const float* __restrict__ lr_dev, float alpha, float eps) {
   const float coef = scalars[1] * scale;
+  if (lr_dev) lr = *lr_dev;
   for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     const float g = grads[i] * coef;
     const float s = sq[i] * alpha + (1.0f - alpha) * g * g;
@@ -227,6 +232,21 @@ __global__ __launch_bounds__(kPostThreads) void step_post_kernel(const int32_t* 
   }
 }
 
+// Device-side trainer schedule, one thread, launched first in every update:
+//   state[2] (counter of this update) = state[0]; state[0] += T (policy sampling counter base,
+//   = updates * T); lr = lr0 * (1 - min(state[1] / max_steps, 1)) in double as the host's
+//   LinearSchedule (experiments/thor_cached_auxiliary.py:37) computes it, rounded once to f32;
+//   state[1] += steps_per_update (env-steps of all ranks).
+__global__ void a2c_schedule_kernel(int64_t* state, float* lr_out, double lr0, double max_steps,
+                                    int64_t steps_per_update, int T) {
+  const int64_t total = state[1];
+  const double frac = max_steps > 0.0 ? fmin((double)total / max_steps, 1.0) : 0.0;
+  *lr_out = (float)(lr0 * (1.0 - frac));
+  state[2] = state[0];
+  state[0] += T;
+  state[1] = total + steps_per_update;
+}
+
 }  // namespace vn
 
 using namespace vn;
@@ -238,7 +258,29 @@ int vn_policy_sample(const float* out, int n, int num_actions, uint64_t seed, ui
   if (!out || !actions || n <= 0 || num_actions < 1 || num_actions > 7)
     return fail(VN_EINVAL, "vn_policy_sample: bad args");
   hipLaunchKernelGGL(sample_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, out, n, num_actions,
-                     (uint32_t)seed, (uint32_t)(seed >> 32), counter, actions, logp, entropy, value);
+                     (uint32_t)seed, (uint32_t)(seed >> 32), counter, (const int64_t*)nullptr, actions, logp, entropy,
+                     value);
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
+
+int vn_policy_sample_dev(const float* out, int n, int num_actions, uint64_t seed, const int64_t* counter_base_dev,
+                         uint64_t counter_offset, int32_t* actions, float* logp, float* entropy, float* value,
+                         vn_stream_t stream) {
+  if (!out || !actions || !counter_base_dev || n <= 0 || num_actions < 1 || num_actions > 7)
+    return fail(VN_EINVAL, "vn_policy_sample_dev: bad args");
+  hipLaunchKernelGGL(sample_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, out, n, num_actions,
+                     (uint32_t)seed, (uint32_t)(seed >> 32), counter_offset, counter_base_dev, actions, logp, entropy,
+                     value);
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
+
+int vn_a2c_schedule(int64_t* state3, float* lr_out, double lr0, double max_time_steps, int64_t steps_per_update,
+                    int T, vn_stream_t stream) {
+  if (!state3 || !lr_out || T <= 0 || steps_per_update < 0) return fail(VN_EINVAL, "vn_a2c_schedule: bad args");
+  hipLaunchKernelGGL(a2c_schedule_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, state3, lr_out, lr0,
+                     max_time_steps, steps_per_update, T);
   VN_HIP(hipGetLastError());
   return VN_OK;
 }
@@ -289,7 +331,18 @@ int vn_rmsprop_step(float* params, const float* grads, float* square_avg, int64_
   if (!params || !grads || !square_avg || !scalars2 || n <= 0) return fail(VN_EINVAL, "vn_rmsprop_step: bad args");
   const int blocks = (int)std::min<int64_t>((n + 255) / 256, 2048);
   hipLaunchKernelGGL(rmsprop_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, params, grads, square_avg, n,
-                     scale, scalars2, lr, alpha, eps);
+                     scale, scalars2, lr, (const float*)nullptr, alpha, eps);
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
+
+int vn_rmsprop_step_dev(float* params, const float* grads, float* square_avg, int64_t n, float scale,
+                        const float* scalars2, const float* lr_dev, float alpha, float eps, vn_stream_t stream) {
+  if (!params || !grads || !square_avg || !scalars2 || !lr_dev || n <= 0)
+    return fail(VN_EINVAL, "vn_rmsprop_step_dev: bad args");
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 2048);
+  hipLaunchKernelGGL(rmsprop_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, params, grads, square_avg, n,
+                     scale, scalars2, 0.0f, lr_dev, alpha, eps);
   VN_HIP(hipGetLastError());
   return VN_OK;
 }

@@ -383,6 +383,11 @@ struct PolicyLayout {
   // W2 [48][4][4][8] (block diagonal), b2 [8]; maps X4 [h3][w3] -> A1 [AH][AW] -> P [PH][PW]
   int aux, AH, AW, PH, PW;
   int64_t aw1, ab1, aw2, ab2;
+  // split-K scratch on the policy's device (vn_policy_create_ex): slabs of the products whose
+  // tiles alone cannot fill the chip (small batches), see launch_gemm_x6_sk
+  float* sk;
+  int64_t sk_cap;  // floats
+  int sk_dev;
 };
 
 inline PolicyLayout make_layout(int H, int W, int A, int lstm = 0, int aux = 0, int arch = 0) {
@@ -539,6 +544,77 @@ inline void launch_gemm32(FA fa, FB fb, EP ep, int M, int N, int K, hipStream_t 
   if (kchunk <= 0) kchunk = K;
   hipLaunchKernelGGL((gemm32_kernel<BM, BN, BK, WM, WN, FA, FB, EP>), grid_for(M, N, BM, BN, splits), dim3(256), 0,
                      st, fa, fb, ep, M, N, K, kchunk);
+}
+
+// Epilogue of a split-K product: element (row, col) = the fixed-order sum of its `splits`
+// slab partials, then the product's own epilogue functor (any of its three forms).
+template <class EP>
+__global__ __launch_bounds__(256) void splitk_epilogue_kernel(const float* __restrict__ slab, int splits, int M, int N,
+                                                              EP ep) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t MN = (int64_t)M * N;
+  if (idx >= MN) return;
+  const int row = (int)(idx / N), col = (int)(idx - (idx / N) * N);
+  float v = 0.0f;
+  for (int z = 0; z < splits; ++z) v += slab[z * MN + idx];
+  if constexpr (has_pre_col<EP>::value)
+    ep.post(row, col, v, ep.pre_col(col), 0);
+  else if constexpr (has_pre_row<EP>::value)
+    ep.post(row, col, v, ep.pre_row(row), 0);
+  else if constexpr (has_pre<EP>::value)
+    ep.post(row, col, v, ep.pre(row, col), 0);
+  else
+    ep(row, col, v, 0);
+}
+
+// Splits of a product whose BM x BN tiles alone leave most of the chip idle (a 4-env rollout
+// step: M = 4): the K range is cut into chunks of >= 2 K tiles so that ~512 workgroups run,
+// partial products go to the policy's scratch slabs, and splitk_epilogue_kernel applies the
+// epilogue. 1 = no split (every training batch of the bench: >= 128 tiles).
+inline int splitk_count(int M, int N, int K, int BM, int BN, int BK, const PolicyLayout& L) {
+  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  if (!L.sk || tiles >= 128 || K < 4 * BK) return 1;
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess || dev != L.sk_dev) return 1;
+  int splits = std::min((512 + tiles - 1) / tiles, K / (2 * BK));
+  while (splits > 1 && (int64_t)splits * M * N > L.sk_cap) --splits;
+  return std::max(splits, 1);
+}
+
+template <int BM, int BN, int BK, int WM, int WN, class FA, class FB, class EP>
+inline void launch_gemm_x6_sk(FA fa, FB fb, EP ep, int M, int N, int K, hipStream_t st, const PolicyLayout& L) {
+  if (M <= 0 || N <= 0) return;
+  int splits = splitk_count(M, N, K, BM, BN, BK, L);
+  if (splits <= 1) {
+    launch_gemm_x6<BM, BN, BK, WM, WN>(fa, fb, ep, M, N, K, st);
+    return;
+  }
+  const int kchunk = ((K + splits - 1) / splits + BK - 1) / BK * BK;
+  splits = (K + kchunk - 1) / kchunk;
+  EpiSlab es{L.sk, M, N};
+  hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, BK, WM, WN, FA, FB, EpiSlab>), grid_for(M, N, BM, BN, splits), dim3(256),
+                     0, st, fa, fb, es, M, N, K, kchunk);
+  const int64_t MN = (int64_t)M * N;
+  hipLaunchKernelGGL(splitk_epilogue_kernel<EP>, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, st, L.sk, splits, M,
+                     N, ep);
+}
+
+// The f32 MFMA core's form (the heads: N = actions + 1, K = 512).
+template <int BM, int BN, int BK, int WM, int WN, class FA, class FB, class EP>
+inline void launch_gemm_sk(FA fa, FB fb, EP ep, int M, int N, int K, hipStream_t st, const PolicyLayout& L) {
+  if (M <= 0 || N <= 0) return;
+  int splits = splitk_count(M, N, K, BM, BN, BK, L);
+  if (splits <= 1) {
+    launch_gemm<BM, BN, BK, WM, WN>(fa, fb, ep, M, N, K, st);
+    return;
+  }
+  const int kchunk = ((K + splits - 1) / splits + BK - 1) / BK * BK;
+  splits = (K + kchunk - 1) / kchunk;
+  EpiSlab es{L.sk, M, N};
+  launch_gemm<BM, BN, BK, WM, WN>(fa, fb, es, M, N, K, st, splits, kchunk);
+  const int64_t MN = (int64_t)M * N;
+  hipLaunchKernelGGL(splitk_epilogue_kernel<EP>, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, st, L.sk, splits, M,
+                     N, ep);
 }
 
 // Split-K wgrad: dW [M][KP] and db [M] of a layer from A^T (dZ [P][M]) x B (im2col [P][KP]).
@@ -728,7 +804,7 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
     NhwcIm2col<32, 4, 4, 2, G::OH1, G::OW1, G::OH2, G::OW2, 1> fa{a.X[0], 2 * n * G::OH2 * G::OW2};
     DenseRows fb{P + L.l[1].w, 512, 32};
     EpiBiasAct ep{a.X[1], 32, P + L.l[1].b, 1};
-    launch_gemm_x6<128, 32, 32, 4, 1>(fa, fb, ep, fa.M, 32, 512, st);
+    launch_gemm_x6_sk<128, 32, 32, 4, 1>(fa, fb, ep, fa.M, 32, 512, st, L);
   }
   // conv3 over concat(image, goal) (X2 -> X3)
   {
@@ -736,9 +812,9 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
     DenseRows fb{P + L.l[2].w, 1024, 64};
     EpiBiasAct ep{a.X[2], 64, P + L.l[2].b, 1};
     if constexpr (G::OH3 * G::OW3 >= 64)  // 174x174, 300x400: 128-row tiles (A split over more MFMAs)
-      launch_gemm_x6<128, 64, 32, 2, 2>(fa, fb, ep, fa.M, 64, 1024, st);
+      launch_gemm_x6_sk<128, 64, 32, 2, 2>(fa, fb, ep, fa.M, 64, 1024, st, L);
     else  // 84x84: 3x3 maps, 64-row tiles keep >= 2 tiles per CU
-      launch_gemm_x6<64, 64, 32, 2, 2>(fa, fb, ep, fa.M, 64, 1024, st);
+      launch_gemm_x6_sk<64, 64, 32, 2, 2>(fa, fb, ep, fa.M, 64, 1024, st, L);
   }
   // conv4 1x1 (X3 -> X4)
   {
@@ -752,14 +828,14 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
     DenseRows fa{a.X[3], G::FCIN, n};
     DenseRows fb{P + L.l[4].w, G::FCIN, 512};
     EpiBiasAct ep{a.X[4], 512, P + L.l[4].b, 1};
-    launch_gemm_x6<64, 64, 32, 2, 2>(fa, fb, ep, n, 512, G::FCIN, st);
+    launch_gemm_x6_sk<64, 64, 32, 2, 2>(fa, fb, ep, n, 512, G::FCIN, st, L);
   }
   // heads (X5 -> out[n][8]: logits, value); out == NULL runs the trunk only (recurrent policy)
   if (out) {
     DenseRows fa{a.X[4], 512, n};
     DenseRows fb{P + L.l[5].w, 512, A1};
     EpiBiasAct ep{out, OUT_LD, P + L.l[5].b, 0};
-    launch_gemm<64, 16, 32, 4, 1>(fa, fb, ep, n, A1, 512, st);
+    launch_gemm_sk<64, 16, 32, 4, 1>(fa, fb, ep, n, A1, 512, st, L);
   }
   VN_HIP(hipGetLastError());
   return VN_OK;
@@ -984,13 +1060,13 @@ int forward_bignet(const PolicyLayout& L, const float* P, const FrameSrc& src, i
     DenseRows fa{a.X[2], FCIN, n};
     DenseRows fb{P + L.l[4].w, FCIN, 512};
     EpiBiasAct ep{a.X[4], 512, P + L.l[4].b, 1};
-    launch_gemm_x6<64, 64, 32, 2, 2>(fa, fb, ep, n, 512, FCIN, st);
+    launch_gemm_x6_sk<64, 64, 32, 2, 2>(fa, fb, ep, n, 512, FCIN, st, L);
   }
   if (out) {
     DenseRows fa{a.X[4], 512, n};
     DenseRows fb{P + L.l[5].w, 512, L.A + 1};
     EpiBiasAct ep{out, OUT_LD, P + L.l[5].b, 0};
-    launch_gemm<64, 16, 32, 4, 1>(fa, fb, ep, n, L.A + 1, 512, st);
+    launch_gemm_sk<64, 16, 32, 4, 1>(fa, fb, ep, n, L.A + 1, 512, st, L);
   }
   VN_HIP(hipGetLastError());
   return VN_OK;
@@ -1068,7 +1144,7 @@ inline int lstm_forward_step(const PolicyLayout& L, const float* P, int E, const
     DenseRows fa{xc, L.xcat, E};
     DenseRows fb{P + L.lw, L.xcat, 2048};
     EpiBias2 ep{gates, 2048, P + L.lbih, P + L.lbhh};
-    launch_gemm_x6<128, 128, 32, 2, 2>(fa, fb, ep, E, 2048, L.xcat, st);
+    launch_gemm_x6_sk<128, 128, 32, 2, 2>(fa, fb, ep, E, 2048, L.xcat, st, L);
   }
   const int64_t nc = (int64_t)E * 512;
   hipLaunchKernelGGL(lstm_cell_kernel, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, st, E, gates, c_prev, mask,
@@ -1081,7 +1157,7 @@ inline int heads_forward(const PolicyLayout& L, const float* P, const float* fea
   DenseRows fa{feat, 512, n};
   DenseRows fb{P + L.l[5].w, 512, L.A + 1};
   EpiBiasAct ep{out, OUT_LD, P + L.l[5].b, 0};
-  launch_gemm<64, 16, 32, 4, 1>(fa, fb, ep, n, L.A + 1, 512, st);
+  launch_gemm_sk<64, 16, 32, 4, 1>(fa, fb, ep, n, L.A + 1, 512, st, L);
   VN_HIP(hipGetLastError());
   return VN_OK;
 }
@@ -1166,7 +1242,7 @@ inline int lstm_backward(const PolicyLayout& L, const float* P, int T, int E, co
     DenseRows fa{dg, 2048, E};
     DenseRows fb{w.wcat_t + (int64_t)L.xoff * 2048, 2048, 512};
     EpiLstmDh ep{w.dh[cur], mask};
-    launch_gemm_x6<64, 64, 32, 2, 2>(fa, fb, ep, E, 512, 2048, st);
+    launch_gemm_x6_sk<64, 64, 32, 2, 2>(fa, fb, ep, E, 512, 2048, st, L);
   }
   {  // the trunk's input gradient of all T steps in one product: dz5 = relu'(x5) (dgates x W_ih[:, :512])
     DenseRows fa{w.dgates, 2048, N};
@@ -1418,11 +1494,23 @@ int vn_policy_create_ex(int frame_h, int frame_w, int num_actions, int flags, vn
   if (!p) return fail(VN_ENOMEM, "vn_policy_create: host allocation");
   p->L = make_layout(frame_h, frame_w, num_actions, (flags & VN_POLICY_LSTM) ? 1 : 0, (flags & VN_POLICY_AUX) ? 1 : 0,
                      (flags & VN_POLICY_BIGHOUSE) ? 1 : 0);
+  // split-K scratch on the current device (16 MB; without it small batches run unsplit)
+  p->L.sk = nullptr;
+  p->L.sk_cap = 0;
+  p->L.sk_dev = -1;
+  constexpr int64_t kSplitKFloats = 4 << 20;
+  if (hipGetDevice(&p->L.sk_dev) == hipSuccess && hipMalloc((void**)&p->L.sk, kSplitKFloats * 4) == hipSuccess) {
+    p->L.sk_cap = kSplitKFloats;
+  } else {
+    p->L.sk = nullptr;
+    (void)hipGetLastError();
+  }
   *out = p;
   return VN_OK;
 }
 
 int vn_policy_destroy(vn_policy* p) {
+  if (p && p->L.sk) (void)hipFree(p->L.sk);
   delete p;
   return VN_OK;
 }

@@ -12,7 +12,11 @@ reference — deep-rl 0.2.9 is absent — so parity is unpinned at this level).
 Everything per step is a device launch: policy forward on frames gathered zero-copy
 from the scene cache by row index, categorical sampling, env step (index-only), then
 returns, loss gradient, backward, one flat-buffer all-reduce, norm, clip + RMSprop. No
-host synchronisation inside ``step(sync=False)``.
+host synchronisation inside ``step(sync=False)``. The per-update values (sampling counter,
+learning rate) come from a device-side schedule (``vn_a2c_schedule``), so one update has no
+per-call host arguments: with ``cuda_graph=True`` it is captured once in a hipGraph and
+replayed (single process), which removes the per-launch host cost that dominates small
+batches (the reference's own run is 4 envs x 20 steps, ~400 launches per update).
 
 With a recurrent net (``recurrent=True``) each step also runs the LSTM core: the input is
 [conv_merge features | one-hot last action | last reward] and the carried (h, c), both
@@ -41,7 +45,7 @@ class A2CTrainer:
     def __init__(self, env, net=None, params=None, num_steps=20, gamma=0.99, learning_rate=7e-4,
                  max_time_steps=2e6, rms_alpha=0.99, rms_epsilon=1e-5, max_gradient_norm=0.5,
                  value_coefficient=0.5, entropy_coefficient=0.01, seed=0, process_group=None, recurrent=False,
-                 aux_weight=0.0, arch="goal"):
+                 aux_weight=0.0, arch="goal", cuda_graph=False):
         self.env = env
         self.lib = _lib.load()
         self.device = env.device
@@ -88,6 +92,10 @@ class A2CTrainer:
         self.norm_partial = torch.zeros(512, dtype=torch.float64, **kw)
         self.scalars = torch.zeros(2, dtype=torch.float32, **kw)
         self.episode_stats = torch.zeros(3, dtype=torch.float32, **kw)  # count, return sum, length sum
+        # device schedule: [next sampling-counter base (updates * T), env-steps so far, this
+        # update's counter base] and the learning rate of the update (vn_a2c_schedule)
+        self.sched = torch.zeros(3, dtype=torch.int64, **kw)
+        self.lr_dev = torch.zeros(1, dtype=torch.float32, **kw)
         self.workspace = torch.empty(self.net.workspace_floats(N), dtype=torch.float32, **kw)
         if self.recurrent:
             X = self.net.lstm["xcat"]
@@ -123,11 +131,18 @@ class A2CTrainer:
             self.aux_table = self.net.aux_target_table(*env.aux_arena)  # once per scene cache
             self._aux_targets = AuxTargets(self.aux_table.data_ptr(), self.rows_img.data_ptr(),
                                            self.rows_goal.data_ptr())
+            ph, pw = self.net.aux_layout["p_hw"]
+            self._aux_numel = torch.tensor([1.0, 3.0, 3.0], device=self.device) * (N * ph * pw)
         arena, fb, _, _ = env.frame_arena()
         self._arena, self._fb = arena, fb
         env.observe(gather=False)  # refresh the obs row buffers for the first forward
         self.num_updates = 0
         self.total_steps = 0
+        self.cuda_graph = bool(cuda_graph)
+        if self.cuda_graph and self.world > 1:
+            raise ValueError("cuda_graph=True is single-process only (the RCCL all-reduce is not captured)")
+        self._graph = None
+        self._graph_out = None
 
     # deep_rl hook names (experiments/thor_cached_auxiliary.py:50-56)
     def create_env(self, kwargs):
@@ -190,15 +205,20 @@ class A2CTrainer:
         N = T * E
         info = env._info
         self.episode_stats.zero_()
+        _lib.check(lib.vn_a2c_schedule(_lib.ptr(self.sched), _lib.ptr(self.lr_dev), ctypes.c_double(self.learning_rate),
+                                       ctypes.c_double(self.max_time_steps), ctypes.c_int64(N * self.world), T,
+                                       self._stream()), "vn_a2c_schedule")
+        ctr_base = ctypes.c_void_p(self.sched.data_ptr() + 2 * self.sched.element_size())
         for t in range(T):
             sl = slice(t * E, (t + 1) * E)
             self.rows_img[sl].copy_(info["img_row"])
             self.rows_goal[sl].copy_(info["goal_row"])
             self._policy_step(t, self._frames(self.rows_img[sl], self.rows_goal[sl]))
-            counter = (self.num_updates * T + t) & (2 ** 64 - 1)
-            _lib.check(lib.vn_policy_sample(_lib.ptr(self.out[sl]), E, A, ctypes.c_uint64(vdist.rank_seed(self.seed, self.rank)),
-                                            ctypes.c_uint64(counter), _lib.ptr(self.actions[sl]), None, None, None,
-                                            self._stream()), "vn_policy_sample")
+            # Philox counter = updates * T + t (base from the device schedule)
+            _lib.check(lib.vn_policy_sample_dev(_lib.ptr(self.out[sl]), E, A,
+                                                ctypes.c_uint64(vdist.rank_seed(self.seed, self.rank)), ctr_base,
+                                                ctypes.c_uint64(t), _lib.ptr(self.actions[sl]), None, None, None,
+                                                self._stream()), "vn_policy_sample_dev")
             env.step(self.actions[sl], out=dict(reward=self.rewards[t], done=self.dones[t], state=self.states),
                      gather=False)
             # next step's (last action, last reward) * mask and mask (bootstrap slots after the
@@ -248,28 +268,48 @@ class A2CTrainer:
         _lib.check(lib.vn_grad_norm(_lib.ptr(self.grads), P, ctypes.c_float(scale),
                                     ctypes.c_float(self.max_gradient_norm), _lib.ptr(self.norm_partial),
                                     _lib.ptr(self.scalars), st), "vn_grad_norm")
-        _lib.check(lib.vn_rmsprop_step(_lib.ptr(self.params), _lib.ptr(self.grads), _lib.ptr(self.square_avg), P,
-                                       ctypes.c_float(scale), _lib.ptr(self.scalars),
-                                       ctypes.c_float(self.current_lr()), ctypes.c_float(self.rms_alpha),
-                                       ctypes.c_float(self.rms_epsilon), st), "vn_rmsprop_step")
+        # lr of this update from the device schedule (== current_lr() of the host counters)
+        _lib.check(lib.vn_rmsprop_step_dev(_lib.ptr(self.params), _lib.ptr(self.grads), _lib.ptr(self.square_avg), P,
+                                           ctypes.c_float(scale), _lib.ptr(self.scalars), _lib.ptr(self.lr_dev),
+                                           ctypes.c_float(self.rms_alpha), ctypes.c_float(self.rms_epsilon), st),
+                   "vn_rmsprop_step_dev")
+
+    def _update_metrics(self):
+        """rollout + update; returns the device metric vector [value_loss, action_loss,
+        entropy, return mean, grad norm, aux loss, episodes, return sum, length sum]."""
+        self.rollout()
+        self.update()
+        N = self.num_steps * self.env.num_envs
+        if self.aux_weight > 0:  # sum of the per-head MSEs (trainer.py:51-54)
+            aux = (self.aux_stats[:3] / self._aux_numel).sum().view(1)
+        else:
+            aux = torch.zeros(1, device=self.device)
+        m = torch.cat([self.stats / N, self.scalars[:1], aux, self.episode_stats])
+        vdist.reduce_metrics_(m, 6, self.group)
+        return m
+
+    def _graph_update(self):
+        """The update through a captured hipGraph: the first update runs eagerly (kernel
+        attributes and occupancy caches are set up), the second is captured — capture
+        records the launches without running them — and every update replays it."""
+        if self._graph is None:
+            if self.num_updates == 0:
+                return self._update_metrics()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._graph_out = self._update_metrics()
+            self._graph = g
+        self._graph.replay()
+        return self._graph_out
 
     def step(self, sync=True):
         """One rollout (num_steps x num_envs) + one update. Returns the metric dict
         (deep_rl log keys) as floats when sync, else as device tensors."""
         t0 = time.perf_counter()
-        self.rollout()
-        self.update()
+        m = self._graph_update() if self.cuda_graph else self._update_metrics()
         N = self.num_steps * self.env.num_envs
         self.total_steps += N * self.world
         self.num_updates += 1
-        if self.aux_weight > 0:  # sum of the per-head MSEs (trainer.py:51-54)
-            ph, pw = self.net.aux_layout["p_hw"]
-            numel = torch.tensor([1.0, 3.0, 3.0], device=self.device) * (N * ph * pw)
-            aux = (self.aux_stats[:3] / numel).sum().view(1)
-        else:
-            aux = torch.zeros(1, device=self.device)
-        m = torch.cat([self.stats / N, self.scalars[:1], aux, self.episode_stats])
-        vdist.reduce_metrics_(m, 6, self.group)
         if not sync:
             return {"raw": m}
         vals = m.tolist()
@@ -311,6 +351,7 @@ class A2CTrainer:
         self.env.set_episode_returns(sd["env_ep_return"])
         self.num_updates = int(sd["num_updates"])
         self.total_steps = int(sd["total_steps"])
+        self.sched.copy_(torch.tensor([self.num_updates * self.num_steps, self.total_steps, 0], dtype=torch.int64))
         if self.recurrent:
             for k in self._RECURRENT_STATE:
                 getattr(self, k).copy_(sd[k].to(self.device))

@@ -87,8 +87,9 @@ class PolicyNet:
         h = ctypes.c_void_p()
         # VN_POLICY_LSTM | VN_POLICY_AUX | VN_POLICY_BIGHOUSE
         flags = (1 if recurrent else 0) | (2 if aux else 0) | (4 if arch == "bighouse" else 0)
-        _lib.check(self.lib.vn_policy_create_ex(frame_hw[0], frame_hw[1], num_actions, flags, ctypes.byref(h)),
-                   "vn_policy_create_ex")
+        with torch.cuda.device(self.device):  # the policy's split-K scratch lives on its device
+            _lib.check(self.lib.vn_policy_create_ex(frame_hw[0], frame_hw[1], num_actions, flags, ctypes.byref(h)),
+                       "vn_policy_create_ex")
         self._h = h
         n, a = ctypes.c_int64(), ctypes.c_int64()
         lay = (ctypes.c_int64 * 12)()

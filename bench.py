@@ -201,7 +201,7 @@ def aux_scenes(n, frame, seed=0):
 
 
 def bench_train(args, scenes, dev, world, rank, recurrent, aux_weight=0.0, envs=None, updates=None, warmup=None,
-                model=None):
+                model=None, cuda_graph=False):
     """A2C training throughput: one step = rollout of num_steps on every local env (policy
     forward + sampling + env step) + backward + one RCCL all-reduce of the flat gradient +
     clip + RMSprop. recurrent: the full BigGoalHouseModel (LSTM core, BPTT over the rollout);
@@ -211,7 +211,8 @@ def bench_train(args, scenes, dev, world, rank, recurrent, aux_weight=0.0, envs=
     updates = updates or args.train_steps
     warmup = args.train_warmup if warmup is None else warmup
     env = vnav.VectorEnv(scenes, E, seed=2000 + rank, device=dev)
-    tr = vnav.A2CTrainer(env, num_steps=T, seed=7, max_time_steps=1e12, recurrent=recurrent, aux_weight=aux_weight)
+    tr = vnav.A2CTrainer(env, num_steps=T, seed=7, max_time_steps=1e12, recurrent=recurrent, aux_weight=aux_weight,
+                         cuda_graph=cuda_graph)
     for _ in range(warmup):
         tr.step(sync=False)
     torch.cuda.synchronize(dev)
@@ -236,6 +237,7 @@ def bench_train(args, scenes, dev, world, rank, recurrent, aux_weight=0.0, envs=
         model = "BigGoalHouseModel (LSTM core)" if recurrent else "BigGoalHouseModel trunk + heads (no LSTM)"
     res = {"model": model, "frame": [h, w, 3],
            "value": steps / el, "unit": "env-steps/s", "updates": updates, "envs_per_gpu": E,
+           **({"cuda_graph": True} if cuda_graph else {}),
            "num_steps": T, "ms_per_update": el / updates * 1e3, "dtype": "f32",
            "roofline": {"bound": "mfma", "achieved": tflops, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                         "frac": tflops / FP32_MFMA_PEAK_TFLOPS, "flops_per_env_step": flops,
@@ -366,7 +368,7 @@ def main():
         elapsed, kern_ms = float(t[0]), float(t[1])
     flags = env.error_flags()
     del env, out
-    train = train_ff = train_ref = train_c5 = None
+    train = train_ff = train_ref = train_ref4 = train_c5 = None
     if args.train_steps > 0:
         torch.cuda.empty_cache()
         if not args.no_train_84:
@@ -383,6 +385,21 @@ def main():
                                     aux_weight=AUX_WEIGHT_LOGGED, updates=3, warmup=1,
                                     model="AuxiliaryBigGoalHouseModel (LSTM + deconv heads), 174x174")
             train_ref["reference_log_fps"] = REFERENCE_LOG_FPS
+            torch.cuda.empty_cache()
+        if not args.no_train_ref and world == 1:
+            # the logged run's exact shape: 4 envs x 20 steps per update (outputs/output.txt), where
+            # ~400 launches per update make it launch-bound: eager vs one captured hipGraph per update
+            sc4 = aux_scenes(4, (174, 174, 3))
+            eager = bench_train(args, sc4, dev, world, rank, recurrent=True, aux_weight=AUX_WEIGHT_LOGGED, envs=4,
+                                updates=100, warmup=3, model="AuxiliaryBigGoalHouseModel, 174x174, 4 envs (eager)")
+            train_ref4 = bench_train(args, sc4, dev, world, rank, recurrent=True, aux_weight=AUX_WEIGHT_LOGGED,
+                                     envs=4, updates=400, warmup=3, cuda_graph=True,
+                                     model="AuxiliaryBigGoalHouseModel (LSTM + deconv heads), 174x174, 4 envs "
+                                           "(the logged run's batch), hipGraph per update")
+            train_ref4["eager_value"] = eager["value"]
+            train_ref4["eager_ms_per_update"] = eager["ms_per_update"]
+            train_ref4["reference_log_fps"] = REFERENCE_LOG_FPS
+            del sc4
             torch.cuda.empty_cache()
         if args.c5:
             train_c5 = bench_train(args, aux_scenes(4, (300, 400, 3)), dev, world, rank, recurrent=True,
@@ -429,6 +446,7 @@ def main():
             "train": train,
             "train_feedforward": train_ff,
             "train_174_lstm_aux": train_ref,
+            "train_174_lstm_aux_4env": train_ref4,
             **({"train_c5_300x400": train_c5} if train_c5 else {}),
             "error_flags": flags,
         }

@@ -319,6 +319,24 @@ int vn_grad_norm(const float* grads, int64_t n, float scale, float max_norm, dou
 int vn_rmsprop_step(float* params, const float* grads, float* square_avg, int64_t n, float scale,
                     const float* scalars2, float lr, float alpha, float eps, vn_stream_t stream);
 
+/* Device-side schedule, so that one update has no per-call host arguments and can be
+ * captured once in a hipGraph and replayed (A2CTrainer(cuda_graph=True)):
+ *   vn_a2c_schedule: state3 = int64 [next counter base, env-steps so far, this update's
+ *     counter base]; this update's base = state3[0] (then += T), lr_out = lr0 * (1 -
+ *     min(state3[1] / max_time_steps, 1)) computed in double (LinearSchedule,
+ *     experiments/thor_cached_auxiliary.py:37), then state3[1] += steps_per_update;
+ *   vn_policy_sample_dev: vn_policy_sample with counter = *counter_base_dev + offset;
+ *   vn_rmsprop_step_dev: vn_rmsprop_step with lr read from lr_dev.
+ * Bit-identical to the host-argument forms fed the same values. */
+int vn_a2c_schedule(int64_t* state3, float* lr_out, double lr0, double max_time_steps,
+                    int64_t steps_per_update, int T, vn_stream_t stream);
+int vn_policy_sample_dev(const float* out, int n, int num_actions, uint64_t seed,
+                         const int64_t* counter_base_dev, uint64_t counter_offset, int32_t* actions,
+                         float* logp, float* entropy, float* value, vn_stream_t stream);
+int vn_rmsprop_step_dev(float* params, const float* grads, float* square_avg, int64_t n, float scale,
+                        const float* scalars2, const float* lr_dev, float alpha, float eps,
+                        vn_stream_t stream);
+
 /* Copy the message of the calling thread's last error (NUL-terminated). */
 int vn_last_error(char* buf, size_t len);
 const char* vn_version(void);

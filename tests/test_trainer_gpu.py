@@ -124,3 +124,30 @@ def test_checkpoint_resume_is_exact(recurrent):
     for x, y in zip(ma, mb):
         for k in keys:
             assert (x[k] == y[k]) or (np.isnan(x[k]) and np.isnan(y[k])), (k, x[k], y[k])
+
+
+@pytest.mark.parametrize("recurrent", [False, True])
+def test_cuda_graph_updates_are_bit_identical(recurrent):
+    """A2CTrainer(cuda_graph=True) — the update captured once in a hipGraph and replayed —
+    gives bit-identical parameters, optimiser state, env state and metrics to the eager
+    updates, with a learning rate that changes every update (device-side schedule)."""
+    import vnav
+    sc = [vnav.synthetic_scene(k) for k in range(2)]
+
+    def run(graph):
+        env = vnav.VectorEnv(sc, 8, seed=5, max_episode_steps=12)
+        tr = vnav.A2CTrainer(env, num_steps=5, seed=9, max_time_steps=400, recurrent=recurrent, cuda_graph=graph)
+        ms = [tr.step(sync=True) for _ in range(6)]
+        return (tr.params.detach().cpu(), tr.square_avg.cpu(), env.get_state().cpu(), ms, tr.lr_dev.cpu(),
+                tr.current_lr())
+
+    pe, se, ee, me, lre, lr_host = run(False)
+    pg, sg, eg, mg, lrg, _ = run(True)
+    assert torch.equal(pe, pg) and torch.equal(se, sg) and torch.equal(ee, eg)
+    assert torch.equal(lre, lrg)
+    # the device schedule's lr of the last update is the host LinearSchedule's value before it
+    assert float(lre[0]) == float(np.float32(7e-4 * (1.0 - min(5 * 8 * 5 / 400.0, 1.0))))
+    keys = ("value_loss", "action_loss", "entropy", "episodes", "reward", "episode_length", "grad_norm")
+    for x, y in zip(me, mg):
+        for k in keys:
+            assert (x[k] == y[k]) or (np.isnan(x[k]) and np.isnan(y[k])), (k, x[k], y[k])
