@@ -945,9 +945,17 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
       float* bias_slab = w.slab + (int64_t)blocks * 32 * 512;
       hipLaunchKernelGGL((conv2_wgrad_kernel<G::OH1, G::OW1, G::OH2, G::OW2>), dim3(blocks), dim3(256), lds, st,
                          a.X[0], w.dz2, frames, w.slab, bias_slab);
-      hipLaunchKernelGGL(sum_slabs_kernel, dim3((32 * 512 + 255) / 256), dim3(256), 0, st, w.slab, blocks,
+      // two-stage fixed-order reduce of the per-workgroup slabs (one pass over 512 slabs per
+      // element ran 118 us, latency-bound)
+      constexpr int kParts = 32;
+      float* part = bias_slab + (int64_t)blocks * 32;
+      float* bpart = part + (int64_t)kParts * 32 * 512;
+      hipLaunchKernelGGL(slab_partial_kernel, dim3((32 * 512 + 255) / 256, kParts), dim3(256), 0, st, w.slab, blocks,
+                         (int64_t)32 * 512, part);
+      hipLaunchKernelGGL(slab_partial_kernel, dim3(1, kParts), dim3(32), 0, st, bias_slab, blocks, (int64_t)32, bpart);
+      hipLaunchKernelGGL(sum_slabs_kernel, dim3((32 * 512 + 255) / 256), dim3(256), 0, st, part, kParts,
                          (int64_t)32 * 512, Gr + L.l[1].w);
-      hipLaunchKernelGGL(sum_slabs_kernel, dim3(1), dim3(32), 0, st, bias_slab, blocks, (int64_t)32, Gr + L.l[1].b);
+      hipLaunchKernelGGL(sum_slabs_kernel, dim3(1), dim3(32), 0, st, bpart, kParts, (int64_t)32, Gr + L.l[1].b);
     } else {  // a conv1 map row too wide for a band in half the LDS: generic split-K path
       using Im = NhwcIm2col<32, 4, 4, 2, G::OH1, G::OW1, G::OH2, G::OW2, 1>;
       const int P2 = 2 * n * G::OH2 * G::OW2;
