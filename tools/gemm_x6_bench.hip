@@ -259,7 +259,43 @@ __global__ __launch_bounds__(256) void xdb(FA fa, FB fb, EP ep, int M, int N, in
   });
 }
 
-int main() {
+template <int BM, int BN, int WM, int WN>
+static void dh_shape(int M, int N, int K, const char* name) {
+  float* a = dalloc((int64_t)M * K, 31, -0.5f);
+  float* b = dalloc((int64_t)N * K, 32, -0.05f);
+  float* c = dalloc((int64_t)M * N, 33, 0.f);
+  float* bias = dalloc(N, 34, 0.f);
+  DenseRows fa{a, K, M};
+  DenseRows fb{b, K, N};
+  EpiBias2 ep{c, N, bias, bias};
+  const double fl = 2.0 * M * N * K;
+  float ms = timeit([&] { launch_gemm_x6<BM, BN, 32, WM, WN>(fa, fb, ep, M, N, K, 0); });
+  printf("%-12s M %6d N %5d K %5d <%3d,%3d,%d,%d>  %8.1f us %7.1f TF(f32-equiv) %5.1f%% x6 peak\n", name, M, N, K, BM, BN,
+         WM, WN, ms * 1e3, fl / ms / 1e9, 100.0 * fl * 6 / (ms * 1e-3) / 2.5e15);
+  hipFree(a);
+  hipFree(b);
+  hipFree(c);
+  hipFree(bias);
+}
+
+int main(int argc, char** argv) {
+  if (argc > 1 && atoi(argv[1]) == 2) {
+    for (int rep = 0; rep < 2; ++rep) {
+      dh_shape<64, 64, 2, 2>(4096, 512, 2048, "lstm dh");
+      dh_shape<128, 64, 2, 2>(4096, 512, 2048, "lstm dh");
+      dh_shape<64, 128, 2, 2>(4096, 512, 2048, "lstm dh");
+      dh_shape<128, 128, 2, 2>(4096, 512, 2048, "lstm dh");
+      dh_shape<64, 64, 2, 2>(4096, 512, 288, "fc 84");
+      dh_shape<128, 64, 2, 2>(4096, 512, 288, "fc 84");
+      dh_shape<128, 128, 2, 2>(4096, 512, 288, "fc 84");
+      dh_shape<128, 128, 2, 2>(81920, 512, 2048, "dz5 batched");
+      dh_shape<128, 64, 2, 2>(81920, 512, 2048, "dz5 batched");
+      dh_shape<128, 128, 2, 2>(4096, 2048, 1032, "gates");
+      dh_shape<128, 64, 2, 2>(4096, 2048, 1032, "gates");
+      dh_shape<64, 128, 2, 2>(4096, 2048, 1032, "gates");
+    }
+    return 0;
+  }
   const int E = 4096, XC = 1032, N = 2048;
   float* xc = dalloc((int64_t)E * XC, 21, -0.5f);
   float* wc = dalloc((int64_t)N * XC, 22, -0.05f);
