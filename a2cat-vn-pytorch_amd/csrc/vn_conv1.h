@@ -1124,19 +1124,23 @@ __global__ __launch_bounds__(512, 2) void conv2_fwd_x6_kernel(const float* __res
     }
   const int n_items = n_frames * NB;
   auto band_f4 = [&](int band) { return min(BRI, IH - 2 * BR * band) * IW * 8; };
-  f4 pre[NV];
-  auto load_item = [&](int it) {
+  // two items' X1 in flight: item it + 2 * gridDim.x is loaded into the registers item it
+  // just split into LDS (one item of MFMA work was shorter than the load under full load)
+  f4 pre[2][NV];
+  auto load_item = [&](f4 (&pr)[NV], int it) {
     const int f = it / NB, band = it - (it / NB) * NB;
     const f4* s4 = reinterpret_cast<const f4*>(X1 + ((int64_t)f * IH + 2 * BR * band) * IW * 32);
     const int nv = band_f4(band);
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
       const int i = tid + j * 512;
-      if (i < nv) pre[j] = s4[i];
+      if (i < nv) pr[j] = s4[i];
     }
   };
-  if ((int)blockIdx.x < n_items) load_item(blockIdx.x);
-  for (int it = blockIdx.x; it < n_items; it += gridDim.x) {
+  if ((int)blockIdx.x < n_items) load_item(pre[0], blockIdx.x);
+  if ((int)(blockIdx.x + gridDim.x) < n_items) load_item(pre[1], blockIdx.x + gridDim.x);
+  auto item = [&](auto stage, int it) {
+    constexpr int S = decltype(stage)::value;
     const int f = it / NB, band = it - (it / NB) * NB;
     const int oy0 = BR * band, nr = min(BR, OH - oy0), npb = nr * OW;
     {  // split the band's X1 rows into the three planes
@@ -1147,7 +1151,7 @@ __global__ __launch_bounds__(512, 2) void conv2_fwd_x6_kernel(const float* __res
         if (i < nv) {
           const int c4 = i & 7, px = i >> 3, y = px / IW, x = px - (px / IW) * IW;
           uint2 t0, t1, t2;
-          split3_pack(pre[j], t0, t1, t2);
+          split3_pack(pre[S][j], t0, t1, t2);
           uint16_t* d = xs + y * RSP + ((x & 1) * WH + (x >> 1)) * PSX + 4 * c4;
           *reinterpret_cast<uint2*>(d) = t0;
           *reinterpret_cast<uint2*>(d + PL) = t1;
@@ -1156,7 +1160,7 @@ __global__ __launch_bounds__(512, 2) void conv2_fwd_x6_kernel(const float* __res
       }
     }
     __syncthreads();
-    if (it + (int)gridDim.x < n_items) load_item(it + gridDim.x);
+    if (it + 2 * (int)gridDim.x < n_items) load_item(pre[S], it + 2 * gridDim.x);
     const int tiles = (npb + 15) / 16;
     for (int t = ph; t < tiles; t += 2) {
       const int p = min(t * 16 + i16, npb - 1);  // this lane's band pixel (B column)
@@ -1197,6 +1201,10 @@ __global__ __launch_bounds__(512, 2) void conv2_fwd_x6_kernel(const float* __res
       for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r] + b4[r], 0.0f);
       *reinterpret_cast<f4*>(X2 + out0 + (int64_t)i * 4) = v;
     }
+  };
+  for (int it = blockIdx.x; it < n_items; it += 2 * gridDim.x) {
+    item(std::integral_constant<int, 0>{}, it);
+    if (it + (int)gridDim.x < n_items) item(std::integral_constant<int, 1>{}, it + gridDim.x);
   }
 }
 
