@@ -695,10 +695,43 @@ inline void dgrad_class(const float* dz, const float* WT, float* out, const floa
 
 // All G input-channel groups of a class in one product (N = G * cin): the gathered and
 // split dZ operand serves twice the columns.
+// Rows / columns of an H x W input that a k4 s2 conv with an OH x OW output reads at all
+// (84x84 conv3: 8 of 9 — row 8 and column 8 get no gradient).
+template <int H, int OH>
+constexpr int k4s2_covered() {
+  return H < 2 * (OH - 1) + 4 ? H : 2 * (OH - 1) + 4;
+}
+
+// dX = 0 at the input pixels no output window covers (all G groups of every image).
+template <int H, int W, int CH, int CW>
+__global__ void zero_uncovered_kernel(float* __restrict__ out, int nimg_g, int cin) {
+  constexpr int NU = H * W - CH * CW;  // uncovered pixels per image
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int c4n = cin / 4;
+  if (i >= (int64_t)nimg_g * NU * c4n) return;
+  const int c4 = (int)(i % c4n);
+  const int64_t q = i / c4n;
+  const int u = (int)(q % NU);
+  const int64_t ng = q / NU;
+  int y, x;
+  if (u < (H - CH) * W) {  // whole uncovered rows
+    y = CH + u / W;
+    x = u % W;
+  } else {  // uncovered columns of the covered rows
+    const int v = u - (H - CH) * W;
+    y = v / (W - CW);
+    x = CW + v % (W - CW);
+  }
+  *reinterpret_cast<f4*>(out + ((ng * H + y) * W + x) * cin + 4 * c4) = f4zero();
+}
+
 template <int COUT, int CIN, int H, int W, int OH, int OW, int PY, int PX>
 inline void dgrad_class_groups(const float* dz, const float* WT, float* out, const float* X, int nimg, int G,
                                hipStream_t st) {
-  constexpr int HYC = (H - PY + 1) / 2, WXC = (W - PX + 1) / 2;
+  // only the covered pixels: at 84x84 the 5x5 / 5x4 classes of conv3's 9x9 input shrink to
+  // 4x4 (64 of 81 rows per image; the uncovered 17 are zeroed by dgrad_all_classes_groups)
+  constexpr int CH = k4s2_covered<H, OH>(), CW = k4s2_covered<W, OW>();
+  constexpr int HYC = (CH - PY + 1) / 2, WXC = (CW - PX + 1) / 2;
   const int M = nimg * HYC * WXC;
   DgradA<COUT, 4, 2, OH, OW, HYC, WXC> fa{dz, M};
   static_assert(CIN == 32, "conv3: two groups of 32 channels (W^T rows of 64)");
@@ -714,6 +747,12 @@ inline void dgrad_all_classes_groups(const float* dz, const float* WT, float* ou
   dgrad_class_groups<COUT, CIN, H, W, OH, OW, 0, 1>(dz, WT, out, X, nimg, G, st);
   dgrad_class_groups<COUT, CIN, H, W, OH, OW, 1, 0>(dz, WT, out, X, nimg, G, st);
   dgrad_class_groups<COUT, CIN, H, W, OH, OW, 1, 1>(dz, WT, out, X, nimg, G, st);
+  constexpr int CH = k4s2_covered<H, OH>(), CW = k4s2_covered<W, OW>();
+  if constexpr (CH < H || CW < W) {
+    const int64_t total = (int64_t)nimg * G * (H * W - CH * CW) * (CIN / 4);
+    hipLaunchKernelGGL((zero_uncovered_kernel<H, W, CH, CW>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
+                       out, nimg * G, CIN);
+  }
 }
 
 template <int COUT, int CINF, int H, int W, int OH, int OW>
