@@ -58,6 +58,8 @@ def parse():
     p.add_argument("--no-train-84", action="store_true", help="skip the 84x84 LSTM train leg")
     p.add_argument("--no-train-ref", action="store_true",
                    help="skip the 174x174 LSTM + aux-deconv train leg (the reference's logged experiment shape)")
+    p.add_argument("--no-train-ref4", action="store_true",
+                   help="skip the 4-env (the logged run's batch) 174x174 leg")
     p.add_argument("--c5", action="store_true", help="add the 300x400 + goal + aux-depth train leg (config C5)")
     p.add_argument("--num-steps", type=int, default=20, help="A2C rollout length (reference: 20)")
     p.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
@@ -386,7 +388,7 @@ def main():
                                     model="AuxiliaryBigGoalHouseModel (LSTM + deconv heads), 174x174")
             train_ref["reference_log_fps"] = REFERENCE_LOG_FPS
             torch.cuda.empty_cache()
-        if not args.no_train_ref and world == 1:
+        if not args.no_train_ref and not args.no_train_ref4 and world == 1:
             # the logged run's exact shape: 4 envs x 20 steps per update (outputs/output.txt), where
             # ~400 launches per update make it launch-bound: eager vs one captured hipGraph per update
             sc4 = aux_scenes(4, (174, 174, 3))
