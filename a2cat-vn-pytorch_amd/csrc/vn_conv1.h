@@ -1073,7 +1073,10 @@ struct Conv2FwdBand {
   static constexpr int rows_of(int br) { return 2 * br + 2 < IH ? 2 * br + 2 : IH; }
   static constexpr int tiles_of(int br) { return (br * OW + 15) / 16; }
   static constexpr size_t planes_of(int br) { return (size_t)3 * rows_of(br) * RSP * 2; }
-  static constexpr size_t lds_of(int br) { return planes_of(br) + (size_t)4 * tiles_of(br) * 16 * 32 * 4; }
+  // partial sums [4 kernel rows][band pixels][PP]: rows padded to 36 floats so the 16 pixels
+  // of an MFMA tile's f4 stores land on distinct bank quads (32: 8-way conflicts)
+  static constexpr int PP = 36;
+  static constexpr size_t lds_of(int br) { return planes_of(br) + (size_t)4 * tiles_of(br) * 16 * PP * 4; }
   static constexpr int br_max() {
     int br = OH;
     while (br > 1 && lds_of(br) > 160 * 1024) --br;
@@ -1105,7 +1108,8 @@ __global__ __launch_bounds__(512, 2) void conv2_fwd_x6_kernel(const float* __res
   constexpr int NV = (BRI * IW * 8 + 511) / 512;                       // prefetched f4 per thread
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_c2[];
   uint16_t* xs = reinterpret_cast<uint16_t*>(smem_c2);
-  float* part = reinterpret_cast<float*>(smem_c2 + (size_t)3 * PL * 2);  // [4][TP][32]
+  float* part = reinterpret_cast<float*>(smem_c2 + (size_t)3 * PL * 2);  // [4][TP][PP]
+  constexpr int PP = Bd::PP;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ky = wave & 3, ph = wave >> 2;
   const int i16 = lane & 15, q = lane >> 4;
@@ -1188,14 +1192,15 @@ __global__ __launch_bounds__(512, 2) void conv2_fwd_x6_kernel(const float* __res
       // lane (pixel i16, q) holds co nt*16 + 4q .. +3 of its pixel
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt)
-        *reinterpret_cast<f4*>(part + ((ky * TP + t * 16 + i16) * 32 + nt * 16 + 4 * q)) = acc[nt];
+        *reinterpret_cast<f4*>(part + ((ky * TP + t * 16 + i16) * PP + nt * 16 + 4 * q)) = acc[nt];
     }
     __syncthreads();
     const int64_t out0 = ((int64_t)f * NP + oy0 * OW) * 32;
     for (int i = tid; i < npb * 8; i += 512) {  // (pixel, co quad): fixed-order sum of the 4 rows
       const int p = i >> 3, c4 = i & 7;
-      const f4* pp = reinterpret_cast<const f4*>(part) + p * 8 + c4;
-      f4 v = ((pp[0] + pp[TP * 8]) + pp[2 * TP * 8]) + pp[3 * TP * 8];
+      const f4* pp = reinterpret_cast<const f4*>(part + p * PP) + c4;
+      constexpr int RS4 = TP * PP / 4;  // one kernel row's partials, in f4
+      f4 v = ((pp[0] + pp[RS4]) + pp[2 * RS4]) + pp[3 * RS4];
       const f4 b4 = *reinterpret_cast<const f4*>(bias + 4 * c4);
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r] + b4[r], 0.0f);
