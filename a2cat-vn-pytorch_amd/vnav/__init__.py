@@ -9,5 +9,6 @@ from .scenes import (Scene, grid_tables, load_graph_pickle, load_h5, load_npz, m
 from .envs import VectorEnv, make, to_float_chw  # noqa: F401
 from .policy import BigHousePolicy, GoalNavPolicy, PolicyNet  # noqa: F401
 from .a2c import A2CTrainer  # noqa: F401
+from ._lib import VnavError  # noqa: F401
 
 __version__ = "0.1.0"

@@ -178,6 +178,22 @@ class VectorEnv:
     def _stream(self):
         return _lib.stream_ptr(self.device)
 
+    def _check_out(self, name, t, dtype, numel):
+        """Caller-owned output buffers are written by the kernel through raw pointers: refuse
+        anything the launch would write past or misread (wrong device, dtype, size, layout)."""
+        if t is None:
+            return
+        if not isinstance(t, torch.Tensor) or t.device != self.device:
+            raise ValueError("%s must be a tensor on %s" % (name, self.device))
+        if t.dtype != dtype or not t.is_contiguous() or t.numel() != numel:
+            raise ValueError("%s must be a contiguous %s tensor of %d elements (got %s, %d, contiguous=%s)"
+                             % (name, dtype, numel, t.dtype, t.numel(), t.is_contiguous()))
+
+    def _check_frames_out(self, img, goal):
+        F = int(np.prod(self.frame_shape))
+        self._check_out("image", img, torch.uint8, self.num_envs * F)
+        self._check_out("goal", goal, torch.uint8, self.num_envs * F)
+
     def _frames(self):
         shape = (self.num_envs,) + self.frame_shape
         return (torch.empty(shape, dtype=torch.uint8, device=self.device),
@@ -187,6 +203,8 @@ class VectorEnv:
         m = None
         if mask is not None:
             m = torch.as_tensor(mask, device=self.device).to(torch.int32).contiguous()
+            if m.shape != (self.num_envs,):
+                raise ValueError("reset mask must have shape [num_envs]")
         _lib.check(self.lib.vn_reset(self._ctx, _lib.ptr(m), self._stream()), "vn_reset")
         return self.observe()
 
@@ -196,6 +214,7 @@ class VectorEnv:
             _lib.check(self.lib.vn_observe(self._ctx, None, None, None, self._stream()), "vn_observe")
             return None, None
         img, goal = out if out is not None else self._frames()
+        self._check_frames_out(img, goal)
         _lib.check(self.lib.vn_observe(self._ctx, _lib.ptr(img), _lib.ptr(goal), None, self._stream()), "vn_observe")
         if self.aux_observations:
             return (img, goal) + self._gather_aux()
@@ -220,7 +239,11 @@ class VectorEnv:
             state = torch.empty(self.num_envs, dtype=torch.int32, device=self.device)
         else:
             img, goal = (out["image"], out["goal"]) if gather else (None, None)
-            reward, done, state = out["reward"], out["done"], out["state"]
+            reward, done, state = out.get("reward"), out.get("done"), out.get("state")
+            self._check_frames_out(img, goal)
+            self._check_out("reward", reward, torch.float32, self.num_envs)
+            self._check_out("done", done, torch.bool, self.num_envs)
+            self._check_out("state", state, torch.int32, self.num_envs)
         _lib.check(self.lib.vn_step(self._ctx, _lib.ptr(a), _lib.ptr(img), _lib.ptr(goal), _lib.ptr(reward),
                                     _lib.ptr(done), _lib.ptr(state), self._stream()), "vn_step")
         info = dict(self._info)

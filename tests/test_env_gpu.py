@@ -101,7 +101,10 @@ def small_scenes(shape=(6, 10, 3)):
     for k, (X, Y, p) in enumerate([(6, 8, 0.3), (5, 5, 0.0), (7, 4, 0.25)]):
         maze = np.random.RandomState(40 + k).rand(X, Y) >= p
         graph, spd, _ = og.h5_tables(maze)
-        frames = synth_frames(7 + k, np.arange(len(graph)), shape)
+        if np.prod(shape) % 4 == 0:
+            frames = synth_frames(7 + k, np.arange(len(graph)), shape)
+        else:  # the hash frames are whole words; odd frame sizes get seeded random bytes
+            frames = np.random.RandomState(7 + k).randint(0, 256, size=(len(graph),) + tuple(shape)).astype(np.uint8)
         out.append(vnav.scene_from_arrays(graph, spd, frames))
     return out
 
@@ -154,6 +157,99 @@ def test_vector_env_matches_oracle(mode):
         out = env.step(torch.as_tensor(a, device="cuda"))
         compare_step(out, o.step(a), arena, (mode, t))
     assert env.error_flags() == o.flags == oe.FLAG_BAD_ACTION
+
+
+@pytest.mark.parametrize("shape,offset", [((5, 7, 3), 0), ((6, 10, 3), 0), ((4, 8, 3), 0), ((4, 8, 3), 1),
+                                          ((4, 8, 3), 4)])
+def test_frame_copy_paths_ragged(shape, offset):
+    """The 16-B, 4-B and 1-B frame copy paths of vn_step (frame bytes 96 / 180 / 105, and 96
+    into output buffers offset by 1 and 4 bytes) at a ragged env count (37 = 9 full
+    workgroups + 1 env), bit-exact vs the oracle, with caller-owned outputs."""
+    vnav = _vnav()
+    sc = small_scenes(shape)
+    arena = np.concatenate([s.observations for s in sc])
+    n, F = 37, int(np.prod(shape))
+    env = vnav.VectorEnv(sc, n, seed=4242, max_episode_steps=11)
+    o = oracle_of(sc, n, 4242, max_steps=11)
+    buf = torch.zeros(2 * (n * F + 16), dtype=torch.uint8, device="cuda")
+    img = buf[offset:offset + n * F].view((n,) + shape)
+    g0 = n * F + 16 + offset
+    goal = buf[g0:g0 + n * F].view((n,) + shape)
+    out = dict(image=img, goal=goal, reward=torch.empty(n, dtype=torch.float32, device="cuda"),
+               done=torch.empty(n, dtype=torch.bool, device="cuda"), state=torch.empty(n, dtype=torch.int32, device="cuda"))
+    rng = np.random.RandomState(5)
+    for t in range(50):
+        a = rng.randint(0, 4, size=n).astype(np.int32)
+        compare_step(env.step(torch.as_tensor(a, device="cuda"), out=out), o.step(a), arena, (shape, offset, t))
+    # nothing outside the two output rows was touched
+    b = buf.cpu().numpy()
+    assert not b[:offset].any() and not b[offset + n * F:g0].any() and not b[g0 + n * F:].any()
+
+
+def test_bad_buffers_are_refused():
+    """Caller-owned buffers the kernels would write past (or misread) raise before launch."""
+    vnav = _vnav()
+    sc = small_scenes()
+    n = 8
+    env = vnav.VectorEnv(sc, n, seed=1)
+    F = int(np.prod(env.frame_shape))
+    ok = dict(image=torch.empty((n,) + env.frame_shape, dtype=torch.uint8, device="cuda"),
+              goal=torch.empty((n,) + env.frame_shape, dtype=torch.uint8, device="cuda"),
+              reward=torch.empty(n, dtype=torch.float32, device="cuda"),
+              done=torch.empty(n, dtype=torch.bool, device="cuda"),
+              state=torch.empty(n, dtype=torch.int32, device="cuda"))
+    a = torch.zeros(n, dtype=torch.int32, device="cuda")
+    env.step(a, out=ok)
+    bad = [("image", torch.empty(n * F - 1, dtype=torch.uint8, device="cuda")),
+           ("goal", torch.empty((n,) + env.frame_shape, dtype=torch.float32, device="cuda")),
+           ("image", torch.empty((n, 2 * F), dtype=torch.uint8, device="cuda")[:, ::2]),
+           ("reward", torch.empty(n + 1, dtype=torch.float32, device="cuda")),
+           ("done", torch.empty(n, dtype=torch.uint8, device="cuda")),
+           ("state", torch.empty(n, dtype=torch.int64, device="cuda")),
+           ("image", torch.empty((n,) + env.frame_shape, dtype=torch.uint8))]
+    for k, t in bad:
+        with pytest.raises(ValueError):
+            env.step(a, out=dict(ok, **{k: t}))
+    with pytest.raises(ValueError):
+        env.step(torch.zeros(n + 1, dtype=torch.int32, device="cuda"))
+    with pytest.raises(ValueError):
+        env.reset(torch.ones(n - 1, dtype=torch.bool, device="cuda"))
+    with pytest.raises(ValueError):
+        env.observe(out=(ok["image"], ok["goal"][:1]))
+    with pytest.raises(vnav.VnavError):
+        vnav.VectorEnv(sc, 0)
+    assert env.error_flags() == 0
+
+
+def test_c4_env_count_on_one_gpu():
+    """Config C4's whole env count (32768 envs, 20 synthetic scenes, 84x84 frames) on one
+    GPU: states, rewards, dones and frame rows bit-exact vs the oracle over 12 steps,
+    gathered bytes checked on a sample, no error flags."""
+    vnav = _vnav()
+    sc = [vnav.synthetic_scene(k) for k in range(20)]
+    n = 32768
+    env = vnav.VectorEnv(sc, n, seed=2024)
+    o = oracle_of(sc, n, 2024, max_steps=900)
+    bases = np.concatenate([[0], np.cumsum([s.n_states for s in sc])[:-1]])
+    rng = np.random.RandomState(11)
+    sample = np.sort(rng.choice(n, 48, replace=False))
+    idx = torch.as_tensor(sample, device="cuda")
+    for t in range(12):
+        a = rng.randint(0, 4, size=n).astype(np.int32)
+        (img, goal), reward, done, info = env.step(torch.as_tensor(a, device="cuda"))
+        ob = o.step(a)
+        assert np.array_equal(info["state"].cpu().numpy(), ob["state"]), t
+        assert np.array_equal(done.cpu().numpy(), ob["done"]), t
+        assert np.array_equal(reward.cpu().numpy().view(np.uint32), ob["reward"].view(np.uint32)), t
+        assert np.array_equal(info["img_row"].cpu().numpy(), ob["img_row"]), t
+        assert np.array_equal(info["goal_row"].cpu().numpy(), ob["goal_row"]), t
+        if t % 4 == 3:
+            im, gl = img[idx].cpu().numpy(), goal[idx].cpu().numpy()
+            for j, e in enumerate(sample):
+                k = int(o.scene[e])
+                assert np.array_equal(im[j], synth_frames(k, [ob["img_row"][e] - bases[k]], FRAME)[0])
+                assert np.array_equal(gl[j], synth_frames(k, [ob["goal_row"][e] - bases[k]], FRAME)[0])
+    assert env.error_flags() == 0
 
 
 def test_index_only_step_and_masked_reset():
