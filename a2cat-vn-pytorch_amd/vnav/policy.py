@@ -122,6 +122,20 @@ class PolicyNet:
             self.aux_layout = dict(w1=info[0], b1=info[1], w2=info[2], b2=info[3], a_hw=(info[4], info[5]),
                                    p_hw=(info[6], info[7]))
 
+    def check_frames(self, image, goal):
+        """Dense frame batches are read by the kernels through raw pointers at this net's
+        geometry: refuse any other shape, dtype, device or layout before a launch."""
+        H, W = self.frame_hw
+        for name, t in (("image", image), ("goal", goal)):
+            if not isinstance(t, torch.Tensor) or t.device != self.device or not t.is_contiguous():
+                raise ValueError("%s frames must be a contiguous tensor on %s" % (name, self.device))
+            want = {torch.uint8: (H, W, 3), torch.float32: (3, H, W)}.get(t.dtype)
+            if want is None or t.dim() != 4 or tuple(t.shape[1:]) != want:
+                raise ValueError("%s frames must be uint8 [n,%d,%d,3] or float32 [n,3,%d,%d] (got %s %s)"
+                                 % (name, H, W, H, W, t.dtype, tuple(t.shape)))
+        if image.dtype != goal.dtype or image.shape[0] != goal.shape[0]:
+            raise ValueError("image and goal frames must have the same dtype and batch size")
+
     def __del__(self):
         try:
             if getattr(self, "_h", None):
@@ -426,6 +440,7 @@ class _ReferenceNames:
 class _GoalNavFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, params, image, goal, net):
+        net.check_frames(image, goal)
         n = image.shape[0]
         acts = net.new_acts(n)
         out = torch.empty((n, OUT_LD), dtype=torch.float32, device=params.device)
@@ -455,7 +470,11 @@ class _RecurrentGoalNavFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, params, image, goal, lra, masks, h0, c0, net, T, B):
+        net.check_frames(image, goal)
         n = T * B
+        if image.shape[0] != n or lra.shape != (n, net.num_actions + 1) or masks.shape != (T, B) or \
+                h0.shape != (B, 512) or c0.shape != (B, 512):
+            raise ValueError("recurrent inputs do not match T=%d, B=%d" % (T, B))
         dev = params.device
         acts = net.new_acts(n)
         frames = frames_from_batch(image, goal)
@@ -503,6 +522,7 @@ class _AuxDeconvFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, params, image, goal, net):
+        net.check_frames(image, goal)
         n = image.shape[0]
         dev = params.device
         acts = net.new_acts(n)
@@ -566,12 +586,13 @@ class GoalNavPolicy(torch.nn.Module):
         if self.net.recurrent:
             return self._forward_recurrent(image, goal, _last_reward_action, masks, states)
         lead = image.shape[:2]
+        dev = self.params.device
         if image.dtype == torch.uint8:   # env frames [B,T,H,W,3]
-            img = image.reshape(-1, *image.shape[2:]).contiguous()
-            gl = goal.reshape(-1, *goal.shape[2:]).contiguous()
+            img = image.to(dev).reshape(-1, *image.shape[2:]).contiguous()
+            gl = goal.to(dev).reshape(-1, *goal.shape[2:]).contiguous()
         else:                            # reference wrapper output [B,T,3,H,W] float
-            img = image.reshape(-1, *image.shape[2:]).float().contiguous()
-            gl = goal.reshape(-1, *goal.shape[2:]).float().contiguous()
+            img = image.to(dev).reshape(-1, *image.shape[2:]).float().contiguous()
+            gl = goal.to(dev).reshape(-1, *goal.shape[2:]).float().contiguous()
         out = _GoalNavFunction.apply(self.params, img, gl, self.net)
         A = self.net.num_actions
         return [out[:, :A].reshape(*lead, A), out[:, A:A + 1].reshape(*lead, 1), states]

@@ -325,3 +325,28 @@ def test_sampling_distribution():
     cdf = np.cumsum(p)
     ref = np.minimum(np.searchsorted(cdf[:-1], u, side="right"), 3)
     assert (ref == a).mean() > 0.999
+
+
+def test_policy_refuses_mismatched_frames_and_moves_host_frames():
+    """Frames the kernels would misread (another geometry, dtype, layout, batch) raise
+    before launch; host-resident frames are moved to the policy's device (same outputs)."""
+    import vnav
+    pol = vnav.GoalNavPolicy(frame_hw=(84, 84), seed=3)
+    g = torch.Generator().manual_seed(0)
+    img = torch.randint(0, 256, (2, 3, 84, 84, 3), generator=g, dtype=torch.uint8)
+    goal = torch.randint(0, 256, (2, 3, 84, 84, 3), generator=g, dtype=torch.uint8)
+    on_dev = pol(((img.cuda(), goal.cuda()), None))[0]
+    on_host = pol(((img, goal), None))[0]
+    assert torch.equal(on_dev, on_host)
+    bad = [(torch.zeros((2, 3, 174, 174, 3), dtype=torch.uint8), torch.zeros((2, 3, 174, 174, 3), dtype=torch.uint8)),
+           (img.cuda(), goal.cuda()[:1]),
+           (img.cuda().to(torch.int32), goal.cuda().to(torch.int32)),
+           (img.cuda()[..., :2], goal.cuda()[..., :2])]
+    for a, b in bad:
+        with pytest.raises(ValueError):
+            pol(((a, b), None))
+    net = pol.net
+    with pytest.raises(ValueError):  # non-contiguous batch straight into the autograd function
+        from vnav.policy import _GoalNavFunction
+        x = torch.zeros((4, 84, 84, 3), dtype=torch.uint8, device="cuda")[::2]
+        _GoalNavFunction.apply(pol.params, x, x, net)
