@@ -332,6 +332,30 @@ class A2CTrainer:
                 logger(metrics)
         return self
 
+    def evaluate(self, episodes=10, max_rollouts=10000):
+        """deep_rl's Trainer.test() on this trainer's envs: the current policy (sampled
+        actions), no update, until ``episodes`` episodes have finished on all ranks together
+        (or ``max_rollouts`` rollouts). The recurrent state carries across rollouts as in
+        training; the learning-rate step count is left as it was. Returns the episode count
+        and the mean reward and length of the finished episodes."""
+        saved_steps = self.sched[1:2].clone()
+        E, T = self.env.num_envs, self.num_steps
+        tot = torch.zeros(3, dtype=torch.float64)
+        for _ in range(int(max_rollouts)):
+            self.rollout()
+            if self.recurrent:  # (h, c) after the last step carry on, as update() does
+                self.h0.copy_(self.h_all[(T - 1) * E:])
+                self.c0.copy_(self.c_all[(T - 1) * E:])
+            st = self.episode_stats.to(torch.float64)
+            vdist.reduce_metrics_(st, 0, self.group)
+            tot += st.cpu()
+            if tot[0] >= episodes:
+                break
+        self.sched[1:2].copy_(saved_steps)
+        n, rsum, lsum = tot.tolist()
+        return {"episodes": n, "reward": rsum / n if n else float("nan"),
+                "episode_length": lsum / n if n else float("nan")}
+
     _RECURRENT_STATE = ("h0", "c0", "prev_action", "prev_reward", "prev_mask")
 
     def state_dict(self):

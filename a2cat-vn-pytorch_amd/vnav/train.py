@@ -1,0 +1,313 @@
+"""The reference's experiment entry points over vnav: ``register_trainer`` / ``make_trainer``
+/ ``Trainer.run()`` / ``Trainer.test()`` and the ``train.py NAME`` / ``test-train.py NAME``
+command line (train.py:10-25, test-train.py:11-26; the Trainer surface is deep_rl's,
+driven by experiments/thor_cached_auxiliary.py:26-84).
+
+    python -m vnav.train thor-cached-auxiliary [--scene thor-cached-212-174.pkl] [--save-dir D]
+    python -m vnav.train thor-cached-auxiliary --test [--episodes 100]      # test-train.py
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m vnav.train cached-thor --envs 4096
+
+An experiment is a class registered under its name with the deep_rl trainer arguments
+(max_time_steps, validation_period, validation_episodes, episode_log_interval,
+saving_period, save) and the reference's hyper-parameters as attributes; ``create_env``
+builds the batched VectorEnv (one process per GPU instead of one per env) and
+``create_trainer`` the A2CTrainer. ``run()`` trains to max_time_steps, prints deep_rl's
+metric table every ``episode_log_interval`` finished episodes and saves a checkpoint every
+``saving_period`` env-steps (and at the end); ``test()`` loads that checkpoint and runs
+``validation_episodes`` episodes of the policy. Scenes the reference downloads (the pickled
+THOR grids) are loaded from ``--scene`` when given; otherwise a synthetic scene of the same
+geometry stands in (no network in this image).
+"""
+import argparse
+import os
+import time
+
+import numpy as np
+import torch
+
+from . import dist as vdist
+from .a2c import A2CTrainer
+from .envs import VectorEnv
+from .scenes import load_graph_pickle, load_h5, load_npz, oriented_scene, synthetic_scene
+
+_TRAINERS = {}
+
+
+def register_trainer(name, max_time_steps=None, validation_period=None, validation_episodes=None,
+                     episode_log_interval=None, saving_period=None, save=True):
+    """deep_rl's ``@register_trainer(...)`` (experiments/thor_cached_auxiliary.py:26): the
+    decorated experiment class is made by ``make_trainer(name)`` with these attributes."""
+    def wrap(cls):
+        cls.name = name
+        cls.max_time_steps = max_time_steps
+        cls.validation_period = validation_period
+        cls.validation_episodes = validation_episodes
+        cls.episode_log_interval = episode_log_interval
+        cls.saving_period = saving_period
+        cls.save = save
+        _TRAINERS[name] = cls
+        return cls
+    return wrap
+
+
+def make_trainer(name, env_kwargs=None, model_kwargs=None, **kwargs):
+    """deep_rl's ``make_trainer(name, **default_args())`` (train.py:24)."""
+    if name not in _TRAINERS:
+        raise KeyError("unknown experiment %r (registered: %s)" % (name, sorted(_TRAINERS)))
+    return _TRAINERS[name](env_kwargs=env_kwargs or {}, model_kwargs=model_kwargs or {}, **kwargs)
+
+
+def registered():
+    return sorted(_TRAINERS)
+
+
+def _format_table(metrics):
+    """deep_rl's logger table (outputs/output.txt)."""
+    keys = ["step"] + sorted(k for k in metrics if k != "step")
+    rows = []
+    for k in keys:
+        v = metrics[k]
+        if isinstance(v, float):
+            v = "%.3g" % v
+        rows.append((k, str(v)))
+    w1 = max(len(k) for k, _ in rows) + 2
+    w2 = max(8, max(len(v) for _, v in rows))
+    line = "-" * (w1 + w2 + 6)
+    return "\n".join([line] + ["| %-*s| %-*s |" % (w1, k, w2, v) for k, v in rows] + [line])
+
+
+class Experiment:
+    """Base of the registered experiments: hyper-parameters as attributes (the deep_rl
+    Trainer fields the reference sets), create_env / create_trainer hooks, run / test."""
+
+    name = None
+    max_time_steps = 2e6
+    validation_period = None
+    validation_episodes = None
+    episode_log_interval = 10
+    saving_period = 100000
+    save = True
+    # A2C / RMSprop (experiments/thor_cached_auxiliary.py:29-37)
+    num_processes = 4
+    num_steps = 20
+    gamma = 0.99
+    learning_rate = 7e-4
+    rms_alpha = 0.99
+    rms_epsilon = 1e-5
+    max_gradient_norm = 0.5
+    recurrent = True
+    auxiliary_weight = 0.0
+    hardness = None
+    cuda_graph = False
+
+    def __init__(self, env_kwargs=None, model_kwargs=None, save_dir=None, seed=0, device=None, logger=print,
+                 **overrides):
+        for k, v in overrides.items():
+            if not hasattr(type(self), k):
+                raise TypeError("unknown experiment attribute %r" % k)
+            setattr(self, k, v)
+        self.env_kwargs = dict(env_kwargs or {})
+        self.model_kwargs = dict(model_kwargs or {})
+        self.seed = int(seed)
+        self.rank, self.world, local = vdist.env_rank()
+        if device is None:
+            device = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
+        self.device = torch.device(device)
+        self.save_dir = save_dir or os.path.join(os.path.expanduser("~/.visual_navigation/models"), self.name)
+        self.logger = logger
+        self.env = None
+        self.trainer = None
+
+    # --- hooks (deep_rl names)
+    def create_env(self, kwargs):
+        raise NotImplementedError
+
+    def create_trainer(self):
+        return A2CTrainer(self.env, num_steps=self.num_steps, gamma=self.gamma, learning_rate=self.learning_rate,
+                          max_time_steps=self.max_time_steps, rms_alpha=self.rms_alpha,
+                          rms_epsilon=self.rms_epsilon, max_gradient_norm=self.max_gradient_norm,
+                          seed=self.seed, recurrent=self.recurrent,
+                          aux_weight=self.auxiliary_weight, cuda_graph=self.cuda_graph and self.world == 1)
+
+    def _setup(self):
+        if self.trainer is None:
+            torch.cuda.set_device(self.device)
+            self.env = self.create_env(self.env_kwargs)
+            if self.hardness is not None:
+                # experiments/thor_cached_auxiliary.py:68-70 sets it before the first reset;
+                # the VectorEnv constructor already reset, so draw the starts again
+                self.env.set_hardness(self.hardness)
+                self.env.reset()
+            self.trainer = self.create_trainer()
+        return self.trainer
+
+    @property
+    def checkpoint_path(self):
+        return os.path.join(self.save_dir, "checkpoint.pt")
+
+    def save_checkpoint(self, path=None):
+        path = path or self.checkpoint_path
+        if self.rank != 0:
+            return path
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        tmp = path + ".tmp"
+        torch.save(self.trainer.state_dict(), tmp)
+        os.replace(tmp, path)
+        return path
+
+    def load_checkpoint(self, path=None):
+        sd = torch.load(path or self.checkpoint_path, map_location="cpu", weights_only=True)
+        self._setup().load_state_dict(sd)
+        return self
+
+    def _log(self, m):
+        if self.rank == 0 and self.logger:
+            self.logger(_format_table(m))
+
+    def run(self):
+        """Train to max_time_steps: deep_rl's Trainer.run() (train.py:25)."""
+        tr = self._setup()
+        window = dict(episodes=0.0, rsum=0.0, lsum=0.0)
+        last = None
+        next_save = (tr.total_steps // self.saving_period + 1) * self.saving_period if self.saving_period else None
+        t0, s0 = time.perf_counter(), tr.total_steps
+        while tr.total_steps < self.max_time_steps:
+            m = tr.step(sync=True)
+            last = m
+            if m["episodes"]:
+                window["episodes"] += m["episodes"]
+                window["rsum"] += m["reward"] * m["episodes"]
+                window["lsum"] += m["episode_length"] * m["episodes"]
+            if self.episode_log_interval and window["episodes"] >= self.episode_log_interval:
+                now = time.perf_counter()
+                row = {k: m[k] for k in ("step", "updates", "value_loss", "action_loss", "entropy", "loss")}
+                if "aux_loss" in m:
+                    row["aux_loss"] = m["aux_loss"]
+                row.update(episodes=int(window["episodes"]), reward=window["rsum"] / window["episodes"],
+                           episode_length=window["lsum"] / window["episodes"],
+                           fps=int((tr.total_steps - s0) / max(now - t0, 1e-9)))
+                self._log(row)
+                window = dict(episodes=0.0, rsum=0.0, lsum=0.0)
+                t0, s0 = now, tr.total_steps
+            if self.save and next_save is not None and tr.total_steps >= next_save:
+                self.save_checkpoint()
+                next_save += self.saving_period
+        if self.save:
+            self.save_checkpoint()
+        return last
+
+    def test(self, episodes=None, checkpoint=None):
+        """deep_rl's Trainer.test() (test-train.py:26): the saved policy (when a checkpoint
+        exists) over ``episodes`` (default validation_episodes, else 100) episodes."""
+        path = checkpoint or self.checkpoint_path
+        if os.path.exists(path):
+            self.load_checkpoint(path)
+        else:
+            self._setup()
+        n = episodes or self.validation_episodes or 100
+        res = self.trainer.evaluate(episodes=n)
+        self._log(dict(step=self.trainer.total_steps, **res))
+        return res
+
+
+def _synthetic_oriented(grid, frame, goal, seed=0, aux=True):
+    """A random oriented grid whose frames (and depth / segmentation) are fixed random
+    images per (cell, rotation): the stand-in for a pickled THOR scene."""
+    rng = np.random.default_rng(seed)
+    maze = rng.random(grid) >= 0.25
+    maze[goal[0], goal[1]] = True
+    from scipy.ndimage import label
+    lab, _ = label(maze)
+    maze = lab == lab[goal[0], goal[1]]
+    X, Y = grid
+    h, w = frame
+    obs = rng.integers(0, 256, size=(X, Y, 4, h, w, 3), dtype=np.uint8)
+    kw = {}
+    if aux:
+        kw = dict(depths=rng.integers(0, 256, size=(X, Y, 4, h, w, 1), dtype=np.uint8),
+                  segmentations=rng.integers(0, 256, size=(X, Y, 4, h, w, 3), dtype=np.uint8))
+    return oriented_scene(maze, obs, goals=[tuple(goal)], name="synthetic-oriented-%dx%d" % (h, w), **kw)
+
+
+@register_trainer("thor-cached-auxiliary", max_time_steps=2e6, validation_period=None, validation_episodes=None,
+                  episode_log_interval=10, saving_period=100000, save=True)
+class ThorCachedAuxiliary(Experiment):
+    """experiments/thor_cached_auxiliary.py: AuxiliaryGraph-v0 on thor-cached-212-174 with the
+    fixed goal (10, 14, 0), 4 envs, hardness 0.01, LSTM policy + deconv heads with
+    auxiliary_weight 0.1 (:42), frames 174x174 (screen_size is not forwarded).
+    env_kwargs: scene (a ThorGridWorld pickle path) or grid / frame / goal of the synthetic
+    stand-in. The UNREAL replay losses (rp / pc / vr weights, :39-41) are deep_rl's and not
+    part of this path."""
+
+    num_processes = 4
+    auxiliary_weight = 0.1
+    hardness = 0.01
+
+    def create_env(self, kwargs):
+        goal = tuple(kwargs.get("goal", (10, 14, 0)))
+        if kwargs.get("scene"):
+            scene = load_graph_pickle(kwargs["scene"], goals=[goal], auxiliary=True)
+        else:
+            scene = _synthetic_oriented(tuple(kwargs.get("grid", (16, 16))), tuple(kwargs.get("frame", (174, 174))),
+                                        goal, seed=kwargs.get("scene_seed", 0))
+        return VectorEnv([scene], kwargs.get("num_envs", self.num_processes),
+                         seed=vdist.rank_seed(self.seed + 1, self.rank), device=self.device, max_episode_steps=900)
+
+
+@register_trainer("cached-thor", max_time_steps=1e9, validation_period=None, validation_episodes=None,
+                  episode_log_interval=1000, saving_period=int(5e7), save=True)
+class CachedThor(Experiment):
+    """CachedThor-v0 (environments/gym_ai2thor/envs/cached.py) at the north-star shape: h5 /
+    npz scene caches (env_kwargs scenes=[paths]) or synthetic 24x24 scenes (n_scenes), 84x84
+    frames, num_envs envs per GPU (4096), the LSTM policy without deconv heads."""
+
+    num_processes = 4096
+
+    def create_env(self, kwargs):
+        paths = kwargs.get("scenes") or []
+        if paths:
+            scenes = [load_h5(p) if p.endswith((".h5", ".hdf5")) else load_npz(p) for p in paths]
+        else:
+            scenes = [synthetic_scene(k) for k in range(int(kwargs.get("n_scenes", 20)))]
+        return VectorEnv(scenes, kwargs.get("num_envs", self.num_processes),
+                         seed=vdist.rank_seed(self.seed + 1, self.rank), device=self.device, max_episode_steps=900)
+
+
+def main(argv=None):
+    p = argparse.ArgumentParser(description="train.py / test-train.py over vnav")
+    p.add_argument("name", help="experiment name (%s)" % ", ".join(registered()))
+    p.add_argument("--test", action="store_true", help="test-train.py: evaluate the saved policy")
+    p.add_argument("--scene", action="append", default=[], help="scene file(s): .pkl (ThorGridWorld), .h5 or .npz")
+    p.add_argument("--envs", type=int, default=None, help="envs per GPU (default: the experiment's num_processes)")
+    p.add_argument("--max-time-steps", type=float, default=None)
+    p.add_argument("--save-dir", default=None)
+    p.add_argument("--episodes", type=int, default=None, help="--test: episodes to run")
+    p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--cuda-graph", action="store_true", help="replay each update as a captured hipGraph (1 GPU)")
+    a = p.parse_args(argv)
+    vdist.init_distributed()
+    env_kwargs = {}
+    if a.envs:
+        env_kwargs["num_envs"] = a.envs
+    if a.scene:
+        if a.name == "thor-cached-auxiliary":
+            env_kwargs["scene"] = a.scene[0]
+        else:
+            env_kwargs["scenes"] = a.scene
+    over = {}
+    if a.max_time_steps is not None:
+        over["max_time_steps"] = a.max_time_steps
+    if a.cuda_graph:
+        over["cuda_graph"] = True
+    exp = make_trainer(a.name, env_kwargs=env_kwargs, save_dir=a.save_dir, seed=a.seed, **over)
+    if a.test:
+        exp.test(episodes=a.episodes)
+    else:
+        exp.run()
+    if vdist.world_of()[0] > 1:
+        torch.distributed.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -1,0 +1,59 @@
+"""The experiment surface (vnav.train): register_trainer / make_trainer / run / test and the
+train.py / test-train.py command line (reference train.py:10-25, test-train.py:11-26,
+experiments/thor_cached_auxiliary.py:26-84)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+
+def _train():
+    from vnav import train
+    return train
+
+
+def test_registry_and_hyperparameters():
+    train = _train()
+    assert {"thor-cached-auxiliary", "cached-thor"} <= set(train.registered())
+    cls = train._TRAINERS["thor-cached-auxiliary"]
+    # experiments/thor_cached_auxiliary.py:26-42
+    assert (cls.max_time_steps, cls.episode_log_interval, cls.saving_period, cls.save) == (2e6, 10, 100000, True)
+    assert (cls.num_processes, cls.num_steps, cls.gamma, cls.learning_rate) == (4, 20, 0.99, 7e-4)
+    assert (cls.rms_alpha, cls.rms_epsilon, cls.max_gradient_norm) == (0.99, 1e-5, 0.5)
+    assert (cls.auxiliary_weight, cls.hardness, cls.recurrent) == (0.1, 0.01, True)
+    with pytest.raises(KeyError):
+        train.make_trainer("no-such-experiment")
+    with pytest.raises(TypeError):
+        train.make_trainer("cached-thor", not_an_attribute=1)
+
+
+def test_metric_table_format():
+    t = _train()._format_table({"step": 2240, "reward": 0.9, "episodes": 10, "fps": 32})
+    lines = t.split("\n")
+    assert lines[0].startswith("---") and lines[-1].startswith("---")
+    assert lines[1].startswith("| step") and "2240" in lines[1]
+    assert len({len(x) for x in lines}) == 1
+
+
+@pytest.mark.gpu
+def test_run_saves_and_test_reloads(tmp_path):
+    """run() trains to max_time_steps with periodic + final checkpoints, test() reloads the
+    saved policy into a fresh experiment and runs evaluation episodes."""
+    train = _train()
+    logs = []
+    kw = dict(env_kwargs=dict(grid=(6, 6), frame=(84, 84), goal=(3, 3, 0), num_envs=8), save_dir=str(tmp_path),
+              max_time_steps=8 * 20 * 3, saving_period=160, episode_log_interval=1, logger=logs.append)
+    exp = train.make_trainer("thor-cached-auxiliary", **kw)
+    m = exp.run()
+    assert m["step"] == 480 and m["updates"] == 3 and np.isfinite(m["loss"])
+    assert os.path.exists(exp.checkpoint_path)
+    sd = torch.load(exp.checkpoint_path, weights_only=True)
+    assert torch.equal(sd["params"], exp.trainer.params.cpu()) and sd["total_steps"] == 480
+    assert logs and all(x.startswith("---") for x in logs)
+    ev = train.make_trainer("thor-cached-auxiliary", **kw)
+    res = ev.test(episodes=5)
+    assert torch.equal(ev.trainer.params.cpu(), sd["params"])
+    assert res["episodes"] >= 5 and 0.0 < res["reward"] <= 1.0 and res["episode_length"] >= 1
+    # evaluation does not advance the learning-rate schedule
+    assert int(ev.trainer.sched[1]) == 480
