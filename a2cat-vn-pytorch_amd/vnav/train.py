@@ -161,11 +161,23 @@ class Experiment:
         return self
 
     def _log(self, m):
-        if self.rank == 0 and self.logger:
+        """deep_rl's console table, and the same row appended to save_dir/metrics.jsonl."""
+        if self.rank != 0:
+            return
+        if self.logger:
             self.logger(_format_table(m))
+        if self.save:
+            import json
+            os.makedirs(self.save_dir, exist_ok=True)
+            with open(os.path.join(self.save_dir, "metrics.jsonl"), "a") as f:
+                f.write(json.dumps(m) + "\n")
 
-    def run(self):
-        """Train to max_time_steps: deep_rl's Trainer.run() (train.py:25)."""
+    def run(self, resume=False):
+        """Train to max_time_steps: deep_rl's Trainer.run() (train.py:25). resume=True
+        continues from save_dir's checkpoint when there is one (parameters, RMSprop state,
+        per-env state and running returns, recurrent carry, update / step counters)."""
+        if resume and os.path.exists(self.checkpoint_path):
+            self.load_checkpoint()
         tr = self._setup()
         window = dict(episodes=0.0, rsum=0.0, lsum=0.0)
         last = None
@@ -190,11 +202,15 @@ class Experiment:
                 window = dict(episodes=0.0, rsum=0.0, lsum=0.0)
                 t0, s0 = now, tr.total_steps
             if self.save and next_save is not None and tr.total_steps >= next_save:
-                self.save_checkpoint()
+                self._saving(self.save_checkpoint())
                 next_save += self.saving_period
         if self.save:
-            self.save_checkpoint()
+            self._saving(self.save_checkpoint())
         return last
+
+    def _saving(self, path):
+        if self.rank == 0 and self.logger:
+            self.logger("Saving %s (step %d)" % (path, self.trainer.total_steps))  # outputs/output.txt:462
 
     def test(self, episodes=None, checkpoint=None):
         """deep_rl's Trainer.test() (test-train.py:26): the saved policy (when a checkpoint
@@ -284,6 +300,7 @@ def main(argv=None):
     p.add_argument("--episodes", type=int, default=None, help="--test: episodes to run")
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--cuda-graph", action="store_true", help="replay each update as a captured hipGraph (1 GPU)")
+    p.add_argument("--resume", action="store_true", help="continue from the checkpoint in --save-dir")
     a = p.parse_args(argv)
     vdist.init_distributed()
     env_kwargs = {}
@@ -303,7 +320,7 @@ def main(argv=None):
     if a.test:
         exp.test(episodes=a.episodes)
     else:
-        exp.run()
+        exp.run(resume=a.resume)
     if vdist.world_of()[0] > 1:
         torch.distributed.destroy_process_group()
     return 0

@@ -50,10 +50,36 @@ def test_run_saves_and_test_reloads(tmp_path):
     assert os.path.exists(exp.checkpoint_path)
     sd = torch.load(exp.checkpoint_path, weights_only=True)
     assert torch.equal(sd["params"], exp.trainer.params.cpu()) and sd["total_steps"] == 480
-    assert logs and all(x.startswith("---") for x in logs)
+    tables = [x for x in logs if x.startswith("---")]
+    saves = [x for x in logs if x.startswith("Saving")]
+    assert tables and len(saves) >= 3 and len(tables) + len(saves) == len(logs)
     ev = train.make_trainer("thor-cached-auxiliary", **kw)
     res = ev.test(episodes=5)
     assert torch.equal(ev.trainer.params.cpu(), sd["params"])
     assert res["episodes"] >= 5 and 0.0 < res["reward"] <= 1.0 and res["episode_length"] >= 1
     # evaluation does not advance the learning-rate schedule
     assert int(ev.trainer.sched[1]) == 480
+    rows = [l for l in open(os.path.join(str(tmp_path), "metrics.jsonl"))]
+    assert len(rows) == len(tables) + 1  # + the test() row
+
+
+@pytest.mark.gpu
+def test_resume_continues_exactly(tmp_path):
+    """run(resume=True) from a checkpoint reaches the same parameters as an uninterrupted
+    run of the same length (deep_rl saving_period checkpoints)."""
+    train = _train()
+    kw = dict(env_kwargs=dict(grid=(6, 6), frame=(84, 84), goal=(3, 3, 0), num_envs=8), saving_period=0,
+              episode_log_interval=0, logger=None)
+    full = train.make_trainer("thor-cached-auxiliary", save_dir=str(tmp_path / "a"), max_time_steps=640, **kw)
+    full.run()
+    # the same experiment interrupted after two updates (the LinearSchedule horizon is
+    # max_time_steps, so the interrupted run keeps it), checkpointed, then resumed
+    part = train.make_trainer("thor-cached-auxiliary", save_dir=str(tmp_path / "b"), max_time_steps=640, **kw)
+    tr = part._setup()
+    tr.step()
+    tr.step()
+    part.save_checkpoint()
+    rest = train.make_trainer("thor-cached-auxiliary", save_dir=str(tmp_path / "b"), max_time_steps=640, **kw)
+    rest.run(resume=True)
+    assert rest.trainer.total_steps == 640
+    assert torch.equal(rest.trainer.params, full.trainer.params)
