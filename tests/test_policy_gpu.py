@@ -234,6 +234,44 @@ def test_policy_174_large_batch_consistency():
     assert not bad, bad
 
 
+def test_policy_174_offsets_past_2g_elements():
+    """20480 samples at 174x174 in one batch: conv1's output alone is 2.31e9 floats, so every
+    kernel addresses activations past int32 element offsets. The first and last 64 samples
+    give the outputs they give alone, and the gradient of a loss on the last 64 samples,
+    taken inside the full batch (zero output gradient elsewhere), equals that loss's
+    gradient run alone — both to 1e-5 of scale (the north-star bar; small batches split K,
+    so the long sums run in another order). An addressing error would be O(1)."""
+    pol = _policy_174(9)
+    N, k = 20480, 64
+    g = torch.Generator(device="cuda").manual_seed(0)
+    img = torch.randint(0, 256, (N, 1, 174, 174, 3), dtype=torch.uint8, device="cuda", generator=g)
+    gl = torch.randint(0, 256, (N, 1, 174, 174, 3), dtype=torch.uint8, device="cuda", generator=g)
+    cl = torch.randn((k, 1, 4), device="cuda", generator=g)
+    cv = torch.randn((k, 1, 1), device="cuda", generator=g)
+
+    def run(a, b, sl):
+        pol.params.grad = None
+        logits, value, _ = pol(((a, b), None), None, None)
+        ((logits[sl] * cl).sum() + (value[sl] * cv).sum()).backward()
+        return logits.detach(), value.detach(), pol.params.grad.clone()
+
+    logits, value, grad = run(img, gl, slice(N - k, N))
+    l_last, v_last, g_last = run(img[-k:], gl[-k:], slice(0, k))
+    _close(logits[-k:].cpu(), l_last.cpu(), 1e-5, "logits of the last samples")
+    _close(value[-k:].cpu(), v_last.cpu(), 1e-5, "values of the last samples")
+    l_first, v_first, _ = run(img[:k], gl[:k], slice(0, k))
+    _close(logits[:k].cpu(), l_first.cpu(), 1e-5, "logits of the first samples")
+    _close(value[:k].cpu(), v_first.cpu(), 1e-5, "values of the first samples")
+    mine, ref = pol.net.to_reference(grad), pol.net.to_reference(g_last)
+    bad = {}
+    for key in ref:
+        b = ref[key].numpy().astype(np.float64)
+        e = np.abs(mine[key].numpy() - b).max() / max(np.abs(b).max(), 1e-30)
+        if e > 1e-5:
+            bad[key] = "%.3g" % e
+    assert not bad, bad
+
+
 def test_row_gather_equals_dense_batch():
     import vnav
     from vnav.policy import PolicyNet, frames_from_batch, frames_from_rows
