@@ -234,18 +234,24 @@ def test_policy_174_large_batch_consistency():
     assert not bad, bad
 
 
-def test_policy_174_offsets_past_2g_elements():
-    """20480 samples at 174x174 in one batch: conv1's output alone is 2.31e9 floats, so every
+@pytest.mark.parametrize("hw,N", [((174, 174), 20480), ((300, 400), 4608)])
+def test_policy_offsets_past_2g_elements(hw, N):
+    """20480 samples at 174x174 (4608 at 300x400, config C5) in one batch: conv1's output
+    alone is 2.31e9 (2.16e9) floats, so every
     kernel addresses activations past int32 element offsets. The first and last 64 samples
     give the outputs they give alone, and the gradient of a loss on the last 64 samples,
     taken inside the full batch (zero output gradient elsewhere), equals that loss's
     gradient run alone — both to 1e-5 of scale (the north-star bar; small batches split K,
     so the long sums run in another order). An addressing error would be O(1)."""
-    pol = _policy_174(9)
-    N, k = 20480, 64
+    from vnav.policy import GoalNavPolicy
+    torch.manual_seed(9)
+    pol = GoalNavPolicy(3, 4, hw)
+    with torch.no_grad():
+        pol.params.add_(torch.randn_like(pol.params) * 0.01)
+    k = 64
     g = torch.Generator(device="cuda").manual_seed(0)
-    img = torch.randint(0, 256, (N, 1, 174, 174, 3), dtype=torch.uint8, device="cuda", generator=g)
-    gl = torch.randint(0, 256, (N, 1, 174, 174, 3), dtype=torch.uint8, device="cuda", generator=g)
+    img = torch.randint(0, 256, (N, 1) + hw + (3,), dtype=torch.uint8, device="cuda", generator=g)
+    gl = torch.randint(0, 256, (N, 1) + hw + (3,), dtype=torch.uint8, device="cuda", generator=g)
     cl = torch.randn((k, 1, 4), device="cuda", generator=g)
     cv = torch.randn((k, 1, 1), device="cuda", generator=g)
 
