@@ -178,15 +178,21 @@ __global__ __launch_bounds__(256) void aux_loss_grad_kernel(int n, int PH, int P
 // Second head layer (48 -> 8 transposed conv, k4 s2, block-diagonal weights) as a direct
 // kernel, optionally fused with the loss: SPI samples' A1 maps are staged in LDS (pixel
 // stride 52 floats: 16 consecutive pixels on distinct bank quads, one zero pixel for the
-// taps outside the map); every wave works on one parity class at a time so the weights of
-// its taps are wave-uniform (scalar loads); a thread computes the 7 real outputs of one
-// pixel from the 2x2 taps that reach it (4 x (16 + 48 + 48) = 448 FMAs, only the head's
-// own 16 input channels per output — the GEMM form multiplied the 2/3 structural zeros and
-// padded N = 8 to 16). !LOSS: writes pred [n][PH][PW][8]. LOSS: the per-head MSE gradient
-// against the target table goes straight to dpred (pred is never written) and the squared
-// errors to stats[0..2] (aux_loss_grad_kernel's contract).
+// taps outside the map). Each pair of waves owns one parity class (py, px), so the weights
+// of its taps are wave-uniform, and a lane computes FOUR output pixels of its class that
+// sit next to each other along x (2yy + py, 2(xx0 + i) + px), i = 0..3: every weight it
+// reads feeds 4 pixels (the one-pixel form read 4 broadcast weight vectors per 16-B A1 read
+// and was bound by LDS reads). Each output sums the 2x2 taps that reach it over only its
+// head's own 16 input channels (4 x (16 + 48 + 48) = 448 FMAs per pixel; the GEMM form
+// multiplied the 2/3 structural zeros and padded N = 8 to 16), in the same order as before
+// (bit-identical): 174x174 7.74 -> 6.74 ms per update. The weights stay in LDS
+// [cls][tap][ci][8]; scalar loads from the constant address space measured 7.35 ms.
+// !LOSS: writes pred [n][PH][PW][8]. LOSS: the per-head MSE gradient against the target
+// table goes straight to dpred (pred is never written) and the squared errors to
+// stats[0..2] (aux_loss_grad_kernel's contract).
 constexpr int kAux2Threads = 512;
 constexpr int kAux2Pst = 52;
+constexpr int kAux2Px = 4;  // output pixels per lane
 
 template <int AH, int AW>
 constexpr int aux2_spi() {
@@ -215,15 +221,18 @@ __global__ __launch_bounds__(kAux2Threads) void aux_deconv2_kernel(const float* 
                                                                     float* __restrict__ stats) {
   constexpr int SPI = aux2_spi<AH, AW>();
   constexpr int NPX = AH * AW, SST = (NPX + 1) * kAux2Pst;  // pixels, per-sample LDS stride
-  constexpr int HYC = PH / 2, WXC = PW / 2, NPC = HYC * WXC;
+  constexpr int HYC = PH / 2, WXC = PW / 2;                 // output pixels per class: HYC x WXC
+  constexpr int XB = (WXC + kAux2Px - 1) / kAux2Px, RT = HYC * XB;  // lane tasks per class and sample
   static_assert(PH == 2 * AH + 2 && PW == 2 * AW + 2, "k4 s2 transposed conv geometry");
+  static_assert(kAux2Threads == 512, "two waves per parity class");
   extern __shared__ __attribute__((aligned(16))) float as_aux[];
   float* ws_aux = as_aux + SPI * SST;  // [cls][tap = 2a + b][ci][8]
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int cls = __builtin_amdgcn_readfirstlane(wave >> 1), py = cls >> 1, px = cls & 1;
   for (int i = tid; i < SPI * 48; i += kAux2Threads) as_aux[(i / 48) * SST + NPX * kAux2Pst + i % 48] = 0.0f;
   for (int i = tid; i < kAux2Wfl; i += kAux2Threads) {
-    const int c = i & 7, ci = (i >> 3) % kAuxC1, tap = (i / (8 * kAuxC1)) & 3, cls = i / (32 * kAuxC1);
-    const int ky = (cls >> 1) + 2 * (tap >> 1), kx = (cls & 1) + 2 * (tap & 1);
+    const int c = i & 7, ci = (i >> 3) % kAuxC1, tap = (i / (8 * kAuxC1)) & 3, cl = i / (32 * kAuxC1);
+    const int ky = (cl >> 1) + 2 * (tap >> 1), kx = (cl & 1) + 2 * (tap & 1);
     ws_aux[i] = W2[(ci * 4 + ky) * 32 + kx * 8 + c];
   }
   float bias[7];
@@ -251,66 +260,85 @@ __global__ __launch_bounds__(kAux2Threads) void aux_deconv2_kernel(const float* 
     for (int j = 0; j < NV; ++j) {
       const int i = tid + j * kAux2Threads;
       if (i < ns * NPX * 12) {
-        const int sp = i / (NPX * 12), r = i - sp * (NPX * 12), px = r / 12, c4 = r - (r / 12) * 12;
-        *reinterpret_cast<f4*>(as_aux + sp * SST + px * kAux2Pst + 4 * c4) = pre[j];
+        const int sp = i / (NPX * 12), r = i - sp * (NPX * 12), pxl = r / 12, c4 = r - (r / 12) * 12;
+        *reinterpret_cast<f4*>(as_aux + sp * SST + pxl * kAux2Pst + 4 * c4) = pre[j];
       }
     }
     __syncthreads();
     if (s0 + (int)gridDim.x * SPI < n) load_item(s0 + gridDim.x * SPI);
-    for (int cls = 0; cls < 4; ++cls) {  // wave-uniform parity class -> broadcast weight reads
-      const int py = cls >> 1, px = cls & 1;
-      for (int q = tid; q < ns * NPC; q += kAux2Threads) {
-        const int sp = q / NPC, p = q - sp * NPC, yy = p / WXC, xx = p - (p / WXC) * WXC;
-        const int Y = 2 * yy + py, X = 2 * xx + px, s = s0 + sp;
-        f4 ti, tg;  // targets issued before the products
-        if constexpr (LOSS) {
-          ti = table[(int64_t)img_rows[s] * PH * PW + Y * PW + X];
-          tg = table[(int64_t)goal_rows[s] * PH * PW + Y * PW + X];
+    for (int t = (wave & 1) * 64 + lane; t < ns * RT; t += 128) {
+      const int sp = t / RT, r = t - sp * RT, yy = r / XB, xx0 = (r - (r / XB) * XB) * kAux2Px, s = s0 + sp;
+      const int npx = min(kAux2Px, WXC - xx0);
+      f4 ti[kAux2Px], tg[kAux2Px];  // targets issued before the products
+      if constexpr (LOSS) {
+        const int64_t ib = (int64_t)img_rows[s] * PH * PW, gb = (int64_t)goal_rows[s] * PH * PW;
+#pragma unroll
+        for (int i = 0; i < kAux2Px; ++i) {
+          const int pix = (2 * yy + py) * PW + 2 * min(xx0 + i, WXC - 1) + px;
+          ti[i] = table[ib + pix];
+          tg[i] = table[gb + pix];
         }
-        float o[7];
+      }
+      float o[kAux2Px][7];
 #pragma unroll
-        for (int c = 0; c < 7; ++c) o[c] = bias[c];
+      for (int i = 0; i < kAux2Px; ++i)
 #pragma unroll
-        for (int a = 0; a < 2; ++a)
+        for (int c = 0; c < 7; ++c) o[i][c] = bias[c];
 #pragma unroll
-          for (int b = 0; b < 2; ++b) {
-            const int iy = yy - a, ix = xx - b;
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const int iy = yy - a;
+          const float* ap[kAux2Px];
+#pragma unroll
+          for (int i = 0; i < kAux2Px; ++i) {
+            const int ix = xx0 + i - b;
             const bool ok = iy >= 0 && iy < AH && ix >= 0 && ix < AW;
-            const float* ap = as_aux + sp * SST + (ok ? iy * AW + ix : NPX) * kAux2Pst;
-            const float* wp = ws_aux + ((cls * 4 + 2 * a + b) * kAuxC1) * 8;
+            ap[i] = as_aux + sp * SST + (ok ? iy * AW + ix : NPX) * kAux2Pst;
+          }
+          const float* wl = ws_aux + ((cls * 4 + 2 * a + b) * kAuxC1) * 8;
 #pragma unroll
-            for (int hd = 0; hd < 3; ++hd)  // head hd reads input channels 16hd .. 16hd + 15
+          for (int hd = 0; hd < 3; ++hd)  // head hd reads input channels 16hd .. 16hd + 15
 #pragma unroll 2
-              for (int kq = 0; kq < 4; ++kq) {
-                const int k = 4 * hd + kq;
-                const f4 av = *reinterpret_cast<const f4*>(ap + 4 * k);
+            for (int kq = 0; kq < 4; ++kq) {
+              const int k = 4 * hd + kq;
+              f4 av[kAux2Px];
 #pragma unroll
-                for (int jj = 0; jj < 4; ++jj) {
-                  const f4 wv = reinterpret_cast<const f4*>(wp + (4 * k + jj) * 8)[hd < 2 ? 0 : 1];
+              for (int i = 0; i < kAux2Px; ++i) av[i] = *reinterpret_cast<const f4*>(ap[i] + 4 * k);
+#pragma unroll
+              for (int jj = 0; jj < 4; ++jj) {
+                const int ci = 4 * k + jj;
+                const f4 wv = reinterpret_cast<const f4*>(wl + ci * 8)[hd < 2 ? 0 : 1];
+#pragma unroll
+                for (int i = 0; i < kAux2Px; ++i) {
                   if (hd == 0) {
-                    o[0] = fmaf(av[jj], wv[0], o[0]);
+                    o[i][0] = fmaf(av[i][jj], wv[0], o[i][0]);
                   } else if (hd == 1) {
-                    o[1] = fmaf(av[jj], wv[1], o[1]);
-                    o[2] = fmaf(av[jj], wv[2], o[2]);
-                    o[3] = fmaf(av[jj], wv[3], o[3]);
+                    o[i][1] = fmaf(av[i][jj], wv[1], o[i][1]);
+                    o[i][2] = fmaf(av[i][jj], wv[2], o[i][2]);
+                    o[i][3] = fmaf(av[i][jj], wv[3], o[i][3]);
                   } else {
-                    o[4] = fmaf(av[jj], wv[0], o[4]);
-                    o[5] = fmaf(av[jj], wv[1], o[5]);
-                    o[6] = fmaf(av[jj], wv[2], o[6]);
+                    o[i][4] = fmaf(av[i][jj], wv[0], o[i][4]);
+                    o[i][5] = fmaf(av[i][jj], wv[1], o[i][5]);
+                    o[i][6] = fmaf(av[i][jj], wv[2], o[i][6]);
                   }
                 }
               }
-          }
-        const int64_t pix = (int64_t)s * PH * PW + Y * PW + X;
+            }
+        }
+#pragma unroll
+      for (int i = 0; i < kAux2Px; ++i) {
+        if (i >= npx) break;
+        const int64_t pix = (int64_t)s * PH * PW + (2 * yy + py) * PW + 2 * (xx0 + i) + px;
         if constexpr (!LOSS) {
-          *reinterpret_cast<f4*>(pred + pix * kAuxC2) = f4{o[0], o[1], o[2], o[3]};
-          *reinterpret_cast<f4*>(pred + pix * kAuxC2 + 4) = f4{o[4], o[5], o[6], 0.0f};
+          *reinterpret_cast<f4*>(pred + pix * kAuxC2) = f4{o[i][0], o[i][1], o[i][2], o[i][3]};
+          *reinterpret_cast<f4*>(pred + pix * kAuxC2 + 4) = f4{o[i][4], o[i][5], o[i][6], 0.0f};
         } else {
-          const float t[7] = {ti[0], ti[1], ti[2], ti[3], tg[1], tg[2], tg[3]};
+          const float tv[7] = {ti[i][0], ti[i][1], ti[i][2], ti[i][3], tg[i][1], tg[i][2], tg[i][3]};
           float g[8];
 #pragma unroll
           for (int c = 0; c < 7; ++c) {
-            const float d = o[c] - t[c];
+            const float d = o[i][c] - tv[c];
             const int h = c == 0 ? 0 : (c <= 3 ? 1 : 2);
             sq[h] += d * d;
             g[c] = d * inv[h];
