@@ -179,10 +179,12 @@ __global__ __launch_bounds__(256) void aux_loss_grad_kernel(int n, int PH, int P
 // kernel, optionally fused with the loss: SPI samples' A1 maps are staged in LDS (pixel
 // stride 52 floats: 16 consecutive pixels on distinct bank quads, one zero pixel for the
 // taps outside the map). Each pair of waves owns one parity class (py, px), so the weights
-// of its taps are wave-uniform, and a lane computes FOUR output pixels of its class that
-// sit next to each other along x (2yy + py, 2(xx0 + i) + px), i = 0..3: every weight it
-// reads feeds 4 pixels (the one-pixel form read 4 broadcast weight vectors per 16-B A1 read
-// and was bound by LDS reads). Each output sums the 2x2 taps that reach it over only its
+// of its taps are wave-uniform, and a lane computes FOUR output pixels of its class along x,
+// (2yy + py, 2(xb + i XB) + px), i = 0..3: every weight it reads feeds 4 pixels (the
+// one-pixel form read 4 broadcast weight vectors per 16-B A1 read and was bound by LDS
+// reads). The four are XB apart so that consecutive lanes read consecutive A1 pixels (the
+// pixel stride 52 puts 16 of them on distinct bank quads; 4 adjacent pixels per lane put
+// lanes 4 pixels apart: 4-way conflicts, 56 % of the LDS cycles). Each output sums the 2x2 taps that reach it over only its
 // head's own 16 input channels (4 x (16 + 48 + 48) = 448 FMAs per pixel; the GEMM form
 // multiplied the 2/3 structural zeros and padded N = 8 to 16), in the same order as before
 // (bit-identical): 174x174 7.74 -> 6.74 ms per update. The weights stay in LDS
@@ -267,14 +269,14 @@ __global__ __launch_bounds__(kAux2Threads) void aux_deconv2_kernel(const float* 
     __syncthreads();
     if (s0 + (int)gridDim.x * SPI < n) load_item(s0 + gridDim.x * SPI);
     for (int t = (wave & 1) * 64 + lane; t < ns * RT; t += 128) {
-      const int sp = t / RT, r = t - sp * RT, yy = r / XB, xx0 = (r - (r / XB) * XB) * kAux2Px, s = s0 + sp;
-      const int npx = min(kAux2Px, WXC - xx0);
+      const int sp = t / RT, r = t - sp * RT, yy = r / XB, xb = r - (r / XB) * XB, s = s0 + sp;
+      const int npx = (WXC - xb + XB - 1) / XB;  // pixels xb + i XB < WXC
       f4 ti[kAux2Px], tg[kAux2Px];  // targets issued before the products
       if constexpr (LOSS) {
         const int64_t ib = (int64_t)img_rows[s] * PH * PW, gb = (int64_t)goal_rows[s] * PH * PW;
 #pragma unroll
         for (int i = 0; i < kAux2Px; ++i) {
-          const int pix = (2 * yy + py) * PW + 2 * min(xx0 + i, WXC - 1) + px;
+          const int pix = (2 * yy + py) * PW + 2 * min(xb + i * XB, WXC - 1) + px;
           ti[i] = table[ib + pix];
           tg[i] = table[gb + pix];
         }
@@ -292,7 +294,7 @@ __global__ __launch_bounds__(kAux2Threads) void aux_deconv2_kernel(const float* 
           const float* ap[kAux2Px];
 #pragma unroll
           for (int i = 0; i < kAux2Px; ++i) {
-            const int ix = xx0 + i - b;
+            const int ix = xb + i * XB - b;
             const bool ok = iy >= 0 && iy < AH && ix >= 0 && ix < AW;
             ap[i] = as_aux + sp * SST + (ok ? iy * AW + ix : NPX) * kAux2Pst;
           }
@@ -329,7 +331,7 @@ __global__ __launch_bounds__(kAux2Threads) void aux_deconv2_kernel(const float* 
 #pragma unroll
       for (int i = 0; i < kAux2Px; ++i) {
         if (i >= npx) break;
-        const int64_t pix = (int64_t)s * PH * PW + (2 * yy + py) * PW + 2 * (xx0 + i) + px;
+        const int64_t pix = (int64_t)s * PH * PW + (2 * yy + py) * PW + 2 * (xb + i * XB) + px;
         if constexpr (!LOSS) {
           *reinterpret_cast<f4*>(pred + pix * kAuxC2) = f4{o[i][0], o[i][1], o[i][2], o[i][3]};
           *reinterpret_cast<f4*>(pred + pix * kAuxC2 + 4) = f4{o[i][4], o[i][5], o[i][6], 0.0f};
