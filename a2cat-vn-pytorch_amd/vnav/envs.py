@@ -324,3 +324,54 @@ def make(id, scenes, num_envs, **kwargs):
     opts = dict(REGISTRY[id])
     opts.update(kwargs)
     return VectorEnv(scenes, num_envs, **opts)
+
+
+class CachedThorEnv:
+    """One gym-style env over the same kernel: the single-env surface of
+    THORDiscreteCachedEnv (environments/gym_ai2thor/envs/cached.py:10-99) under gym's
+    TimeLimit, for callers that drive one env at a time (gym.make + a hand-written loop,
+    test-time episodes). ``reset() -> (image, goal)``; ``step(a) -> (obs, reward, done,
+    info)`` with no auto-reset: on a terminal step the previous observation is returned
+    (cached.py:90-96) and the caller resets, as with the reference. Frames are float64 in
+    [0, 1], HWC, as ``_preprocess_frame`` returns at equal size (cached.py:62-64; resize
+    offline with tools/h5_to_npz.py --size). Every call synchronises with the device; the
+    batched ``VectorEnv`` is the fast path."""
+
+    def __init__(self, scene, seed=0, device=None, max_episode_steps=900, float_frames=True):
+        self._env = VectorEnv([scene], 1, seed=seed, device=device, max_episode_steps=max_episode_steps,
+                              autoreset=False)
+        self.float_frames = bool(float_frames)
+        self.action_size = VectorEnv.num_actions  # get_action_size (cached.py:66-68)
+        self.max_episode_steps = max_episode_steps
+
+    def _obs(self, img, goal):
+        img, goal = img[0].cpu().numpy(), goal[0].cpu().numpy()
+        if self.float_frames:
+            return img.astype(np.float64) / 255.0, goal.astype(np.float64) / 255.0
+        return img, goal
+
+    def reset(self):
+        return self._obs(*self._env.reset())
+
+    def step(self, action):
+        (img, goal), reward, done, info = self._env.step(torch.tensor([int(action)], dtype=torch.int32))
+        info_out = {}
+        if bool(info["truncated"][0].item()):
+            info_out["TimeLimit.truncated"] = True  # gym's TimeLimit (environments/gym_ai2thor/__init__.py:48)
+        return self._obs(img, goal), float(reward[0].item()), bool(done[0].item()), info_out
+
+    @property
+    def state(self):
+        """(state, goal) indices of the env (cached.py: self.state, self.goal)."""
+        st = self._env.get_state().cpu().numpy()
+        return int(st[ST_FIELDS.index("state"), 0]), int(st[ST_FIELDS.index("goal"), 0])
+
+    def set_schedule(self, starts_goals):
+        """Exact replay: the (start, goal) pairs the following resets take, in order."""
+        self._env.set_schedule(np.asarray(starts_goals, dtype=np.int32)[None])
+
+    def set_complexity(self, complexity=None):
+        self._env.set_complexity(complexity)
+
+    def close(self):
+        self._env.close()

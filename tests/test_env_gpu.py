@@ -95,6 +95,54 @@ def test_golden_no_reset_last_state_quirk(golden):
         assert np.array_equal(goal[0].cpu().numpy(), frames[d[p + "goal_idx"][t]])
 
 
+def test_single_env_gym_surface_replays_golden(golden):
+    """CachedThorEnv (the single THORDiscreteCachedEnv surface, no auto-reset) replays the
+    reference's no-reset trajectory: states, reward bits, dones, and the float64 frames
+    _preprocess_frame returns at equal size (u8 / 255), previous obs on terminal steps."""
+    vnav = _vnav()
+    d = golden("cached_env.npz")
+    sc = golden_scenes(golden)
+    p = "c3_"
+    scene = int(d[p + "meta"][0])
+    env = vnav.CachedThorEnv(sc[scene], seed=2, max_episode_steps=0)
+    env.set_schedule(d[p + "resets"][1:])
+    img, goal = env.reset()
+    assert img.dtype == np.float64 and img.shape == FRAME
+    frames = sc[scene].observations
+    s0, g0 = d[p + "resets"][1]
+    assert env.state == (s0, g0)
+    assert np.array_equal(img, frames[s0] / 255.0) and np.array_equal(goal, frames[g0] / 255.0)
+    for t, a in enumerate(d[p + "actions"]):
+        (img, goal), reward, done, info = env.step(int(a))
+        assert env.state[0] == d[p + "states"][t], t
+        assert np.float32(reward).view(np.uint32) == d[p + "reward_bits"][t], t
+        assert done == bool(d[p + "dones"][t]), t
+        assert info == {}
+        assert np.array_equal(img, frames[d[p + "img_idx"][t]] / 255.0), t
+        assert np.array_equal(goal, frames[d[p + "goal_idx"][t]] / 255.0), t
+    env.close()
+
+
+def test_single_env_time_limit_truncates():
+    """gym's TimeLimit under the single-env surface: done with TimeLimit.truncated at the
+    step limit, then reset() starts a new episode."""
+    vnav = _vnav()
+    sc = small_scenes()
+    env = vnav.CachedThorEnv(sc[1], seed=5, max_episode_steps=3)
+    env.reset()
+    g = env.state[1]
+    seen = None
+    for t in range(3):
+        _, _, done, info = env.step(0)
+        if done:
+            seen = (t, info)
+            break
+    assert seen is not None
+    if env.state[0] != g:  # not at the goal: the limit ended it
+        assert seen == (2, {"TimeLimit.truncated": True})
+    env.close()
+
+
 def small_scenes(shape=(6, 10, 3)):
     vnav = _vnav()
     out = []
