@@ -211,14 +211,22 @@ class A2CTrainer:
         ctr_base = ctypes.c_void_p(self.sched.data_ptr() + 2 * self.sched.element_size())
         for t in range(T):
             sl = slice(t * E, (t + 1) * E)
-            self.rows_img[sl].copy_(info["img_row"])
-            self.rows_goal[sl].copy_(info["goal_row"])
+            if t == 0:  # later steps' rows are written into their slots by the env step before them
+                self.rows_img[sl].copy_(info["img_row"])
+                self.rows_goal[sl].copy_(info["goal_row"])
             self._policy_step(t, self._frames(self.rows_img[sl], self.rows_goal[sl]))
             # Philox counter = updates * T + t (base from the device schedule)
             _lib.check(lib.vn_policy_sample_dev(_lib.ptr(self.out[sl]), E, A,
                                                 ctypes.c_uint64(vdist.rank_seed(self.seed, self.rank)), ctr_base,
                                                 ctypes.c_uint64(t), _lib.ptr(self.actions[sl]), None, None, None,
                                                 self._stream()), "vn_policy_sample_dev")
+            # the emitted frames' arena rows go straight into step t + 1's slots (the last step's
+            # into the env's own info rows: the bootstrap and the next rollout read them there)
+            nxt = slice((t + 1) * E, (t + 2) * E)
+            if t + 1 < T:
+                env.set_row_outputs(self.rows_img[nxt], self.rows_goal[nxt])
+            else:
+                env.set_row_outputs(None, None)
             env.step(self.actions[sl], out=dict(reward=self.rewards[t], done=self.dones[t], state=self.states),
                      gather=False)
             # next step's (last action, last reward) * mask and mask (bootstrap slots after the

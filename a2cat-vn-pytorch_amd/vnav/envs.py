@@ -77,11 +77,7 @@ class VectorEnv:
             img_row=torch.zeros(E, dtype=torch.int32, **kw),
             goal_row=torch.zeros(E, dtype=torch.int32, **kw),
         )
-        i = self._info
-        _lib.check(self.lib.vn_set_info_buffers(self._ctx, _lib.ptr(i["ep_return"]), _lib.ptr(i["ep_length"]),
-                                                _lib.ptr(i["terminal_state"]), _lib.ptr(i["truncated"]),
-                                                _lib.ptr(i["img_row"]), _lib.ptr(i["goal_row"])),
-                   "vn_set_info_buffers")
+        self.set_row_outputs(None, None)
         self.set_max_episode_steps(max_episode_steps)
         if not autoreset:
             _lib.check(self.lib.vn_set_autoreset(self._ctx, 0), "vn_set_autoreset")
@@ -177,6 +173,19 @@ class VectorEnv:
     # -- gym VecEnv API -------------------------------------------------------
     def _stream(self):
         return _lib.stream_ptr(self.device)
+
+    def set_row_outputs(self, img_rows, goal_rows):
+        """Where the next steps write the arena rows of the frames they emit: int32 [E] device
+        tensors (e.g. the trainer's per-step rollout slots, so no copy follows each step), or
+        None for this env's own info["img_row"] / info["goal_row"]."""
+        i = self._info
+        if img_rows is None:
+            img_rows, goal_rows = i["img_row"], i["goal_row"]
+        self._check_out("img_rows", img_rows, torch.int32, self.num_envs)
+        self._check_out("goal_rows", goal_rows, torch.int32, self.num_envs)
+        _lib.check(self.lib.vn_set_info_buffers(self._ctx, _lib.ptr(i["ep_return"]), _lib.ptr(i["ep_length"]),
+                                                _lib.ptr(i["terminal_state"]), _lib.ptr(i["truncated"]),
+                                                _lib.ptr(img_rows), _lib.ptr(goal_rows)), "vn_set_info_buffers")
 
     def _check_out(self, name, t, dtype, numel):
         """Caller-owned output buffers are written by the kernel through raw pointers: refuse
