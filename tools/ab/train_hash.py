@@ -16,10 +16,11 @@ from oracle.frames import synth_frames  # noqa: E402
 graph, spd, _ = h5_tables(np.ones((3, 3), dtype=bool))
 frames = synth_frames(3, np.arange(len(graph)), (84, 84, 3))
 scene = vnav.scene_from_arrays(graph, spd, frames)
-env = vnav.VectorEnv([scene], 256, seed=1, max_episode_steps=60, tasks=[(0, 5)])
 U = int(sys.argv[1]) if len(sys.argv) > 1 else 400
 SEED = int(sys.argv[2]) if len(sys.argv) > 2 else 0
 LR = float(sys.argv[3]) if len(sys.argv) > 3 else 2e-3
+E = int(sys.argv[4]) if len(sys.argv) > 4 else 256
+env = vnav.VectorEnv([scene], E, seed=1, max_episode_steps=60, tasks=[(0, 5)])
 tr = vnav.A2CTrainer(env, num_steps=20, seed=SEED, max_time_steps=1e9, recurrent=True, learning_rate=LR)
 lengths = []
 for u in range(U):
