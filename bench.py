@@ -248,6 +248,28 @@ def bench_train(args, scenes, dev, world, rank, recurrent, aux_weight=0.0, envs=
     return res
 
 
+def device_copy_rate(dev, nbytes, reps=20):
+    """The chip's device-to-device copy rate at the env step's byte count: one copy of
+    nbytes (= the step's frame reads, = its frame writes) moves 2 x nbytes through HBM.
+    Context for roofline.frac: the env step is a gather + copy of the same volume."""
+    src = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    dst = torch.empty_like(src)
+    src.fill_(1)
+    for _ in range(3):
+        dst.copy_(src)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize(dev)
+    e0.record()
+    for _ in range(reps):
+        dst.copy_(src)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / reps
+    del src, dst
+    torch.cuda.empty_cache()
+    return 2 * nbytes / (ms * 1e-3) / 1e9
+
+
 # ---------------------------------------------------------------- CPU baseline
 _CPU_SHARED = {}
 
@@ -370,6 +392,7 @@ def main():
         elapsed, kern_ms = float(t[0]), float(t[1])
     flags = env.error_flags()
     del env, out
+    copy_gbs = device_copy_rate(dev, E * 2 * fb)
     train = train_ff = train_ref = train_ref4 = train_c5 = None
     if args.train_steps > 0:
         torch.cuda.empty_cache()
@@ -443,7 +466,9 @@ def main():
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_detail": traffic_info, "bytes_per_env_step": bpe,
-                         "bytes_per_launch": bpe * E, "kernel_ms": kern_ms},
+                         "bytes_per_launch": bpe * E, "kernel_ms": kern_ms,
+                         # torch's device copy of the same frame bytes (read + write), same process
+                         "device_copy_gbs": copy_gbs, "frac_of_device_copy": achieved / copy_gbs},
             "cpu_baseline": cpu,
             "train": train,
             "train_feedforward": train_ff,
