@@ -725,6 +725,142 @@ __global__ void zero_uncovered_kernel(float* __restrict__ out, int nimg_g, int c
   *reinterpret_cast<f4*>(out + ((ng * H + y) * W + x) * cin + 4 * c4) = f4zero();
 }
 
+// conv3 input gradient (k4 s2, 64 output channels, 2 input groups of 32) on bf16 MFMA with
+// split operands, all four parity classes in one persistent kernel — the x6 scheme of
+// conv2_dgrad_x6_kernel (vn_conv1.h) at conv3's widths. Wave w owns parity class
+// (py, px) = (w >> 2, (w >> 1) & 1) and input group g = w & 1: its split weights (4 taps x 2
+// co halves x 2 ci tiles x 3 terms, 192 VGPRs) stay in registers for the kernel's lifetime.
+// A work item is IMG images: their dZ3 maps are split once when staged (three bf16 planes,
+// pixel rows padded to 72 so the 16 rows of a fragment fall on distinct bank quads; row
+// IMG*NP is the zero row of out-of-range taps), where the generic class product re-split
+// every dZ3 value at each of its 16 uses (22 VALU per MFMA). Product transposed (rows = ci,
+// columns = class pixels): each lane stores 4 channels of a pixel with one 16-B store.
+template <int IH, int IW, int OH, int OW>
+struct Conv3Dg {
+  static constexpr int CH = k4s2_covered<IH, OH>(), CW = k4s2_covered<IW, OW>();
+  static constexpr int NPC = (CH / 2) * (CW / 2);  // class pixels per image
+  static constexpr int NP = OH * OW;
+  static constexpr int IMG = NPC >= 64 ? 1 : 64 / NPC;  // images per work item
+  static constexpr int PS = 72;                          // plane row stride (bf16)
+  static constexpr size_t LDS = (size_t)3 * (IMG * NP + 1) * PS * 2;
+  static constexpr bool fits = CH % 2 == 0 && CW % 2 == 0 && LDS <= 160 * 1024;
+};
+
+template <int IH, int IW, int OH, int OW>
+__global__ __launch_bounds__(512, 1) void conv3_dgrad_x6_kernel(const float* __restrict__ dZ3,
+                                                             const float* __restrict__ WT,
+                                                             const float* __restrict__ X2, float* __restrict__ dX2,
+                                                             int n) {
+  using C = Conv3Dg<IH, IW, OH, OW>;
+  constexpr int WXC = C::CW / 2, NPC = C::NPC, NP = C::NP, IMG = C::IMG, PS = C::PS;
+  constexpr int ROWS = IMG * NP, PL = (ROWS + 1) * PS;
+  constexpr int TILES = (IMG * NPC + 15) / 16;
+  constexpr int NT = 512, NZ = (ROWS * 16 + NT - 1) / NT;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem_c3[];
+  uint16_t* zs = reinterpret_cast<uint16_t*>(smem_c3);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int py = wave >> 2, px = (wave >> 1) & 1, g = wave & 1;
+  const int i16 = lane & 15, q = lane >> 4;
+  bf16x8_t bw[4][2][2][3];  // [tap][co half][ci tile][term]: A[ci][k = co 32h + 8q + j]
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int ky = py + 2 * (t >> 1), kx = px + 2 * (t & 1);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        union { uint16_t u[8]; bf16x8_t v; } b0, b1, b2;
+        const float* w = WT + ((ky * 4 + kx) * 64 + 32 * g + 16 * nt + i16) * 64 + 32 * h + 8 * q;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) split3_bf16(w[j], b0.u[j], b1.u[j], b2.u[j]);
+        bw[t][h][nt][0] = b0.v;
+        bw[t][h][nt][1] = b1.v;
+        bw[t][h][nt][2] = b2.v;
+      }
+  }
+  for (int i = tid; i < 3 * PS / 2; i += NT) {  // zero rows
+    const int pl = i / (PS / 2), e = i - pl * (PS / 2);
+    reinterpret_cast<uint32_t*>(zs + pl * PL + ROWS * PS)[e] = 0u;
+  }
+  const int items = (n + IMG - 1) / IMG;
+  f4 zr[NZ];
+  auto load_z = [&](int it) {  // the item's dZ3 rows (images consecutive), zeros past n
+    const int64_t r0 = (int64_t)it * ROWS, rend = (int64_t)n * NP;
+    const f4* z4 = reinterpret_cast<const f4*>(dZ3);
+#pragma unroll
+    for (int j = 0; j < NZ; ++j) {
+      const int i = tid + j * NT;
+      if (i < ROWS * 16) zr[j] = r0 + (i >> 4) < rend ? z4[(r0 + (i >> 4)) * 16 + (i & 15)] : f4zero();
+    }
+  };
+  if ((int)blockIdx.x < items) load_z(blockIdx.x);
+  for (int it = blockIdx.x; it < items; it += gridDim.x) {
+#pragma unroll
+    for (int j = 0; j < NZ; ++j) {
+      const int i = tid + j * NT;
+      if (i < ROWS * 16) {
+        uint2 t0, t1, t2;
+        split3_pack(zr[j], t0, t1, t2);
+        uint16_t* d = zs + (i >> 4) * PS + 4 * (i & 15);
+        *reinterpret_cast<uint2*>(d) = t0;
+        *reinterpret_cast<uint2*>(d + PL) = t1;
+        *reinterpret_cast<uint2*>(d + 2 * PL) = t2;
+      }
+    }
+    __syncthreads();
+    if (it + (int)gridDim.x < items) load_z(it + gridDim.x);
+    const int img0 = it * IMG;
+#pragma unroll 1
+    for (int tile = 0; tile < TILES; ++tile) {
+      const int pc = tile * 16 + i16;  // this lane's class pixel (B column) within the item
+      const int im = pc / NPC, r = pc - (pc / NPC) * NPC;
+      const int yy = r / WXC, xx = r - (r / WXC) * WXC;
+      const bool live = pc < IMG * NPC && img0 + im < n;
+      int off[4];
+#pragma unroll
+      for (int tap = 0; tap < 4; ++tap) {
+        const int oy = yy - (tap >> 1), ox = xx - (tap & 1);
+        const bool ok = live && oy >= 0 && oy < OH && ox >= 0 && ox < OW;
+        off[tap] = (ok ? im * NP + oy * OW + ox : ROWS) * PS + 8 * q;
+      }
+      f4 acc[2] = {f4zero(), f4zero()};
+#pragma unroll
+      for (int tap = 0; tap < 4; ++tap)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          bf16x8_t a[3];
+#pragma unroll
+          for (int tm = 0; tm < 3; ++tm) a[tm] = *reinterpret_cast<const bf16x8_t*>(zs + tm * PL + off[tap] + 32 * h);
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) {  // small terms first
+            f4 c = acc[nt];
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[tap][h][nt][0], a[2], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[tap][h][nt][2], a[0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[tap][h][nt][1], a[1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[tap][h][nt][0], a[1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[tap][h][nt][1], a[0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[tap][h][nt][0], a[0], c, 0, 0, 0);
+            acc[nt] = c;
+          }
+        }
+      if (live) {  // lane (pixel, q) holds channels 16 nt + 4q .. +3 of group g, under X2's ReLU
+        const int y = 2 * yy + py, x = 2 * xx + px;
+        const int64_t base = ((((int64_t)(img0 + im) * 2 + g) * IH + y) * IW + x) * 32 + 4 * q;
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          const f4 xm = *reinterpret_cast<const f4*>(X2 + base + 16 * nt);
+          f4 v = acc[nt];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = xm[e] > 0.0f ? v[e] : 0.0f;
+          *reinterpret_cast<f4*>(dX2 + base + 16 * nt) = v;
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
 template <int COUT, int CIN, int H, int W, int OH, int OW, int PY, int PX>
 inline void dgrad_class_groups(const float* dz, const float* WT, float* out, const float* X, int nimg, int G,
                                hipStream_t st) {
@@ -741,18 +877,35 @@ inline void dgrad_class_groups(const float* dz, const float* WT, float* out, con
 }
 
 template <int COUT, int CIN, int H, int W, int OH, int OW>
-inline void dgrad_all_classes_groups(const float* dz, const float* WT, float* out, const float* X, int nimg, int G,
+inline int dgrad_all_classes_groups(const float* dz, const float* WT, float* out, const float* X, int nimg, int G,
                                      hipStream_t st) {
-  dgrad_class_groups<COUT, CIN, H, W, OH, OW, 0, 0>(dz, WT, out, X, nimg, G, st);
-  dgrad_class_groups<COUT, CIN, H, W, OH, OW, 0, 1>(dz, WT, out, X, nimg, G, st);
-  dgrad_class_groups<COUT, CIN, H, W, OH, OW, 1, 0>(dz, WT, out, X, nimg, G, st);
-  dgrad_class_groups<COUT, CIN, H, W, OH, OW, 1, 1>(dz, WT, out, X, nimg, G, st);
+  using C3 = Conv3Dg<H, W, OH, OW>;
+  // VN_CONV3_DGRAD_GENERIC set: the four class products instead (A/B and parity checks; read
+  // per call, once per backward)
+  const bool generic = getenv("VN_CONV3_DGRAD_GENERIC") != nullptr;
+  if (C3::fits && COUT == 64 && CIN == 32 && G == 2 && !generic) {
+    if constexpr (C3::fits) {
+      const void* kfn = (const void*)conv3_dgrad_x6_kernel<H, W, OH, OW>;
+      VN_HIP(ensure_dyn_lds(kfn, C3::LDS));
+      const int items = (nimg + C3::IMG - 1) / C3::IMG;
+      const int blocks = std::min(items, resident_blocks(kfn, 512, C3::LDS));
+      if (blocks > 0)
+        hipLaunchKernelGGL((conv3_dgrad_x6_kernel<H, W, OH, OW>), dim3(blocks), dim3(512), C3::LDS, st, dz, WT, X, out,
+                           nimg);
+    }
+  } else {
+    dgrad_class_groups<COUT, CIN, H, W, OH, OW, 0, 0>(dz, WT, out, X, nimg, G, st);
+    dgrad_class_groups<COUT, CIN, H, W, OH, OW, 0, 1>(dz, WT, out, X, nimg, G, st);
+    dgrad_class_groups<COUT, CIN, H, W, OH, OW, 1, 0>(dz, WT, out, X, nimg, G, st);
+    dgrad_class_groups<COUT, CIN, H, W, OH, OW, 1, 1>(dz, WT, out, X, nimg, G, st);
+  }
   constexpr int CH = k4s2_covered<H, OH>(), CW = k4s2_covered<W, OW>();
   if constexpr (CH < H || CW < W) {
     const int64_t total = (int64_t)nimg * G * (H * W - CH * CW) * (CIN / 4);
     hipLaunchKernelGGL((zero_uncovered_kernel<H, W, CH, CW>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
                        out, nimg * G, CIN);
   }
+  return VN_OK;
 }
 
 template <int COUT, int CINF, int H, int W, int OH, int OW>
@@ -971,7 +1124,8 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
     using Im = NhwcIm2col<32, 4, 4, 2, G::OH2, G::OW2, G::OH3, G::OW3, 2>;
     Im2colT<Im> fbw{Im{a.X[1], n9}, 1024};
     launch_wgrad6<64, 128, 2, 2>(w.dz3, 64, 64, fbw, 1024, n9, w.slab, w.slab_cap, Gr + L.l[2].w, Gr + L.l[2].b, st);
-    dgrad_all_classes_groups<64, 32, G::OH2, G::OW2, G::OH3, G::OW3>(w.dz3, T(2), w.dz2, a.X[1], n, 2, st);
+    const int rc = dgrad_all_classes_groups<64, 32, G::OH2, G::OW2, G::OH3, G::OW3>(w.dz3, T(2), w.dz2, a.X[1], n, 2, st);
+    if (rc != VN_OK) return rc;
   }
   // ---- conv2 (k4 s2): wgrad (needs X1), then dgrad into dz1 written over X1
   {
