@@ -725,53 +725,59 @@ __global__ void zero_uncovered_kernel(float* __restrict__ out, int nimg_g, int c
   *reinterpret_cast<f4*>(out + ((ng * H + y) * W + x) * cin + 4 * c4) = f4zero();
 }
 
-// conv3 input gradient (k4 s2, 64 output channels, 2 input groups of 32) on bf16 MFMA with
-// split operands, all four parity classes in one persistent kernel — the x6 scheme of
-// conv2_dgrad_x6_kernel (vn_conv1.h) at conv3's widths. Wave w owns parity class
-// (py, px) = (w >> 2, (w >> 1) & 1) and input group g = w & 1: its split weights (4 taps x 2
-// co halves x 2 ci tiles x 3 terms, 192 VGPRs) stay in registers for the kernel's lifetime.
-// A work item is IMG images: their dZ3 maps are split once when staged (three bf16 planes,
-// pixel rows padded to 72 so the 16 rows of a fragment fall on distinct bank quads; row
-// IMG*NP is the zero row of out-of-range taps), where the generic class product re-split
-// every dZ3 value at each of its 16 uses (22 VALU per MFMA). Product transposed (rows = ci,
-// columns = class pixels): each lane stores 4 channels of a pixel with one 16-B store.
-template <int IH, int IW, int OH, int OW>
-struct Conv3Dg {
-  static constexpr int CH = k4s2_covered<IH, OH>(), CW = k4s2_covered<IW, OW>();
-  static constexpr int NPC = (CH / 2) * (CW / 2);  // class pixels per image
-  static constexpr int NP = OH * OW;
+// Stride-2 k4 parity-class products on bf16 MFMA with split operands, all four classes
+// (py, px) in one persistent kernel: output pixel (2yy + py, 2xx + px) sums, over the 2x2
+// taps (ky, kx) = (py + 2 tky, px + 2 tkx) that reach it, the staged map's pixel
+// (yy - tky, xx - tkx) (KC channels) times W[tap][col][KC]. Two products use it: conv3's input
+// gradient (map dZ3, 64 -> 2 x 32 channels under X2's ReLU) and the aux heads' first
+// transposed conv (map X4, 32 -> 48 channels, bias + ReLU) — the x6 scheme of
+// conv2_dgrad_x6_kernel (vn_conv1.h). Wave w owns class w / WPC and the NTL 16-wide column
+// tiles of column group w % WPC; its split weights (4 taps x KC/32 k steps x NTL tiles x 3
+// terms) stay in registers for the kernel's lifetime. A work item is IMG images: their maps
+// are split once when staged (three bf16 planes, pixel rows padded to KC + 8 so the 16 rows of
+// a fragment fall on distinct bank quads; row IMG*NP is the zero row of out-of-range taps),
+// where the generic class products re-split every map value at each of its 16 uses (22 VALU
+// per MFMA). The product is transposed (rows = columns of W, MFMA columns = class pixels), so
+// each lane hands the epilogue 4 consecutive channels of one output pixel.
+template <int SH_, int SW_, int YC_, int XC_, int KC_, int NCOL_, int WPC_>
+struct ParityDg {
+  static constexpr int SH = SH_, SW = SW_, YC = YC_, XC = XC_, KC = KC_, NCOL = NCOL_, WPC = WPC_;
+  static constexpr int NP = SH * SW;                     // staged map pixels per image
+  static constexpr int NPC = YC * XC;                    // class pixels per image
   static constexpr int IMG = NPC >= 64 ? 1 : 64 / NPC;  // images per work item
-  static constexpr int PS = 72;                          // plane row stride (bf16)
+  static constexpr int PS = KC + 8;                      // plane row stride (bf16)
+  static constexpr int NTL = NCOL / (16 * WPC);          // column tiles per wave
+  static constexpr int KS = KC / 32;                     // MFMA k steps per tap
+  static constexpr int NT = 256 * WPC;
   static constexpr size_t LDS = (size_t)3 * (IMG * NP + 1) * PS * 2;
-  static constexpr bool fits = CH % 2 == 0 && CW % 2 == 0 && LDS <= 160 * 1024;
+  static constexpr bool fits = LDS <= 160 * 1024;
+  static_assert(KC % 32 == 0 && NCOL % (16 * WPC) == 0, "k steps of 32, whole 16-column tiles per wave");
 };
 
-template <int IH, int IW, int OH, int OW>
-__global__ __launch_bounds__(512, 1) void conv3_dgrad_x6_kernel(const float* __restrict__ dZ3,
-                                                             const float* __restrict__ WT,
-                                                             const float* __restrict__ X2, float* __restrict__ dX2,
-                                                             int n) {
-  using C = Conv3Dg<IH, IW, OH, OW>;
-  constexpr int WXC = C::CW / 2, NPC = C::NPC, NP = C::NP, IMG = C::IMG, PS = C::PS;
-  constexpr int ROWS = IMG * NP, PL = (ROWS + 1) * PS;
-  constexpr int TILES = (IMG * NPC + 15) / 16;
-  constexpr int NT = 512, NZ = (ROWS * 16 + NT - 1) / NT;
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem_c3[];
-  uint16_t* zs = reinterpret_cast<uint16_t*>(smem_c3);
+template <class S, class EP>
+__global__ __launch_bounds__(S::NT, S::NT >= 512 ? 1 : 2) void parity_dgrad_x6_kernel(const float* __restrict__ map,
+                                                                const float* __restrict__ WT, EP ep, int n) {
+  constexpr int SH = S::SH, SW = S::SW, XC = S::XC, KC = S::KC, NCOL = S::NCOL, WPC = S::WPC;
+  constexpr int NP = S::NP, NPC = S::NPC, IMG = S::IMG, PS = S::PS, NTL = S::NTL, KS = S::KS, NT = S::NT;
+  constexpr int ROWS = IMG * NP, PL = (ROWS + 1) * PS, C4 = KC / 4;
+  constexpr int TILES = (IMG * NPC + 15) / 16, NZ = (ROWS * C4 + NT - 1) / NT;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem_pdg[];
+  uint16_t* zs = reinterpret_cast<uint16_t*>(smem_pdg);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int py = wave >> 2, px = (wave >> 1) & 1, g = wave & 1;
+  const int cls = wave / WPC, py = cls >> 1, px = cls & 1;
+  const int col0 = (wave % WPC) * NTL * 16;
   const int i16 = lane & 15, q = lane >> 4;
-  bf16x8_t bw[4][2][2][3];  // [tap][co half][ci tile][term]: A[ci][k = co 32h + 8q + j]
+  bf16x8_t bw[4][KS][NTL][3];  // [tap][k step][column tile][term]: A[col][k = 32h + 8q + j]
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     const int ky = py + 2 * (t >> 1), kx = px + 2 * (t & 1);
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+    for (int h = 0; h < KS; ++h)
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
+      for (int nt = 0; nt < NTL; ++nt) {
         union { uint16_t u[8]; bf16x8_t v; } b0, b1, b2;
-        const float* w = WT + ((ky * 4 + kx) * 64 + 32 * g + 16 * nt + i16) * 64 + 32 * h + 8 * q;
+        const float* w = WT + ((int64_t)(ky * 4 + kx) * NCOL + col0 + 16 * nt + i16) * KC + 32 * h + 8 * q;
 #pragma unroll
         for (int j = 0; j < 8; ++j) split3_bf16(w[j], b0.u[j], b1.u[j], b2.u[j]);
         bw[t][h][nt][0] = b0.v;
@@ -785,55 +791,61 @@ __global__ __launch_bounds__(512, 1) void conv3_dgrad_x6_kernel(const float* __r
   }
   const int items = (n + IMG - 1) / IMG;
   f4 zr[NZ];
-  auto load_z = [&](int it) {  // the item's dZ3 rows (images consecutive), zeros past n
+  auto load_z = [&](int it) {  // the item's map rows (images consecutive), zeros past n
     const int64_t r0 = (int64_t)it * ROWS, rend = (int64_t)n * NP;
-    const f4* z4 = reinterpret_cast<const f4*>(dZ3);
+    const f4* z4 = reinterpret_cast<const f4*>(map);
 #pragma unroll
     for (int j = 0; j < NZ; ++j) {
       const int i = tid + j * NT;
-      if (i < ROWS * 16) zr[j] = r0 + (i >> 4) < rend ? z4[(r0 + (i >> 4)) * 16 + (i & 15)] : f4zero();
+      if (i < ROWS * C4) zr[j] = r0 + i / C4 < rend ? z4[(r0 + i / C4) * C4 + i % C4] : f4zero();
     }
   };
-  if ((int)blockIdx.x < items) load_z(blockIdx.x);
+  // the next item's map is prefetched into registers while this one multiplies, unless it
+  // would not fit beside the weights (300x400's 17x23 map: loaded at the item's start)
+  constexpr bool PF = NZ <= 6;
+  if (PF && (int)blockIdx.x < items) load_z(blockIdx.x);
   for (int it = blockIdx.x; it < items; it += gridDim.x) {
+    if constexpr (!PF) load_z(it);
 #pragma unroll
     for (int j = 0; j < NZ; ++j) {
       const int i = tid + j * NT;
-      if (i < ROWS * 16) {
+      if (i < ROWS * C4) {
         uint2 t0, t1, t2;
         split3_pack(zr[j], t0, t1, t2);
-        uint16_t* d = zs + (i >> 4) * PS + 4 * (i & 15);
+        uint16_t* d = zs + (i / C4) * PS + 4 * (i % C4);
         *reinterpret_cast<uint2*>(d) = t0;
         *reinterpret_cast<uint2*>(d + PL) = t1;
         *reinterpret_cast<uint2*>(d + 2 * PL) = t2;
       }
     }
     __syncthreads();
-    if (it + (int)gridDim.x < items) load_z(it + gridDim.x);
+    if (PF && it + (int)gridDim.x < items) load_z(it + gridDim.x);
     const int img0 = it * IMG;
 #pragma unroll 1
     for (int tile = 0; tile < TILES; ++tile) {
-      const int pc = tile * 16 + i16;  // this lane's class pixel (B column) within the item
+      const int pc = tile * 16 + i16;  // this lane's class pixel (MFMA column) within the item
       const int im = pc / NPC, r = pc - (pc / NPC) * NPC;
-      const int yy = r / WXC, xx = r - (r / WXC) * WXC;
+      const int yy = r / XC, xx = r - (r / XC) * XC;
       const bool live = pc < IMG * NPC && img0 + im < n;
       int off[4];
 #pragma unroll
       for (int tap = 0; tap < 4; ++tap) {
         const int oy = yy - (tap >> 1), ox = xx - (tap & 1);
-        const bool ok = live && oy >= 0 && oy < OH && ox >= 0 && ox < OW;
-        off[tap] = (ok ? im * NP + oy * OW + ox : ROWS) * PS + 8 * q;
+        const bool ok = live && oy >= 0 && oy < SH && ox >= 0 && ox < SW;
+        off[tap] = (ok ? im * NP + oy * SW + ox : ROWS) * PS + 8 * q;
       }
-      f4 acc[2] = {f4zero(), f4zero()};
+      f4 acc[NTL];
+#pragma unroll
+      for (int nt = 0; nt < NTL; ++nt) acc[nt] = f4zero();
 #pragma unroll
       for (int tap = 0; tap < 4; ++tap)
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < KS; ++h) {
           bf16x8_t a[3];
 #pragma unroll
           for (int tm = 0; tm < 3; ++tm) a[tm] = *reinterpret_cast<const bf16x8_t*>(zs + tm * PL + off[tap] + 32 * h);
 #pragma unroll
-          for (int nt = 0; nt < 2; ++nt) {  // small terms first
+          for (int nt = 0; nt < NTL; ++nt) {  // small terms first
             f4 c = acc[nt];
             c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[tap][h][nt][0], a[2], c, 0, 0, 0);
             c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[tap][h][nt][2], a[0], c, 0, 0, 0);
@@ -844,21 +856,64 @@ __global__ __launch_bounds__(512, 1) void conv3_dgrad_x6_kernel(const float* __r
             acc[nt] = c;
           }
         }
-      if (live) {  // lane (pixel, q) holds channels 16 nt + 4q .. +3 of group g, under X2's ReLU
+      if (live) {  // lane (pixel, q) holds columns col0 + 16 nt + 4q .. +3
+        // every epilogue load before the first store: vmcnt counts stores too, so a load
+        // issued after a store would wait for it (+8 % per launch measured)
         const int y = 2 * yy + py, x = 2 * xx + px;
-        const int64_t base = ((((int64_t)(img0 + im) * 2 + g) * IH + y) * IW + x) * 32 + 4 * q;
+        f4 pre[NTL];
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt) {
-          const f4 xm = *reinterpret_cast<const f4*>(X2 + base + 16 * nt);
-          f4 v = acc[nt];
+        for (int nt = 0; nt < NTL; ++nt) pre[nt] = ep.pre(img0 + im, y, x, col0 + 16 * nt + 4 * q);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = xm[e] > 0.0f ? v[e] : 0.0f;
-          *reinterpret_cast<f4*>(dX2 + base + 16 * nt) = v;
-        }
+        for (int nt = 0; nt < NTL; ++nt) ep.post(img0 + im, y, x, col0 + 16 * nt + 4 * q, acc[nt], pre[nt]);
       }
     }
     __syncthreads();
   }
+}
+
+// conv3's input gradient: column c is channel c % 32 of input group c / 32 (X2 layout
+// [n][2][IH][IW][32]), masked by the ReLU that produced X2 (as EpiMaskParityG).
+template <int IH, int IW>
+struct EpiDgMaskG2 {
+  const float* X;
+  float* out;
+  __device__ __forceinline__ int64_t index(int img, int y, int x, int col) const {
+    return ((((int64_t)img * 2 + (col >> 5)) * IH + y) * IW + x) * 32 + (col & 31);
+  }
+  __device__ __forceinline__ f4 pre(int img, int y, int x, int col) const {
+    return *reinterpret_cast<const f4*>(X + index(img, y, x, col));
+  }
+  __device__ __forceinline__ void post(int img, int y, int x, int col, f4 v, f4 xm) const {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = xm[e] > 0.0f ? v[e] : 0.0f;
+    *reinterpret_cast<f4*>(out + index(img, y, x, col)) = v;
+  }
+};
+
+// Transposed conv output: bias (+ ReLU), NHWC with C channels (as EpiDeconv).
+template <int OH, int OW, int C>
+struct EpiDgBias {
+  float* out;
+  const float* bias;
+  int relu;
+  __device__ __forceinline__ f4 pre(int, int, int, int col) const {
+    return *reinterpret_cast<const f4*>(bias + col);
+  }
+  __device__ __forceinline__ void post(int img, int y, int x, int col, f4 v, f4 b) const {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = relu ? fmaxf(v[e] + b[e], 0.0f) : v[e] + b[e];
+    *reinterpret_cast<f4*>(out + (((int64_t)img * OH + y) * OW + x) * C + col) = v;
+  }
+};
+
+template <class S, class EP>
+inline int launch_parity_dgrad_x6(const float* map, const float* WT, EP ep, int n, hipStream_t st) {
+  const void* kfn = (const void*)parity_dgrad_x6_kernel<S, EP>;
+  VN_HIP(ensure_dyn_lds(kfn, S::LDS));
+  const int items = (n + S::IMG - 1) / S::IMG;
+  const int blocks = std::min(items, resident_blocks(kfn, S::NT, S::LDS));
+  if (blocks > 0) hipLaunchKernelGGL((parity_dgrad_x6_kernel<S, EP>), dim3(blocks), dim3(S::NT), S::LDS, st, map, WT, ep, n);
+  return VN_OK;
 }
 
 template <int COUT, int CIN, int H, int W, int OH, int OW, int PY, int PX>
@@ -879,19 +934,16 @@ inline void dgrad_class_groups(const float* dz, const float* WT, float* out, con
 template <int COUT, int CIN, int H, int W, int OH, int OW>
 inline int dgrad_all_classes_groups(const float* dz, const float* WT, float* out, const float* X, int nimg, int G,
                                      hipStream_t st) {
-  using C3 = Conv3Dg<H, W, OH, OW>;
-  // VN_CONV3_DGRAD_GENERIC set: the four class products instead (A/B and parity checks; read
-  // per call, once per backward)
-  const bool generic = getenv("VN_CONV3_DGRAD_GENERIC") != nullptr;
-  if (C3::fits && COUT == 64 && CIN == 32 && G == 2 && !generic) {
-    if constexpr (C3::fits) {
-      const void* kfn = (const void*)conv3_dgrad_x6_kernel<H, W, OH, OW>;
-      VN_HIP(ensure_dyn_lds(kfn, C3::LDS));
-      const int items = (nimg + C3::IMG - 1) / C3::IMG;
-      const int blocks = std::min(items, resident_blocks(kfn, 512, C3::LDS));
-      if (blocks > 0)
-        hipLaunchKernelGGL((conv3_dgrad_x6_kernel<H, W, OH, OW>), dim3(blocks), dim3(512), C3::LDS, st, dz, WT, X, out,
-                           nimg);
+  constexpr int CH = k4s2_covered<H, OH>(), CW = k4s2_covered<W, OW>();
+  // the covered class pixels (CH/2 x CW/2 per class when even) over the dZ3 map
+  using S = ParityDg<OH, OW, CH / 2, CW / 2, COUT, 2 * CIN, 2>;
+  // VN_DGRAD_GENERIC set: the four class products instead (A/B and parity checks; read per
+  // call, once per backward)
+  const bool generic = getenv("VN_DGRAD_GENERIC") != nullptr;
+  if (CH % 2 == 0 && CW % 2 == 0 && S::fits && COUT == 64 && CIN == 32 && G == 2 && !generic) {
+    if constexpr (CH % 2 == 0 && CW % 2 == 0 && S::fits) {
+      const int rc = launch_parity_dgrad_x6<S>(dz, WT, EpiDgMaskG2<H, W>{X, out}, nimg, st);
+      if (rc != VN_OK) return rc;
     }
   } else {
     dgrad_class_groups<COUT, CIN, H, W, OH, OW, 0, 0>(dz, WT, out, X, nimg, G, st);
@@ -899,7 +951,6 @@ inline int dgrad_all_classes_groups(const float* dz, const float* WT, float* out
     dgrad_class_groups<COUT, CIN, H, W, OH, OW, 1, 0>(dz, WT, out, X, nimg, G, st);
     dgrad_class_groups<COUT, CIN, H, W, OH, OW, 1, 1>(dz, WT, out, X, nimg, G, st);
   }
-  constexpr int CH = k4s2_covered<H, OH>(), CW = k4s2_covered<W, OW>();
   if constexpr (CH < H || CW < W) {
     const int64_t total = (int64_t)nimg * G * (H * W - CH * CW) * (CIN / 4);
     hipLaunchKernelGGL((zero_uncovered_kernel<H, W, CH, CW>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
@@ -1482,13 +1533,23 @@ inline void deconv_class(const float* in, const float* WT, float* out, const flo
 }
 
 template <int CIN, int COUT, int IH, int IW, int OH, int OW>
-inline void deconv_all(const float* in, const float* WT, float* out, const float* bias, int relu, int nimg,
+inline int deconv_all(const float* in, const float* WT, float* out, const float* bias, int relu, int nimg,
                        hipStream_t st) {
   static_assert(OH == 2 * IH + 2 && OW == 2 * IW + 2, "k4 s2 transposed conv geometry");
+  // the first layer (32 -> 48) on the persistent parity-class kernel, one wave per class
+  using S = ParityDg<IH, IW, OH / 2, OW / 2, 32, 48, 1>;
+  if constexpr (CIN == 32 && COUT == 48 && S::fits) {
+    if (!getenv("VN_DGRAD_GENERIC")) {  // read per call (A/B and parity checks)
+      const int rc = launch_parity_dgrad_x6<S>(in, WT, EpiDgBias<OH, OW, COUT>{out, bias, relu}, nimg, st);
+      if (rc != VN_OK) return rc;
+      return VN_OK;
+    }
+  }
   deconv_class<CIN, COUT, IH, IW, OH, OW, 0, 0>(in, WT, out, bias, relu, nimg, st);
   deconv_class<CIN, COUT, IH, IW, OH, OW, 0, 1>(in, WT, out, bias, relu, nimg, st);
   deconv_class<CIN, COUT, IH, IW, OH, OW, 1, 0>(in, WT, out, bias, relu, nimg, st);
   deconv_class<CIN, COUT, IH, IW, OH, OW, 1, 1>(in, WT, out, bias, relu, nimg, st);
+  return VN_OK;
 }
 
 struct AuxWork {
@@ -1546,11 +1607,11 @@ int aux_forward_impl(const PolicyLayout& L, const float* P, const float* X4, int
   constexpr int IH = G::OH3, IW = G::OW3, AH = 2 * IH + 2, AW = 2 * IW + 2, PH = 2 * AH + 2, PW = 2 * AW + 2;
   hipLaunchKernelGGL(transpose_kernel, dim3((32 * 768 + 255) / 256), dim3(256), 0, st, P + L.aw1, 32, 768, w.w1t);
   hipLaunchKernelGGL(transpose_kernel, dim3((48 * 128 + 255) / 256), dim3(256), 0, st, P + L.aw2, 48, 128, w.w2t);
-  deconv_all<32, kAuxC1, IH, IW, AH, AW>(X4, w.w1t, A1, P + L.ab1, 1, n, st);
+  if (const int rc = deconv_all<32, kAuxC1, IH, IW, AH, AW>(X4, w.w1t, A1, P + L.ab1, 1, n, st); rc != VN_OK) return rc;
   if constexpr (aux2_fits<AH, AW>()) {
     launch_aux2<AH, AW, PH, PW, false>(A1, n, P + L.aw2, P + L.ab2, Pout, nullptr, 0.0f, nullptr, nullptr, st);
   } else {
-    deconv_all<kAuxC1, kAuxC2, AH, AW, PH, PW>(A1, w.w2t, Pout, P + L.ab2, 0, n, st);
+    if (const int rc = deconv_all<kAuxC1, kAuxC2, AH, AW, PH, PW>(A1, w.w2t, Pout, P + L.ab2, 0, n, st); rc != VN_OK) return rc;
   }
   VN_HIP(hipGetLastError());
   return VN_OK;
@@ -1567,7 +1628,7 @@ int aux_forward_loss_impl(const PolicyLayout& L, const float* P, const float* X4
   constexpr int IH = G::OH3, IW = G::OW3, AH = 2 * IH + 2, AW = 2 * IW + 2, PH = 2 * AH + 2, PW = 2 * AW + 2;
   if constexpr (aux2_fits<AH, AW>()) {
     hipLaunchKernelGGL(transpose_kernel, dim3((32 * 768 + 255) / 256), dim3(256), 0, st, P + L.aw1, 32, 768, w.w1t);
-    deconv_all<32, kAuxC1, IH, IW, AH, AW>(X4, w.w1t, A1, P + L.ab1, 1, n, st);
+    if (const int rc = deconv_all<32, kAuxC1, IH, IW, AH, AW>(X4, w.w1t, A1, P + L.ab1, 1, n, st); rc != VN_OK) return rc;
     launch_aux2<AH, AW, PH, PW, true>(A1, n, P + L.aw2, P + L.ab2, nullptr, tg, weight, dpred, stats, st);
   } else {
     const int rc = aux_forward_impl<H0, W0>(L, P, X4, n, A1, pred, w, st);

@@ -1,0 +1,94 @@
+"""The persistent parity-class kernel (`parity_dgrad_x6_kernel`, vn_policy.hip) against the
+four generic parity-class products it replaced (`VN_DGRAD_GENERIC`, read per call), for its
+two products: conv3's input gradient (k4 s2, 64 -> 2 x 32 channels) and the aux heads'
+first transposed conv (32 -> 48 channels, bias + ReLU). Both compute the same exact
+split-bf16 products in another summation order, so every parameter gradient — conv3's
+input gradient feeds conv2's and conv1's — agrees to rounding (1e-5 of scale). Batch sizes
+cover a partial last work item (84x84 packs 4 images per item) and persistent-grid wraps
+(more items than resident workgroups). The reference-level checks of these gradients are
+tests/test_policy_gpu.py (84x84 golden, 174x174 float64 oracle)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _grads(pol, img, gl, cl, cv, generic):
+    if generic:
+        os.environ["VN_DGRAD_GENERIC"] = "1"
+    try:
+        pol.params.grad = None
+        logits, value, _ = pol(((img, gl), None), None, None)
+        ((logits * cl).sum() + (value * cv).sum()).backward()
+        torch.cuda.synchronize()
+        return pol.params.grad.clone()
+    finally:
+        os.environ.pop("VN_DGRAD_GENERIC", None)
+
+
+@pytest.mark.parametrize("hw,N", [((84, 84), 37), ((84, 84), 1030), ((174, 174), 5), ((174, 174), 300)])
+def test_conv3_dgrad_kernel_matches_class_products(hw, N):
+    from vnav.policy import GoalNavPolicy
+    torch.manual_seed(11)
+    pol = GoalNavPolicy(3, 4, hw)
+    with torch.no_grad():
+        pol.params.add_(torch.randn_like(pol.params) * 0.01)
+    g = torch.Generator(device="cuda").manual_seed(1)
+    img = torch.randint(0, 256, (N, 1) + hw + (3,), dtype=torch.uint8, device="cuda", generator=g)
+    gl = torch.randint(0, 256, (N, 1) + hw + (3,), dtype=torch.uint8, device="cuda", generator=g)
+    cl = torch.randn((N, 1, 4), device="cuda", generator=g)
+    cv = torch.randn((N, 1, 1), device="cuda", generator=g)
+    fast = pol.net.to_reference(_grads(pol, img, gl, cl, cv, generic=False))
+    gen = pol.net.to_reference(_grads(pol, img, gl, cl, cv, generic=True))
+    bad = {}
+    for k in gen:
+        b = gen[k].numpy().astype(np.float64)
+        e = np.abs(fast[k].numpy() - b).max() / max(np.abs(b).max(), 1e-30)
+        if e > 1e-5:
+            bad[k] = "%.3g" % e
+    assert not bad, bad
+    # the kernel ran (not a no-op): conv3's input gradient reaches conv2's weights
+    assert np.abs(fast["shared_base.0.2.weight"].numpy()).max() > 0
+
+
+@pytest.mark.parametrize("hw,N", [((84, 84), 37), ((174, 174), 300), ((300, 400), 3)])
+def test_aux_first_deconv_matches_class_products(hw, N):
+    """The aux heads' predictions (first layer on the parity kernel, the second as before)
+    and every parameter gradient of their MSE, both paths."""
+    from vnav.policy import GoalNavPolicy
+    torch.manual_seed(12)
+    pol = GoalNavPolicy(3, 4, hw, aux=True)
+    with torch.no_grad():
+        pol.params.add_(torch.randn_like(pol.params) * 0.01)
+    g = torch.Generator(device="cuda").manual_seed(2)
+    img = torch.randint(0, 256, (N, 1) + hw + (3,), dtype=torch.uint8, device="cuda", generator=g)
+    gl = torch.randint(0, 256, (N, 1) + hw + (3,), dtype=torch.uint8, device="cuda", generator=g)
+
+    def run(generic):
+        if generic:
+            os.environ["VN_DGRAD_GENERIC"] = "1"
+        try:
+            pol.params.grad = None
+            preds, _ = pol.forward_deconv(((img, gl), None))
+            sum((p * p).mean() for p in preds).backward()
+            torch.cuda.synchronize()
+            return [p.detach().cpu() for p in preds], pol.net.to_reference(pol.params.grad.clone())
+        finally:
+            os.environ.pop("VN_DGRAD_GENERIC", None)
+
+    (pf, gf), (pg, gg) = run(False), run(True)
+    for a, b in zip(pf, pg):
+        e = float((a - b).abs().max()) / max(float(b.abs().max()), 1e-30)
+        assert e < 1e-5, e
+    bad = {}
+    for k in gg:
+        b = gg[k].numpy().astype(np.float64)
+        if np.abs(b).max() == 0.0:
+            continue
+        e = np.abs(gf[k].numpy() - b).max() / np.abs(b).max()
+        if e > 1e-5:
+            bad[k] = "%.3g" % e
+    assert not bad, bad
