@@ -296,27 +296,34 @@ __device__ __forceinline__ void commit_rows_x6(const f4* r, uint16_t* s, int tid
 }
 
 // Transposing source (wgrad: both operands gathered along the reduction index, fetch_trans
-// slots): the 4 rows of slot i at k = kk are split and written as 16-bit elements of the
-// three k-contiguous planes the MFMA loop reads.
-template <int ROWS, int BK, int LDK>
+// slots): the 4 rows of slot i at k = kk are split and stored k-major — planes [term][k][row]
+// with row stride trans_ld(ROWS) — as one 8-byte run per term (the former row-major image
+// took twelve 2-byte LDS stores per slot); the MFMA loop reads its fragments back with the
+// hardware transpose read (frag_tr below).
+constexpr int trans_ld(int rows) {  // 4 rows of a 32-lane half of ds_read_b64_tr_b16 on distinct banks
+  return (rows * 2) % 128 == 0 ? rows + 32 : rows;
+}
+
+template <int ROWS, int BK>
 __device__ __forceinline__ void commit_trans_x6(const f4* r, uint16_t* s, int tid) {
-  constexpr int R4 = ROWS / 4, T = R4 * BK, NS = (T + 255) / 256, PLANE = ROWS * LDK;
+  constexpr int R4 = ROWS / 4, T = R4 * BK, NS = (T + 255) / 256, LDT = trans_ld(ROWS), PLANE = BK * LDT;
 #pragma unroll
   for (int j = 0; j < NS; ++j) {
     const int i = tid + j * 256;
     if (T % 256 == 0 || i < T) {
       const int kk = (i >> 1) % BK, rq = (i & 1) + 2 * (i / (2 * BK));
+      uint32_t t0[4], t1[4], t2[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         float r1, r2, r3;
-        const uint32_t t0 = bf16_split_bits(r[j][e], r1);
-        const uint32_t t1 = bf16_split_bits(r1, r2);
-        const uint32_t t2 = bf16_split_bits(r2, r3);
-        uint16_t* d = s + (4 * rq + e) * LDK + kk;
-        d[0] = (uint16_t)t0;
-        d[PLANE] = (uint16_t)t1;
-        d[2 * PLANE] = (uint16_t)t2;
+        t0[e] = bf16_split_bits(r[j][e], r1);
+        t1[e] = bf16_split_bits(r1, r2);
+        t2[e] = bf16_split_bits(r2, r3);
       }
+      uint16_t* d = s + kk * LDT + 4 * rq;
+      *reinterpret_cast<uint2*>(d) = uint2{t0[0] | (t0[1] << 16), t0[2] | (t0[3] << 16)};
+      *reinterpret_cast<uint2*>(d + PLANE) = uint2{t1[0] | (t1[1] << 16), t1[2] | (t1[3] << 16)};
+      *reinterpret_cast<uint2*>(d + 2 * PLANE) = uint2{t2[0] | (t2[1] << 16), t2[2] | (t2[3] << 16)};
     }
   }
 }
@@ -324,9 +331,27 @@ __device__ __forceinline__ void commit_trans_x6(const f4* r, uint16_t* s, int ti
 template <int ROWS, int BK, int LDK, class L>
 __device__ __forceinline__ void commit_x6(const f4* r, uint16_t* s, int tid) {
   if constexpr (L::kTrans)
-    commit_trans_x6<ROWS, BK, LDK>(r, s, tid);
+    commit_trans_x6<ROWS, BK>(r, s, tid);
   else
     commit_rows_x6<ROWS, BK, LDK>(r, s, tid);
+}
+
+// The 32x32x16 fragment (row m0 + (l & 31), k = kk + 8(l >> 5) .. +7) of a k-major plane
+// [k][LDT] via two ds_read_b64_tr_b16: in each 16-lane group, lane 4q + p addresses row
+// k0 + q, columns 4p .. 4p+3 of the group's 16 columns, and lane i receives column i of the
+// four k rows (element q = k0 + q). Uniform control flow only (the read gathers across lanes).
+typedef short s16x4_ __attribute__((ext_vector_type(4)));
+template <int LDT>
+__device__ __forceinline__ bf16x8_ frag_tr(const uint16_t* plane, int m0, int kk, int lane) {
+  const int q = (lane >> 2) & 3, p = lane & 3, g = (lane >> 4) & 1, h = lane >> 5;
+  const uint16_t* a = plane + (kk + 8 * h + q) * LDT + m0 + 16 * g + 4 * p;
+  typedef __attribute__((address_space(3))) s16x4_ lds_s16x4;
+  const s16x4_ lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a));
+  const s16x4_ hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a + 4 * LDT));
+  union { s16x4_ s[2]; bf16x8_ v; } u;
+  u.s[0] = lo;
+  u.s[1] = hi;
+  return u.v;
 }
 
 template <int BM, int BN, int BK, int WM, int WN, class FA, class FB, class EP>
@@ -338,8 +363,11 @@ __global__ __launch_bounds__(256) void gemm_x6_kernel(FA fa, FB fb, EP ep, int M
   static_assert(TM >= 1 && TN >= 1, "tile too small for the wave layout");
   constexpr int NA = (FA::template slots<BM, BK>() + 255) / 256;
   constexpr int NB = (FB::template slots<BN, BK>() + 255) / 256;
-  __shared__ __attribute__((aligned(16))) uint16_t As[3 * BM * LDK];
-  __shared__ __attribute__((aligned(16))) uint16_t Bs[3 * BN * LDK];
+  // row-major planes [term][row][LDK], or k-major [term][k][trans_ld(rows)] for a transposing loader
+  constexpr int LTA = trans_ld(BM), LTB = trans_ld(BN);
+  constexpr int PA = FA::kTrans ? BK * LTA : BM * LDK, PB = FB::kTrans ? BK * LTB : BN * LDK;
+  __shared__ __attribute__((aligned(16))) uint16_t As[3 * PA];
+  __shared__ __attribute__((aligned(16))) uint16_t Bs[3 * PB];
   typedef float f16v_ __attribute__((ext_vector_type(16)));
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WM, wn = wave / WM;
@@ -378,11 +406,19 @@ __global__ __launch_bounds__(256) void gemm_x6_kernel(FA fa, FB fb, EP ep, int M
 #pragma unroll
       for (int t = 0; t < 3; ++t) {
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
-          a[t][i] = *reinterpret_cast<const bf16x8_*>(&As[t * BM * LDK + ra + i * 32 * LDK + kk]);
+        for (int i = 0; i < TM; ++i) {
+          if constexpr (FA::kTrans)
+            a[t][i] = frag_tr<LTA>(As + t * PA, wm * TM * 32 + i * 32, kk, lane);
+          else
+            a[t][i] = *reinterpret_cast<const bf16x8_*>(&As[t * PA + ra + i * 32 * LDK + kk]);
+        }
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
-          b[t][j] = *reinterpret_cast<const bf16x8_*>(&Bs[t * BN * LDK + rb + j * 32 * LDK + kk]);
+        for (int j = 0; j < TN; ++j) {
+          if constexpr (FB::kTrans)
+            b[t][j] = frag_tr<LTB>(Bs + t * PB, wn * TN * 32 + j * 32, kk, lane);
+          else
+            b[t][j] = *reinterpret_cast<const bf16x8_*>(&Bs[t * PB + rb + j * 32 * LDK + kk]);
+        }
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
