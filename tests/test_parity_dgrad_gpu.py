@@ -1,7 +1,8 @@
-"""The persistent parity-class kernel (`parity_dgrad_x6_kernel`, vn_policy.hip) against the
-four generic parity-class products it replaced (`VN_DGRAD_GENERIC`, read per call), for its
-two products: conv3's input gradient (k4 s2, 64 -> 2 x 32 channels) and the aux heads'
-first transposed conv (32 -> 48 channels, bias + ReLU). Both compute the same exact
+"""The persistent specialised kernels against the generic products they replaced (selected
+back per call by an environment switch): the parity-class kernel (`parity_dgrad_x6_kernel`,
+`VN_DGRAD_GENERIC`) for conv3's input gradient (k4 s2, 64 -> 2 x 32 channels) and the aux
+heads' first transposed conv (32 -> 48 channels, bias + ReLU), and conv3's weight gradient
+(`conv3_wgrad_x6_kernel`, `VN_WGRAD_GENERIC`). Both compute the same exact
 split-bf16 products in another summation order, so every parameter gradient — conv3's
 input gradient feeds conv2's and conv1's — agrees to rounding (1e-5 of scale). Batch sizes
 cover a partial last work item (84x84 packs 4 images per item) and persistent-grid wraps
@@ -18,7 +19,7 @@ pytestmark = pytest.mark.gpu
 
 def _grads(pol, img, gl, cl, cv, generic):
     if generic:
-        os.environ["VN_DGRAD_GENERIC"] = "1"
+        os.environ[generic] = "1"
     try:
         pol.params.grad = None
         logits, value, _ = pol(((img, gl), None), None, None)
@@ -26,11 +27,16 @@ def _grads(pol, img, gl, cl, cv, generic):
         torch.cuda.synchronize()
         return pol.params.grad.clone()
     finally:
-        os.environ.pop("VN_DGRAD_GENERIC", None)
+        if generic:
+            os.environ.pop(generic, None)
 
 
+@pytest.mark.parametrize("switch", ["VN_DGRAD_GENERIC", "VN_WGRAD_GENERIC"])
 @pytest.mark.parametrize("hw,N", [((84, 84), 37), ((84, 84), 1030), ((174, 174), 5), ((174, 174), 300)])
-def test_conv3_dgrad_kernel_matches_class_products(hw, N):
+def test_conv3_kernels_match_generic_products(hw, N, switch):
+    """VN_DGRAD_GENERIC: conv3's input gradient; VN_WGRAD_GENERIC: conv3's weight and bias
+    gradient (`conv3_wgrad_x6_kernel`, per-workgroup slabs + fixed-order reduce) against the
+    split-K product over the gathered im2col."""
     from vnav.policy import GoalNavPolicy
     torch.manual_seed(11)
     pol = GoalNavPolicy(3, 4, hw)
@@ -41,8 +47,8 @@ def test_conv3_dgrad_kernel_matches_class_products(hw, N):
     gl = torch.randint(0, 256, (N, 1) + hw + (3,), dtype=torch.uint8, device="cuda", generator=g)
     cl = torch.randn((N, 1, 4), device="cuda", generator=g)
     cv = torch.randn((N, 1, 1), device="cuda", generator=g)
-    fast = pol.net.to_reference(_grads(pol, img, gl, cl, cv, generic=False))
-    gen = pol.net.to_reference(_grads(pol, img, gl, cl, cv, generic=True))
+    fast = pol.net.to_reference(_grads(pol, img, gl, cl, cv, generic=None))
+    gen = pol.net.to_reference(_grads(pol, img, gl, cl, cv, generic=switch))
     bad = {}
     for k in gen:
         b = gen[k].numpy().astype(np.float64)
@@ -50,8 +56,10 @@ def test_conv3_dgrad_kernel_matches_class_products(hw, N):
         if e > 1e-5:
             bad[k] = "%.3g" % e
     assert not bad, bad
-    # the kernel ran (not a no-op): conv3's input gradient reaches conv2's weights
-    assert np.abs(fast["shared_base.0.2.weight"].numpy()).max() > 0
+    # the kernels ran (not no-ops): conv3's input gradient reaches conv2's weights, and
+    # conv3's own weight and bias gradients are live
+    for k in ("shared_base.0.2.weight", "conv_base.0.0.weight", "conv_base.0.0.bias"):
+        assert np.abs(fast[k].numpy()).max() > 0, k
 
 
 @pytest.mark.parametrize("hw,N", [((84, 84), 37), ((174, 174), 300), ((300, 400), 3)])
