@@ -916,30 +916,34 @@ inline int launch_parity_dgrad_x6(const float* map, const float* WT, EP ep, int 
   return VN_OK;
 }
 
-// conv3 weight gradient (k4 s2, 2 input groups of 32 -> 64 channels) on bf16 MFMA with split
-// operands: dW[co][tap][g, ci] = sum over images and dZ3 pixels o of dZ3[o][co] *
-// X2[g][2oy + ky][2ox + kx][ci], db[co] = sum of dZ3[o][co]. The generic split-K product
-// gathered each X2 value once per tap (4x) and split it at every use. Here a workgroup
-// (one input group g = blockIdx.y) stages a work item — IMG images' dZ3 maps and their
-// group-g X2 maps — split once into bf16 LDS planes in their natural [pixel][channel] layout,
-// and reads both MFMA operands with ds_read_b64_tr_b16, whose per-lane row addresses do the
-// im2col gather for free: the reduction index k runs over the item's dZ3 pixels (32 per
-// 16x16x32 step), so the A fragment (co x 8 pixels) reads dZ3 rows k and the B fragment
-// ((tap, ci) x 8 pixels) reads the X2 rows under each pixel's tap. Wave w owns taps 2w, 2w+1:
-// 4 co tiles x 4 (tap, ci) tiles = 64 accumulators, kept across all of the workgroup's
-// items; each workgroup writes one partial slab row, reduced in a fixed order by
-// wgrad_reduce_kernel (the bias from the g = 0 workgroups' fp32 column sums of dZ3).
-template <int IH, int IW, int OH, int OW>
-struct Conv3Wg {
-  static constexpr int NPO = OH * OW;                    // dZ3 pixels per image (reduction)
-  static constexpr int NPX = IH * IW;                    // X2 pixels per image and group
-  static constexpr int IMG = NPO >= 32 ? 1 : 32 / NPO;  // images per work item
-  static constexpr int KP = IMG * NPO, KSTEPS = (KP + 31) / 32;
-  static constexpr int PZ = 72, PX = 40;                 // plane row strides (bf16)
-  static constexpr int RZ = KP + 1, RX = IMG * NPX + 1;  // rows + one zero row each
+// Weight gradient of a k4 s2 conv with 32-channel input groups on bf16 MFMA with split
+// operands: dW[co][tap][g, ci] = sum over images and dZ pixels o of dZ[o][co] *
+// X[g][2oy + ky][2ox + kx][ci], db[co] = sum of dZ[o][co] — conv3 (64 <- 2 x 32 channels)
+// and conv2 (32 <- 32, image and goal frames as separate images). The generic split-K
+// product gathered each X value once per tap (4x) and split it at every use; conv2's f32
+// kernel ran its pipe at 85 %. Here a workgroup (input group g = blockIdx.y) stages a work
+// item — IMG images x a band of BR dZ rows, with the 2 BR + 2 X rows under it — split once
+// into bf16 LDS planes in their natural [pixel][channel] layout, and reads both MFMA operands
+// with ds_read_b64_tr_b16, whose per-lane row addresses do the im2col gather for free: the
+// reduction index k runs over the item's dZ pixels (32 per 16x16x32 step), so the A fragment
+// (co x 8 pixels) reads dZ rows k and the B fragment ((tap, ci) x 8 pixels) reads the X rows
+// under each pixel's tap. Wave w owns taps 2w, 2w+1: CO/16 co tiles x 4 (tap, ci) tiles of
+// accumulators, kept across all of the workgroup's items; each workgroup writes one partial
+// slab row, reduced in a fixed order by wgrad_reduce_kernel (the bias from the g = 0
+// workgroups' fp32 column sums of dZ). The next item is prefetched into registers.
+template <int IH_, int IW_, int OH_, int OW_, int CO_, int G_, int BR_, int IMG_>
+struct WgSpec {
+  static constexpr int IH = IH_, IW = IW_, OH = OH_, OW = OW_, CO = CO_, G = G_, BR = BR_, IMG = IMG_;
+  static constexpr int NB = OH / BR;                        // bands per image
+  static constexpr int XR = 2 * BR + 2 < IH ? 2 * BR + 2 : IH;  // X rows under a band
+  static constexpr int NPX = XR * IW;                       // staged X pixels per image
+  static constexpr int KP = IMG * BR * OW, KSTEPS = (KP + 31) / 32;
+  static constexpr int PZ = CO + 8, PX = 40;                // plane row strides (bf16)
+  static constexpr int RZ = KP + 1, RX = IMG * NPX + 1;     // rows + one zero row each
   static constexpr size_t LDS = (size_t)3 * (RZ * PZ + RX * PX) * 2;
-  static constexpr bool fits = LDS <= 160 * 1024;
-  static constexpr int SLAB_N = 1025;                    // 1024 weight columns + the bias
+  static constexpr bool fits = OH % BR == 0 && LDS <= 160 * 1024;
+  static constexpr int SLAB_N = 16 * G * 32 + 1;            // weight columns + the bias
+  static constexpr int MT = CO / 16, C4 = CO / 4;
 };
 
 __device__ __forceinline__ s16x4_ lds_tr(const uint16_t* p) {
@@ -947,22 +951,22 @@ __device__ __forceinline__ s16x4_ lds_tr(const uint16_t* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
 }
 
-template <int IH, int IW, int OH, int OW>
-__global__ __launch_bounds__(512, 1) void conv3_wgrad_x6_kernel(const float* __restrict__ dZ3,
-                                                             const float* __restrict__ X2, float* __restrict__ slab,
-                                                             int n) {
-  using S = Conv3Wg<IH, IW, OH, OW>;
-  constexpr int NPO = S::NPO, NPX = S::NPX, IMG = S::IMG, KP = S::KP, PZ = S::PZ, PX = S::PX;
-  constexpr int PLZ = S::RZ * PZ, PLX = S::RX * PX, NT = 512;
-  constexpr int NZ = (KP * 16 + NT - 1) / NT, NX = (IMG * NPX * 8 + NT - 1) / NT;
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem_wg3[];
-  uint16_t* zs = reinterpret_cast<uint16_t*>(smem_wg3);
+template <class S>
+__global__ __launch_bounds__(512, 1) void conv_wgrad_x6_kernel(const float* __restrict__ dZ, const float* __restrict__ X,
+                                                            float* __restrict__ slab, int n) {
+  constexpr int IH = S::IH, IW = S::IW, OH = S::OH, OW = S::OW, CO = S::CO, G = S::G, BR = S::BR, IMG = S::IMG;
+  constexpr int NPX = S::NPX, KP = S::KP, PZ = S::PZ, PX = S::PX, MT = S::MT, C4 = S::C4;
+  constexpr int PLZ = S::RZ * PZ, PLX = S::RX * PX, NT = 512, BP = BR * OW;
+  constexpr int NZ = (KP * C4 + NT - 1) / NT, NX = (IMG * NPX * 8 + NT - 1) / NT;
+  static_assert(NT % C4 == 0, "a thread's dZ channel quad is fixed");
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem_wg[];
+  uint16_t* zs = reinterpret_cast<uint16_t*>(smem_wg);
   uint16_t* xs = zs + 3 * PLZ;
-  float* red = reinterpret_cast<float*>(smem_wg3);  // bias reduction, after the last item
+  float* red = reinterpret_cast<float*>(smem_wg);  // bias reduction, after the last item
   const int g = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int G = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int Gq = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
   for (int i = tid; i < 3 * (PZ + PX) / 2; i += NT) {  // zero rows
     const int pl = i / ((PZ + PX) / 2), e = i - pl * ((PZ + PX) / 2);
     if (e < PZ / 2)
@@ -970,73 +974,71 @@ __global__ __launch_bounds__(512, 1) void conv3_wgrad_x6_kernel(const float* __r
     else
       reinterpret_cast<uint32_t*>(xs + pl * PLX + IMG * NPX * PX)[e - PZ / 2] = 0u;
   }
-  f4 acc[4][4];
+  f4 acc[MT][4];
 #pragma unroll
-  for (int mt = 0; mt < 4; ++mt)
+  for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = f4zero();
-  f4 dbs = f4zero();  // fp32 column sums of dZ3 (channels 4 (tid & 15) .. +3), g == 0 only
-  const int items = (n + IMG - 1) / IMG;
+  f4 dbs = f4zero();  // fp32 column sums of dZ (channels 4 (tid % C4) .. +3), g == 0 only
+  const int items = (n + IMG - 1) / IMG * S::NB;
   f4 zr[NZ], xr[NX];
-  auto load = [&](int it) {  // the item's dZ3 rows and its images' group-g X2 maps, into registers
-    const int img0 = it * IMG;
-    const int64_t zr0 = (int64_t)img0 * NPO, zend = (int64_t)n * NPO;
+  auto load = [&](int it) {  // the item's dZ band rows and the X rows under them, into registers
+    const int img0 = (it / S::NB) * IMG, band = it - (it / S::NB) * S::NB;
 #pragma unroll
     for (int j = 0; j < NZ; ++j) {
       const int i = tid + j * NT;
-      zr[j] = (i < KP * 16 && zr0 + (i >> 4) < zend) ? reinterpret_cast<const f4*>(dZ3)[(zr0 + (i >> 4)) * 16 + (i & 15)]
-                                                     : f4zero();
+      const int k = i / C4, im = k / BP;
+      zr[j] = (i < KP * C4 && img0 + im < n)
+                  ? reinterpret_cast<const f4*>(dZ)[(((int64_t)(img0 + im) * OH + band * BR) * OW + (k - im * BP)) * C4 + i % C4]
+                  : f4zero();
     }
 #pragma unroll
     for (int j = 0; j < NX; ++j) {
       const int i = tid + j * NT;
       const int r = i >> 3, im = r / NPX;
       xr[j] = (i < IMG * NPX * 8 && img0 + im < n)
-                  ? reinterpret_cast<const f4*>(X2)[(((int64_t)(img0 + im) * 2 + g) * NPX + (r - im * NPX)) * 8 + (i & 7)]
+                  ? reinterpret_cast<const f4*>(X)[((((int64_t)(img0 + im) * G + g) * IH + 2 * band * BR) * IW + (r - im * NPX)) * 8 + (i & 7)]
                   : f4zero();
     }
   };
   if ((int)blockIdx.x < items) load(blockIdx.x);
   for (int it = blockIdx.x; it < items; it += gridDim.x) {
-    {  // stage: split into the planes
 #pragma unroll
-      for (int j = 0; j < NZ; ++j) {
-        const int i = tid + j * NT;
-        if (i < KP * 16) {
-          if (g == 0) dbs += zr[j];
-          uint2 t0, t1, t2;
-          split3_pack(zr[j], t0, t1, t2);
-          uint16_t* d = zs + (i >> 4) * PZ + 4 * (i & 15);
-          *reinterpret_cast<uint2*>(d) = t0;
-          *reinterpret_cast<uint2*>(d + PLZ) = t1;
-          *reinterpret_cast<uint2*>(d + 2 * PLZ) = t2;
-        }
+    for (int j = 0; j < NZ; ++j) {  // split into the planes
+      const int i = tid + j * NT;
+      if (i < KP * C4) {
+        if (g == 0) dbs += zr[j];
+        uint2 t0, t1, t2;
+        split3_pack(zr[j], t0, t1, t2);
+        uint16_t* d = zs + (i / C4) * PZ + 4 * (i % C4);
+        *reinterpret_cast<uint2*>(d) = t0;
+        *reinterpret_cast<uint2*>(d + PLZ) = t1;
+        *reinterpret_cast<uint2*>(d + 2 * PLZ) = t2;
       }
+    }
 #pragma unroll
-      for (int j = 0; j < NX; ++j) {
-        const int i = tid + j * NT;
-        if (i < IMG * NPX * 8) {
-          uint2 t0, t1, t2;
-          split3_pack(xr[j], t0, t1, t2);
-          uint16_t* d = xs + (i >> 3) * PX + 4 * (i & 7);
-          *reinterpret_cast<uint2*>(d) = t0;
-          *reinterpret_cast<uint2*>(d + PLX) = t1;
-          *reinterpret_cast<uint2*>(d + 2 * PLX) = t2;
-        }
+    for (int j = 0; j < NX; ++j) {
+      const int i = tid + j * NT;
+      if (i < IMG * NPX * 8) {
+        uint2 t0, t1, t2;
+        split3_pack(xr[j], t0, t1, t2);
+        uint16_t* d = xs + (i >> 3) * PX + 4 * (i & 7);
+        *reinterpret_cast<uint2*>(d) = t0;
+        *reinterpret_cast<uint2*>(d + PLX) = t1;
+        *reinterpret_cast<uint2*>(d + 2 * PLX) = t2;
       }
     }
     __syncthreads();
     if (it + (int)gridDim.x < items) load(it + gridDim.x);  // next item's loads under this one's MFMAs
-#pragma unroll 1
-    for (int ks = 0; ks < S::KSTEPS; ++ks) {
-      // this lane's rows of the two tr reads (k = 32 ks + 8G + 4s + q): dZ3 row k and, per tap
-      // of the wave, the X2 row under it (the zero rows past the item)
+    auto kstep = [&](int ks) {
+      // this lane's rows of the two tr reads (k = 32 ks + 8 Gq + 4s + q): dZ row k and, per tap
+      // of the wave, the X row under it (the zero rows past the item)
       int zrow[2], xrow[2][2];
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const int k = ks * 32 + 8 * G + 4 * s + q;
-        const int im = k / NPO, o = k - (k / NPO) * NPO;
-        const int oy = o / OW, ox = o - (o / OW) * OW;
+        const int k = ks * 32 + 8 * Gq + 4 * s + q;
+        const int im = k / BP, o = k - (k / BP) * BP;
+        const int oy = o / OW, ox = o - (o / OW) * OW;  // oy within the band
         const bool ok = k < KP;
         zrow[s] = (ok ? k : KP) * PZ;
 #pragma unroll
@@ -1045,12 +1047,12 @@ __global__ __launch_bounds__(512, 1) void conv3_wgrad_x6_kernel(const float* __r
           xrow[s][tt] = (ok ? im * NPX + (2 * oy + ky) * IW + 2 * ox + kx : IMG * NPX) * PX;
         }
       }
-      bf16x8_ a[3][4], b[3][4];
+      bf16x8_ a[3][MT], b[3][4];
       union U { s16x4_ s[2]; bf16x8_ v; };
 #pragma unroll
       for (int t = 0; t < 3; ++t) {
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {  // A: co 16 mt + (lane & 15) x pixels
+        for (int mt = 0; mt < MT; ++mt) {  // A: co 16 mt + (lane & 15) x pixels
           U u;
           u.s[0] = lds_tr(zs + t * PLZ + zrow[0] + 16 * mt + 4 * p);
           u.s[1] = lds_tr(zs + t * PLZ + zrow[1] + 16 * mt + 4 * p);
@@ -1065,7 +1067,7 @@ __global__ __launch_bounds__(512, 1) void conv3_wgrad_x6_kernel(const float* __r
         }
       }
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
+      for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) {  // small terms first
           f4 c = acc[mt][nt];
@@ -1077,46 +1079,62 @@ __global__ __launch_bounds__(512, 1) void conv3_wgrad_x6_kernel(const float* __r
           c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][mt], b[0][nt], c, 0, 0, 0);
           acc[mt][nt] = c;
         }
+    };
+    // unrolled (the next step's fragment reads scheduled under this step's MFMAs) where the
+    // registers allow: conv2's 2 co tiles; conv3's 4 would spill
+    if constexpr (MT <= 2) {
+#pragma unroll
+      for (int ks = 0; ks < S::KSTEPS; ++ks) kstep(ks);
+    } else {
+#pragma unroll 1
+      for (int ks = 0; ks < S::KSTEPS; ++ks) kstep(ks);
     }
     __syncthreads();
   }
   // the workgroup's partial: lane holds column (lane & 15) of each (tap, ci) tile and rows
   // (co) 4 (lane >> 4) .. +3 of each co tile
-  float* row = slab + (int64_t)blockIdx.x * 64 * S::SLAB_N;
+  float* row = slab + (int64_t)blockIdx.x * CO * S::SLAB_N;
 #pragma unroll
-  for (int mt = 0; mt < 4; ++mt)
+  for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
-      const int col = (2 * wave + (nt >> 1)) * 64 + g * 32 + 16 * (nt & 1) + (lane & 15);
+      const int col = (2 * wave + (nt >> 1)) * (G * 32) + g * 32 + 16 * (nt & 1) + (lane & 15);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) row[(int64_t)(16 * mt + 4 * G + r) * S::SLAB_N + col] = acc[mt][nt][r];
+      for (int r = 0; r < 4; ++r) row[(int64_t)(16 * mt + 4 * Gq + r) * S::SLAB_N + col] = acc[mt][nt][r];
     }
-  if (g == 0) {  // bias partial: the 32 threads of each channel quad, summed in a fixed order
+  if (g == 0) {  // bias partial: the threads of each channel quad, summed in a fixed order
     *reinterpret_cast<f4*>(red + 4 * tid) = dbs;
     __syncthreads();
-    if (tid < 64) {
+    if (tid < CO) {
       const int c4 = tid >> 2, e = tid & 3;
       float s = 0.0f;
-      for (int k = 0; k < NT / 16; ++k) s += red[4 * (c4 + 16 * k) + e];
-      row[(int64_t)(4 * c4 + e) * S::SLAB_N + 1024] = s;
+      for (int k = 0; k < NT / C4; ++k) s += red[4 * (c4 + C4 * k) + e];
+      row[(int64_t)(4 * c4 + e) * S::SLAB_N + S::SLAB_N - 1] = s;
     }
   }
 }
 
-template <int IH, int IW, int OH, int OW>
-inline int launch_conv3_wgrad_x6(const float* dz3, const float* X2, int n, float* slab, int64_t slab_cap, float* dW,
-                                 float* db, hipStream_t st) {
-  using S = Conv3Wg<IH, IW, OH, OW>;
-  const void* kfn = (const void*)conv3_wgrad_x6_kernel<IH, IW, OH, OW>;
+template <class S>
+inline int launch_conv_wgrad_x6(const float* dz, const float* X, int n, float* slab, int64_t slab_cap, float* dW,
+                                float* db, hipStream_t st) {
+  const void* kfn = (const void*)conv_wgrad_x6_kernel<S>;
   VN_HIP(ensure_dyn_lds(kfn, S::LDS));
-  const int items = (n + S::IMG - 1) / S::IMG;
-  int bx = std::max(1, std::min(items, resident_blocks(kfn, 512, S::LDS) / 2));
-  bx = (int)std::min<int64_t>(bx, slab_cap / (64 * S::SLAB_N));
-  hipLaunchKernelGGL((conv3_wgrad_x6_kernel<IH, IW, OH, OW>), dim3(bx, 2), dim3(512), S::LDS, st, dz3, X2, slab, n);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((64 * S::SLAB_N + 255) / 256), dim3(256), 0, st, slab, bx, 64,
-                     S::SLAB_N, 1024, dW, db);
+  const int items = (n + S::IMG - 1) / S::IMG * S::NB;
+  int bx = std::max(1, std::min(items, resident_blocks(kfn, 512, S::LDS) / S::G));
+  bx = (int)std::min<int64_t>(bx, slab_cap / ((int64_t)S::CO * S::SLAB_N));
+  hipLaunchKernelGGL((conv_wgrad_x6_kernel<S>), dim3(bx, S::G), dim3(512), S::LDS, st, dz, X, slab, n);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((S::CO * S::SLAB_N + 255) / 256), dim3(256), 0, st, slab, bx, S::CO,
+                     S::SLAB_N, S::SLAB_N - 1, dW, db);
   return VN_OK;
 }
+
+// conv3: whole 9x9 / 3x3 dZ3 maps, images packed to >= 32 reduction pixels per item
+template <int IH, int IW, int OH, int OW>
+using Conv3Wg = WgSpec<IH, IW, OH, OW, 64, 2, OH, (OH * OW >= 32 ? 1 : 32 / (OH * OW))>;
+// conv2: frames (image and goal) as images; bands of 4 dZ2 rows at 174x174 (X1 rows 10 x 42),
+// whole maps at 84x84
+template <int IH, int IW, int OH, int OW>
+using Conv2Wg = WgSpec<IH, IW, OH, OW, 32, 1, (OH % 4 == 0 && OH > 9 ? 4 : OH), 1>;
 
 template <int COUT, int CIN, int H, int W, int OH, int OW, int PY, int PX>
 inline void dgrad_class_groups(const float* dz, const float* WT, float* out, const float* X, int nimg, int G,
@@ -1379,8 +1397,7 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
     using Wg = Conv3Wg<G::OH2, G::OW2, G::OH3, G::OW3>;
     if (Wg::fits && !getenv("VN_WGRAD_GENERIC")) {  // read per call (A/B and parity checks)
       if constexpr (Wg::fits) {
-        const int rc = launch_conv3_wgrad_x6<G::OH2, G::OW2, G::OH3, G::OW3>(w.dz3, a.X[1], n, w.slab, w.slab_cap,
-                                                                             Gr + L.l[2].w, Gr + L.l[2].b, st);
+        const int rc = launch_conv_wgrad_x6<Wg>(w.dz3, a.X[1], n, w.slab, w.slab_cap, Gr + L.l[2].w, Gr + L.l[2].b, st);
         if (rc != VN_OK) return rc;
       }
     } else {
@@ -1395,7 +1412,14 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
     using Bd2 = Conv2WgBand<G::OH1, G::OW1, G::OH2, G::OW2>;
     const int blocks = std::min(frames * Bd2::NB, kConv2WgradBlocks);
     constexpr size_t lds = conv2_wgrad_lds<G::OH1, G::OW1, G::OH2, G::OW2>();
-    if constexpr (lds <= 80 * 1024) {  // two workgroups per CU (bands of output rows)
+    using Wg2 = Conv2Wg<G::OH1, G::OW1, G::OH2, G::OW2>;
+    if (Wg2::fits && !getenv("VN_WGRAD_GENERIC")) {  // x6 form; read per call (A/B and parity checks)
+      if constexpr (Wg2::fits) {
+        const int rc = launch_conv_wgrad_x6<Wg2>(w.dz2, a.X[0], frames, w.slab, w.slab_cap, Gr + L.l[1].w, Gr + L.l[1].b,
+                                                 st);
+        if (rc != VN_OK) return rc;
+      }
+    } else if constexpr (lds <= 80 * 1024) {  // f32 MFMA, two workgroups per CU (bands of output rows)
       VN_HIP(ensure_dyn_lds((const void*)conv2_wgrad_kernel<G::OH1, G::OW1, G::OH2, G::OW2>, lds));  // > 64 KiB dynamic LDS: opt-in
       float* bias_slab = w.slab + (int64_t)blocks * 32 * 512;
       hipLaunchKernelGGL((conv2_wgrad_kernel<G::OH1, G::OW1, G::OH2, G::OW2>), dim3(blocks), dim3(256), lds, st,
