@@ -931,18 +931,22 @@ inline int launch_parity_dgrad_x6(const float* map, const float* WT, EP ep, int 
 // accumulators, kept across all of the workgroup's items; each workgroup writes one partial
 // slab row, reduced in a fixed order by wgrad_reduce_kernel (the bias from the g = 0
 // workgroups' fp32 column sums of dZ). The next item is prefetched into registers.
-template <int IH_, int IW_, int OH_, int OW_, int CO_, int G_, int BR_, int IMG_>
+template <int IH_, int IW_, int OH_, int OW_, int CO_, int G_, int BR_, int IMG_, int CX_ = 32, bool BIAS_ = true>
 struct WgSpec {
   static constexpr int IH = IH_, IW = IW_, OH = OH_, OW = OW_, CO = CO_, G = G_, BR = BR_, IMG = IMG_;
+  static constexpr int CX = CX_;        // X channels per input group (32, or the aux heads' 48)
+  static constexpr bool BIAS = BIAS_;   // a bias column (the aux heads take theirs from column sums)
+  static constexpr int NTW = CX / 16;   // (tap, channel) tiles per tap
   static constexpr int NB = OH / BR;                        // bands per image
   static constexpr int XR = 2 * BR + 2 < IH ? 2 * BR + 2 : IH;  // X rows under a band
   static constexpr int NPX = XR * IW;                       // staged X pixels per image
   static constexpr int KP = IMG * BR * OW, KSTEPS = (KP + 31) / 32;
-  static constexpr int PZ = CO + 8, PX = 40;                // plane row strides (bf16)
+  static constexpr int PZ = CO + 8, PX = CX + 8;            // plane row strides (bf16)
   static constexpr int RZ = KP + 1, RX = IMG * NPX + 1;     // rows + one zero row each
   static constexpr size_t LDS = (size_t)3 * (RZ * PZ + RX * PX) * 2;
   static constexpr bool fits = OH % BR == 0 && LDS <= 160 * 1024;
-  static constexpr int SLAB_N = 16 * G * 32 + 1;            // weight columns + the bias
+  static constexpr int KW = 16 * G * CX;                     // weight columns
+  static constexpr int SLAB_N = KW + (BIAS ? 1 : 0);          // + the bias
   static constexpr int MT = CO / 16, C4 = CO / 4;
 };
 
@@ -956,8 +960,9 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_x6_kernel(const float* __re
                                                             float* __restrict__ slab, int n) {
   constexpr int IH = S::IH, IW = S::IW, OH = S::OH, OW = S::OW, CO = S::CO, G = S::G, BR = S::BR, IMG = S::IMG;
   constexpr int NPX = S::NPX, KP = S::KP, PZ = S::PZ, PX = S::PX, MT = S::MT, C4 = S::C4;
+  constexpr int CX = S::CX, X4 = CX / 4, NTW = S::NTW, NTT = 2 * NTW;
   constexpr int PLZ = S::RZ * PZ, PLX = S::RX * PX, NT = 512, BP = BR * OW;
-  constexpr int NZ = (KP * C4 + NT - 1) / NT, NX = (IMG * NPX * 8 + NT - 1) / NT;
+  constexpr int NZ = (KP * C4 + NT - 1) / NT, NX = (IMG * NPX * X4 + NT - 1) / NT;
   static_assert(NT % C4 == 0, "a thread's dZ channel quad is fixed");
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_wg[];
   uint16_t* zs = reinterpret_cast<uint16_t*>(smem_wg);
@@ -974,11 +979,11 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_x6_kernel(const float* __re
     else
       reinterpret_cast<uint32_t*>(xs + pl * PLX + IMG * NPX * PX)[e - PZ / 2] = 0u;
   }
-  f4 acc[MT][4];
+  f4 acc[MT][NTT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = f4zero();
+    for (int nt = 0; nt < NTT; ++nt) acc[mt][nt] = f4zero();
   f4 dbs = f4zero();  // fp32 column sums of dZ (channels 4 (tid % C4) .. +3), g == 0 only
   const int items = (n + IMG - 1) / IMG * S::NB;
   f4 zr[NZ], xr[NX];
@@ -995,9 +1000,9 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_x6_kernel(const float* __re
 #pragma unroll
     for (int j = 0; j < NX; ++j) {
       const int i = tid + j * NT;
-      const int r = i >> 3, im = r / NPX;
-      xr[j] = (i < IMG * NPX * 8 && img0 + im < n)
-                  ? reinterpret_cast<const f4*>(X)[((((int64_t)(img0 + im) * G + g) * IH + 2 * band * BR) * IW + (r - im * NPX)) * 8 + (i & 7)]
+      const int r = i / X4, im = r / NPX;
+      xr[j] = (i < IMG * NPX * X4 && img0 + im < n)
+                  ? reinterpret_cast<const f4*>(X)[((((int64_t)(img0 + im) * G + g) * IH + 2 * band * BR) * IW + (r - im * NPX)) * X4 + i % X4]
                   : f4zero();
     }
   };
@@ -1007,7 +1012,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_x6_kernel(const float* __re
     for (int j = 0; j < NZ; ++j) {  // split into the planes
       const int i = tid + j * NT;
       if (i < KP * C4) {
-        if (g == 0) dbs += zr[j];
+        if (S::BIAS && g == 0) dbs += zr[j];
         uint2 t0, t1, t2;
         split3_pack(zr[j], t0, t1, t2);
         uint16_t* d = zs + (i / C4) * PZ + 4 * (i % C4);
@@ -1019,10 +1024,10 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_x6_kernel(const float* __re
 #pragma unroll
     for (int j = 0; j < NX; ++j) {
       const int i = tid + j * NT;
-      if (i < IMG * NPX * 8) {
+      if (i < IMG * NPX * X4) {
         uint2 t0, t1, t2;
         split3_pack(xr[j], t0, t1, t2);
-        uint16_t* d = xs + (i >> 3) * PX + 4 * (i & 7);
+        uint16_t* d = xs + (i / X4) * PX + 4 * (i % X4);
         *reinterpret_cast<uint2*>(d) = t0;
         *reinterpret_cast<uint2*>(d + PLX) = t1;
         *reinterpret_cast<uint2*>(d + 2 * PLX) = t2;
@@ -1047,7 +1052,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_x6_kernel(const float* __re
           xrow[s][tt] = (ok ? im * NPX + (2 * oy + ky) * IW + 2 * ox + kx : IMG * NPX) * PX;
         }
       }
-      bf16x8_ a[3][MT], b[3][4];
+      bf16x8_ a[3][MT], b[3][NTT];
       union U { s16x4_ s[2]; bf16x8_ v; };
 #pragma unroll
       for (int t = 0; t < 3; ++t) {
@@ -1059,17 +1064,17 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_x6_kernel(const float* __re
           a[t][mt] = u.v;
         }
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {  // B: (tap 2w + nt / 2, ci 16 (nt & 1) + (lane & 15)) x pixels
+        for (int nt = 0; nt < NTT; ++nt) {  // B: (tap 2w + nt / NTW, channel 16 (nt % NTW) + (lane & 15)) x pixels
           U u;
-          u.s[0] = lds_tr(xs + t * PLX + xrow[0][nt >> 1] + 16 * (nt & 1) + 4 * p);
-          u.s[1] = lds_tr(xs + t * PLX + xrow[1][nt >> 1] + 16 * (nt & 1) + 4 * p);
+          u.s[0] = lds_tr(xs + t * PLX + xrow[0][nt / NTW] + 16 * (nt % NTW) + 4 * p);
+          u.s[1] = lds_tr(xs + t * PLX + xrow[1][nt / NTW] + 16 * (nt % NTW) + 4 * p);
           b[t][nt] = u.v;
         }
       }
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {  // small terms first
+        for (int nt = 0; nt < NTT; ++nt) {  // small terms first
           f4 c = acc[mt][nt];
           c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2][mt], b[0][nt], c, 0, 0, 0);
           c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][mt], b[2][nt], c, 0, 0, 0);
@@ -1081,8 +1086,8 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_x6_kernel(const float* __re
         }
     };
     // unrolled (the next step's fragment reads scheduled under this step's MFMAs) where the
-    // registers allow: conv2's 2 co tiles; conv3's 4 would spill
-    if constexpr (MT <= 2) {
+    // registers allow: conv2's 2 x 4 tiles; conv3's 4 x 4 and the aux heads' 2 x 6 would spill
+    if constexpr (MT * NTT <= 8) {
 #pragma unroll
       for (int ks = 0; ks < S::KSTEPS; ++ks) kstep(ks);
     } else {
@@ -1097,12 +1102,12 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_x6_kernel(const float* __re
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      const int col = (2 * wave + (nt >> 1)) * (G * 32) + g * 32 + 16 * (nt & 1) + (lane & 15);
+    for (int nt = 0; nt < NTT; ++nt) {
+      const int col = (2 * wave + nt / NTW) * (G * CX) + g * CX + 16 * (nt % NTW) + (lane & 15);
 #pragma unroll
       for (int r = 0; r < 4; ++r) row[(int64_t)(16 * mt + 4 * Gq + r) * S::SLAB_N + col] = acc[mt][nt][r];
     }
-  if (g == 0) {  // bias partial: the threads of each channel quad, summed in a fixed order
+  if (S::BIAS && g == 0) {  // bias partial: the threads of each channel quad, summed in a fixed order
     *reinterpret_cast<f4*>(red + 4 * tid) = dbs;
     __syncthreads();
     if (tid < CO) {
@@ -1124,7 +1129,7 @@ inline int launch_conv_wgrad_x6(const float* dz, const float* X, int n, float* s
   bx = (int)std::min<int64_t>(bx, slab_cap / ((int64_t)S::CO * S::SLAB_N));
   hipLaunchKernelGGL((conv_wgrad_x6_kernel<S>), dim3(bx, S::G), dim3(512), S::LDS, st, dz, X, slab, n);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((S::CO * S::SLAB_N + 255) / 256), dim3(256), 0, st, slab, bx, S::CO,
-                     S::SLAB_N, S::SLAB_N - 1, dW, db);
+                     S::SLAB_N, S::KW, dW, S::BIAS ? db : nullptr);
   return VN_OK;
 }
 
@@ -1919,9 +1924,19 @@ int aux_backward_impl(const PolicyLayout& L, const float* P, const float* X4, in
   } else {
     aux_backward_layer2_gemm<AH, AW, PH, PW>(L, P, n, A1, dP, Gr, w, st);
   }
-  // first layer: dW1 = X4^T x im2col(dA1); dX4 = conv(dA1, W1)
-  launch_wgrad6<32, 128, 1, 4>(X4, 32, 32, Im2colT<Im1>{Im1{A1, P0}, 16 * kAuxC1}, 16 * kAuxC1, P0, w.slab,
-                               slab_floats(L), Gr + L.aw1, nullptr, st);
+  // first layer: dW1 = X4^T x im2col(dA1); dX4 = conv(dA1, W1). The weight gradient is a
+  // stride-2 k4 weight gradient with X4 as the reduced map and dA1 (48 channels) under it:
+  // dW1[ci][tap][co] = sum X4[iy][ix][ci] dA1[2iy + ky][2ix + kx][co] (no bias column)
+  using Wa = WgSpec<AH, AW, IH, IW, 32, 1, IH, (IH * IW >= 32 ? 1 : 32 / (IH * IW)), kAuxC1, false>;
+  if (Wa::fits && !getenv("VN_WGRAD_GENERIC")) {  // read per call (A/B and parity checks)
+    if constexpr (Wa::fits) {
+      const int rc = launch_conv_wgrad_x6<Wa>(X4, A1, n, w.slab, slab_floats(L), Gr + L.aw1, nullptr, st);
+      if (rc != VN_OK) return rc;
+    }
+  } else {
+    launch_wgrad6<32, 128, 1, 4>(X4, 32, 32, Im2colT<Im1>{Im1{A1, P0}, 16 * kAuxC1}, 16 * kAuxC1, P0, w.slab,
+                                 slab_floats(L), Gr + L.aw1, nullptr, st);
+  }
   {
     DenseRows fb{P + L.aw1, 16 * kAuxC1, 32};
     EpiStore ep{dX4, 32};

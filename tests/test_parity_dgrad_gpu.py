@@ -62,10 +62,13 @@ def test_conv3_kernels_match_generic_products(hw, N, switch):
         assert np.abs(fast[k].numpy()).max() > 0, k
 
 
+@pytest.mark.parametrize("switch", ["VN_DGRAD_GENERIC", "VN_WGRAD_GENERIC"])
 @pytest.mark.parametrize("hw,N", [((84, 84), 37), ((174, 174), 300), ((300, 400), 3)])
-def test_aux_first_deconv_matches_class_products(hw, N):
-    """The aux heads' predictions (first layer on the parity kernel, the second as before)
-    and every parameter gradient of their MSE, both paths."""
+def test_aux_first_layer_matches_generic_products(hw, N, switch):
+    """The aux heads' predictions and every parameter gradient of their MSE, both paths:
+    VN_DGRAD_GENERIC for the first transposed conv's forward (parity kernel),
+    VN_WGRAD_GENERIC for its weight gradient (`conv_wgrad_x6_kernel` with X4 as the reduced
+    map and the 48-channel dA1 under it, no bias column)."""
     from vnav.policy import GoalNavPolicy
     torch.manual_seed(12)
     pol = GoalNavPolicy(3, 4, hw, aux=True)
@@ -77,7 +80,7 @@ def test_aux_first_deconv_matches_class_products(hw, N):
 
     def run(generic):
         if generic:
-            os.environ["VN_DGRAD_GENERIC"] = "1"
+            os.environ[switch] = "1"
         try:
             pol.params.grad = None
             preds, _ = pol.forward_deconv(((img, gl), None))
@@ -85,7 +88,7 @@ def test_aux_first_deconv_matches_class_products(hw, N):
             torch.cuda.synchronize()
             return [p.detach().cpu() for p in preds], pol.net.to_reference(pol.params.grad.clone())
         finally:
-            os.environ.pop("VN_DGRAD_GENERIC", None)
+            os.environ.pop(switch, None)
 
     (pf, gf), (pg, gg) = run(False), run(True)
     for a, b in zip(pf, pg):
