@@ -44,12 +44,15 @@ def table(h, E, T):
         (r"EpiBias2", E * 2048 * xcat * 2, (E * xcat + 2048 * xcat + E * 2048) * f4, "x6"),
         (r"conv1_wgrad_x3_kernel<", F * p1 * 32 * 147 * 2, F * (fb + p1 * 32 * f4), "x3"),
         (r"conv2_wgrad_kernel", F * p2 * 32 * 512 * 2, F * (p1 + p2) * 32 * f4, "f32"),
+        (r"WgSpec<%d, %d, %d, %d, 32, 1," % (o1, o1, o2, o2), F * p2 * 32 * 512 * 2, F * (p1 + p2) * 32 * f4, "x6"),
         (r"conv2_dgrad_x6_kernel", F * p2 * 32 * 512 * 2, F * (p2 * 32 * f4 + p1 * 32 * f4 + p1 * 4), "x6"),
         (r"RowsOnes, EpiSlab", N * 2048 * (xcat + 1) * 2, N * (2048 + xcat) * f4, "x6"),
         (r"EpiLstmDh", E * 512 * 2048 * 2, (E * 2048 + 2048 * 512 + E * 512) * f4, "x6"),
         (r"Im2colT<NhwcIm2col<32, 4, 4, 2, %d, %d, %d, %d, 2> >, EpiSlab" % (o2, o2, o3, o3),
          N * p3 * 64 * 1024 * 2, N * (2 * p2 * 32 + p3 * 64) * f4, "x6"),
+        (r"WgSpec<%d, %d, %d, %d, 64, 2," % (o2, o2, o3, o3), N * p3 * 64 * 1024 * 2, N * (2 * p2 * 32 + p3 * 64) * f4, "x6"),
         (r"DgradA<64, 4, 2, %d, %d" % (o3, o3), N * p3 * 64 * 1024 * 2 / 4, None, "x6"),  # per class: 1/4 of the total
+        (r"ParityDg<%d, %d, \d+, \d+, 64, 64, 2>" % (o3, o3), N * p3 * 64 * 1024 * 2, N * (p3 * 64 + 2 * 2 * p2 * 32) * f4, "x6"),
         (r"128, 128, 32, 2, 2, DenseRows, DenseRows, EpiMask>", N * 512 * 2048 * 2, (N * 2048 + N * 512 * 2) * f4, "x6"),
     ]
 
