@@ -1125,10 +1125,21 @@ inline int launch_conv_wgrad_x6(const float* dz, const float* X, int n, float* s
   const void* kfn = (const void*)conv_wgrad_x6_kernel<S>;
   VN_HIP(ensure_dyn_lds(kfn, S::LDS));
   const int items = (n + S::IMG - 1) / S::IMG * S::NB;
+  constexpr int kParts = 32;
+  const int64_t nel = (int64_t)S::CO * S::SLAB_N;
   int bx = std::max(1, std::min(items, resident_blocks(kfn, 512, S::LDS) / S::G));
-  bx = (int)std::min<int64_t>(bx, slab_cap / ((int64_t)S::CO * S::SLAB_N));
+  bx = (int)std::max<int64_t>(1, std::min<int64_t>(bx, slab_cap / nel - kParts));
   hipLaunchKernelGGL((conv_wgrad_x6_kernel<S>), dim3(bx, S::G), dim3(512), S::LDS, st, dz, X, slab, n);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((S::CO * S::SLAB_N + 255) / 256), dim3(256), 0, st, slab, bx, S::CO,
+  const float* src = slab;
+  int nsrc = bx;
+  if (bx >= 2 * kParts) {  // two-stage fixed-order reduce: one pass over hundreds of slabs is latency-bound
+    float* part = slab + (int64_t)bx * nel;
+    hipLaunchKernelGGL(slab_partial_kernel, dim3((unsigned)((nel + 255) / 256), kParts), dim3(256), 0, st, slab, bx, nel,
+                       part);
+    src = part;
+    nsrc = kParts;
+  }
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((nel + 255) / 256)), dim3(256), 0, st, src, nsrc, S::CO,
                      S::SLAB_N, S::KW, dW, S::BIAS ? db : nullptr);
   return VN_OK;
 }
