@@ -941,7 +941,12 @@ struct WgSpec {
   static constexpr int XR = 2 * BR + 2 < IH ? 2 * BR + 2 : IH;  // X rows under a band
   static constexpr int NPX = XR * IW;                       // staged X pixels per image
   static constexpr int KP = IMG * BR * OW, KSTEPS = (KP + 31) / 32;
-  static constexpr int PZ = CO + 8, PX = CX + 8;            // plane row strides (bf16)
+  // k order and plane row strides (bf16): with KPERM the 8 rows a 32-lane half of a
+  // transpose read touches (pixels k..k+7) start 8-bank multiples apart on distinct banks —
+  // dZ rows PZ/2 banks apart (PZ = 48 / 80), X rows 2 pixels = PX banks apart (PX = 40). The
+  // aux heads' 48-channel form keeps the plain order (the permuted one spilled there).
+  static constexpr bool KPERM = CX == 32;
+  static constexpr int PZ = CO + (KPERM ? 16 : 8), PX = CX + 8;
   static constexpr int RZ = KP + 1, RX = IMG * NPX + 1;     // rows + one zero row each
   static constexpr size_t LDS = (size_t)3 * (RZ * PZ + RX * PX) * 2;
   static constexpr bool fits = OH % BR == 0 && LDS <= 160 * 1024;
@@ -1036,12 +1041,15 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_x6_kernel(const float* __re
     __syncthreads();
     if (it + (int)gridDim.x < items) load(it + gridDim.x);  // next item's loads under this one's MFMAs
     auto kstep = [&](int ks) {
-      // this lane's rows of the two tr reads (k = 32 ks + 8 Gq + 4s + q): dZ row k and, per tap
+      // this lane's rows of the two tr reads: with KPERM the MFMA's k slot 8 Gq + 4s + q takes
+      // item pixel 32 ks + 16 (Gq >> 1) + 8s + 4 (Gq & 1) + q (any bijection works when A and B
+      // share it; this one puts a 32-lane half's two lane groups on 8 consecutive pixels per
+      // read): dZ row k and, per tap
       // of the wave, the X row under it (the zero rows past the item)
       int zrow[2], xrow[2][2];
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const int k = ks * 32 + 8 * Gq + 4 * s + q;
+        const int k = S::KPERM ? ks * 32 + 16 * (Gq >> 1) + 8 * s + 4 * (Gq & 1) + q : ks * 32 + 8 * Gq + 4 * s + q;
         const int im = k / BP, o = k - (k / BP) * BP;
         const int oy = o / OW, ox = o - (o / OW) * OW;  // oy within the band
         const bool ok = k < KP;
