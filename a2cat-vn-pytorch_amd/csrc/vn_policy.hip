@@ -744,8 +744,10 @@ struct ParityDg {
   static constexpr int SH = SH_, SW = SW_, YC = YC_, XC = XC_, KC = KC_, NCOL = NCOL_, WPC = WPC_;
   static constexpr int NP = SH * SW;                     // staged map pixels per image
   static constexpr int NPC = YC * XC;                    // class pixels per image
-  static constexpr int IMG = NPC >= 64 ? 1 : 64 / NPC;  // images per work item
   static constexpr int PS = KC + 8;                      // plane row stride (bf16)
+  // images per work item: >= 64 class pixels; two large maps where their planes fit (the
+  // next item then loads at the item's start: prefetch registers would spill), one else
+  static constexpr int IMG = NPC >= 64 ? ((size_t)3 * (2 * NP + 1) * PS * 2 <= 160 * 1024 ? 2 : 1) : 64 / NPC;
   static constexpr int NTL = NCOL / (16 * WPC);          // column tiles per wave
   static constexpr int KS = KC / 32;                     // MFMA k steps per tap
   static constexpr int NT = 256 * WPC;
@@ -801,8 +803,9 @@ __global__ __launch_bounds__(S::NT, S::NT >= 512 ? 1 : 2) void parity_dgrad_x6_k
     }
   };
   // the next item's map is prefetched into registers while this one multiplies, unless it
-  // would not fit beside the weights (300x400's 17x23 map: loaded at the item's start)
-  constexpr bool PF = NZ <= 6;
+  // would not fit beside the weights (two 9x9 maps, 300x400's 17x23 map: loaded at the
+  // item's start)
+  constexpr bool PF = NZ <= 3;
   if (PF && (int)blockIdx.x < items) load_z(blockIdx.x);
   for (int it = blockIdx.x; it < items; it += gridDim.x) {
     if constexpr (!PF) load_z(it);
