@@ -247,11 +247,21 @@ __global__ void a2c_schedule_kernel(int64_t* state, float* lr_out, double lr0, d
   state[1] = total + steps_per_update;
 }
 
+// Trace marker: an empty kernel whose grid size (tag workgroups of 64 lanes) a kernel
+// trace records, so a rocprofv3 trace of a test run can be split per test.
+__global__ void trace_marker_kernel() {}
+
 }  // namespace vn
 
 using namespace vn;
 
 extern "C" {
+
+int vn_trace_marker(int tag, vn_stream_t stream) {
+  if (tag < 1 || tag > 65535) return fail(VN_EINVAL, "vn_trace_marker: tag must be 1..65535");
+  hipLaunchKernelGGL(trace_marker_kernel, dim3(tag), dim3(64), 0, (hipStream_t)stream);
+  return VN_OK;
+}
 
 int vn_policy_sample(const float* out, int n, int num_actions, uint64_t seed, uint64_t counter, int32_t* actions,
                      float* logp, float* entropy, float* value, vn_stream_t stream) {

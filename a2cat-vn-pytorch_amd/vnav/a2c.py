@@ -45,7 +45,7 @@ class A2CTrainer:
     def __init__(self, env, net=None, params=None, num_steps=20, gamma=0.99, learning_rate=7e-4,
                  max_time_steps=2e6, rms_alpha=0.99, rms_epsilon=1e-5, max_gradient_norm=0.5,
                  value_coefficient=0.5, entropy_coefficient=0.01, seed=0, process_group=None, recurrent=False,
-                 aux_weight=0.0, arch="goal", cuda_graph=False):
+                 aux_weight=0.0, arch="goal", cuda_graph=False, aux_source="rollout", replay_size=8):
         self.env = env
         self.lib = _lib.load()
         self.device = env.device
@@ -133,16 +133,49 @@ class A2CTrainer:
                                            self.rows_goal.data_ptr())
             ph, pw = self.net.aux_layout["p_hw"]
             self._aux_numel = torch.tensor([1.0, 3.0, 3.0], device=self.device) * (N * ph * pw)
+        # aux batch source: "rollout" = the on-policy batch (its trunk activations are reused),
+        # "replay" = a sequence from the last replay_size rollouts (AuxiliaryTrainer's
+        # self.replay.sample_sequence(), experiments/ai2_auxiliary/trainer.py:29): its own
+        # trunk forward + backward, gradients added to the on-policy ones
+        if aux_source not in ("rollout", "replay"):
+            raise ValueError("aux_source must be 'rollout' or 'replay'")
+        self.aux_source = aux_source
+        if aux_source == "replay":
+            if self.aux_weight <= 0:
+                raise ValueError("aux_source='replay' needs aux_weight > 0")
+            if cuda_graph:
+                raise ValueError("aux_source='replay' draws its sequence on the host each update: use cuda_graph=False")
+            self.replay_rows = torch.zeros((int(replay_size), 2, N), dtype=torch.int32, **kw)
+            self.replay_filled = 0
+            self.replay_pos = 0
+            self._replay_rng = torch.Generator().manual_seed(vdist.rank_seed(self.seed + 17, self.rank))
+            self.aux_rows = torch.zeros((2, N), dtype=torch.int32, **kw)
+            self.aux_acts = self.net.new_acts(N)
+            self.aux_out = torch.zeros((N, OUT_LD), dtype=torch.float32, **kw)
+            self.aux_dz5 = torch.zeros((N, 512), dtype=torch.float32, **kw)
+            self.aux_grads = torch.zeros(P, dtype=torch.float32, **kw)
+            from .policy import AuxTargets
+            self._aux_targets_replay = AuxTargets(self.aux_table.data_ptr(), self.aux_rows[0].data_ptr(),
+                                                  self.aux_rows[1].data_ptr())
+        # compute_auxiliary_loss overridden by a subclass: called every update (autograd on a
+        # GoalNavPolicy view of the flat parameters), its gradient added before the all-reduce
+        self._custom_aux = type(self).compute_auxiliary_loss is not A2CTrainer.compute_auxiliary_loss
+        if self._custom_aux and cuda_graph:
+            raise ValueError("a compute_auxiliary_loss override runs torch autograd per update: use cuda_graph=False")
+        self.aux_losses = {}
+        self._model_view = None
         arena, fb, _, _ = env.frame_arena()
         self._arena, self._fb = arena, fb
         env.observe(gather=False)  # refresh the obs row buffers for the first forward
         self.num_updates = 0
         self.total_steps = 0
         self.cuda_graph = bool(cuda_graph)
-        if self.cuda_graph and self.world > 1:
-            raise ValueError("cuda_graph=True is single-process only (the RCCL all-reduce is not captured)")
+        if self.cuda_graph and self.world > 1 and not vdist.capturable(process_group):
+            raise ValueError("cuda_graph=True at world > 1 needs the nccl (RCCL) backend: a gloo all-reduce "
+                             "cannot be captured in a hipGraph")
         self._graph = None
         self._graph_out = None
+        self._graph_gen = None
 
     # deep_rl hook names (experiments/thor_cached_auxiliary.py:50-56)
     def create_env(self, kwargs):
@@ -150,6 +183,47 @@ class A2CTrainer:
 
     def create_model(self):
         return self.net
+
+    def sample_training_batch(self):
+        """deep_rl's UnrealTrainer.sample_training_batch (AuxiliaryTrainer adds the
+        'auxiliary_batch', experiments/ai2_auxiliary/trainer.py:27-31): one rollout of
+        num_steps on every local env. Returns (batch, report): the batch references the
+        trainer's device buffers (valid until the next rollout), the report holds the
+        finished-episode statistics [count, return sum, length sum] as a device tensor."""
+        self.rollout()
+        batch = RolloutBatch(self, self.rows_img, self.rows_goal)
+        if self.aux_source == "replay":
+            batch["auxiliary_batch"] = self._replay_push_and_sample()
+        return batch, {"episode_stats": self.episode_stats}
+
+    def compute_auxiliary_loss(self, model, batch, device):
+        """deep_rl hook (experiments/ai2_auxiliary/trainer.py:33-43): extra loss terms on a
+        batch -> (loss tensor or None, {name: float}). The default adds nothing here: the
+        deconv loss of aux_weight > 0 is computed by the fused kernels inside update().
+        An override receives a GoalNavPolicy view of the flat parameters (``model``) and the
+        RolloutBatch; its loss's parameter gradient is added to the update's gradient
+        before the all-reduce, clip and RMSprop."""
+        return None, {}
+
+    def model_view(self):
+        """GoalNavPolicy (BigHousePolicy) over this trainer's PolicyNet whose parameter aliases
+        the flat device buffer the kernels update."""
+        if self._model_view is None:
+            from .policy import GoalNavPolicy
+            self._model_view = GoalNavPolicy.wrap(self.net, self.params)
+        return self._model_view
+
+    def _replay_push_and_sample(self):
+        """Store this rollout's frame rows in the replay ring; draw one stored rollout
+        (uniform over the filled slots) as the aux sequence."""
+        R = self.replay_rows.shape[0]
+        self.replay_rows[self.replay_pos, 0].copy_(self.rows_img)
+        self.replay_rows[self.replay_pos, 1].copy_(self.rows_goal)
+        self.replay_pos = (self.replay_pos + 1) % R
+        self.replay_filled = min(self.replay_filled + 1, R)
+        k = int(torch.randint(self.replay_filled, (1,), generator=self._replay_rng))
+        self.aux_rows.copy_(self.replay_rows[k])
+        return RolloutBatch(self, self.aux_rows[0], self.aux_rows[1])
 
     def _stream(self):
         return _lib.stream_ptr(self.device)
@@ -243,11 +317,14 @@ class A2CTrainer:
         # bootstrap value of the final observation
         self._bootstrap(self._frames(info["img_row"], info["goal_row"]))
 
-    def update(self):
+    def update(self, batch=None):
+        """One A2C update on the rollout just sampled (``batch`` from sample_training_batch;
+        None = the trainer's own rollout buffers with the on-policy aux batch)."""
         lib, net = self.lib, self.net
         E, T, A = self.env.num_envs, self.num_steps, self.A
         N = T * E
         st = self._stream()
+        aux_batch = batch.get("auxiliary_batch") if batch is not None else None
         _lib.check(lib.vn_a2c_returns(_lib.ptr(self.rewards), _lib.ptr(self.dones), _lib.ptr(self.boot_out), T, E, A,
                                       ctypes.c_float(self.gamma), _lib.ptr(self.returns), st), "vn_a2c_returns")
         _lib.check(lib.vn_a2c_loss_grad(_lib.ptr(self.out), _lib.ptr(self.actions), _lib.ptr(self.returns), N, A,
@@ -255,7 +332,18 @@ class A2CTrainer:
                                         ctypes.c_float(self.entropy_coefficient), _lib.ptr(self.dout),
                                         _lib.ptr(self.stats), st), "vn_a2c_loss_grad")
         dx4 = None
-        if self.aux_weight > 0:  # deconv heads: forward, loss gradient, backward -> dL/dX4
+        if self.aux_weight > 0 and aux_batch is not None:
+            # replayed sequence: its own trunk forward, the heads' loss and backward, and the
+            # trunk backward of dL/dX4 alone into aux_grads (added after the main backward)
+            self.aux_stats.zero_()
+            af = self._frames(aux_batch.rows_img, aux_batch.rows_goal)
+            net.forward(self.params, af, N, self.aux_acts, N, 0, None if self.recurrent else self.aux_out)
+            net.aux_forward_loss_grad(self.params, self.aux_acts, N, N, self.a1, self.pred, self._aux_targets_replay,
+                                      self.aux_weight, self.dpred, self.aux_stats, self.aux_ws)
+            net.aux_backward(self.params, self.aux_acts, N, N, self.a1, self.dpred, self.grads, self.dx4, self.aux_ws)
+            net.backward_ex(self.params, af, N, self.aux_acts, N, None, self.aux_dz5, self.dx4, self.aux_grads,
+                            self.workspace)
+        elif self.aux_weight > 0:  # deconv heads: forward, loss gradient, backward -> dL/dX4
             self.aux_stats.zero_()
             net.aux_forward_loss_grad(self.params, self.acts, N, N, self.a1, self.pred, self._aux_targets,
                                       self.aux_weight, self.dpred, self.aux_stats, self.aux_ws)
@@ -271,6 +359,14 @@ class A2CTrainer:
             self.c0.copy_(self.c_all[(T - 1) * E:])
         else:
             net.backward_ex(self.params, frames, N, self.acts, N, self.dout, None, dx4, self.grads, self.workspace)
+        if aux_batch is not None:
+            self._add_trunk_grads(self.aux_grads)
+        if self._custom_aux:
+            loss, self.aux_losses = self.compute_auxiliary_loss(self.model_view(), batch, self.device)
+            if loss is not None:
+                g, = torch.autograd.grad(loss, self.model_view().params, allow_unused=True)
+                if g is not None:
+                    self.grads.add_(g)
         scale = vdist.allreduce_gradients_(self.grads, self.group)  # RCCL, one flat bucket
         P = net.n_params
         _lib.check(lib.vn_grad_norm(_lib.ptr(self.grads), P, ctypes.c_float(scale),
@@ -282,11 +378,19 @@ class A2CTrainer:
                                            ctypes.c_float(self.rms_alpha), ctypes.c_float(self.rms_epsilon), st),
                    "vn_rmsprop_step_dev")
 
+    def _add_trunk_grads(self, g):
+        """grads[trunk] += g[trunk]: the conv / conv_merge layers (the only ones backward_ex
+        writes when it is given dZ5 instead of the heads' output gradient)."""
+        w, _ = self.net.offsets["conv1"]
+        _, b = self.net.offsets["fc"]
+        end = b + self.net.shapes["fc"][0]
+        self.grads[w:end].add_(g[w:end])
+
     def _update_metrics(self):
         """rollout + update; returns the device metric vector [value_loss, action_loss,
         entropy, return mean, grad norm, aux loss, episodes, return sum, length sum]."""
-        self.rollout()
-        self.update()
+        batch, _ = self.sample_training_batch()
+        self.update(batch)
         N = self.num_steps * self.env.num_envs
         if self.aux_weight > 0:  # sum of the per-head MSEs (trainer.py:51-54)
             aux = (self.aux_stats[:3] / self._aux_numel).sum().view(1)
@@ -300,13 +404,18 @@ class A2CTrainer:
         """The update through a captured hipGraph: the first update runs eagerly (kernel
         attributes and occupancy caches are set up), the second is captured — capture
         records the launches without running them — and every update replays it."""
+        gen = getattr(self.env, "config_generation", 0)
+        if self._graph is not None and gen != self._graph_gen:
+            # the env was reconfigured after capture (tables, schedule, curriculum, limits):
+            # the graph's launches point at the old buffers and arguments — capture again
+            self._graph, self._graph_out = None, None
         if self._graph is None:
             if self.num_updates == 0:
                 return self._update_metrics()
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 self._graph_out = self._update_metrics()
-            self._graph = g
+            self._graph, self._graph_gen = g, gen
         self._graph.replay()
         return self._graph_out
 
@@ -319,7 +428,8 @@ class A2CTrainer:
         self.total_steps += N * self.world
         self.num_updates += 1
         if not sync:
-            return {"raw": m}
+            # a graph replay writes the same static tensor every update: hand out a copy
+            return {"raw": m.clone() if self.cuda_graph else m}
         vals = m.tolist()
         vl, al, ent, ret_mean, gnorm, aux_loss, eps, rsum, lsum = vals
         dt = time.perf_counter() - t0
@@ -346,7 +456,7 @@ class A2CTrainer:
         (or ``max_rollouts`` rollouts). The recurrent state carries across rollouts as in
         training; the learning-rate step count is left as it was. Returns the episode count
         and the mean reward and length of the finished episodes."""
-        saved_steps = self.sched[1:2].clone()
+        saved_sched = self.sched.clone()  # sampling counter and step count: evaluation leaves both
         E, T = self.env.num_envs, self.num_steps
         tot = torch.zeros(3, dtype=torch.float64)
         for _ in range(int(max_rollouts)):
@@ -359,7 +469,7 @@ class A2CTrainer:
             tot += st.cpu()
             if tot[0] >= episodes:
                 break
-        self.sched[1:2].copy_(saved_steps)
+        self.sched.copy_(saved_sched)
         n, rsum, lsum = tot.tolist()
         return {"episodes": n, "reward": rsum / n if n else float("nan"),
                 "episode_length": lsum / n if n else float("nan")}
@@ -369,22 +479,60 @@ class A2CTrainer:
     def state_dict(self):
         sd = {"params": self.params.detach().cpu(), "square_avg": self.square_avg.cpu(),
               "env_state": self.env.get_state().cpu(), "env_ep_return": self.env.get_episode_returns().cpu(),
-              "num_updates": self.num_updates,
-              "total_steps": self.total_steps, "seed": self.seed}
+              "num_updates": self.num_updates, "sched": self.sched.cpu(),
+              "total_steps": self.total_steps, "seed": self.seed, "rank": self.rank, "world": self.world}
         if self.recurrent:
             for k in self._RECURRENT_STATE:
                 sd[k] = getattr(self, k).cpu()
         return sd
 
     def load_state_dict(self, sd):
+        """Restore a state_dict() of this rank (env shard, running returns, recurrent carry
+        are per rank; the env count must match)."""
+        E = self.env.num_envs
+        if tuple(sd["env_ep_return"].shape) != (E,):
+            raise ValueError("checkpoint holds %d envs, this trainer has %d" % (sd["env_ep_return"].shape[0], E))
+        if "world" in sd and (int(sd["world"]), int(sd["rank"])) != (self.world, self.rank):
+            raise ValueError("checkpoint of rank %d/%d loaded on rank %d/%d"
+                             % (int(sd["rank"]), int(sd["world"]), self.rank, self.world))
         self.params.copy_(sd["params"].to(self.device))
         self.square_avg.copy_(sd["square_avg"].to(self.device))
         self.env.set_state(sd["env_state"])
         self.env.set_episode_returns(sd["env_ep_return"])
         self.num_updates = int(sd["num_updates"])
         self.total_steps = int(sd["total_steps"])
-        self.sched.copy_(torch.tensor([self.num_updates * self.num_steps, self.total_steps, 0], dtype=torch.int64))
+        if "sched" in sd:
+            self.sched.copy_(sd["sched"].to(self.device))
+        else:  # checkpoints from before the schedule was saved
+            self.sched.copy_(torch.tensor([self.num_updates * self.num_steps, self.total_steps, 0], dtype=torch.int64))
         if self.recurrent:
             for k in self._RECURRENT_STATE:
                 getattr(self, k).copy_(sd[k].to(self.device))
         self.env.observe(gather=False)
+
+
+class RolloutBatch(dict):
+    """A sampled batch (deep_rl's batch dict): the frame rows of every sample in the scene
+    cache (time-major, row t*E + e) plus the trainer's rollout buffers; ``observations()``
+    gathers the uint8 frames batch-first [E, T, H, W, 3] as the reference's wrappers
+    deliver them (a device copy: only hooks that need pixels call it)."""
+
+    def __init__(self, trainer, rows_img, rows_goal):
+        super().__init__()
+        self.trainer, self.rows_img, self.rows_goal = trainer, rows_img, rows_goal
+        T, E = trainer.num_steps, trainer.env.num_envs
+        self["actions"] = trainer.actions.view(T, E)
+        self["rewards"] = trainer.rewards
+        self["dones"] = trainer.dones
+
+    def observations(self):
+        tr = self.trainer
+        T, E = tr.num_steps, tr.env.num_envs
+        shape = tuple(tr.env.frame_shape)
+        out = []
+        for rows in (self.rows_img, self.rows_goal):
+            dst = torch.empty((T * E,) + shape, dtype=torch.uint8, device=tr.device)
+            _lib.check(tr.lib.vn_gather_rows(ctypes.c_void_p(tr._arena), int(tr._fb), _lib.ptr(rows), T * E,
+                                             _lib.ptr(dst), tr._stream()), "vn_gather_rows")
+            out.append(dst.view((T, E) + shape).transpose(0, 1))
+        return tuple(out)

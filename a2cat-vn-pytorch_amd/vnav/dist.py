@@ -38,6 +38,12 @@ def world_of(group=None):
     return 1, 0
 
 
+def capturable(group=None):
+    """Whether the group's collectives can be captured in a hipGraph (RCCL can, gloo not)."""
+    world, _ = world_of(group)
+    return world == 1 or dist.get_backend(group) == "nccl"
+
+
 def allreduce_gradients_(flat, group=None):
     """SUM-all-reduce the flat gradient in place; returns the 1/world scale the update
     kernels fold into the gradient norm and the RMSprop step (no extra pass)."""

@@ -67,6 +67,11 @@ class VectorEnv:
                                           ctypes.c_uint64(self.seed & (2**64 - 1)),
                                           self.device.index, ctypes.byref(handle)), "vn_create")
         self._ctx = handle
+        # bumped by every call that replaces the kernels' per-ctx configuration (tables,
+        # schedules, limits): a captured hipGraph holds the old launch arguments and must be
+        # recaptured (A2CTrainer checks it before each replay)
+        self.config_generation = 0
+        self._out_cache = None
         E = self.num_envs
         kw = dict(device=self.device)
         self._info = dict(
@@ -123,11 +128,13 @@ class VectorEnv:
 
     # -- configuration -------------------------------------------------------
     def set_max_episode_steps(self, n):
+        self.config_generation += 1
         _lib.check(self.lib.vn_set_max_episode_steps(self._ctx, int(n or 0)), "vn_set_max_episode_steps")
 
     def set_tasks(self, tasks):
         """tasks: [(scene_index, goal_state or -1)] sampled uniformly at each reset."""
         arr = np.ascontiguousarray(np.asarray(tasks, dtype=np.int32).reshape(-1, 2))
+        self.config_generation += 1
         _lib.check(self.lib.vn_set_tasks(self._ctx, arr.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), len(arr)),
                    "vn_set_tasks")
 
@@ -135,11 +142,13 @@ class VectorEnv:
         arr = np.ascontiguousarray(np.asarray(env_scenes, dtype=np.int32))
         if arr.shape != (self.num_envs,):
             raise ValueError("env_scenes must have one entry per env")
+        self.config_generation += 1
         _lib.check(self.lib.vn_set_env_scenes(self._ctx, arr.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))),
                    "vn_set_env_scenes")
 
     def set_schedule(self, schedule):
         """Exact-replay test mode: schedule [E, L, 2] int32 (start, goal) per reset."""
+        self.config_generation += 1
         if schedule is None:
             _lib.check(self.lib.vn_set_schedule(self._ctx, None, 0), "vn_set_schedule")
             self._schedule = None
@@ -157,6 +166,7 @@ class VectorEnv:
         goal on the device (vn_set_curriculum); None switches back to uniform starts.
         mode/offset default to each scene's own semantics (Scene.curriculum)."""
         self.complexity = complexity
+        self.config_generation += 1
         if complexity is None:
             _lib.check(self.lib.vn_set_curriculum(self._ctx, 0.0, 0, 0.0), "vn_set_curriculum")
             return
@@ -235,12 +245,29 @@ class VectorEnv:
         ``out`` = dict of preallocated outputs (image, goal, reward, done, state) to write
         in place; ``gather=False`` skips the frame copy (index-only step: info img_row /
         goal_row address the frames in the scene cache)."""
-        a = torch.as_tensor(actions, device=self.device)
-        if a.dtype != torch.int32:
-            a = a.to(torch.int32)
-        a = a.contiguous()
-        if a.shape != (self.num_envs,):
-            raise ValueError("actions must have shape [num_envs]")
+        if type(actions) is torch.Tensor and actions.dtype == torch.int32 and actions.device == self.device \
+                and actions.shape == (self.num_envs,) and actions.is_contiguous():
+            a = actions
+        else:
+            a = torch.as_tensor(actions, device=self.device)
+            if a.dtype != torch.int32:
+                a = a.to(torch.int32)
+            a = a.contiguous()
+            if a.shape != (self.num_envs,):
+                raise ValueError("actions must have shape [num_envs]")
+        if out is not None and gather:
+            # the same caller-owned buffers as the previous call: validated then, pointers cached
+            bufs = (out["image"], out["goal"], out.get("reward"), out.get("done"), out.get("state"))
+            c = self._out_cache
+            if c is not None and all(x is y for x, y in zip(bufs, c[0])):
+                P = c[1]
+                _lib.check(self.lib.vn_step(self._ctx, _lib.ptr(a), P[0], P[1], P[2], P[3], P[4], self._stream()),
+                           "vn_step")
+                info = dict(self._info)
+                info["state"] = bufs[4]
+                if self.aux_observations:
+                    return (bufs[0], bufs[1]) + self._gather_aux(), bufs[2], bufs[3], info
+                return (bufs[0], bufs[1]), bufs[2], bufs[3], info
         if out is None:
             img, goal = self._frames() if gather else (None, None)
             reward = torch.empty(self.num_envs, dtype=torch.float32, device=self.device)
@@ -253,6 +280,9 @@ class VectorEnv:
             self._check_out("reward", reward, torch.float32, self.num_envs)
             self._check_out("done", done, torch.bool, self.num_envs)
             self._check_out("state", state, torch.int32, self.num_envs)
+            if gather:
+                bufs = (img, goal, reward, done, state)
+                self._out_cache = (bufs, tuple(_lib.ptr(t) for t in bufs))
         _lib.check(self.lib.vn_step(self._ctx, _lib.ptr(a), _lib.ptr(img), _lib.ptr(goal), _lib.ptr(reward),
                                     _lib.ptr(done), _lib.ptr(state), self._stream()), "vn_step")
         info = dict(self._info)
@@ -274,6 +304,12 @@ class VectorEnv:
         return buf
 
     def set_state(self, buf):
+        """Restore get_state()'s [len(ST_FIELDS), num_envs] int32 table (checked before the
+        device copy: a table of another env count would be read past or misaligned)."""
+        buf = torch.as_tensor(buf)
+        if tuple(buf.shape) != (len(ST_FIELDS), self.num_envs):
+            raise ValueError("env state must be [%d, %d] (this env), got %s"
+                             % (len(ST_FIELDS), self.num_envs, tuple(buf.shape)))
         buf = buf.to(device=self.device, dtype=torch.int32).contiguous()
         _lib.check(self.lib.vn_set_state(self._ctx, _lib.ptr(buf), self._stream()), "vn_set_state")
 
@@ -285,6 +321,9 @@ class VectorEnv:
         return buf
 
     def set_episode_returns(self, buf):
+        buf = torch.as_tensor(buf)
+        if tuple(buf.shape) != (self.num_envs,):
+            raise ValueError("episode returns must be [%d] (this env), got %s" % (self.num_envs, tuple(buf.shape)))
         buf = buf.to(device=self.device, dtype=torch.float32).contiguous()
         _lib.check(self.lib.vn_set_episode_returns(self._ctx, _lib.ptr(buf), self._stream()),
                    "vn_set_episode_returns")

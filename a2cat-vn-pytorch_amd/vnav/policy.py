@@ -567,6 +567,20 @@ class GoalNavPolicy(torch.nn.Module):
         self.params = torch.nn.Parameter(self.net.init_params(seed))
         self.lstm_layers, self.lstm_hidden_size = 1, 512  # goal.py:61-62 (state shape contract)
 
+    @classmethod
+    def wrap(cls, net, params):
+        """A policy over an existing PolicyNet whose parameter aliases ``params`` (the flat
+        device buffer of a trainer: no copy, the kernels' updates are seen here)."""
+        if net.arch != cls._ARCH:
+            cls = BigHousePolicy if net.arch == "bighouse" else GoalNavPolicy
+        self = cls.__new__(cls)
+        torch.nn.Module.__init__(self)
+        self.net = net
+        self.deconv_cell_size = 4
+        self.params = torch.nn.Parameter(params)
+        self.lstm_layers, self.lstm_hidden_size = 1, 512
+        return self
+
     def initial_states(self, batch_size):
         return tuple(torch.zeros([batch_size, self.lstm_layers, self.lstm_hidden_size], dtype=torch.float32)
                      for _ in range(2))

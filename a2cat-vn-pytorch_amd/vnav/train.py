@@ -127,7 +127,7 @@ class Experiment:
                           max_time_steps=self.max_time_steps, rms_alpha=self.rms_alpha,
                           rms_epsilon=self.rms_epsilon, max_gradient_norm=self.max_gradient_norm,
                           seed=self.seed, recurrent=self.recurrent,
-                          aux_weight=self.auxiliary_weight, cuda_graph=self.cuda_graph and self.world == 1)
+                          aux_weight=self.auxiliary_weight, cuda_graph=self.cuda_graph and vdist.capturable())
 
     def _setup(self):
         if self.trainer is None:
@@ -143,12 +143,14 @@ class Experiment:
 
     @property
     def checkpoint_path(self):
+        """One file per rank when world > 1: the env shard, running returns and recurrent
+        carry are per rank (the parameters and RMSprop state are the same on every rank)."""
+        if self.world > 1:
+            return os.path.join(self.save_dir, "checkpoint.rank%d.pt" % self.rank)
         return os.path.join(self.save_dir, "checkpoint.pt")
 
     def save_checkpoint(self, path=None):
         path = path or self.checkpoint_path
-        if self.rank != 0:
-            return path
         os.makedirs(os.path.dirname(path), exist_ok=True)
         tmp = path + ".tmp"
         torch.save(self.trainer.state_dict(), tmp)

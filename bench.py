@@ -293,6 +293,21 @@ def _cpu_worker(args):
     return steps * n_envs, time.perf_counter() - t0
 
 
+def host_cpu_info():
+    """The host the CPU baseline ran on: logical CPUs of the machine (os.cpu_count / nproc),
+    the CPUs this process may use (its affinity: the box's share), and the CPU model."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"nproc": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)), "model": model}
+
+
 def cpu_baseline(scenes, seconds, workers):
     """The oracle ('port') batched VectorEnv in numpy, one process per core (fork, before
     any GPU initialisation), each stepping 256 envs incl. the two-frame gather."""
@@ -311,7 +326,7 @@ def cpu_baseline(scenes, seconds, workers):
     wall = time.perf_counter() - t0
     total = sum(r[0] for r in res)
     rate = sum(r[0] / r[1] for r in res)
-    return dict(value=rate, unit="env-steps/s", cores=workers, kind="port",
+    return dict(value=rate, unit="env-steps/s", cores=workers, kind="port", host=host_cpu_info(),
                 sample="oracle VectorEnvOracle (numpy) %d procs x %d envs, %.0f s each, %d env-steps incl. "
                        "2-frame gather from a %d-row arena (wall %.1f s)" % (workers, per, seconds, total, rows, wall))
 
@@ -369,6 +384,7 @@ def main():
             torch.distributed.barrier()
 
     K = args.steps
+    step_actions = list(actions.unbind(0))  # per-step views made before the timed region
     # one HIP event pair around the K launches (vn_step runs on torch's current stream): the
     # per-launch duration is the region's device time / K, inter-kernel gaps included. Event
     # records between every launch cost ~5 us of device time each step and slowed the
@@ -379,9 +395,14 @@ def main():
     t0 = time.perf_counter()
     ev0.record()
     for k in range(K):
-        env.step(actions[step], out=out)
+        env.step(step_actions[step], out=out)
         step += 1
     ev1.record()
+    # poll the end event before the synchronize: a blocking wait that outlasts the runtime's
+    # spin phase sleeps and is woken by an interrupt, which can add ~0.1-0.2 ms to a short
+    # window (the driver's 20-step run measured 0.2 ms outside the kernels' event pair)
+    while not ev1.query():
+        pass
     torch.cuda.synchronize(dev)
     barrier()
     elapsed = time.perf_counter() - t0

@@ -341,6 +341,11 @@ int vn_rmsprop_step_dev(float* params, const float* grads, float* square_avg, in
 int vn_last_error(char* buf, size_t len);
 const char* vn_version(void);
 
+/* Diagnostics: launch an empty kernel of `tag` (1..65535) workgroups of 64 lanes on the
+ * stream. A kernel trace records its grid size, which marks where a test (or any phase of
+ * a program) begins in a trace (tests/conftest.py, tools/test_kernel_map.py). */
+int vn_trace_marker(int tag, vn_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

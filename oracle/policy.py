@@ -44,6 +44,28 @@ class GoalNetOracle(nn.Module):
         f = self.features(image, goal)
         return self.policy_logits(f), self.critic(f)
 
+    def forward_masked(self, image, goal, masks):
+        """The same network with every ReLU replaced by multiplication with a given 0/1 mask
+        (masks = dict m1i, m1g, m2i, m2g, m3, m4, m5 in NCHW / [N,512]). Fed the masks of
+        the GPU forward, the gradients are those of the function the GPU differentiated,
+        so a pre-activation within rounding of zero (a ReLU tie) cannot make the two
+        disagree. Returns (logits, value, x4, pre) with pre = the pre-activations, for the
+        check that the masks are the signs of the oracle's own pre-activations wherever
+        those are not ties."""
+        pre = {}
+
+        def base(x, a, b):
+            pre["z1" + a[-1]] = z1 = self.conv1(x)
+            pre["z2" + a[-1]] = z2 = self.conv2(z1 * masks[a])
+            return z2 * masks[b]
+        x = torch.cat((base(image, "m1i", "m2i"), base(goal, "m1g", "m2g")), 1)
+        pre["z3"] = z3 = self.conv3(x)
+        pre["z4"] = z4 = self.conv4(z3 * masks["m3"])
+        x4 = z4 * masks["m4"]
+        pre["z5"] = z5 = self.fc(x4.flatten(1))
+        f = z5 * masks["m5"]
+        return self.policy_logits(f), self.critic(f), x4, pre
+
     def load_reference(self, sd):
         """Reference state-dict names (deep_rl TimeDistributed wrapping an nn.Sequential)."""
         m = {"shared_base.0.0": self.conv1, "shared_base.0.2": self.conv2,
@@ -105,6 +127,12 @@ class AuxHeadsOracle(nn.Module):
 
     def forward(self, features):
         return tuple(h(features) for h in self.heads)
+
+    def forward_masked(self, features, masks):
+        """forward() with each head's ReLU replaced by its given 0/1 mask [N,16,AH,AW]
+        (see GoalNetOracle.forward_masked); returns (predictions, pre-activations)."""
+        pre = [h[0](features) for h in self.heads]
+        return tuple(h[2](z * m) for h, z, m in zip(self.heads, pre, masks)), pre
 
     def load_reference(self, sd):
         for h, name in zip(self.heads, ("deconv_depth", "deconv_mask", "deconv_mask_goal")):

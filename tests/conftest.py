@@ -36,3 +36,28 @@ def golden():
         return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
 
     return load
+
+
+_TRACE = {"n": 0}
+
+
+@pytest.fixture(autouse=True)
+def _trace_marker(request):
+    """VN_TRACE_TESTS=<file>: before each GPU test, record its node id (line k of the file)
+    and launch vn_trace_marker(k) so a rocprofv3 kernel trace of the run splits per test
+    (tools/test_kernel_map.py). Off unless the variable is set."""
+    path = os.environ.get("VN_TRACE_TESTS")
+    if not path or request.node.get_closest_marker("gpu") is None:
+        yield
+        return
+    import torch
+    from vnav import _lib
+    torch.cuda.synchronize()
+    _TRACE["n"] += 1
+    with open(path, "a") as f:
+        f.write("%d\t%s\n" % (_TRACE["n"], request.node.nodeid))
+    _lib.check(_lib.load().vn_trace_marker(_TRACE["n"], _lib.stream_ptr(torch.device("cuda", 0))),
+               "vn_trace_marker")
+    torch.cuda.synchronize()
+    yield
+    torch.cuda.synchronize()

@@ -83,3 +83,17 @@ def test_resume_continues_exactly(tmp_path):
     rest.run(resume=True)
     assert rest.trainer.total_steps == 640
     assert torch.equal(rest.trainer.params, full.trainer.params)
+
+
+def test_checkpoint_file_per_rank(tmp_path, monkeypatch):
+    """world > 1: each rank writes and reads its own checkpoint (the env shard, running
+    returns and recurrent carry are per rank); one process keeps checkpoint.pt."""
+    train = _train()
+    exp = train.make_trainer("cached-thor", save_dir=str(tmp_path))
+    assert exp.checkpoint_path == os.path.join(str(tmp_path), "checkpoint.pt")
+    for r in range(2):
+        monkeypatch.setenv("RANK", str(r))
+        monkeypatch.setenv("WORLD_SIZE", "2")
+        monkeypatch.setenv("LOCAL_RANK", str(r))
+        exp = train.make_trainer("cached-thor", save_dir=str(tmp_path))
+        assert exp.checkpoint_path == os.path.join(str(tmp_path), "checkpoint.rank%d.pt" % r)
