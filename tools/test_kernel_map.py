@@ -70,7 +70,8 @@ def main(argv=None):
     with open(a.tests) as f:
         for line in f:
             k, nodeid = line.rstrip("\n").split("\t", 1)
-            tests[int(k)] = nodeid
+            i = nodeid.find("tests/")
+            tests[int(k)] = nodeid[i:] if i >= 0 else nodeid
     per = split(load_trace(a.trace), tests)
     out = ["# Kernels dispatched per GPU test", "",
            "From `%s` split at the `vn_trace_marker` launches (`tests/conftest.py`)." % a.trace, ""]
