@@ -15,20 +15,6 @@ namespace vn {
 
 constexpr int OUT_LD_A2C = 8;
 
-__device__ __forceinline__ void softmax_stats(const float* lg, int A, float* p, float* logp, float& H) {
-  float mx = lg[0];
-  for (int j = 1; j < A; ++j) mx = fmaxf(mx, lg[j]);
-  float s = 0.0f;
-  for (int j = 0; j < A; ++j) s += expf(lg[j] - mx);
-  const float ls = logf(s);
-  H = 0.0f;
-  for (int j = 0; j < A; ++j) {
-    logp[j] = lg[j] - mx - ls;
-    p[j] = expf(logp[j]);
-    H -= p[j] * logp[j];
-  }
-}
-
 // ctr_dev (optional): the Philox counter is *ctr_dev + ctr (a device-side update counter, so
 // a captured hipGraph of the update samples with a fresh counter on every replay).
 __global__ void sample_kernel(const float* __restrict__ out, int n, int A, uint32_t k0, uint32_t k1, uint64_t ctr,
@@ -39,18 +25,7 @@ __global__ void sample_kernel(const float* __restrict__ out, int n, int A, uint3
   if (ctr_dev) ctr += (uint64_t)*ctr_dev;
   float lg[7], p[7], lp[7], H;
   for (int j = 0; j < A; ++j) lg[j] = out[(int64_t)i * OUT_LD_A2C + j];
-  softmax_stats(lg, A, p, lp, H);
-  const u32x4 r = philox4x32_10(u32x4{(uint32_t)i, (uint32_t)ctr, (uint32_t)(ctr >> 32), STREAM_POLICY}, k0, k1);
-  const float u = (float)(r.x >> 8) * (1.0f / 16777216.0f);
-  int a = A - 1;
-  float c = 0.0f;
-  for (int j = 0; j < A - 1; ++j) {
-    c += p[j];
-    if (u < c) {
-      a = j;
-      break;
-    }
-  }
+  const int a = sample_action(lg, A, k0, k1, ctr, (uint32_t)i, p, lp, H);
   actions[i] = a;
   if (logp_out) logp_out[i] = lp[a];
   if (ent_out) ent_out[i] = H;
@@ -232,6 +207,32 @@ __global__ __launch_bounds__(kPostThreads) void step_post_kernel(const int32_t* 
   }
 }
 
+// Fixed-order sums of the per-env episode statistics of a rollout (vn_step_a2c), then zeroed.
+__global__ __launch_bounds__(kPostThreads) void episode_stats_kernel(float* __restrict__ st_env, int E,
+                                                                     float* __restrict__ stats3) {
+  float s[3] = {0.0f, 0.0f, 0.0f};
+  for (int e = threadIdx.x; e < E; e += kPostThreads)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      s[k] += st_env[(int64_t)k * E + e];
+      st_env[(int64_t)k * E + e] = 0.0f;
+    }
+  __shared__ float red[3][kPostThreads / 64];
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+    for (int o = 32; o > 0; o >>= 1) s[k] += __shfl_xor(s[k], o);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) red[k][w] = s[k];
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    float t = 0.0f;
+    for (int i = 0; i < kPostThreads / 64; ++i) t += red[threadIdx.x][i];
+    stats3[threadIdx.x] = t;
+  }
+}
+
 // Device-side trainer schedule, one thread, launched first in every update:
 //   state[2] (counter of this update) = state[0]; state[0] += T (policy sampling counter base,
 //   = updates * T); lr = lr0 * (1 - min(state[1] / max_steps, 1)) in double as the host's
@@ -256,6 +257,14 @@ __global__ void trace_marker_kernel() {}
 using namespace vn;
 
 extern "C" {
+
+int vn_a2c_episode_stats(float* episode_stats_env, int E, float* stats3, vn_stream_t stream) {
+  if (!episode_stats_env || !stats3 || E <= 0) return fail(VN_EINVAL, "vn_a2c_episode_stats: bad args");
+  hipLaunchKernelGGL(episode_stats_kernel, dim3(1), dim3(kPostThreads), 0, (hipStream_t)stream, episode_stats_env, E,
+                     stats3);
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
 
 int vn_trace_marker(int tag, vn_stream_t stream) {
   if (tag < 1 || tag > 65535) return fail(VN_EINVAL, "vn_trace_marker: tag must be 1..65535");

@@ -57,6 +57,41 @@ __host__ __device__ inline uint32_t uniform_below(uint32_t r, uint32_t n) {
   return (uint32_t)(((uint64_t)r * (uint64_t)n) >> 32);
 }
 
+// ---- the policy's categorical draw (vn_a2c.hip sample_kernel, vn_env.hip's fused A2C step) --
+__device__ __forceinline__ void softmax_stats(const float* lg, int A, float* p, float* logp, float& H) {
+  float mx = lg[0];
+  for (int j = 1; j < A; ++j) mx = fmaxf(mx, lg[j]);
+  float s = 0.0f;
+  for (int j = 0; j < A; ++j) s += expf(lg[j] - mx);
+  const float ls = logf(s);
+  H = 0.0f;
+  for (int j = 0; j < A; ++j) {
+    logp[j] = lg[j] - mx - ls;
+    p[j] = expf(logp[j]);
+    H -= p[j] * logp[j];
+  }
+}
+
+// Inverse-CDF draw of sample i from the logits lg[0..A-1] (A <= 7): u = the top 24 bits of
+// Philox4x32-10 (i, ctr_lo, ctr_hi, STREAM_POLICY) under key (k0, k1). Returns the action;
+// p / lp / H receive the distribution, its log and its entropy.
+__device__ __forceinline__ int sample_action(const float* lg, int A, uint32_t k0, uint32_t k1, uint64_t ctr,
+                                             uint32_t i, float* p, float* lp, float& H) {
+  softmax_stats(lg, A, p, lp, H);
+  const u32x4 r = philox4x32_10(u32x4{i, (uint32_t)ctr, (uint32_t)(ctr >> 32), STREAM_POLICY}, k0, k1);
+  const float u = (float)(r.x >> 8) * (1.0f / 16777216.0f);
+  int a = A - 1;
+  float c = 0.0f;
+  for (int j = 0; j < A - 1; ++j) {
+    c += p[j];
+    if (u < c) {
+      a = j;
+      break;
+    }
+  }
+  return a;
+}
+
 // Synthetic frame hash: 32-bit word w of frame (scene, state).
 __host__ __device__ inline uint32_t frame_hash(uint32_t scene, uint32_t state, uint32_t w) {
   uint32_t x = (w * 0x9E3779B1u) ^ (state * 0x85EBCA77u) ^ (scene * 0xC2B2AE3Du) ^ 0x27D4EB2Fu;

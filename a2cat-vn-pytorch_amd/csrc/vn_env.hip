@@ -86,6 +86,19 @@ struct EnvArgs {
   uint8_t* info_trunc;
   int32_t* info_img_row;
   int32_t* info_goal_row;
+  // vn_step_a2c: action sampled in the step, then the rollout's per-step bookkeeping
+  const float* pol_out;
+  int pol_A;
+  uint32_t pk0, pk1;
+  const int64_t* pctr_dev;
+  uint64_t pctr;
+  int32_t* act_out;
+  int64_t* prev_action;
+  float* prev_reward;
+  float* prev_mask;
+  float* lra_next;
+  float* mask_next;
+  float* stats_env;
 };
 
 enum { MODE_STEP = 0, MODE_RESET = 1, MODE_OBSERVE = 2 };
@@ -233,7 +246,15 @@ __global__ __launch_bounds__(256) void env_kernel(EnvArgs a) {
   if constexpr (MODE == MODE_STEP) {
     int t = st[ST_ELAPSED * n_envs + e];
     const SceneDev S = a.scenes[sc];
-    const int act = a.actions[e];
+    int act;
+    if (a.pol_out) {  // the policy's categorical draw for this env (vn_policy_sample_dev's)
+      float lg[7], p[7], lp[7], H;
+      for (int j = 0; j < a.pol_A; ++j) lg[j] = a.pol_out[(int64_t)e * 8 + j];
+      const uint64_t ctr = a.pctr + (a.pctr_dev ? (uint64_t)*a.pctr_dev : 0ull);
+      act = uni(sample_action(lg, a.pol_A, a.pk0, a.pk1, ctr, (uint32_t)e, p, lp, H));
+    } else {
+      act = a.actions[e];
+    }
     const bool bad = (unsigned)act > 3u;
     int nxt = -1;
     if (!bad) nxt = a.graph[((int64_t)S.graph_off + s) * 4 + act];
@@ -273,6 +294,23 @@ __global__ __launch_bounds__(256) void env_kernel(EnvArgs a) {
       if (a.info_len) a.info_len[e] = ep_len;
       if (a.info_term) a.info_term[e] = term_state;
       if (a.info_trunc) a.info_trunc[e] = (limit && !terminal) ? 1 : 0;
+      if (a.pol_out) {  // vn_a2c_step_post's bookkeeping for this env
+        const float m = done ? 0.0f : 1.0f;
+        a.act_out[e] = act;
+        if (a.prev_action) a.prev_action[e] = act;
+        if (a.prev_reward) a.prev_reward[e] = r;
+        if (a.prev_mask) a.prev_mask[e] = m;
+        if (a.mask_next) a.mask_next[e] = m;
+        if (a.lra_next) {
+          for (int j = 0; j < a.pol_A; ++j) a.lra_next[(int64_t)e * (a.pol_A + 1) + j] = j == act ? m : 0.0f;
+          a.lra_next[(int64_t)e * (a.pol_A + 1) + a.pol_A] = r * m;
+        }
+        if (a.stats_env && done) {
+          a.stats_env[e] += 1.0f;
+          a.stats_env[n_envs + e] += ret;
+          a.stats_env[2 * (int64_t)n_envs + e] += (float)ep_len;
+        }
+      }
     }
   } else if constexpr (MODE == MODE_RESET) {
     if (a.mask == nullptr || a.mask[e] != 0) {
@@ -635,6 +673,32 @@ int vn_step(vn_ctx* c, const int32_t* actions_dev, uint8_t* obs_dev, uint8_t* go
   a.reward = reward_dev;
   a.done = done_dev;
   a.state_out = state_dev;
+  return launch_env<MODE_STEP>(c, a, (hipStream_t)stream);
+}
+
+int vn_step_a2c(vn_ctx* c, const vn_a2c_step* p, float* reward_dev, uint8_t* done_dev, int32_t* state_dev,
+                vn_stream_t stream) {
+  if (!c) return fail(VN_EINVAL, "vn_step_a2c: NULL ctx");
+  if (!p || !p->policy_out || !p->actions || p->num_actions < 1 || p->num_actions > 7)
+    return fail(VN_EINVAL, "vn_step_a2c: bad a2c arguments");
+  DeviceGuard guard(c->device);
+  EnvArgs a = make_args(c);
+  a.reward = reward_dev;
+  a.done = done_dev;
+  a.state_out = state_dev;
+  a.pol_out = p->policy_out;
+  a.pol_A = p->num_actions;
+  a.pk0 = (uint32_t)p->seed;
+  a.pk1 = (uint32_t)(p->seed >> 32);
+  a.pctr_dev = p->counter_base_dev;
+  a.pctr = p->counter;
+  a.act_out = p->actions;
+  a.prev_action = p->prev_action;
+  a.prev_reward = p->prev_reward;
+  a.prev_mask = p->prev_mask;
+  a.lra_next = p->lra_next;
+  a.mask_next = p->mask_next;
+  a.stats_env = p->episode_stats_env;
   return launch_env<MODE_STEP>(c, a, (hipStream_t)stream);
 }
 

@@ -27,6 +27,7 @@
 #include "vn_gemm.h"
 #include "vn_lstm.h"
 #include "vn_aux.h"
+#include "vn_skinny.h"
 
 #include "vn_frames.h"
 #include "vn_conv1.h"
@@ -1291,10 +1292,26 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
     hipLaunchKernelGGL((conv2_fwd_x6_kernel<G::OH1, G::OW1, G::OH2, G::OW2>), dim3(blocks), dim3(512), Bd::LDS, st,
                        a.X[0], P + L.l[1].w, P + L.l[1].b, a.X[1], frames);
   } else {
-    NhwcIm2col<32, 4, 4, 2, G::OH1, G::OW1, G::OH2, G::OW2, 1> fa{a.X[0], 2 * n * G::OH2 * G::OW2};
-    DenseRows fb{P + L.l[1].w, 512, 32};
-    EpiBiasAct ep{a.X[1], 32, P + L.l[1].b, 1};
-    launch_gemm_x6_sk<128, 32, 32, 4, 1>(fa, fb, ep, fa.M, 32, 512, st, L);
+    using Bd = Conv2FwdBand<G::OH1, G::OW1, G::OH2, G::OW2>;
+    bool done = false;
+    if constexpr (Bd::LDS <= 160 * 1024) {
+      // a few envs (174x174, 300x400): the banded kernel is one launch where the split-K
+      // product needs two; at training batches the generic product is faster (see above)
+      if (n <= kSkinnyRows) {
+        const void* kfn = (const void*)conv2_fwd_x6_kernel<G::OH1, G::OW1, G::OH2, G::OW2>;
+        VN_HIP(ensure_dyn_lds(kfn, Bd::LDS));
+        const int blocks = std::min(frames * Bd::NB, resident_blocks(kfn, 512, Bd::LDS));
+        hipLaunchKernelGGL((conv2_fwd_x6_kernel<G::OH1, G::OW1, G::OH2, G::OW2>), dim3(blocks), dim3(512), Bd::LDS, st,
+                           a.X[0], P + L.l[1].w, P + L.l[1].b, a.X[1], frames);
+        done = true;
+      }
+    }
+    if (!done) {
+      NhwcIm2col<32, 4, 4, 2, G::OH1, G::OW1, G::OH2, G::OW2, 1> fa{a.X[0], 2 * n * G::OH2 * G::OW2};
+      DenseRows fb{P + L.l[1].w, 512, 32};
+      EpiBiasAct ep{a.X[1], 32, P + L.l[1].b, 1};
+      launch_gemm_x6_sk<128, 32, 32, 4, 1>(fa, fb, ep, fa.M, 32, 512, st, L);
+    }
   }
   // conv3 over concat(image, goal) (X2 -> X3)
   {
@@ -1315,17 +1332,25 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
   }
   // conv_merge Linear (X4 flattened NHWC -> X5)
   {
-    DenseRows fa{a.X[3], G::FCIN, n};
-    DenseRows fb{P + L.l[4].w, G::FCIN, 512};
     EpiBiasAct ep{a.X[4], 512, P + L.l[4].b, 1};
-    launch_gemm_x6_sk<64, 64, 32, 2, 2>(fa, fb, ep, n, 512, G::FCIN, st, L);
+    if (n <= kSkinnyRows) {  // a few envs: whole-K VALU columns, no split-K pass (vn_skinny.h)
+      launch_skinny(a.X[3], G::FCIN, P + L.l[4].w, G::FCIN, ep, n, 512, G::FCIN, st);
+    } else {
+      DenseRows fa{a.X[3], G::FCIN, n};
+      DenseRows fb{P + L.l[4].w, G::FCIN, 512};
+      launch_gemm_x6_sk<64, 64, 32, 2, 2>(fa, fb, ep, n, 512, G::FCIN, st, L);
+    }
   }
   // heads (X5 -> out[n][8]: logits, value); out == NULL runs the trunk only (recurrent policy)
   if (out) {
-    DenseRows fa{a.X[4], 512, n};
-    DenseRows fb{P + L.l[5].w, 512, A1};
     EpiBiasAct ep{out, OUT_LD, P + L.l[5].b, 0};
-    launch_gemm_sk<64, 16, 32, 4, 1>(fa, fb, ep, n, A1, 512, st, L);
+    if (n <= kSkinnyRows) {
+      launch_skinny(a.X[4], 512, P + L.l[5].w, 512, ep, n, A1, 512, st);
+    } else {
+      DenseRows fa{a.X[4], 512, n};
+      DenseRows fb{P + L.l[5].w, 512, A1};
+      launch_gemm_sk<64, 16, 32, 4, 1>(fa, fb, ep, n, A1, 512, st, L);
+    }
   }
   VN_HIP(hipGetLastError());
   return VN_OK;
@@ -1651,6 +1676,21 @@ int backward_bignet(const PolicyLayout& L, const float* P, const FrameSrc& src, 
 inline int lstm_forward_step(const PolicyLayout& L, const float* P, int E, const float* x5, const float* lra,
                              const float* mask, const float* h_prev, const float* c_prev, float* xc, float* gates,
                              float* acts, float* c_out, float* h_out, hipStream_t st) {
+  if (E <= kSkinnyRows) {  // xcat build + gates + cell in one launch (vn_skinny.h)
+    XcatFill xf{x5, lra, mask, h_prev, L.A + 1, L.xoff};
+    const dim3 grid(256), block(256);  // 2 hidden units (8 gate columns) per workgroup
+    if (E <= 4)
+      hipLaunchKernelGGL(lstm_step_skinny_kernel<4>, grid, block, 0, st, xf, E, L.xcat, P + L.lw, P + L.lbih,
+                         P + L.lbhh, c_prev, xc, acts, c_out, h_out);
+    else if (E <= 8)
+      hipLaunchKernelGGL(lstm_step_skinny_kernel<8>, grid, block, 0, st, xf, E, L.xcat, P + L.lw, P + L.lbih,
+                         P + L.lbhh, c_prev, xc, acts, c_out, h_out);
+    else
+      hipLaunchKernelGGL(lstm_step_skinny_kernel<kSkinnyRows>, grid, block, 0, st, xf, E, L.xcat, P + L.lw,
+                         P + L.lbih, P + L.lbhh, c_prev, xc, acts, c_out, h_out);
+    VN_HIP(hipGetLastError());
+    return VN_OK;
+  }
   const int64_t nx = (int64_t)E * L.xcat;
   hipLaunchKernelGGL(lstm_prep_kernel, dim3((unsigned)((nx + 255) / 256)), dim3(256), 0, st, E, L.A, L.xcat, L.xoff,
                      x5, lra, mask, h_prev, xc);
@@ -1668,10 +1708,14 @@ inline int lstm_forward_step(const PolicyLayout& L, const float* P, int E, const
 }
 
 inline int heads_forward(const PolicyLayout& L, const float* P, const float* feat, int n, float* out, hipStream_t st) {
-  DenseRows fa{feat, 512, n};
-  DenseRows fb{P + L.l[5].w, 512, L.A + 1};
   EpiBiasAct ep{out, OUT_LD, P + L.l[5].b, 0};
-  launch_gemm_sk<64, 16, 32, 4, 1>(fa, fb, ep, n, L.A + 1, 512, st, L);
+  if (n <= kSkinnyRows) {
+    launch_skinny(feat, 512, P + L.l[5].w, 512, ep, n, L.A + 1, 512, st);
+  } else {
+    DenseRows fa{feat, 512, n};
+    DenseRows fb{P + L.l[5].w, 512, L.A + 1};
+    launch_gemm_sk<64, 16, 32, 4, 1>(fa, fb, ep, n, L.A + 1, 512, st, L);
+  }
   VN_HIP(hipGetLastError());
   return VN_OK;
 }
@@ -1744,7 +1788,40 @@ inline int lstm_backward(const PolicyLayout& L, const float* P, int T, int E, co
                                st);
   }
   const unsigned cb = (unsigned)((e512 + 255) / 256);
-  for (int t = T - 1, cur = 0; t >= 0; --t, cur ^= 1) {
+  if (E <= kSkinnyRows) {
+    // a few envs: the cell backward of the last step, then per step t one launch with the
+    // sequential product dh_{t-1} = m_t (dgates_t W_hh) and step t-1's cell backward
+    // (dh_{-1} is not needed: no launch for t = 0)
+    {
+      const int t = T - 1;
+      hipLaunchKernelGGL(lstm_cell_bwd_kernel, dim3(cb), dim3(256), 0, st, E, w.dh_heads + (int64_t)t * e512, nullptr,
+                         nullptr, acts_all + (int64_t)t * E * 2048, c_all + (int64_t)t * e512,
+                         t > 0 ? c_all + (int64_t)(t - 1) * e512 : c_init, mask_all ? mask_all + (int64_t)t * E : nullptr,
+                         w.dgates + (int64_t)t * E * 2048, w.dc[0]);
+    }
+    for (int t = T - 1, cur = 0; t >= 1; --t, cur ^= 1) {
+      LstmBwdStep p;
+      p.dgates_t = w.dgates + (int64_t)t * E * 2048;
+      p.whh_t = w.wcat_t + (int64_t)L.xoff * 2048;
+      p.mask_t = mask_all ? mask_all + (int64_t)t * E : nullptr;
+      p.dh_heads = w.dh_heads + (int64_t)(t - 1) * e512;
+      p.dc_next = w.dc[cur];
+      p.acts = acts_all + (int64_t)(t - 1) * E * 2048;
+      p.c = c_all + (int64_t)(t - 1) * e512;
+      p.c_prev = t - 1 > 0 ? c_all + (int64_t)(t - 2) * e512 : c_init;
+      p.mask_prev = mask_all ? mask_all + (int64_t)(t - 1) * E : nullptr;
+      p.dgates_prev = w.dgates + (int64_t)(t - 1) * E * 2048;
+      p.dc_prev_out = w.dc[cur ^ 1];
+      const dim3 grid(512 / kSkCols);
+      if (E <= 4)
+        hipLaunchKernelGGL(lstm_bwd_skinny_kernel<4>, grid, dim3(256), 0, st, p, E);
+      else if (E <= 8)
+        hipLaunchKernelGGL(lstm_bwd_skinny_kernel<8>, grid, dim3(256), 0, st, p, E);
+      else
+        hipLaunchKernelGGL(lstm_bwd_skinny_kernel<kSkinnyRows>, grid, dim3(256), 0, st, p, E);
+    }
+  }
+  for (int t = T - 1, cur = 0; t >= 0 && E > kSkinnyRows; --t, cur ^= 1) {
     const bool last = (t == T - 1);
     const float* mask = mask_all ? mask_all + (int64_t)t * E : nullptr;
     const float* cprev = t > 0 ? c_all + (int64_t)(t - 1) * e512 : c_init;

@@ -1,0 +1,251 @@
+// vn_skinny.h — products of a few rows on the fp32 VALU (included by vn_policy.hip).
+//
+// A rollout step of E envs runs its conv_merge, LSTM-gate and head products with M = E rows.
+// For E <= kSkinnyRows the tensor-core tiles cannot fill the chip: the x6 path splits K into
+// slabs and needs a second launch to reduce them and apply the epilogue, and each of those
+// launches costs more than its arithmetic (the reference's own run is 4 envs). Here one
+// workgroup computes kSkCols output columns of all M rows over the WHOLE K range — A staged
+// in LDS chunk by chunk and read by every column group, B (weights, [N][K] k-contiguous) read
+// once — with plain fp32 FMAs (the products are exact fp32 arithmetic like the x6 path, summed
+// in another order), a 32-lane reduction, and the epilogue in the same launch. The LSTM step
+// also folds in the xcat build and the cell (one launch instead of four), and the BPTT step
+// its dh product and the next cell backward (one launch instead of three).
+#pragma once
+
+namespace vn {
+
+constexpr int kSkinnyRows = 16;  // M at or below which the skinny path runs
+constexpr int kSkCols = 8;       // output columns per workgroup: one 32-lane group each
+
+template <class EP>
+__device__ __forceinline__ void apply_epi(const EP& ep, int row, int col, float v) {
+  if constexpr (has_pre_col<EP>::value)
+    ep.post(row, col, v, ep.pre_col(col), 0);
+  else if constexpr (has_pre_row<EP>::value)
+    ep.post(row, col, v, ep.pre_row(row), 0);
+  else if constexpr (has_pre<EP>::value)
+    ep.post(row, col, v, ep.pre(row, col), 0);
+  else
+    ep(row, col, v, 0);
+}
+
+__device__ __forceinline__ float sum32(float v) {
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 32);
+  return v;
+}
+
+// acc[m] (m < M) += this lane's share of sum_k A[m][k] B[k] over k < K. A comes from
+// fill(m, k) -> f4 (k % 4 == 0, zeros past K), staged in As [MR][kc]; B is a 16-B aligned
+// row. Per chunk of kc <= kSkKB * 128 values the lane's B loads are issued first, then the
+// A loads of the chunk's staging, so both latencies are paid once (a chunk per memory round
+// trip, not per 128 values). All 256 threads of the workgroup call it (it synchronises).
+constexpr int kSkKB = 24;  // B f4 registers per lane: chunks of up to 3072 values
+
+template <int MR>
+constexpr int skinny_kc() {  // chunk length: kSkKB * 128 values, as the LDS allows (<= 128 KiB)
+  return (MR * kSkKB * 128 * 4 <= 128 * 1024) ? kSkKB * 128 : (128 * 1024 / (MR * 4)) / 128 * 128;
+}
+
+template <int MR, class FILL>
+__device__ __forceinline__ void skinny_dot(const FILL& fill, const float* __restrict__ B, int M, int K, float* As,
+                                           float (&acc)[MR]) {
+  constexpr int KC = skinny_kc<MR>(), NB = KC / 128;
+  const int tid = threadIdx.x, kl = tid & 31;
+  for (int k0 = 0; k0 < K; k0 += KC) {
+    const int kc = min(KC, K - k0);
+    f4 b[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+      if (4 * kl + 128 * i < kc) b[i] = *reinterpret_cast<const f4*>(B + k0 + 4 * kl + 128 * i);
+    __syncthreads();  // the previous chunk's reads are done
+    const int q4 = (kc + 3) / 4;
+    for (int i = tid; i < M * q4; i += 256) {
+      const int m = i / q4, q = i - m * q4;
+      *reinterpret_cast<f4*>(&As[m * KC + 4 * q]) = fill(m, k0 + 4 * q);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int kk = 4 * kl + 128 * i;
+      if (kk < kc) {
+#pragma unroll
+        for (int m = 0; m < MR; ++m) {
+          if (m < M) {
+            const f4 a = *reinterpret_cast<const f4*>(&As[m * KC + kk]);
+            float s = acc[m];
+            s = fmaf(a[0], b[i][0], s);
+            s = fmaf(a[1], b[i][1], s);
+            s = fmaf(a[2], b[i][2], s);
+            s = fmaf(a[3], b[i][3], s);
+            acc[m] = s;
+          }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < MR; ++m) acc[m] = sum32(acc[m]);
+}
+
+struct RowsFill {  // dense rows A [M][lda] (16-B aligned, lda % 4 == 0)
+  const float* A;
+  int64_t lda;
+  __device__ __forceinline__ f4 operator()(int m, int k) const {
+    return *reinterpret_cast<const f4*>(A + (int64_t)m * lda + k);
+  }
+};
+
+// C[m][col] = A[m] . B[col] for m < M <= MR, col < N; then the epilogue.
+template <int MR, class EP>
+__global__ __launch_bounds__(256) void skinny_kernel(const float* __restrict__ A, int64_t lda,
+                                                     const float* __restrict__ B, int64_t ldb, EP ep, int M, int N,
+                                                     int K) {
+  __shared__ __attribute__((aligned(16))) float As[MR * skinny_kc<MR>()];
+  const int cg = threadIdx.x >> 5, kl = threadIdx.x & 31;
+  const int col = blockIdx.x * kSkCols + cg;
+  float acc[MR];
+#pragma unroll
+  for (int m = 0; m < MR; ++m) acc[m] = 0.0f;
+  skinny_dot<MR>(RowsFill{A, lda}, B + (int64_t)min(col, N - 1) * ldb, M, K, As, acc);
+  if (kl == 0 && col < N) {
+#pragma unroll
+    for (int m = 0; m < MR; ++m)
+      if (m < M) apply_epi(ep, m, col, acc[m]);
+  }
+}
+
+template <class EP>
+inline void launch_skinny(const float* A, int64_t lda, const float* B, int64_t ldb, EP ep, int M, int N, int K,
+                          hipStream_t st) {
+  const dim3 grid((N + kSkCols - 1) / kSkCols);
+  if (M <= 4)
+    hipLaunchKernelGGL((skinny_kernel<4, EP>), grid, dim3(256), 0, st, A, lda, B, ldb, ep, M, N, K);
+  else if (M <= 8)
+    hipLaunchKernelGGL((skinny_kernel<8, EP>), grid, dim3(256), 0, st, A, lda, B, ldb, ep, M, N, K);
+  else
+    hipLaunchKernelGGL((skinny_kernel<kSkinnyRows, EP>), grid, dim3(256), 0, st, A, lda, B, ldb, ep, M, N, K);
+}
+
+// ---- LSTM step: xcat build + gates product + cell, one launch ----------------------
+struct XcatFill {  // xcat_t[m] = [x5 (512) | lra (A+1) | 0 pad | m_t h_{t-1} (512)] (vn_lstm.h)
+  const float* x5;
+  const float* lra;
+  const float* mask;
+  const float* h_prev;
+  int A1, xoff;
+  __device__ __forceinline__ float at(int m, int k) const {
+    if (k < 512) return x5[(int64_t)m * 512 + k];
+    if (k < 512 + A1) return lra ? lra[(int64_t)m * A1 + (k - 512)] : 0.0f;
+    if (k < xoff) return 0.0f;
+    return h_prev ? h_prev[(int64_t)m * 512 + (k - xoff)] * (mask ? mask[m] : 1.0f) : 0.0f;
+  }
+  __device__ __forceinline__ f4 operator()(int m, int k) const {
+    if (k + 3 < 512) return *reinterpret_cast<const f4*>(x5 + (int64_t)m * 512 + k);
+    if (k >= xoff && h_prev && (xoff & 3) == 0) {
+      const f4 h = *reinterpret_cast<const f4*>(h_prev + (int64_t)m * 512 + (k - xoff));
+      const float mk = mask ? mask[m] : 1.0f;
+      return f4{h[0] * mk, h[1] * mk, h[2] * mk, h[3] * mk};
+    }
+    return f4{at(m, k), at(m, k + 1), at(m, k + 2), at(m, k + 3)};
+  }
+};
+
+// Workgroup b: hidden units 2b, 2b+1; column group cg = (gate cg >> 1, unit 2b + (cg & 1)).
+template <int MR>
+__global__ __launch_bounds__(256) void lstm_step_skinny_kernel(XcatFill xf, int E, int xcat,
+                                                               const float* __restrict__ Wcat,
+                                                               const float* __restrict__ bih,
+                                                               const float* __restrict__ bhh,
+                                                               const float* __restrict__ c_prev, float* xc_out,
+                                                               float* acts, float* c_out, float* h_out) {
+  __shared__ __attribute__((aligned(16))) float As[MR * skinny_kc<MR>()];
+  __shared__ float gs[MR][kSkCols];
+  const int tid = threadIdx.x, cg = tid >> 5, kl = tid & 31;
+  const int gate = cg >> 1, unit = 2 * blockIdx.x + (cg & 1), col = gate * 512 + unit;
+  {  // this workgroup's slice of the xcat rows the backward keeps
+    const int64_t total = (int64_t)E * xcat, per = (total + gridDim.x - 1) / gridDim.x;
+    const int64_t lo = blockIdx.x * per, hi = min(total, lo + per);
+    for (int64_t i = lo + tid; i < hi; i += 256) {
+      const int m = (int)(i / xcat), k = (int)(i - (int64_t)m * xcat);
+      xc_out[i] = xf.at(m, k);
+    }
+  }
+  float acc[MR];
+#pragma unroll
+  for (int m = 0; m < MR; ++m) acc[m] = 0.0f;
+  skinny_dot<MR>(xf, Wcat + (int64_t)col * xcat, E, xcat, As, acc);
+  if (kl == 0) {
+    const float b0 = bih[col], b1 = bhh[col];
+#pragma unroll
+    for (int m = 0; m < MR; ++m)
+      if (m < E) gs[m][cg] = acc[m] + b0 + b1;  // EpiBias2's order
+  }
+  __syncthreads();
+  if (tid < 2 * E) {  // the cell of (env m, unit): lstm_cell_kernel's arithmetic
+    const int m = tid >> 1, u = tid & 1, j = 2 * blockIdx.x + u;
+    const float mk = xf.mask ? xf.mask[m] : 1.0f;
+    const float cp = c_prev ? c_prev[(int64_t)m * 512 + j] * mk : 0.0f;
+    const float i = sigmoidf_(gs[m][0 + u]), f = sigmoidf_(gs[m][2 + u]), g = tanhf(gs[m][4 + u]),
+                o = sigmoidf_(gs[m][6 + u]);
+    const float c = f * cp + i * g;
+    const float h = o * tanhf(c);
+    float* a4 = acts + (int64_t)m * 2048;
+    a4[j] = i;
+    a4[512 + j] = f;
+    a4[1024 + j] = g;
+    a4[1536 + j] = o;
+    c_out[(int64_t)m * 512 + j] = c;
+    h_out[(int64_t)m * 512 + j] = h;
+  }
+}
+
+// ---- BPTT step t: dh_{t-1} = m_t (dgates_t W_hh) and the cell backward of step t-1 --------
+struct LstmBwdStep {
+  const float* dgates_t;   // [E][2048] (read)
+  const float* whh_t;      // W_hh^T rows: [512][2048] (row j = the weights of hidden input j)
+  const float* mask_t;     // m_t [E] (may be NULL)
+  const float* dh_heads;   // step t-1's [E][512]
+  const float* dc_next;    // dc from step t's cell backward [E][512]
+  const float* acts;       // step t-1's [E][2048]
+  const float* c;          // c_{t-1} [E][512]
+  const float* c_prev;     // c_{t-2} (or c_init) [E][512] (may be NULL)
+  const float* mask_prev;  // m_{t-1} [E] (may be NULL)
+  float* dgates_prev;      // step t-1's [E][2048] (out)
+  float* dc_prev_out;      // [E][512] (out)
+};
+
+template <int MR>
+__global__ __launch_bounds__(256) void lstm_bwd_skinny_kernel(LstmBwdStep p, int E) {
+  __shared__ __attribute__((aligned(16))) float As[MR * skinny_kc<MR>()];
+  const int cg = threadIdx.x >> 5, kl = threadIdx.x & 31;
+  const int j = blockIdx.x * kSkCols + cg;
+  float acc[MR];
+#pragma unroll
+  for (int m = 0; m < MR; ++m) acc[m] = 0.0f;
+  skinny_dot<MR>(RowsFill{p.dgates_t, 2048}, p.whh_t + (int64_t)j * 2048, E, 2048, As, acc);
+  if (kl < MR && kl < E) {  // lane m of the group: env m (lstm_cell_bwd_kernel's arithmetic)
+    float v = 0.0f;
+#pragma unroll
+    for (int m = 0; m < MR; ++m)
+      if (m == kl) v = acc[m];
+    const int m = kl;
+    const int64_t idx = (int64_t)m * 512 + j;
+    const float dhn = v * (p.mask_t ? p.mask_t[m] : 1.0f);  // EpiLstmDh
+    const float mk = p.mask_prev ? p.mask_prev[m] : 1.0f;
+    const float* a4 = p.acts + (int64_t)m * 2048;
+    const float i = a4[j], f = a4[512 + j], g = a4[1024 + j], o = a4[1536 + j];
+    const float tc = tanhf(p.c[idx]);
+    const float dh = p.dh_heads[idx] + dhn;
+    const float dc = p.dc_next[idx] + dh * o * (1.0f - tc * tc);
+    const float cp = p.c_prev ? p.c_prev[idx] * mk : 0.0f;
+    float* d4 = p.dgates_prev + (int64_t)m * 2048;
+    d4[j] = dc * g * i * (1.0f - i);
+    d4[512 + j] = dc * cp * f * (1.0f - f);
+    d4[1024 + j] = dc * i * (1.0f - g * g);
+    d4[1536 + j] = dh * tc * o * (1.0f - o);
+    p.dc_prev_out[idx] = dc * f * mk;
+  }
+}
+
+}  // namespace vn

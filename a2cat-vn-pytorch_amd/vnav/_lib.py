@@ -43,6 +43,24 @@ class SceneDesc(ctypes.Structure):
     ]
 
 
+class A2CStep(ctypes.Structure):
+    """vn_a2c_step (include/vnav.h)."""
+    _fields_ = [
+        ("policy_out", c_void_p),
+        ("num_actions", c_int),
+        ("seed", c_uint64),
+        ("counter_base_dev", c_void_p),
+        ("counter", c_uint64),
+        ("actions", c_void_p),
+        ("prev_action", c_void_p),
+        ("prev_reward", c_void_p),
+        ("prev_mask", c_void_p),
+        ("lra_next", c_void_p),
+        ("mask_next", c_void_p),
+        ("episode_stats_env", c_void_p),
+    ]
+
+
 # name -> (restype, argtypes). Every symbol here is declared in include/vnav.h.
 SIGNATURES = {
     "vn_version": (ctypes.c_char_p, []),
@@ -70,6 +88,7 @@ SIGNATURES = {
     "vn_error_flags_sync": (c_int, [c_void_p, P(c_uint32), c_int]),
     "vn_num_envs": (c_int, [c_void_p]),
     "vn_gather_rows": (c_int, [c_void_p, c_int64, c_void_p, c_int, c_void_p, c_void_p]),
+    "vn_step_a2c": (c_int, [c_void_p, P(A2CStep), c_void_p, c_void_p, c_void_p, c_void_p]),
 }
 
 SIGNATURES.update({
@@ -125,6 +144,7 @@ SIGNATURES.update({
     "vn_policy_sample_dev": (c_int, [c_void_p, c_int, c_int, c_uint64, c_void_p, c_uint64, c_void_p, c_void_p,
                                      c_void_p, c_void_p, c_void_p]),
     "vn_trace_marker": (c_int, [c_int, c_void_p]),
+    "vn_a2c_episode_stats": (c_int, [c_void_p, c_int, c_void_p, c_void_p]),
     "vn_rmsprop_step_dev": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_float, c_void_p, c_void_p, c_float,
                                     c_float, c_void_p]),
 })

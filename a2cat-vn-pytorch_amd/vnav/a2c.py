@@ -166,6 +166,10 @@ class A2CTrainer:
         self._model_view = None
         arena, fb, _, _ = env.frame_arena()
         self._arena, self._fb = arena, fb
+        # the rollout's fused env steps (vn_step_a2c): sampling + step + bookkeeping, one launch
+        # per step; per-env episode statistics reduced once per rollout (vn_a2c_episode_stats)
+        self.stats_env = torch.zeros((3, E), dtype=torch.float32, **kw)
+        self._a2c_steps = [self._a2c_step_args(t) for t in range(T)]
         env.observe(gather=False)  # refresh the obs row buffers for the first forward
         self.num_updates = 0
         self.total_steps = 0
@@ -228,6 +232,28 @@ class A2CTrainer:
     def _stream(self):
         return _lib.stream_ptr(self.device)
 
+    def _a2c_step_args(self, t):
+        """vn_a2c_step of rollout step t: sample from out[t], write actions[t], the next step's
+        (last action, last reward) * mask and mask (the bootstrap slots after the last step),
+        the recurrent carries and the per-env episode statistics."""
+        E, T = self.env.num_envs, self.num_steps
+        sl = slice(t * E, (t + 1) * E)
+        s = _lib.A2CStep()
+        s.policy_out = self.out[sl].data_ptr()
+        s.num_actions = self.A
+        s.seed = vdist.rank_seed(self.seed, self.rank)
+        s.counter_base_dev = self.sched.data_ptr() + 2 * self.sched.element_size()
+        s.counter = t
+        s.actions = self.actions[sl].data_ptr()
+        if self.recurrent:
+            s.prev_action = self.prev_action.data_ptr()
+            s.prev_reward = self.prev_reward.data_ptr()
+            s.prev_mask = self.prev_mask.data_ptr()
+            s.lra_next = (self.lra[t + 1] if t + 1 < T else self.boot_lra).data_ptr()
+            s.mask_next = (self.masks[t + 1] if t + 1 < T else self.boot_mask).data_ptr()
+        s.episode_stats_env = self.stats_env.data_ptr()
+        return s
+
     def _frames(self, img_rows, goal_rows):
         return frames_from_rows(self._arena, self._fb, img_rows, goal_rows)
 
@@ -278,22 +304,15 @@ class A2CTrainer:
         E, T, A = env.num_envs, self.num_steps, self.A
         N = T * E
         info = env._info
-        self.episode_stats.zero_()
         _lib.check(lib.vn_a2c_schedule(_lib.ptr(self.sched), _lib.ptr(self.lr_dev), ctypes.c_double(self.learning_rate),
                                        ctypes.c_double(self.max_time_steps), ctypes.c_int64(N * self.world), T,
                                        self._stream()), "vn_a2c_schedule")
-        ctr_base = ctypes.c_void_p(self.sched.data_ptr() + 2 * self.sched.element_size())
         for t in range(T):
             sl = slice(t * E, (t + 1) * E)
             if t == 0:  # later steps' rows are written into their slots by the env step before them
                 self.rows_img[sl].copy_(info["img_row"])
                 self.rows_goal[sl].copy_(info["goal_row"])
             self._policy_step(t, self._frames(self.rows_img[sl], self.rows_goal[sl]))
-            # Philox counter = updates * T + t (base from the device schedule)
-            _lib.check(lib.vn_policy_sample_dev(_lib.ptr(self.out[sl]), E, A,
-                                                ctypes.c_uint64(vdist.rank_seed(self.seed, self.rank)), ctr_base,
-                                                ctypes.c_uint64(t), _lib.ptr(self.actions[sl]), None, None, None,
-                                                self._stream()), "vn_policy_sample_dev")
             # the emitted frames' arena rows go straight into step t + 1's slots (the last step's
             # into the env's own info rows: the bootstrap and the next rollout read them there)
             nxt = slice((t + 1) * E, (t + 2) * E)
@@ -301,19 +320,12 @@ class A2CTrainer:
                 env.set_row_outputs(self.rows_img[nxt], self.rows_goal[nxt])
             else:
                 env.set_row_outputs(None, None)
-            env.step(self.actions[sl], out=dict(reward=self.rewards[t], done=self.dones[t], state=self.states),
-                     gather=False)
-            # next step's (last action, last reward) * mask and mask (bootstrap slots after the
-            # last step), the prev_* carries, and the finished-episode statistics: one kernel
-            rec = self.recurrent
-            lra_n = (self.lra[t + 1] if t + 1 < T else self.boot_lra) if rec else None
-            mask_n = (self.masks[t + 1] if t + 1 < T else self.boot_mask) if rec else None
-            _lib.check(lib.vn_a2c_step_post(
-                _lib.ptr(self.actions[sl]), _lib.ptr(self.rewards[t]), _lib.ptr(self.dones[t]),
-                _lib.ptr(info["ep_return"]), _lib.ptr(info["ep_length"]), E, A,
-                _lib.ptr(self.prev_action) if rec else None, _lib.ptr(self.prev_reward) if rec else None,
-                _lib.ptr(self.prev_mask) if rec else None, _lib.ptr(lra_n), _lib.ptr(mask_n),
-                _lib.ptr(self.episode_stats), self._stream()), "vn_a2c_step_post")
+            # one launch: the categorical draw from out[t] (Philox counter = updates * T + t from
+            # the device schedule), the index-only env step, and the next step's recurrent
+            # inputs, carries and episode statistics
+            env.step_a2c(self._a2c_steps[t], self.rewards[t], self.dones[t], self.states)
+        _lib.check(lib.vn_a2c_episode_stats(_lib.ptr(self.stats_env), E, _lib.ptr(self.episode_stats), self._stream()),
+                   "vn_a2c_episode_stats")
         # bootstrap value of the final observation
         self._bootstrap(self._frames(info["img_row"], info["goal_row"]))
 

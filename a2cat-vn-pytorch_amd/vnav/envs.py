@@ -291,6 +291,14 @@ class VectorEnv:
             return (img, goal) + self._gather_aux(), reward, done, info
         return (img, goal), reward, done, info
 
+    def step_a2c(self, a2c, reward, done, state):
+        """The trainer's rollout step (vn_step_a2c): the actions are sampled in the step from
+        the policy outputs named by ``a2c`` (a prepared _lib.A2CStep whose buffers the caller
+        keeps alive), index-only, with the per-step bookkeeping fused. reward / done / state
+        are the caller's [E] buffers (checked once by the caller)."""
+        _lib.check(self.lib.vn_step_a2c(self._ctx, ctypes.byref(a2c), _lib.ptr(reward), _lib.ptr(done),
+                                        _lib.ptr(state), self._stream()), "vn_step_a2c")
+
     def random_actions(self, step, out=None):
         out = torch.empty(self.num_envs, dtype=torch.int32, device=self.device) if out is None else out
         _lib.check(self.lib.vn_random_actions(self._ctx, _lib.ptr(out), ctypes.c_uint64(int(step)), self._stream()),

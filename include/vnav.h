@@ -107,6 +107,32 @@ int vn_observe(vn_ctx* ctx, uint8_t* obs_dev, uint8_t* goal_dev, int32_t* state_
 int vn_step(vn_ctx* ctx, const int32_t* actions_dev, uint8_t* obs_dev, uint8_t* goal_dev,
             float* reward_dev, uint8_t* done_dev, int32_t* state_dev, vn_stream_t stream);
 
+/* The A2C rollout's env step (the trainer's fast path; vn_step stays the gym/VecEnv
+ * boundary): the action of env e is sampled in the step from the policy's output row e
+ * (categorical over logits 0..A-1 of policy_out [E][8], Philox stream 3 with counter
+ * (e, *counter_base_dev + counter), key seed — the draw of vn_policy_sample_dev), the
+ * index-only step runs on it, and the per-step bookkeeping of vn_a2c_step_post follows
+ * in the same launch: the next step's recurrent inputs (last action one-hot and reward,
+ * times the episode mask m = 1 - done) and the finished-episode statistics accumulated per
+ * env into episode_stats_env [3][E] (count, return sum, length sum; reduced and cleared by
+ * vn_a2c_episode_stats). Optional outputs may be NULL. */
+typedef struct vn_a2c_step {
+  const float* policy_out;          /* [E][8] */
+  int num_actions;                  /* 1..7 */
+  uint64_t seed;
+  const int64_t* counter_base_dev;  /* may be NULL (base 0) */
+  uint64_t counter;
+  int32_t* actions;                 /* [E] sampled actions (out) */
+  int64_t* prev_action;             /* [E] */
+  float* prev_reward;               /* [E] */
+  float* prev_mask;                 /* [E] */
+  float* lra_next;                  /* [E][A+1] */
+  float* mask_next;                 /* [E] */
+  float* episode_stats_env;         /* [3][E], accumulated */
+} vn_a2c_step;
+int vn_step_a2c(vn_ctx* ctx, const vn_a2c_step* a2c, float* reward_dev, uint8_t* done_dev,
+                int32_t* state_dev, vn_stream_t stream);
+
 /* Optional persistent per-env info outputs written by every vn_step (any may be NULL):
  *   ep_return/ep_length: the finished episode's sum of rewards / length where done
  *     (RewardCollector statistics, experiments/thor_cached_auxiliary.py:60);
@@ -313,6 +339,9 @@ int vn_a2c_step_post(const int32_t* actions, const float* rewards, const uint8_t
                      const float* ep_return, const int32_t* ep_length, int E, int num_actions,
                      int64_t* prev_action, float* prev_reward, float* prev_mask, float* lra_next,
                      float* mask_next, float* episode_stats3, vn_stream_t stream);
+/* stats3 = the fixed-order sums over envs of episode_stats_env [3][E] (vn_step_a2c's
+ * accumulators: finished-episode count, return sum, length sum), which are then zeroed. */
+int vn_a2c_episode_stats(float* episode_stats_env, int E, float* stats3, vn_stream_t stream);
 /* scalars2 = (total norm of scale*grads, clip coefficient) computed on the device. */
 int vn_grad_norm(const float* grads, int64_t n, float scale, float max_norm, double* partial_512,
                  float* scalars2, vn_stream_t stream);

@@ -461,3 +461,51 @@ def test_curriculum_maze_distribution_matches_reference(golden):
         ref[lookup[oe.sample_initial_position(maze, dist, goal, opt, rng=rng)]] += 1
     chi2r = (((ref[nz] - w[nz] * 4000) ** 2) / (w[nz] * 4000)).sum()
     assert chi2r < dof + 6 * np.sqrt(2 * dof)
+
+
+def test_maze_config_c1_16_envs(golden):
+    """Config C1's shape (graph/maze_graph.py 8x8 maze, 16 parallel envs): 16 SimpleGraphEnv
+    instances (graph/env.py:73-143) — each with its own start sequence drawn by the reference
+    sampler sample_initial_position (graph/util.py:88-117, restated in oracle/envs.py and
+    pinned to the reference's draws by test_oracle_goldens) and its own random actions —
+    against one 16-env VectorEnv replaying those starts: reward bits, done, the emitted state
+    and observation (render / 255) at every step of every env."""
+    vnav = _vnav()
+    m = golden("maze.npz")
+    maze, goal = m["maze"], tuple(m["goal"].tolist())
+    dist = m["distances"]
+    scene = vnav.maze_scene(maze, goal)
+    lookup = {p: i for i, p in enumerate(scene.locations)}
+    g = scene.goals[0]
+    E, T, L = 16, 400, 400
+    starts = []
+    for e in range(E):
+        rs = np.random.RandomState(100 + e)
+        starts.append([tuple(oe.sample_initial_position(maze, dist, goal, rng=rs)) for _ in range(L)])
+    sched = np.array([[(lookup[s], g) for s in st] for st in starts], dtype=np.int32)
+    env = vnav.VectorEnv([scene], E, seed=0, tasks=[(0, g)], max_episode_steps=0)
+    env.set_schedule(sched)
+    img, _ = env.reset()
+    oracles = [oe.SimpleGraphEnvOracle(maze, goal) for _ in range(E)]
+    nres = [0] * E
+    obs = [o.reset(starts[e][0]) for e, o in enumerate(oracles)]
+    assert np.array_equal(img.cpu().numpy().astype(np.float32) / 255.0, np.stack(obs))
+    rng = np.random.RandomState(7)
+    for t in range(T):
+        a = rng.randint(0, 4, size=E)
+        (img, _), reward, done, info = env.step(torch.as_tensor(a, dtype=torch.int32, device="cuda"))
+        rb, dn = reward.cpu().numpy().view(np.uint32), done.cpu().numpy()
+        ts, st = info["terminal_state"].cpu().numpy(), info["state"].cpu().numpy()
+        frames = img.cpu().numpy().astype(np.float32) / 255.0
+        for e in range(E):
+            ob, r, d, inf = oracles[e].step(int(a[e]))
+            assert rb[e] == np.float32(r).view(np.uint32), (t, e)
+            assert bool(dn[e]) == d, (t, e)
+            assert scene.locations[ts[e]] == tuple(inf["state"]), (t, e)
+            assert np.array_equal(scene.observations[ts[e]].astype(np.float32) / 255.0, ob), (t, e)
+            if d:  # baselines auto-reset: the next start of this env's sequence
+                nres[e] += 1
+                ob = oracles[e].reset(starts[e][nres[e]])
+                assert st[e] == lookup[starts[e][nres[e]]], (t, e)
+            assert np.array_equal(frames[e], ob), (t, e)
+    assert sum(nres) >= E  # episodes finished and restarted on every env on average

@@ -260,17 +260,20 @@ def test_174_batch512_rows_aux_vs_fp64_oracle():
     print("174x174 n=512 + aux: worst gradient error %.3g of scale; tie flips %s" % (worst, flips))
 
 
-def test_lstm_core_1024_envs_vs_fp64_torch_lstm():
+@pytest.mark.parametrize("E", [1024, 16, 5])
+def test_lstm_core_vs_fp64_torch_lstm(E):
     """The recurrent core at 1024 envs x 3 steps (gates / dh products past the split-K
-    threshold, the weight gradient over 3072 rows): per-step (h, c), the heads on h, and
-    the gradients of W_ih, W_hh, both biases, the heads and dL/dZ5 (masked by the
-    features' ReLU) vs torch's float64 nn.LSTM with the restated MaskedRNN convention."""
+    threshold, the weight gradient over 3072 rows) and at 16 / 5 envs (the fused VALU
+    steps of vn_skinny.h: xcat + gates + cell, dh product + next cell backward): per-step
+    (h, c), the heads on h, and the gradients of W_ih, W_hh, both biases, the heads and
+    dL/dZ5 (masked by the features' ReLU) vs torch's float64 nn.LSTM with the restated
+    MaskedRNN convention."""
     from vnav.policy import PolicyNet
     net = PolicyNet((84, 84), 4, recurrent=True)
     params = net.init_params(3)
     with torch.no_grad():
         params.add_(torch.randn(params.shape, generator=torch.Generator().manual_seed(2)).cuda() * 0.01)
-    T, E, A = 3, 1024, 4
+    T, A = 3, 4
     N = T * E
     L = net.lstm
     g = torch.Generator(device="cuda").manual_seed(4)
@@ -339,7 +342,7 @@ def test_lstm_core_1024_envs_vs_fp64_torch_lstm():
         errs[k + ".bias"] = _err(mine[k + ".bias"].numpy(), mod.bias.grad.numpy())
     bad = {k: "%.3g" % e for k, e in errs.items() if e > 1e-4}
     assert not bad, bad
-    print("LSTM E=1024 T=3: worst gradient error %.3g of scale" % max(errs.values()))
+    print("LSTM E=%d T=3: worst gradient error %.3g of scale" % (E, max(errs.values())))
 
 
 def test_logged_run_shape_trainer_update_vs_fp64_oracle():
