@@ -374,6 +374,10 @@ def main():
     for t in range(args.warmup + args.steps):
         env.random_actions(t, out=actions[t])
 
+    # the device-copy reference rate runs before the warmup steps: ~3 ms of HBM-saturating
+    # copies, so the timed window does not start on a GPU that has been idle since the scene
+    # synthesis (the driver's 5-step warmup alone is 0.3 ms of work)
+    copy_gbs = device_copy_rate(dev, E * 2 * fb)
     step = 0
     for _ in range(args.warmup):
         env.step(actions[step], out=out)
@@ -413,7 +417,6 @@ def main():
         elapsed, kern_ms = float(t[0]), float(t[1])
     flags = env.error_flags()
     del env, out
-    copy_gbs = device_copy_rate(dev, E * 2 * fb)
     train = train_ff = train_ref = train_ref4 = train_c5 = None
     if args.train_steps > 0:
         torch.cuda.empty_cache()

@@ -21,6 +21,7 @@ def test_registry_and_hyperparameters():
     assert (cls.max_time_steps, cls.episode_log_interval, cls.saving_period, cls.save) == (2e6, 10, 100000, True)
     assert (cls.num_processes, cls.num_steps, cls.gamma, cls.learning_rate) == (4, 20, 0.99, 7e-4)
     assert (cls.rms_alpha, cls.rms_epsilon, cls.max_gradient_norm) == (0.99, 1e-5, 0.5)
+    assert (cls.value_coefficient, cls.entropy_coefficient) == (0.5, 0.001)
     assert (cls.auxiliary_weight, cls.hardness, cls.recurrent) == (0.1, 0.01, True)
     with pytest.raises(KeyError):
         train.make_trainer("no-such-experiment")

@@ -15,7 +15,11 @@ images per (cell, rotation); the UNREAL replay losses (pixel control, reward pre
 value replay) are deep_rl's and not part of the engine. What is compared is the shape of
 the curve: episode length from the random-walk level down to a few steps, reward -> 1.
 
-    python tools/replicate_log.py [updates] [out.csv]
+    python tools/replicate_log.py [updates] [out.csv] [--entropy-coef C] [--seed S] [--aux-weight W]
+
+The options exist for the late-entropy investigation (DESIGN.md "End-to-end check"): the same
+run with another entropy coefficient / seed / aux weight. Each 10k-step row also carries the
+mean pre-clip gradient norm and the fraction of updates the 0.5 clip scaled down.
 """
 import csv
 import os
@@ -64,13 +68,21 @@ def make_scene(seed=0, grid=(16, 16), frame=(174, 174)):
 
 
 def main():
-    updates = int(sys.argv[1]) if len(sys.argv) > 1 else 12500
-    out = sys.argv[2] if len(sys.argv) > 2 else None
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("updates", nargs="?", type=int, default=12500)
+    ap.add_argument("out", nargs="?", default=None)
+    ap.add_argument("--entropy-coef", type=float, default=0.01)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--aux-weight", type=float, default=0.1)
+    a = ap.parse_args()
+    updates, out = a.updates, a.out
     torch.cuda.set_device(0)
     scene = make_scene()
-    env = vnav.VectorEnv([scene], 4, seed=1, max_episode_steps=900)
+    env = vnav.VectorEnv([scene], 4, seed=1 + a.seed, max_episode_steps=900)
     env.set_complexity(0.01)
-    tr = vnav.A2CTrainer(env, num_steps=20, seed=0, max_time_steps=2e6, recurrent=True, aux_weight=0.1)
+    tr = vnav.A2CTrainer(env, num_steps=20, seed=a.seed, max_time_steps=2e6, recurrent=True,
+                         aux_weight=a.aux_weight, entropy_coefficient=a.entropy_coef)
     ref = reference_curve()
     rows = []
     t0 = time.time()
@@ -85,7 +97,10 @@ def main():
             row = dict(step=m["step"], episodes=eps, reward=rsum / eps if eps else float("nan"),
                        episode_length=lsum / eps if eps else float("nan"),
                        entropy=float(np.mean([x["entropy"] for x in window])),
-                       aux_loss=float(np.mean([x["aux_loss"] for x in window])), wall_s=time.time() - t0)
+                       aux_loss=float(np.mean([x.get("aux_loss", 0.0) for x in window])),
+                       grad_norm=float(np.mean([x["grad_norm"] for x in window])),
+                       clipped=float(np.mean([x["grad_norm"] > tr.max_gradient_norm for x in window])),
+                       wall_s=time.time() - t0)
             rr = [r for r in ref if r[0] <= row["step"]]
             if rr:
                 row.update(ref_reward=rr[-1][1], ref_episode_length=rr[-1][2], ref_entropy=rr[-1][3],
