@@ -27,9 +27,15 @@ __host__ __device__ constexpr int conv1_koff(int k) {
   return k >= 147 ? 0 : (k / 21) * W * 3 + ((k / 3) % 7) * 3 + (k % 3);
 }
 
+// Frame f of a wave-uniform work item (every caller's f is uniform). The arena row index is
+// read with a scalar load (constant address space: lgkmcnt): as a vector load its address
+// dependence made the wave wait for vmcnt(0) — for every load and store in flight, e.g. the
+// weight gradient's dZ prefetch — at each call.
 __device__ __forceinline__ const uint8_t* frame_ptr(const FrameSrc& src, int f) {
+  f = __builtin_amdgcn_readfirstlane(f);
   const int smp = f >> 1, h = f & 1;
-  const int64_t row = src.rows[h] ? (int64_t)src.rows[h][smp] : (int64_t)smp;
+  typedef __attribute__((address_space(4))) const int32_t cint32;
+  const int64_t row = src.rows[h] ? (int64_t)((cint32*)src.rows[h])[smp] : (int64_t)smp;
   return src.base[h] + row * src.stride;
 }
 
@@ -468,17 +474,19 @@ __global__ __launch_bounds__(256) void conv1_wgrad_x3_kernel(FrameSrc src, int n
   // vmcnt retires loads in issue order, so the next item's tasks are issued one per step
   // between the dZ loads (a whole-frame prefetch would stall the first dZ use behind it).
   uint32_t pre[NT][NDW];
+  // Loads are issued unconditionally from clamped addresses (a task past the band reloads the
+  // band's last task, dwords past the window repeat its last dword; stage_q masks both): loads
+  // under a branch cannot be counted by the compiler, which then waits for vmcnt(0) — the dZ
+  // loads in flight included — where their registers are next written or read.
   auto load_task = [&](int r, int it) {
-    const int t = tid + r * 256;
     const int band = it - (it / NB) * NB;
-    if (t < band_rows(band) * PAIRS) {
-      const int y = t / PAIRS, m = t - (t / PAIRS) * PAIRS;
-      const int64_t off = (int64_t)(4 * BR * band + y) * RB + m * 24;
-      const uint32_t* s4 = reinterpret_cast<const uint32_t*>(frame_ptr(src, it / NB) + (off & ~(int64_t)3));
-      const int nbytes = (int)(off & 3) + min(24, RB - m * 24);  // bytes of the aligned window
+    const int t = min(tid + r * 256, band_rows(band) * PAIRS - 1);
+    const int y = t / PAIRS, m = t - (t / PAIRS) * PAIRS;
+    const int64_t off = (int64_t)(4 * BR * band + y) * RB + m * 24;
+    const uint32_t* s4 = reinterpret_cast<const uint32_t*>(frame_ptr(src, it / NB) + (off & ~(int64_t)3));
+    const int nbytes = (int)(off & 3) + min(24, RB - m * 24);  // bytes of the aligned window
 #pragma unroll
-      for (int q = 0; q < NDW; ++q) pre[r][q] = 4 * q < nbytes ? s4[q] : 0u;
-    }
+    for (int q = 0; q < NDW; ++q) pre[r][q] = s4[min(q, (nbytes - 1) >> 2)];
   };
   auto stage_q = [&](int band) {
 #pragma unroll
@@ -513,17 +521,18 @@ __global__ __launch_bounds__(256) void conv1_wgrad_x3_kernel(FrameSrc src, int n
     }
   };
   float zc[8], zn[8];  // steps s and s + 4 in flight
+  // group g's 8 pixels of dZ, unconditionally (a group past the band or a pixel past its row
+  // reloads a valid pixel); step() zeroes what is not the group's (z_valid)
   auto load_z = [&](float (&z)[8], int f, int oy0, int ng, int s) {
-    const int g = 2 * s + h, oy = oy0 + g / GPR, ox0 = 8 * (g - (g / GPR) * GPR);
+    const int g = min(2 * s + h, ng - 1), oy = oy0 + g / GPR, ox0 = 8 * (g - (g / GPR) * GPR);
     const float* zf = dZ + ((int64_t)f * NPIX + oy * OW + ox0) * 32 + c32;
-    const int nv = g < ng ? min(8, OW - ox0) : 0;
-    if (nv == 8) {  // whole group: eight loads off one address
+    const int nv = min(8, OW - ox0);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) z[j] = zf[j * 32];
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) z[j] = j < nv ? zf[j * 32] : 0.0f;
-    }
+    for (int j = 0; j < 8; ++j) z[j] = zf[min(j, nv - 1) * 32];
+  };
+  auto z_valid = [&](int ng, int s) {  // pixels of step s's group that are the band's
+    const int g = 2 * s + h, ox0 = 8 * (g - (g / GPR) * GPR);
+    return g < ng ? min(8, OW - ox0) : 0;
   };
   if ((int)blockIdx.x < n_items)
 #pragma unroll
@@ -542,8 +551,9 @@ __global__ __launch_bounds__(256) void conv1_wgrad_x3_kernel(FrameSrc src, int n
     int ns = 0;  // steps this wave has run in the item
     auto step = [&](int s, float (&z)[8]) {
       union { uint16_t u[8]; bf16x8 v; } a0, a1, a2;
+      const int nvz = z_valid(ng, s);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) split3_bf16(z[j], a0.u[j], a1.u[j], a2.u[j]);
+      for (int j = 0; j < 8; ++j) split3_bf16(j < nvz ? z[j] : 0.0f, a0.u[j], a1.u[j], a2.u[j]);
 #pragma unroll
       for (int r = 0; r < NT; ++r)
         if (ns == r && inext < n_items) load_task(r, inext);
@@ -1216,6 +1226,200 @@ __global__ __launch_bounds__(512, 2) void conv2_fwd_x6_kernel(const float* __res
   for (int it = blockIdx.x; it < n_items; it += 2 * gridDim.x) {
     item(std::integral_constant<int, 0>{}, it);
     if (it + (int)gridDim.x < n_items) item(std::integral_constant<int, 1>{}, it + gridDim.x);
+  }
+}
+
+// ---- conv2 forward, 42x42 -> 20x20 maps (174x174 frames): one frame streamed per workgroup --
+// The banded kernel above re-stages the two X1 rows shared by neighbouring bands and holds a
+// 4-way partial sum per pixel; at one 147 KB workgroup per CU it ran no faster than the generic
+// im2col product (whose A operand is re-split at each of its 4 uses). This kernel walks the
+// bands of a frame in order and keeps the X1 rows in a 14-slot LDS ring (split once into three
+// bf16 planes [slot][x & 1][x >> 1][ci], pixel stride 40 as above): band b (output rows 3b ..
+// 3b+2) reads X1 rows 6b .. 6b+7, of which only 6 are new (8 for a frame's first band, 4 for its
+// last), so every X1 value is loaded from HBM and split exactly once. Slot = row mod 14: the
+// rows of band b and the new rows of band b+1 never share a slot, also across a frame boundary
+// (42 = 3 x 14). Wave w has role (co tile ct = w & 1, kernel-row half kh = (w >> 1) & 1) with
+// its 8 taps' split weights in registers (96 VGPRs), and pixel tiles {w >> 2, (w >> 2) + 2} of
+// the band (<= 64 pixels = 4 tiles of 16). The kh = 1 wave of a (ct, tile) writes its partial
+// sum to LDS (double-buffered by band parity), the kh = 0 wave adds it to its own after the
+// band's barrier, then bias + ReLU and a 16-B store per lane. Schedule per band b, per wave:
+// MFMA(b) -> partial(b) -> split of band b+1's rows (prefetched into registers two bands ahead)
+// -> loads of band b+3's rows -> barrier -> epilogue(b); one barrier per band, and a wave's
+// split runs under the other wave's MFMAs on its SIMD.
+struct Conv2Ring42 {
+  static constexpr int IH = 42, IW = 42, OH = 20, OW = 20, BR = 3, NB = 7, SLOTS = 14;
+  static constexpr int WH = 21, PSX = 32, RSP = 2 * WH * PSX;  // plane row stride (bf16), unpadded
+  static constexpr int PL = SLOTS * RSP;                       // plane size (bf16)
+  static constexpr int TP = 64, PP = 36;                       // padded band pixels; partial row (floats)
+  static constexpr int NV = (8 * IW * 8 + 511) / 512;          // prefetched f4 per thread (<= 8 new rows)
+  static constexpr size_t LDS = (size_t)3 * PL * 2 + (size_t)2 * TP * PP * 4;
+  static_assert(IH % SLOTS == 0 && LDS <= 160 * 1024, "ring geometry");
+  __host__ __device__ static constexpr int new_lo(int b) { return b == 0 ? 0 : 2 * BR * b + 2; }
+  __host__ __device__ static constexpr int new_hi(int b) { return 2 * BR * b + 2 * BR + 2 < IH ? 2 * BR * b + 2 * BR + 2 : IH; }
+  // 16-B chunk swizzle of X1 row y, plane column xi: chunk q of a pixel is stored at q ^ swz.
+  // With the band's tiles (rows 0-2 at ox 0-15, then ox 16-19 of all rows) every 16-lane group
+  // of a B-fragment ds_read_b128 and of the split's ds_write_b64 lands on distinct banks
+  // (exhaustive check over bands, taps and tiles in tools/ring_banks.py).
+  __device__ static int swz(int y, int xi) { return 2 * (((xi >> 2) ^ (y >> 1)) & 1); }
+};
+
+template <int IH, int IW, int OH, int OW>
+constexpr bool conv2_fwd_ring_fits() {
+  return IH == 42 && IW == 42 && OH == 20 && OW == 20;
+}
+
+__global__ __launch_bounds__(512, 1) void conv2_fwd_ring_kernel(const float* __restrict__ X1,
+                                                                const float* __restrict__ W2,
+                                                                const float* __restrict__ bias,
+                                                                float* __restrict__ X2, int n_frames) {
+  using R = Conv2Ring42;
+  constexpr int IW = R::IW, OW = R::OW, NB = R::NB, WH = R::WH, PSX = R::PSX, RSP = R::RSP, PL = R::PL;
+  constexpr int NV = R::NV, PP = R::PP, TP = R::TP, NP = R::OH * R::OW;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem_r2[];
+  uint16_t* xs = reinterpret_cast<uint16_t*>(smem_r2);
+  float* part = reinterpret_cast<float*>(smem_r2 + (size_t)3 * PL * 2);  // [2][TP][PP]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ct = wave & 1, kh = (wave >> 1) & 1, tsel = wave >> 2;
+  const int i16 = lane & 15, q = lane >> 4;
+  bf16x8_t wf[8][3];  // [tap i: ky = 2kh + (i >> 2), kx = i & 3][term]: A[co = ct*16 + i16][k = ci 8q .. 8q+7]
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    union { uint16_t u[8]; bf16x8_t v; } t0, t1, t2;
+    const float* wp = W2 + (ct * 16 + i16) * 512 + ((2 * kh + (i >> 2)) * 4 + (i & 3)) * 32 + 8 * q;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) split3_bf16(wp[j], t0.u[j], t1.u[j], t2.u[j]);
+    wf[i][0] = t0.v;
+    wf[i][1] = t1.v;
+    wf[i][2] = t2.v;
+  }
+  const f4 b4 = *reinterpret_cast<const f4*>(bias + ct * 16 + 4 * q);
+  // make the bias land here: its first use sits in the loop's epilogue, where the compiler
+  // cannot tell it from the band prefetches in flight and would wait for vmcnt(0)
+  asm volatile("" ::"v"(b4[0]), "v"(b4[1]), "v"(b4[2]), "v"(b4[3]));
+  // this workgroup's items: k -> (frame blockIdx.x + (k / NB) * gridDim.x, band k % NB)
+  const int my_frames = (int)blockIdx.x < n_frames ? (n_frames - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  const int n_items = my_frames * NB;
+  auto frame_of = [&](int k) { return (int)blockIdx.x + (k / NB) * (int)gridDim.x; };
+  f4 pre[2][NV];
+  auto load_item = [&](f4 (&pr)[NV], int k) {
+    const int b = k % NB, lo = R::new_lo(b);
+    const int nv = (R::new_hi(b) - lo) * IW * 8;
+    const f4* s4 = reinterpret_cast<const f4*>(X1 + ((int64_t)frame_of(k) * R::IH + lo) * IW * 32);
+    // unconditional (clamped) loads: with loads under a branch the compiler cannot count
+    // them and waits for vmcnt(0) — this band's and the next band's loads — at the split
+#pragma unroll
+    for (int j = 0; j < NV; ++j) pr[j] = s4[min(tid + j * 512, nv - 1)];
+  };
+  auto split_item = [&](const f4 (&pr)[NV], int k) {
+    const int b = k % NB, lo = R::new_lo(b);
+    const int nv = (R::new_hi(b) - lo) * IW * 8;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int i = tid + j * 512;
+      if (i < nv) {
+        const int c4 = i & 7, px = i >> 3, y = lo + px / IW, x = px - (px / IW) * IW;
+        uint2 t0, t1, t2;
+        split3_pack(pr[j], t0, t1, t2);
+        uint16_t* d = xs + (y % R::SLOTS) * RSP + ((x & 1) * WH + (x >> 1)) * PSX +
+                      8 * ((c4 >> 1) ^ R::swz(y, x >> 1)) + 4 * (c4 & 1);
+        *reinterpret_cast<uint2*>(d) = t0;
+        *reinterpret_cast<uint2*>(d + PL) = t1;
+        *reinterpret_cast<uint2*>(d + 2 * PL) = t2;
+      }
+    }
+  };
+  if (n_items > 0) load_item(pre[0], 0);
+  if (n_items > 1) load_item(pre[1], 1);
+  if (n_items > 0) split_item(pre[0], 0);
+  if (n_items > 2) load_item(pre[0], 2);
+  __syncthreads();
+  f4 acc[2];
+  // band k's MFMAs, partial, split of k + 1 (pre[S1]) and loads of k + 3 into it
+  auto band = [&](auto s1, int k) {
+    constexpr int S1 = decltype(s1)::value;
+    const int b = k % NB, oy0 = R::BR * b, nr = min(R::BR, R::OH - oy0);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) acc[u] = f4zero();
+    // tile t < 3: band row t, ox = i16; tile 3: row i16 >> 2, ox = 16 + (i16 & 3); a lane past the
+    // band (or row 3 of tile 3) takes row 0 at its ox: the same pixel as another lane, so its
+    // reads broadcast and its store repeats that lane's bytes
+    const uint16_t* xb[2][2][2];  // [tile][ky - 2kh][kx >> 1]
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int t = tsel + 2 * u;
+      int r = t < 3 ? t : (i16 >> 2), ox = t < 3 ? i16 : 16 + (i16 & 3);
+      if (r >= nr) r = 0;
+#pragma unroll
+      for (int ky = 0; ky < 2; ++ky) {
+        const int y = 2 * (oy0 + r) + 2 * kh + ky;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int xi = ox + h;
+          xb[u][ky][h] = xs + (y % R::SLOTS) * RSP + xi * PSX + 8 * (q ^ R::swz(y, xi));
+        }
+      }
+    }
+    auto read_b = [&](bf16x8_t (&bv)[2][3], int i) {
+      const int ky = i >> 2, kx = i & 3;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const uint16_t* xp = xb[u][ky][kx >> 1] + (kx & 1) * WH * PSX;
+#pragma unroll
+        for (int tm = 0; tm < 3; ++tm) bv[u][tm] = *reinterpret_cast<const bf16x8_t*>(xp + tm * PL);
+      }
+    };
+    bf16x8_t bv[2][2][3];  // [buffer][tile][term]: tap i + 1's fragments load under tap i's MFMAs
+    read_b(bv[0], 0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (i + 1 < 8) read_b(bv[(i + 1) & 1], i + 1);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {  // small terms first
+        const bf16x8_t* b = bv[i & 1][u];
+        f4 c = acc[u];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i][2], b[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i][0], b[2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i][1], b[1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i][1], b[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i][0], b[1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i][0], b[0], c, 0, 0, 0);
+        acc[u] = c;
+      }
+    }
+    // lane (pixel i16, q) holds co ct*16 + 4q .. +3 of its pixel
+    if (kh == 1) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        *reinterpret_cast<f4*>(part + ((k & 1) * TP + (tsel + 2 * u) * 16 + i16) * PP + ct * 16 + 4 * q) = acc[u];
+    }
+    if (k + 1 < n_items) split_item(pre[S1], k + 1);
+    if (k + 3 < n_items) load_item(pre[S1], k + 3);
+  };
+  auto epilogue = [&](int k) {
+    if (kh != 0) return;
+    const int b = k % NB, oy0 = R::BR * b, nr = min(R::BR, R::OH - oy0);
+    const int64_t out0 = ((int64_t)frame_of(k) * NP + oy0 * OW) * 32 + ct * 16 + 4 * q;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int t = tsel + 2 * u;
+      int r = t < 3 ? t : (i16 >> 2), ox = t < 3 ? i16 : 16 + (i16 & 3);
+      if (r >= nr) r = 0;  // the pixel this lane computed (see band): same bytes as its own lane
+      const f4 pv = *reinterpret_cast<const f4*>(part + ((k & 1) * TP + t * 16 + i16) * PP + ct * 16 + 4 * q);
+      f4 v = acc[u] + pv;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e] + b4[e], 0.0f);
+      *reinterpret_cast<f4*>(X2 + out0 + (int64_t)(r * OW + ox) * 32) = v;
+    }
+  };
+  for (int k = 0; k < n_items; k += 2) {
+    band(std::integral_constant<int, 1>{}, k);
+    __syncthreads();
+    epilogue(k);
+    if (k + 1 < n_items) {
+      band(std::integral_constant<int, 0>{}, k + 1);
+      __syncthreads();
+      epilogue(k + 1);
+    }
   }
 }
 

@@ -1294,6 +1294,19 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
   } else {
     using Bd = Conv2FwdBand<G::OH1, G::OW1, G::OH2, G::OW2>;
     bool done = false;
+    if constexpr (conv2_fwd_ring_fits<G::OH1, G::OW1, G::OH2, G::OW2>()) {
+      // training batches at 174x174: frames streamed band by band through the X1 row ring
+      // (every X1 value loaded and split once); VN_CONV2F_GENERIC keeps the im2col product
+      const bool generic = getenv("VN_CONV2F_GENERIC") != nullptr;  // read per call (A/B and parity checks)
+      if (n > kSkinnyRows && !generic) {
+        const void* kfn = (const void*)conv2_fwd_ring_kernel;
+        VN_HIP(ensure_dyn_lds(kfn, Conv2Ring42::LDS));
+        const int blocks = std::min(frames, resident_blocks(kfn, 512, Conv2Ring42::LDS));
+        hipLaunchKernelGGL(conv2_fwd_ring_kernel, dim3(blocks), dim3(512), Conv2Ring42::LDS, st, a.X[0],
+                           P + L.l[1].w, P + L.l[1].b, a.X[1], frames);
+        done = true;
+      }
+    }
     if constexpr (Bd::LDS <= 160 * 1024) {
       // a few envs (174x174, 300x400): the banded kernel is one launch where the split-K
       // product needs two; at training batches the generic product is faster (see above)

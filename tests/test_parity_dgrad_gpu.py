@@ -103,3 +103,65 @@ def test_aux_first_layer_matches_generic_products(hw, N, switch):
         if e > 1e-5:
             bad[k] = "%.3g" % e
     assert not bad, bad
+
+
+@pytest.mark.parametrize("N", [17, 300, 1030])
+def test_conv2_ring_forward_matches_generic_product(N):
+    """conv2's forward at 174x174 (42x42x32 -> 20x20x32) through the ring kernel
+    (`conv2_fwd_ring_kernel`: frames streamed band by band, X1 rows split once into an LDS
+    ring) against the generic im2col product (`VN_CONV2F_GENERIC`): the X2 maps of every frame
+    (the kernel's whole output) to rounding, 1e-6 of scale, and the logits / value. N = 17 is
+    the smallest batch that takes it (34 frames: most workgroups idle), 300 and 1030 wrap the
+    persistent grid (several frames per workgroup: the ring crosses frame boundaries). Every
+    parameter gradient is compared at N <= 300: both paths sum the same exact split products in
+    another order, and at 1030 samples (26 M X2 values) a few values within rounding of 0 take
+    the other side of a ReLU, which moves conv3's gradients by one sample's term (the oracle
+    tests in test_prod_oracle_gpu.py run the float64 backward with the GPU's own masks)."""
+    from vnav.policy import GoalNavPolicy, frames_from_batch
+    torch.manual_seed(13)
+    hw = (174, 174)
+    pol = GoalNavPolicy(3, 4, hw)
+    net = pol.net
+    with torch.no_grad():
+        pol.params.add_(torch.randn_like(pol.params) * 0.01)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    img = torch.randint(0, 256, (N, 1) + hw + (3,), dtype=torch.uint8, device="cuda", generator=g)
+    gl = torch.randint(0, 256, (N, 1) + hw + (3,), dtype=torch.uint8, device="cuda", generator=g)
+    cl = torch.randn((N, 1, 4), device="cuda", generator=g)
+    cv = torch.randn((N, 1, 1), device="cuda", generator=g)
+    m1, x1, x2 = 2 * 42 * 42, 2 * 42 * 42 * 32, 2 * 20 * 20 * 32  # per-sample act regions (vn_policy.hip:471-476)
+
+    def run(generic):
+        if generic:
+            os.environ["VN_CONV2F_GENERIC"] = "1"
+        try:
+            acts = net.new_acts(N)
+            out = torch.zeros((N, 8), device="cuda")
+            net.forward(pol.params.detach(), frames_from_batch(img.view((N,) + hw + (3,)), gl.view((N,) + hw + (3,))),
+                        N, acts, N, 0, out)
+            X2 = acts[N * (m1 + x1):N * (m1 + x1 + x2)].clone()
+            grads = None
+            if N <= 300:
+                pol.params.grad = None
+                logits, value, _ = pol(((img, gl), None), None, None)
+                ((logits * cl).sum() + (value * cv).sum()).backward()
+                grads = net.to_reference(pol.params.grad.clone())
+            torch.cuda.synchronize()
+            return X2, out[:, :5].clone(), grads
+        finally:
+            os.environ.pop("VN_CONV2F_GENERIC", None)
+
+    (xf, of, gf), (xg, og, gg) = run(False), run(True)
+    assert float(xg.abs().max()) > 0
+    e = float((xf - xg).abs().max()) / float(xg.abs().max())
+    assert e < 1e-6, e
+    e = float((of - og).abs().max()) / max(float(og.abs().max()), 1e-30)
+    assert e < 1e-5, e
+    if gg is not None:
+        bad = {}
+        for k in gg:
+            b = gg[k].numpy().astype(np.float64)
+            e = np.abs(gf[k].numpy() - b).max() / max(np.abs(b).max(), 1e-30)
+            if e > 1e-5:
+                bad[k] = "%.3g" % e
+        assert not bad, bad
