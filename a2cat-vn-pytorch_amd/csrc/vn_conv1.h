@@ -1328,10 +1328,12 @@ __global__ __launch_bounds__(512, 1) void conv2_fwd_ring_kernel(const float* __r
       }
     }
   };
-  if (n_items > 0) load_item(pre[0], 0);
-  if (n_items > 1) load_item(pre[1], 1);
-  if (n_items > 0) split_item(pre[0], 0);
-  if (n_items > 2) load_item(pre[0], 2);
+  if (n_items > 0) {
+    load_item(pre[0], 0);
+    load_item(pre[1], min(1, n_items - 1));
+    split_item(pre[0], 0);
+    load_item(pre[0], min(2, n_items - 1));
+  }
   __syncthreads();
   f4 acc[2];
   // band k's MFMAs, partial, split of k + 1 (pre[S1]) and loads of k + 3 into it
@@ -1368,32 +1370,47 @@ __global__ __launch_bounds__(512, 1) void conv2_fwd_ring_kernel(const float* __r
         for (int tm = 0; tm < 3; ++tm) bv[u][tm] = *reinterpret_cast<const bf16x8_t*>(xp + tm * PL);
       }
     };
-    bf16x8_t bv[2][2][3];  // [buffer][tile][term]: tap i + 1's fragments load under tap i's MFMAs
-    read_b(bv[0], 0);
+    auto mma = [&]() {
+      bf16x8_t bv[2][2][3];  // [buffer][tile][term]: tap i + 1's fragments load under tap i's MFMAs
+      read_b(bv[0], 0);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      if (i + 1 < 8) read_b(bv[(i + 1) & 1], i + 1);
+      for (int i = 0; i < 8; ++i) {
+        if (i + 1 < 8) read_b(bv[(i + 1) & 1], i + 1);
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {  // small terms first
-        const bf16x8_t* b = bv[i & 1][u];
-        f4 c = acc[u];
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i][2], b[0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i][0], b[2], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i][1], b[1], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i][1], b[0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i][0], b[1], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i][0], b[0], c, 0, 0, 0);
-        acc[u] = c;
+        for (int u = 0; u < 2; ++u) {  // small terms first
+          const bf16x8_t* bb = bv[i & 1][u];
+          f4 c = acc[u];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i][2], bb[0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i][0], bb[2], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i][1], bb[1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i][1], bb[0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i][0], bb[1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i][0], bb[0], c, 0, 0, 0);
+          acc[u] = c;
+        }
       }
-    }
-    // lane (pixel i16, q) holds co ct*16 + 4q .. +3 of its pixel
-    if (kh == 1) {
+      // lane (pixel i16, q) holds co ct*16 + 4q .. +3 of its pixel
+      if (kh == 1) {
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
-        *reinterpret_cast<f4*>(part + ((k & 1) * TP + (tsel + 2 * u) * 16 + i16) * PP + ct * 16 + 4 * q) = acc[u];
+        for (int u = 0; u < 2; ++u)
+          *reinterpret_cast<f4*>(part + ((k & 1) * TP + (tsel + 2 * u) * 16 + i16) * PP + ct * 16 + 4 * q) = acc[u];
+      }
+    };
+    // next band's rows into the ring, then the loads of band k + 3 into the registers just
+    // freed; past the last item both repeat the last one (same bytes into the same slots)
+    auto stage = [&]() {
+      split_item(pre[S1], min(k + 1, n_items - 1));
+      load_item(pre[S1], min(k + 3, n_items - 1));
+    };
+    // the two waves of a SIMD (w and w + 4) take the phases in opposite orders, so one's split
+    // (VALU, LDS writes) runs under the other's MFMAs instead of both idling the matrix pipe
+    if (tsel == 0) {
+      mma();
+      stage();
+    } else {
+      stage();
+      mma();
     }
-    if (k + 1 < n_items) split_item(pre[S1], k + 1);
-    if (k + 3 < n_items) load_item(pre[S1], k + 3);
   };
   auto epilogue = [&](int k) {
     if (kh != 0) return;
