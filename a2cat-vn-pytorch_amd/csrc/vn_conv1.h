@@ -474,10 +474,8 @@ __global__ __launch_bounds__(256) void conv1_wgrad_x3_kernel(FrameSrc src, int n
   // vmcnt retires loads in issue order, so the next item's tasks are issued one per step
   // between the dZ loads (a whole-frame prefetch would stall the first dZ use behind it).
   uint32_t pre[NT][NDW];
-  // Loads are issued unconditionally from clamped addresses (a task past the band reloads the
-  // band's last task, dwords past the window repeat its last dword; stage_q masks both): loads
-  // under a branch cannot be counted by the compiler, which then waits for vmcnt(0) — the dZ
-  // loads in flight included — where their registers are next written or read.
+  // A task past the band reloads the band's last task (stage_q skips it): one branch fewer
+  // around loads, whose counts the compiler cannot follow across branches.
   auto load_task = [&](int r, int it) {
     const int band = it - (it / NB) * NB;
     const int t = min(tid + r * 256, band_rows(band) * PAIRS - 1);
@@ -486,7 +484,7 @@ __global__ __launch_bounds__(256) void conv1_wgrad_x3_kernel(FrameSrc src, int n
     const uint32_t* s4 = reinterpret_cast<const uint32_t*>(frame_ptr(src, it / NB) + (off & ~(int64_t)3));
     const int nbytes = (int)(off & 3) + min(24, RB - m * 24);  // bytes of the aligned window
 #pragma unroll
-    for (int q = 0; q < NDW; ++q) pre[r][q] = s4[min(q, (nbytes - 1) >> 2)];
+    for (int q = 0; q < NDW; ++q) pre[r][q] = 4 * q < nbytes ? s4[q] : 0u;
   };
   auto stage_q = [&](int band) {
 #pragma unroll
@@ -521,14 +519,15 @@ __global__ __launch_bounds__(256) void conv1_wgrad_x3_kernel(FrameSrc src, int n
     }
   };
   float zc[8], zn[8];  // steps s and s + 4 in flight
-  // group g's 8 pixels of dZ, unconditionally (a group past the band or a pixel past its row
-  // reloads a valid pixel); step() zeroes what is not the group's (z_valid)
+  // group g's 8 pixels of dZ, unconditionally off one address (a group past the band reloads
+  // the band's last group); step() zeroes what is not the group's (z_valid). The last group of
+  // a row reads up to 7 pixels past the row: the next row, or past the frame the next sample's
+  // map or the activation store's next region (dZ is conv1's slice of it) — in bounds, unused.
   auto load_z = [&](float (&z)[8], int f, int oy0, int ng, int s) {
     const int g = min(2 * s + h, ng - 1), oy = oy0 + g / GPR, ox0 = 8 * (g - (g / GPR) * GPR);
     const float* zf = dZ + ((int64_t)f * NPIX + oy * OW + ox0) * 32 + c32;
-    const int nv = min(8, OW - ox0);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) z[j] = zf[min(j, nv - 1) * 32];
+    for (int j = 0; j < 8; ++j) z[j] = zf[j * 32];
   };
   auto z_valid = [&](int ng, int s) {  // pixels of step s's group that are the band's
     const int g = 2 * s + h, ox0 = 8 * (g - (g / GPR) * GPR);
