@@ -99,9 +99,15 @@ struct EnvArgs {
   float* lra_next;
   float* mask_next;
   float* stats_env;
+  const float* head_w;  // optional: heads computed here (vn_a2c_step.head_weight)
+  const float* head_b;
+  const float* head_x;
+  float* head_out;
 };
 
-enum { MODE_STEP = 0, MODE_RESET = 1, MODE_OBSERVE = 2 };
+// MODE_STEP_HEADS: a step of vn_step_a2c that also computes the policy heads (its own
+// instantiation, so the plain step keeps its register budget)
+enum { MODE_STEP = 0, MODE_RESET = 1, MODE_OBSERVE = 2, MODE_STEP_HEADS = 3 };
 constexpr int kEnvsPerBlock = 4;
 constexpr int kStartRounds = 16;  // 1024 rejection attempts before flagging
 
@@ -243,13 +249,54 @@ __global__ __launch_bounds__(256) void env_kernel(EnvArgs a) {
   int g = st[ST_GOAL * n_envs + e];
   int os = st[ST_OBS * n_envs + e];
 
-  if constexpr (MODE == MODE_STEP) {
+  if constexpr (MODE == MODE_STEP || MODE == MODE_STEP_HEADS) {
     int t = st[ST_ELAPSED * n_envs + e];
     const SceneDev S = a.scenes[sc];
     int act;
     if (a.pol_out) {  // the policy's categorical draw for this env (vn_policy_sample_dev's)
       float lg[7], p[7], lp[7], H;
-      for (int j = 0; j < a.pol_A; ++j) lg[j] = a.pol_out[(int64_t)e * 8 + j];
+      if constexpr (MODE == MODE_STEP_HEADS) {
+        // the heads of this env (logits, value): vn_policy_heads' skinny product for one row —
+        // 32 lanes, 4 consecutive k at 4 kl + 128 i, fma chains, a 32-lane xor tree, + bias:
+        // the same sums in the same order (both 32-lane halves compute them)
+        const int kl = lane & 31;
+        const float* x = a.head_x + (int64_t)e * 512;
+        float4 xv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) xv[i] = *reinterpret_cast<const float4*>(x + 4 * kl + 128 * i);
+        float sj[8], bj[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bj[j] = a.head_b[min(j, a.pol_A)];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {  // all rows' loads in flight together (A + 1 <= 8)
+          const float* w = a.head_w + (int64_t)min(j, a.pol_A) * 512;
+          float s = 0.0f;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float4 wv = *reinterpret_cast<const float4*>(w + 4 * kl + 128 * i);
+            s = fmaf(xv[i].x, wv.x, s);
+            s = fmaf(xv[i].y, wv.y, s);
+            s = fmaf(xv[i].z, wv.z, s);
+            s = fmaf(xv[i].w, wv.w, s);
+          }
+          sj[j] = s;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+#pragma unroll
+          for (int o = 16; o > 0; o >>= 1) sj[j] += __shfl_xor(sj[j], o, 32);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (j <= a.pol_A) {
+            const float v = sj[j] + bj[j];
+            if (j < a.pol_A) lg[j] = v;
+            if (lane == 0) a.head_out[(int64_t)e * 8 + j] = v;
+          }
+        }
+      } else {
+        for (int j = 0; j < a.pol_A; ++j) lg[j] = a.pol_out[(int64_t)e * 8 + j];
+      }
       const uint64_t ctr = a.pctr + (a.pctr_dev ? (uint64_t)*a.pctr_dev : 0ull);
       act = uni(sample_action(lg, a.pol_A, a.pk0, a.pk1, ctr, (uint32_t)e, p, lp, H));
     } else {
@@ -699,6 +746,17 @@ int vn_step_a2c(vn_ctx* c, const vn_a2c_step* p, float* reward_dev, uint8_t* don
   a.lra_next = p->lra_next;
   a.mask_next = p->mask_next;
   a.stats_env = p->episode_stats_env;
+  if (p->head_weight) {
+    if (!p->head_bias || !p->head_input || !p->head_out || p->head_out != p->policy_out)
+      return fail(VN_EINVAL, "vn_step_a2c: head_weight needs head_bias, head_input and head_out == policy_out");
+    if ((reinterpret_cast<uintptr_t>(p->head_weight) | reinterpret_cast<uintptr_t>(p->head_input)) & 15)
+      return fail(VN_EINVAL, "vn_step_a2c: head_weight / head_input must be 16-byte aligned");
+    a.head_w = p->head_weight;
+    a.head_b = p->head_bias;
+    a.head_x = p->head_input;
+    a.head_out = p->head_out;
+    return launch_env<MODE_STEP_HEADS>(c, a, (hipStream_t)stream);
+  }
   return launch_env<MODE_STEP>(c, a, (hipStream_t)stream);
 }
 

@@ -1326,8 +1326,16 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
       launch_gemm_x6_sk<128, 32, 32, 4, 1>(fa, fb, ep, fa.M, 32, 512, st, L);
     }
   }
+  // conv3 + conv4 of a few envs: one launch (vn_skinny.h)
+  const bool small34 = n <= kSkinnyRows && !getenv("VN_CONV34_GENERIC");  // read per call (A/B and parity checks)
+  if (small34) {
+    const int M = n * G::OH3 * G::OW3;
+    hipLaunchKernelGGL((conv34_small_kernel<G::OH2, G::OW2, G::OH3, G::OW3>), dim3((M + kC34Rows - 1) / kC34Rows),
+                       dim3(1024), 0, st, a.X[1], M, P + L.l[2].w, P + L.l[2].b, P + L.l[3].w, P + L.l[3].b, a.X[2],
+                       a.X[3]);
+  }
   // conv3 over concat(image, goal) (X2 -> X3)
-  {
+  if (!small34) {
     NhwcIm2col<32, 4, 4, 2, G::OH2, G::OW2, G::OH3, G::OW3, 2> fa{a.X[1], n * G::OH3 * G::OW3};
     DenseRows fb{P + L.l[2].w, 1024, 64};
     EpiBiasAct ep{a.X[2], 64, P + L.l[2].b, 1};
@@ -1337,7 +1345,7 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
       launch_gemm_x6_sk<64, 64, 32, 2, 2>(fa, fb, ep, fa.M, 64, 1024, st, L);
   }
   // conv4 1x1 (X3 -> X4)
-  {
+  if (!small34) {
     DenseRows fa{a.X[2], 64, n * G::OH3 * G::OW3};
     DenseRows fb{P + L.l[3].w, 64, 32};
     EpiBiasAct ep{a.X[3], 32, P + L.l[3].b, 1};
@@ -1852,7 +1860,9 @@ inline int lstm_backward(const PolicyLayout& L, const float* P, int T, int E, co
     DenseRows fa{w.dgates, 2048, N};
     DenseRows fb{w.wcat_t, 2048, 512};
     EpiMask ep{dz5, x5_all, 512};
-    launch_gemm_x6<128, 128, 32, 2, 2>(fa, fb, ep, N, 512, 2048, st);
+    // split-K below 128 tiles: the logged run's 80 rows make 4 tiles, each walking K = 2048
+    // alone (0.14 ms, 6 % of its update); bench batches have thousands of tiles and run as before
+    launch_gemm_x6_sk<128, 128, 32, 2, 2>(fa, fb, ep, N, 512, 2048, st, L);
   }
   {  // dW_cat = dgates^T x xcat over all T*E rows (x6 core on transposed copies, k = rows
      // contiguous); b_ih and b_hh share the bias gradient

@@ -127,6 +127,87 @@ inline void launch_skinny(const float* A, int64_t lda, const float* B, int64_t l
     hipLaunchKernelGGL((skinny_kernel<kSkinnyRows, EP>), grid, dim3(256), 0, st, A, lda, B, ldb, ep, M, N, K);
 }
 
+// ---- conv3 + conv4 of a few envs, one launch ------------------------------------------
+// conv3 (k4 s2 over the channel concat of the image and goal X2 maps, 64 channels) and the
+// 1x1 conv4 (64 -> 32) are both local to an output pixel, so for a few envs one workgroup
+// takes kC34Rows pixels through both: their im2col rows (kC34Rows x 1024) are gathered into
+// LDS, thread (co, k sixteenth) sums 64 exact fp32 products per row against its W3 row
+// segment (its 16 f4 of weights issued in one burst), the sixteen partials are added in a
+// fixed order (+ bias, ReLU) into X3 (kept for the backward) and LDS, and the 32 conv4
+// outputs of each pixel follow from there. Replaces the split-K conv3 product, its
+// reduce/epilogue launch and the conv4 product (three launches per rollout step).
+// k = (ky*4 + kx)*64 + g*32 + c as NhwcIm2col.
+constexpr int kC34Rows = 4;
+
+template <int H, int W, int OH, int OW>
+__global__ __launch_bounds__(1024) void conv34_small_kernel(const float* __restrict__ X2, int M,
+                                                            const float* __restrict__ W3, const float* __restrict__ b3,
+                                                            const float* __restrict__ W4, const float* __restrict__ b4,
+                                                            float* __restrict__ X3, float* __restrict__ X4) {
+  __shared__ __attribute__((aligned(16))) float A[kC34Rows][1024];
+  __shared__ float part[16][kC34Rows][64];
+  __shared__ float x3s[kC34Rows][64];
+  __shared__ float w4s[32][65];  // W4, row stride 65: conv4's 32 lanes read distinct banks
+  __shared__ float bs[96];       // b3 | b4
+  const int tid = threadIdx.x, row0 = blockIdx.x * kC34Rows;
+  const int co = tid & 63, kq = tid >> 6;
+  f4 wv[16];  // W3[co][64 kq .. 64 kq + 63]
+  {
+    const f4* w = reinterpret_cast<const f4*>(W3 + (int64_t)co * 1024 + kq * 64);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) wv[i] = w[i];
+  }
+  // every global read is issued here, before the first barrier: one memory round trip
+  for (int i = tid; i < 32 * 64; i += 1024) w4s[i >> 6][i & 63] = W4[i];
+  if (tid < 96) bs[tid] = tid < 64 ? b3[tid] : b4[tid - 64];
+  {  // gather: f4 i of the block = (row, k / 4)
+    const int r = tid >> 8, k = (tid & 255) * 4, m = min(row0 + r, M - 1);
+    const int n = m / (OH * OW), rr = m - n * (OH * OW), oy = rr / OW, ox = rr - (rr / OW) * OW;
+    const int c = k & 31, g = (k >> 5) & 1, t = k >> 6, ky = t >> 2, kx = t & 3;
+    *reinterpret_cast<f4*>(&A[r][k]) =
+        *reinterpret_cast<const f4*>(X2 + ((((int64_t)n * 2 + g) * H + oy * 2 + ky) * W + ox * 2 + kx) * 32 + c);
+  }
+  __syncthreads();
+  {
+    float acc[kC34Rows];
+#pragma unroll
+    for (int r = 0; r < kC34Rows; ++r) acc[r] = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+#pragma unroll
+      for (int r = 0; r < kC34Rows; ++r) {
+        const f4 a = *reinterpret_cast<const f4*>(&A[r][kq * 64 + 4 * i]);
+        float s = acc[r];
+        s = fmaf(a[0], wv[i][0], s);
+        s = fmaf(a[1], wv[i][1], s);
+        s = fmaf(a[2], wv[i][2], s);
+        s = fmaf(a[3], wv[i][3], s);
+        acc[r] = s;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < kC34Rows; ++r) part[kq][r][co] = acc[r];
+  }
+  __syncthreads();
+  if (tid < kC34Rows * 64) {  // conv3 epilogue: (row, co), the 16 partials in a fixed order
+    const int r = tid >> 6, c = tid & 63;
+    float v = 0.0f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v += part[q][r][c];
+    v = fmaxf(v + bs[c], 0.0f);
+    x3s[r][c] = v;
+    if (row0 + r < M) X3[(int64_t)(row0 + r) * 64 + c] = v;
+  }
+  __syncthreads();
+  if (tid < kC34Rows * 32) {  // conv4: (row, co4)
+    const int r = tid >> 5, c4 = tid & 31;
+    float s = 0.0f;
+#pragma unroll 8
+    for (int k = 0; k < 64; ++k) s = fmaf(x3s[r][k], w4s[c4][k], s);
+    if (row0 + r < M) X4[(int64_t)(row0 + r) * 32 + c4] = fmaxf(s + bs[64 + c4], 0.0f);
+  }
+}
+
 // ---- LSTM step: xcat build + gates product + cell, one launch ----------------------
 struct XcatFill {  // xcat_t[m] = [x5 (512) | lra (A+1) | 0 pad | m_t h_{t-1} (512)] (vn_lstm.h)
   const float* x5;

@@ -58,6 +58,10 @@ class A2CStep(ctypes.Structure):
         ("lra_next", c_void_p),
         ("mask_next", c_void_p),
         ("episode_stats_env", c_void_p),
+        ("head_weight", c_void_p),
+        ("head_bias", c_void_p),
+        ("head_input", c_void_p),
+        ("head_out", c_void_p),
     ]
 
 

@@ -41,6 +41,11 @@ from . import dist as vdist
 from .policy import OUT_LD, PolicyNet, frames_from_rows
 
 
+# rows at or below which vn_policy_heads takes its skinny path (kSkinnyRows, csrc/vn_skinny.h):
+# there the env-step launch computes the heads with the same sums (vn_a2c_step.head_weight)
+_FUSED_HEADS_MAX_ENVS = 16
+
+
 class A2CTrainer:
     def __init__(self, env, net=None, params=None, num_steps=20, gamma=0.99, learning_rate=7e-4,
                  max_time_steps=2e6, rms_alpha=0.99, rms_epsilon=1e-5, max_gradient_norm=0.5,
@@ -169,6 +174,10 @@ class A2CTrainer:
         # the rollout's fused env steps (vn_step_a2c): sampling + step + bookkeeping, one launch
         # per step; per-env episode statistics reduced once per rollout (vn_a2c_episode_stats)
         self.stats_env = torch.zeros((3, E), dtype=torch.float32, **kw)
+        # a few envs, recurrent: the heads of each rollout step run inside its env-step launch
+        # (vn_a2c_step.head_weight: vn_policy_heads' skinny sums, bit-identical), one launch
+        # fewer per step
+        self._fused_heads = self.recurrent and E <= _FUSED_HEADS_MAX_ENVS
         self._a2c_steps = [self._a2c_step_args(t) for t in range(T)]
         env.observe(gather=False)  # refresh the obs row buffers for the first forward
         self.num_updates = 0
@@ -252,6 +261,12 @@ class A2CTrainer:
             s.lra_next = (self.lra[t + 1] if t + 1 < T else self.boot_lra).data_ptr()
             s.mask_next = (self.masks[t + 1] if t + 1 < T else self.boot_mask).data_ptr()
         s.episode_stats_env = self.stats_env.data_ptr()
+        if self._fused_heads:  # the heads of h_t in the same launch (out[t] written there)
+            w_off, b_off = self.net.offsets["head"]
+            s.head_weight = self.params.data_ptr() + 4 * w_off
+            s.head_bias = self.params.data_ptr() + 4 * b_off
+            s.head_input = self.h_all[sl].data_ptr()
+            s.head_out = self.out[sl].data_ptr()
         return s
 
     def _frames(self, img_rows, goal_rows):
@@ -285,7 +300,8 @@ class A2CTrainer:
         cp = self.c0 if t == 0 else self.c_all[(t - 1) * E:t * E]
         net.lstm_step(self.params, E, net.x5(self.acts, N)[sl], self.lra[t], self.masks[t], hp, cp, self.xcat[sl],
                       self.gates, self.lstm_acts[sl], self.c_all[sl], self.h_all[sl])
-        net.heads(self.params, self.h_all[sl], E, self.out[sl])
+        if not self._fused_heads:
+            net.heads(self.params, self.h_all[sl], E, self.out[sl])
 
     def _bootstrap(self, frames):
         net, E = self.net, self.env.num_envs

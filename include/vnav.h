@@ -129,6 +129,15 @@ typedef struct vn_a2c_step {
   float* lra_next;                  /* [E][A+1] */
   float* mask_next;                 /* [E] */
   float* episode_stats_env;         /* [3][E], accumulated */
+  /* Optional (a few envs): the policy heads computed in the same launch. With head_weight
+   * non-NULL the logits and value of env e are head_bias + head_weight . head_input[e]
+   * (head_weight [A+1][512], head_input [E][512], the same sums in the same order as
+   * vn_policy_heads), written to head_out [E][8] — the buffer policy_out points at — and
+   * sampled from; otherwise they are read from policy_out. */
+  const float* head_weight;
+  const float* head_bias;
+  const float* head_input;
+  float* head_out;
 } vn_a2c_step;
 int vn_step_a2c(vn_ctx* ctx, const vn_a2c_step* a2c, float* reward_dev, uint8_t* done_dev,
                 int32_t* state_dev, vn_stream_t stream);

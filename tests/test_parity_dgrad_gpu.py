@@ -165,3 +165,44 @@ def test_conv2_ring_forward_matches_generic_product(N):
             if e > 1e-5:
                 bad[k] = "%.3g" % e
         assert not bad, bad
+
+
+@pytest.mark.parametrize("hw,N", [((84, 84), 1), ((84, 84), 16), ((174, 174), 4), ((174, 174), 13)])
+def test_conv34_small_matches_generic_products(hw, N):
+    """conv3 + conv4 of a few envs (n <= 16) in one launch (`conv34_small_kernel`: exact fp32
+    products per pixel, the k quarters summed in a fixed order) against the x6 products
+    (`VN_CONV34_GENERIC`): logits, value and every parameter gradient to 1e-5 of scale."""
+    from vnav.policy import GoalNavPolicy
+    torch.manual_seed(14)
+    pol = GoalNavPolicy(3, 4, hw)
+    with torch.no_grad():
+        pol.params.add_(torch.randn_like(pol.params) * 0.01)
+    g = torch.Generator(device="cuda").manual_seed(4)
+    img = torch.randint(0, 256, (N, 1) + hw + (3,), dtype=torch.uint8, device="cuda", generator=g)
+    gl = torch.randint(0, 256, (N, 1) + hw + (3,), dtype=torch.uint8, device="cuda", generator=g)
+    cl = torch.randn((N, 1, 4), device="cuda", generator=g)
+    cv = torch.randn((N, 1, 1), device="cuda", generator=g)
+
+    def run(generic):
+        if generic:
+            os.environ["VN_CONV34_GENERIC"] = "1"
+        try:
+            pol.params.grad = None
+            logits, value, _ = pol(((img, gl), None), None, None)
+            ((logits * cl).sum() + (value * cv).sum()).backward()
+            torch.cuda.synchronize()
+            return (logits.detach().cpu(), value.detach().cpu()), pol.net.to_reference(pol.params.grad.clone())
+        finally:
+            os.environ.pop("VN_CONV34_GENERIC", None)
+
+    (of, gf), (og, gg) = run(False), run(True)
+    for a, b in zip(of, og):
+        e = float((a - b).abs().max()) / max(float(b.abs().max()), 1e-30)
+        assert e < 1e-5, e
+    bad = {}
+    for k in gg:
+        b = gg[k].numpy().astype(np.float64)
+        e = np.abs(gf[k].numpy() - b).max() / max(np.abs(b).max(), 1e-30)
+        if e > 1e-5:
+            bad[k] = "%.3g" % e
+    assert not bad, bad
