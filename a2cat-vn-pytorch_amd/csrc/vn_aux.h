@@ -240,6 +240,8 @@ __global__ __launch_bounds__(kAux2Threads) void aux_deconv2_kernel(const float* 
   float bias[7];
 #pragma unroll
   for (int c = 0; c < 7; ++c) bias[c] = b2[c];
+#pragma unroll
+  for (int c = 0; c < 7; ++c) asm volatile("" ::"v"(bias[c]));  // landed before the item loop's prefetches
   const float inv[3] = {2.0f * weight / ((float)n * PH * PW), 2.0f * weight / (3.0f * n * PH * PW),
                         2.0f * weight / (3.0f * n * PH * PW)};
   float sq[3] = {0.0f, 0.0f, 0.0f};

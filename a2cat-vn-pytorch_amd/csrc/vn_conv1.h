@@ -198,6 +198,10 @@ __global__ __launch_bounds__(256, 2) void conv1_fwd_x3_kernel(FrameSrc src, int 
   f4 bs[4];  // the transposed tile's lane holds channels 8j + 4h .. +3 (j = 0..3) of pixel c32
 #pragma unroll
   for (int j = 0; j < 4; ++j) bs[j] = *reinterpret_cast<const f4*>(bias + 8 * j + 4 * h);
+  // land the bias now: its first use sits in the tile loop's epilogue, where the compiler
+  // cannot tell it from the next item's prefetch in flight and waits for vmcnt(0) each tile
+#pragma unroll
+  for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(bs[j][0]), "v"(bs[j][1]), "v"(bs[j][2]), "v"(bs[j][3]));
   const int n_items = n_frames * NB;
   // dwords of item it's band: rows 4*BR*band .. (clamped to the frame)
   auto band_dwords = [&](int band) { return min(BRI, H - 4 * BR * band) * RB / 4; };
@@ -1141,6 +1145,10 @@ __global__ __launch_bounds__(512, 2) void conv2_fwd_x6_kernel(const float* __res
       wf[kx][nt][1] = t1.v;
       wf[kx][nt][2] = t2.v;
     }
+  // the bias of this thread's channel quad (c4 = tid & 7 in every reduce iteration), waited for
+  // here: a first use inside the loop would wait on the item prefetches in flight as well
+  const f4 b4 = *reinterpret_cast<const f4*>(bias + 4 * (tid & 7));
+  asm volatile("" ::"v"(b4[0]), "v"(b4[1]), "v"(b4[2]), "v"(b4[3]));
   const int n_items = n_frames * NB;
   auto band_f4 = [&](int band) { return min(BRI, IH - 2 * BR * band) * IW * 8; };
   // two items' X1 in flight: item it + 2 * gridDim.x is loaded into the registers item it
@@ -1151,10 +1159,7 @@ __global__ __launch_bounds__(512, 2) void conv2_fwd_x6_kernel(const float* __res
     const f4* s4 = reinterpret_cast<const f4*>(X1 + ((int64_t)f * IH + 2 * BR * band) * IW * 32);
     const int nv = band_f4(band);
 #pragma unroll
-    for (int j = 0; j < NV; ++j) {
-      const int i = tid + j * 512;
-      if (i < nv) pr[j] = s4[i];
-    }
+    for (int j = 0; j < NV; ++j) pr[j] = s4[min(tid + j * 512, nv - 1)];  // unconditional: countable
   };
   if ((int)blockIdx.x < n_items) load_item(pre[0], blockIdx.x);
   if ((int)(blockIdx.x + gridDim.x) < n_items) load_item(pre[1], blockIdx.x + gridDim.x);
@@ -1216,7 +1221,6 @@ __global__ __launch_bounds__(512, 2) void conv2_fwd_x6_kernel(const float* __res
       const f4* pp = reinterpret_cast<const f4*>(part + p * PP) + c4;
       constexpr int RS4 = TP * PP / 4;  // one kernel row's partials, in f4
       f4 v = ((pp[0] + pp[RS4]) + pp[2 * RS4]) + pp[3 * RS4];
-      const f4 b4 = *reinterpret_cast<const f4*>(bias + 4 * c4);
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r] + b4[r], 0.0f);
       *reinterpret_cast<f4*>(X2 + out0 + (int64_t)i * 4) = v;
