@@ -1443,6 +1443,168 @@ __global__ __launch_bounds__(512, 1) void conv2_fwd_ring_kernel(const float* __r
   }
 }
 
+// Two-workgroups-per-CU form of the ring kernel: the single 8-wave workgroup above keeps its
+// MFMA pipe 47 % busy, bound by its per-band barrier and phase order rather than by HBM (a
+// no-load ablation runs 10 % faster). Here a workgroup is 4 waves (role = (co tile, kernel-row
+// half), each taking all 4 tiles of a band in two passes) over an 8-slot ring (74 KB of LDS):
+// MFMA(b) -> partial -> barrier -> epilogue(b) + split of band b+1's rows over band b's six
+// oldest slots + loads of band b+2 -> barrier. Its phases are serial, and the other workgroup
+// on the CU fills them. Same sums in the same order as conv2_fwd_ring_kernel (bitwise).
+struct Conv2Ring42x2 {
+  static constexpr int SLOTS = 8, PL = SLOTS * Conv2Ring42::RSP;
+  static constexpr int TP = 64, PP = 36;
+  static constexpr int NV = (8 * Conv2Ring42::IW * 8 + 255) / 256;  // prefetched f4 per thread
+  static constexpr size_t LDS = (size_t)3 * PL * 2 + (size_t)TP * PP * 4;
+  static_assert(LDS <= 80 * 1024, "two workgroups per CU");
+};
+
+__global__ __launch_bounds__(256, 2) void conv2_fwd_ring2_kernel(const float* __restrict__ X1,
+                                                                 const float* __restrict__ W2,
+                                                                 const float* __restrict__ bias,
+                                                                 float* __restrict__ X2, int n_frames) {
+  using R = Conv2Ring42;
+  using Q = Conv2Ring42x2;
+  constexpr int IW = R::IW, OW = R::OW, NB = R::NB, WH = R::WH, PSX = R::PSX, RSP = R::RSP, PL = Q::PL;
+  constexpr int NV = Q::NV, PP = Q::PP, NP = R::OH * R::OW;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem_r3[];
+  uint16_t* xs = reinterpret_cast<uint16_t*>(smem_r3);
+  float* part = reinterpret_cast<float*>(smem_r3 + (size_t)3 * PL * 2);  // [TP][PP]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ct = wave & 1, kh = wave >> 1;
+  const int i16 = lane & 15, q = lane >> 4;
+  bf16x8_t wf[8][3];  // [tap i: ky = 2kh + (i >> 2), kx = i & 3][term]: A[co = ct*16 + i16][k = ci 8q .. 8q+7]
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    union { uint16_t u[8]; bf16x8_t v; } t0, t1, t2;
+    const float* wp = W2 + (ct * 16 + i16) * 512 + ((2 * kh + (i >> 2)) * 4 + (i & 3)) * 32 + 8 * q;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) split3_bf16(wp[j], t0.u[j], t1.u[j], t2.u[j]);
+    wf[i][0] = t0.v;
+    wf[i][1] = t1.v;
+    wf[i][2] = t2.v;
+  }
+  const f4 b4 = *reinterpret_cast<const f4*>(bias + ct * 16 + 4 * q);
+  asm volatile("" ::"v"(b4[0]), "v"(b4[1]), "v"(b4[2]), "v"(b4[3]));  // landed before the loop
+  const int my_frames = (int)blockIdx.x < n_frames ? (n_frames - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  const int n_items = my_frames * NB;
+  auto frame_of = [&](int k) { return (int)blockIdx.x + (k / NB) * (int)gridDim.x; };
+  // ring slot of X1 row y of item k's frame: rows of consecutive frames continue the count
+  // (42 per frame), so a band's 8 rows and the next band's new rows (which replace the band's
+  // six oldest once its MFMAs are done) never collide
+  auto slot = [&](int k, int y) { return (42 * (k / NB) + y) & (Q::SLOTS - 1); };
+  f4 pre[NV];
+  auto load_item = [&](int k) {
+    const int b = k % NB, lo = R::new_lo(b);
+    const int nv = (R::new_hi(b) - lo) * IW * 8;
+    const f4* s4 = reinterpret_cast<const f4*>(X1 + ((int64_t)frame_of(k) * R::IH + lo) * IW * 32);
+#pragma unroll
+    for (int j = 0; j < NV; ++j) pre[j] = s4[min(tid + j * 256, nv - 1)];
+  };
+  auto split_item = [&](int k) {
+    const int b = k % NB, lo = R::new_lo(b);
+    const int nv = (R::new_hi(b) - lo) * IW * 8;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int i = tid + j * 256;
+      if (i < nv) {
+        const int c4 = i & 7, px = i >> 3, y = lo + px / IW, x = px - (px / IW) * IW;
+        uint2 t0, t1, t2;
+        split3_pack(pre[j], t0, t1, t2);
+        uint16_t* d = xs + slot(k, y) * RSP + ((x & 1) * WH + (x >> 1)) * PSX +
+                      8 * ((c4 >> 1) ^ R::swz(y, x >> 1)) + 4 * (c4 & 1);
+        *reinterpret_cast<uint2*>(d) = t0;
+        *reinterpret_cast<uint2*>(d + PL) = t1;
+        *reinterpret_cast<uint2*>(d + 2 * PL) = t2;
+      }
+    }
+  };
+  if (n_items > 0) {
+    load_item(0);
+    split_item(0);
+  }
+  __syncthreads();
+  f4 acc[4];
+  for (int k = 0; k < n_items; ++k) {
+    const int b = k % NB, oy0 = R::BR * b, nr = min(R::BR, R::OH - oy0);
+    // tile t < 3: band row t, ox = i16; tile 3: row i16 >> 2, ox = 16 + (i16 & 3); lanes past the
+    // band take row 0 at their ox (see conv2_fwd_ring_kernel)
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      const uint16_t* xb[2][2][2];  // [tile][ky - 2kh][kx >> 1]
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int t = 2 * pass + u;
+        int r = t < 3 ? t : (i16 >> 2);
+        const int ox = t < 3 ? i16 : 16 + (i16 & 3);
+        if (r >= nr) r = 0;
+#pragma unroll
+        for (int ky = 0; ky < 2; ++ky) {
+          const int y = 2 * (oy0 + r) + 2 * kh + ky;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int xi = ox + h;
+            xb[u][ky][h] = xs + slot(k, y) * RSP + xi * PSX + 8 * (q ^ R::swz(y, xi));
+          }
+        }
+      }
+      auto read_b = [&](bf16x8_t (&bv)[2][3], int i) {
+        const int ky = i >> 2, kx = i & 3;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const uint16_t* xp = xb[u][ky][kx >> 1] + (kx & 1) * WH * PSX;
+#pragma unroll
+          for (int tm = 0; tm < 3; ++tm) bv[u][tm] = *reinterpret_cast<const bf16x8_t*>(xp + tm * PL);
+        }
+      };
+      f4 c2[2] = {f4zero(), f4zero()};
+      bf16x8_t bv[2][2][3];
+      read_b(bv[0], 0);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        if (i + 1 < 8) read_b(bv[(i + 1) & 1], i + 1);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {  // small terms first
+          const bf16x8_t* bb = bv[i & 1][u];
+          f4 c = c2[u];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i][2], bb[0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i][0], bb[2], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i][1], bb[1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i][1], bb[0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i][0], bb[1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i][0], bb[0], c, 0, 0, 0);
+          c2[u] = c;
+        }
+      }
+      acc[2 * pass] = c2[0];
+      acc[2 * pass + 1] = c2[1];
+    }
+    if (kh == 1) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) *reinterpret_cast<f4*>(part + (t * 16 + i16) * PP + ct * 16 + 4 * q) = acc[t];
+    }
+    __syncthreads();  // MFMA(k) and the partials done: band k's oldest slots are free
+    if (kh == 0) {
+      const int64_t out0 = ((int64_t)frame_of(k) * NP + oy0 * OW) * 32 + ct * 16 + 4 * q;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        int r = t < 3 ? t : (i16 >> 2);
+        const int ox = t < 3 ? i16 : 16 + (i16 & 3);
+        if (r >= nr) r = 0;
+        const f4 pv = *reinterpret_cast<const f4*>(part + (t * 16 + i16) * PP + ct * 16 + 4 * q);
+        f4 v = acc[t] + pv;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e] + b4[e], 0.0f);
+        *reinterpret_cast<f4*>(X2 + out0 + (int64_t)(r * OW + ox) * 32) = v;
+      }
+    }
+    if (k + 1 < n_items) {  // loaded here, not a band ahead: the other workgroup on the CU covers
+      load_item(k + 1);     // the latency, and the 44 VGPRs keep the B fragments double-buffered
+      split_item(k + 1);
+    }
+    __syncthreads();  // band k + 1's rows in the ring, the partial buffer read
+  }
+}
+
 // Deterministic column sums of a [rows][32] matrix: per-block partials, then one block.
 __global__ __launch_bounds__(256) void colsum32_partial_kernel(const float* __restrict__ A, int64_t rows,
                                                                float* __restrict__ partial) {

@@ -1299,11 +1299,19 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
       // (every X1 value loaded and split once); VN_CONV2F_GENERIC keeps the im2col product
       const bool generic = getenv("VN_CONV2F_GENERIC") != nullptr;  // read per call (A/B and parity checks)
       if (n > kSkinnyRows && !generic) {
-        const void* kfn = (const void*)conv2_fwd_ring_kernel;
-        VN_HIP(ensure_dyn_lds(kfn, Conv2Ring42::LDS));
-        const int blocks = std::min(frames, resident_blocks(kfn, 512, Conv2Ring42::LDS));
-        hipLaunchKernelGGL(conv2_fwd_ring_kernel, dim3(blocks), dim3(512), Conv2Ring42::LDS, st, a.X[0],
-                           P + L.l[1].w, P + L.l[1].b, a.X[1], frames);
+        if (getenv("VN_CONV2F_RING1")) {  // the one-workgroup-per-CU form (A/B)
+          const void* kfn = (const void*)conv2_fwd_ring_kernel;
+          VN_HIP(ensure_dyn_lds(kfn, Conv2Ring42::LDS));
+          const int blocks = std::min(frames, resident_blocks(kfn, 512, Conv2Ring42::LDS));
+          hipLaunchKernelGGL(conv2_fwd_ring_kernel, dim3(blocks), dim3(512), Conv2Ring42::LDS, st, a.X[0],
+                             P + L.l[1].w, P + L.l[1].b, a.X[1], frames);
+        } else {
+          const void* kfn = (const void*)conv2_fwd_ring2_kernel;
+          VN_HIP(ensure_dyn_lds(kfn, Conv2Ring42x2::LDS));
+          const int blocks = std::min(frames, resident_blocks(kfn, 256, Conv2Ring42x2::LDS));
+          hipLaunchKernelGGL(conv2_fwd_ring2_kernel, dim3(blocks), dim3(256), Conv2Ring42x2::LDS, st, a.X[0],
+                             P + L.l[1].w, P + L.l[1].b, a.X[1], frames);
+        }
         done = true;
       }
     }

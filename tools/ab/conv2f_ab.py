@@ -1,6 +1,6 @@
 """A/B of conv2's forward at 174x174 in one process: the policy trunk forward over 4096
-samples (8192 frames, one rollout step of the bench's 174x174 leg) with the ring kernel and
-with the generic im2col product (VN_CONV2F_GENERIC), alternating; prints the forward's device
+samples (8192 frames, one rollout step of the bench's 174x174 leg) with the ring kernels (two
+workgroups per CU; VN_CONV2F_RING1: one) and with the generic im2col product (VN_CONV2F_GENERIC), alternating; prints the forward's device
 time per call for both and the max relative difference of the conv_merge features. Run under
 rocprofv3 --kernel-trace --stats for per-kernel times.
 
@@ -33,11 +33,13 @@ def main():
     res = {}
     feats = {}
     for rnd in range(2):
-        for mode in ("ring", "generic"):
+        for mode in ("ring", "ring1", "generic"):
+            os.environ.pop("VN_CONV2F_GENERIC", None)
+            os.environ.pop("VN_CONV2F_RING1", None)
             if mode == "generic":
                 os.environ["VN_CONV2F_GENERIC"] = "1"
-            else:
-                os.environ.pop("VN_CONV2F_GENERIC", None)
+            elif mode == "ring1":
+                os.environ["VN_CONV2F_RING1"] = "1"
             net.forward(params, fr, n, acts, n, 0, out)
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -49,8 +51,10 @@ def main():
             res.setdefault(mode, []).append(e0.elapsed_time(e1) / reps)
             feats[mode] = net.x5(acts, n).clone()
     os.environ.pop("VN_CONV2F_GENERIC", None)
+    os.environ.pop("VN_CONV2F_RING1", None)
     d = (feats["ring"] - feats["generic"]).abs().max() / feats["generic"].abs().max()
-    print({"samples": n, "forward_ms": res, "x5_max_rel_diff": float(d)})
+    print({"samples": n, "forward_ms": res, "x5_max_rel_diff": float(d),
+           "ring_vs_ring1_bitwise": bool(torch.equal(feats["ring"], feats["ring1"]))})
 
 
 if __name__ == "__main__":
