@@ -22,7 +22,7 @@ if [ "${TRACE:-1}" = "1" ]; then
   rc=$?; tail -5 $OUT/pytest_gpu_traced_$TAG.log
   f=$(find /tmp/trace_$TAG -name "*kernel_trace.csv" | head -1)
   if [ -n "$f" ]; then
-    python3 tools/test_kernel_map.py "$f" $OUT/tests_$TAG.tsv --top profiles/r02/train_kernel_stats_v12.csv --k 20 \
+    python3 tools/test_kernel_map.py "$f" $OUT/tests_$TAG.tsv --top ${TOP:-profiles/r02/train_kernel_stats_v12.csv} --k 20 \
       --oracle-tests ${ORACLE_TESTS:-test_prod_oracle_gpu} --md $OUT/test_kernels_$TAG.md; echo "map rc=$?"
     gzip -c "$f" > $OUT/kernel_trace_tests_$TAG.csv.gz
   fi
