@@ -455,6 +455,7 @@ __global__ __launch_bounds__(256) void conv1_wgrad_x3_kernel(FrameSrc src, int n
   {  // never-written Q entries (x >> 2 >= 2 * PAIRS, row tails) are read by padding pixels: zero
     uint4* q4 = reinterpret_cast<uint4*>(Q);
     for (int i = tid; i < BRI * RSQ / 8; i += 256) q4[i] = uint4{0u, 0u, 0u, 0u};
+    __syncthreads();  // before any wave stages the first item over the zeroed rows
   }
   int loff[5];
 #pragma unroll
@@ -1087,8 +1088,14 @@ __global__ __launch_bounds__(NW * 64, 2) void conv2_dgrad_x6_kernel(const float*
 template <int IH, int IW, int OH, int OW>
 struct Conv2FwdBand {
   static constexpr int WH = (IW + 1) / 2;  // x >> 1 columns per parity
-  static constexpr int PSX = 40;           // pixel stride in a plane (bf16)
-  static constexpr int RSP = 2 * WH * PSX; // plane row stride (bf16)
+  // 84x84 (20x20 -> 9x9, one band): tiles of 2 rows x 8 pixels plus the last row and column
+  // (pix2x8 below) on unpadded pixels, the odd-x plane 4 quads past the even one and rows 1 quad
+  // apart: 1/8 of the B-fragment read conflict cycles of the row-major tiles at pixel stride 40
+  // and conflict-free split stores (exhaustive check: tools/conv2f84_banks.py)
+  static constexpr bool kTiled = IH == 20 && IW == 20 && OH == 9 && OW == 9;
+  static constexpr int PSX = kTiled ? 32 : 40;              // pixel stride in a plane (bf16)
+  static constexpr int PO = kTiled ? 352 : WH * PSX;        // odd-x plane offset (bf16)
+  static constexpr int RSP = kTiled ? 680 : 2 * WH * PSX;   // plane row stride (bf16)
   static constexpr int rows_of(int br) { return 2 * br + 2 < IH ? 2 * br + 2 : IH; }
   static constexpr int tiles_of(int br) { return (br * OW + 15) / 16; }
   static constexpr size_t planes_of(int br) { return (size_t)3 * rows_of(br) * RSP * 2; }
@@ -1120,7 +1127,26 @@ __global__ __launch_bounds__(512, 2) void conv2_fwd_x6_kernel(const float* __res
                                                               const float* __restrict__ bias,
                                                               float* __restrict__ X2, int n_frames) {
   using Bd = Conv2FwdBand<IH, IW, OH, OW>;
-  constexpr int BR = Bd::BR, NB = Bd::NB, WH = Bd::WH, PSX = Bd::PSX, RSP = Bd::RSP;
+  constexpr int BR = Bd::BR, NB = Bd::NB, PSX = Bd::PSX, RSP = Bd::RSP, PO = Bd::PO;
+  constexpr bool kTiled = Bd::kTiled;
+  static_assert(!kTiled || (NB == 1 && Bd::tiles_of(BR) == 6), "tiled 9x9 map");
+  // tile pixel of slot (t, i) for the 9x9 map: tiles 0-3 = rows 2t, 2t+1 x ox 0-7, tile 4 = row
+  // 8 x ox 0-7 then column 8 x rows 0-7, tile 5 = (8, 8) in every lane; and back
+  auto pix2x8 = [](int t, int i, int& oy, int& ox) {
+    if (t < 4) {
+      oy = 2 * t + (i >> 3);
+      ox = i & 7;
+    } else if (t == 4) {
+      oy = i < 8 ? 8 : i - 8;
+      ox = i < 8 ? i : 8;
+    } else {
+      oy = 8;
+      ox = 8;
+    }
+  };
+  auto slot2x8 = [](int oy, int ox) {
+    return ox < 8 ? (oy < 8 ? (oy >> 1) * 16 + (oy & 1) * 8 + ox : 64 + ox) : (oy < 8 ? 72 + oy : 80);
+  };
   constexpr int BRI = Bd::rows_of(BR), TP = Bd::tiles_of(BR) * 16;  // staged rows, padded band pixels
   constexpr int PL = BRI * RSP;                                        // plane size (bf16)
   constexpr int NP = OH * OW;
@@ -1176,7 +1202,7 @@ __global__ __launch_bounds__(512, 2) void conv2_fwd_x6_kernel(const float* __res
           const int c4 = i & 7, px = i >> 3, y = px / IW, x = px - (px / IW) * IW;
           uint2 t0, t1, t2;
           split3_pack(pre[S][j], t0, t1, t2);
-          uint16_t* d = xs + y * RSP + ((x & 1) * WH + (x >> 1)) * PSX + 4 * c4;
+          uint16_t* d = xs + y * RSP + (x & 1) * PO + (x >> 1) * PSX + 4 * c4;
           *reinterpret_cast<uint2*>(d) = t0;
           *reinterpret_cast<uint2*>(d + PL) = t1;
           *reinterpret_cast<uint2*>(d + 2 * PL) = t2;
@@ -1184,16 +1210,23 @@ __global__ __launch_bounds__(512, 2) void conv2_fwd_x6_kernel(const float* __res
       }
     }
     __syncthreads();
-    if (it + 2 * (int)gridDim.x < n_items) load_item(pre[S], it + 2 * gridDim.x);
+    // (a repeat of the last item past the end: unconditional loads keep the wait counts exact)
+    load_item(pre[S], min(it + 2 * (int)gridDim.x, n_items - 1));
     const int tiles = (npb + 15) / 16;
     for (int t = ph; t < tiles; t += 2) {
-      const int p = min(t * 16 + i16, npb - 1);  // this lane's band pixel (B column)
-      const int oy = p / OW, ox = p - (p / OW) * OW;
+      int oy, ox;
+      if constexpr (kTiled) {
+        pix2x8(t, i16, oy, ox);
+      } else {
+        const int p = min(t * 16 + i16, npb - 1);  // this lane's band pixel (B column)
+        oy = p / OW;
+        ox = p - (p / OW) * OW;
+      }
       const uint16_t* xb = xs + (2 * oy + ky) * RSP + ox * PSX + 8 * q;
       f4 acc[2] = {f4zero(), f4zero()};
 #pragma unroll
       for (int kx = 0; kx < 4; ++kx) {
-        const uint16_t* xp = xb + ((kx & 1) * WH + (kx >> 1)) * PSX;
+        const uint16_t* xp = xb + (kx & 1) * PO + (kx >> 1) * PSX;
         bf16x8_t b[3];
 #pragma unroll
         for (int tm = 0; tm < 3; ++tm) b[tm] = *reinterpret_cast<const bf16x8_t*>(xp + tm * PL);
@@ -1218,7 +1251,8 @@ __global__ __launch_bounds__(512, 2) void conv2_fwd_x6_kernel(const float* __res
     const int64_t out0 = ((int64_t)f * NP + oy0 * OW) * 32;
     for (int i = tid; i < npb * 8; i += 512) {  // (pixel, co quad): fixed-order sum of the 4 rows
       const int p = i >> 3, c4 = i & 7;
-      const f4* pp = reinterpret_cast<const f4*>(part + p * PP) + c4;
+      const int sl = kTiled ? slot2x8(p / OW, p - (p / OW) * OW) : p;  // the pixel's tile slot
+      const f4* pp = reinterpret_cast<const f4*>(part + sl * PP) + c4;
       constexpr int RS4 = TP * PP / 4;  // one kernel row's partials, in f4
       f4 v = ((pp[0] + pp[RS4]) + pp[2 * RS4]) + pp[3 * RS4];
 #pragma unroll
