@@ -16,6 +16,8 @@
 //            deterministic reduce sums (and scales by 1/255).
 #pragma once
 
+#include <utility>
+
 #include "vn_conv1_lanes.h"
 
 namespace vn {
@@ -27,6 +29,17 @@ __host__ __device__ constexpr int conv1_koff(int k) {
   return k >= 147 ? 0 : (k / 21) * W * 3 + ((k / 3) % 7) * 3 + (k % 3);
 }
 
+// f(std::integral_constant<int, 0>{}) ... f(std::integral_constant<int, N - 1>{}): a loop
+// whose index is a compile-time constant in every copy of the body
+template <class F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
 // Frame f of a wave-uniform work item (every caller's f is uniform). The arena row index is
 // read with a scalar load (constant address space: lgkmcnt): as a vector load its address
 // dependence made the wave wait for vmcnt(0) — for every load and store in flight, e.g. the
@@ -35,7 +48,12 @@ __device__ __forceinline__ const uint8_t* frame_ptr(const FrameSrc& src, int f) 
   f = __builtin_amdgcn_readfirstlane(f);
   const int smp = f >> 1, h = f & 1;
   typedef __attribute__((address_space(4))) const int32_t cint32;
-  const int64_t row = src.rows[h] ? (int64_t)((cint32*)src.rows[h])[smp] : (int64_t)smp;
+  // branch-free (a branch between a load and its use costs the compiler its wait counts):
+  // without a rows table the load reads the frame base instead, and its value is not used
+  const int32_t* rp = src.rows[h];
+  const int32_t* a = rp ? rp + smp : reinterpret_cast<const int32_t*>(src.base[h]);
+  const int32_t v = *(cint32*)a;
+  const int64_t row = rp ? (int64_t)v : (int64_t)smp;
   return src.base[h] + row * src.stride;
 }
 
@@ -474,28 +492,35 @@ __global__ __launch_bounds__(256) void conv1_wgrad_x3_kernel(FrameSrc src, int n
     for (int r = 0; r < 16; ++r) acc[nt][r] = 0.0f;
   const int n_items = n_frames * NB;
   auto band_rows = [&](int band) { return min(BRI, H - 4 * BR * band); };
+  // Every wave runs KW steps of every item (KW even: the two dZ register sets alternate across
+  // items too), the ones past the band's KS on zeroed dZ; all loads are unconditional, so the
+  // compiler counts every wait (a load behind a branch, or a trip count it cannot see, made
+  // the waves wait for vmcnt(0): all loads and stores in flight, once per step).
+  constexpr int KS_MAX = (BR * GPR + 1) / 2;
+  constexpr int KW = ((KS_MAX + 3) / 4 + 1) / 2 * 2;
+  static_assert(NT <= KW, "staging tasks are issued one per step");
   // staging task (band row y, pair m): pixels 8m .. 8m+7 of the row = 24 frame bytes (fewer
-  // in the last pair), prefetched into registers one item ahead as NDW aligned dwords.
-  // vmcnt retires loads in issue order, so the next item's tasks are issued one per step
-  // between the dZ loads (a whole-frame prefetch would stall the first dZ use behind it).
+  // in the last pair), prefetched into registers one item ahead as NDW aligned dwords through
+  // a buffer descriptor over the frame: the dwords past its end (last pair of the last row)
+  // read as zero instead of needing a branch. A task past the band reloads the band's last
+  // task (stage_q skips it).
   uint32_t pre[NT][NDW];
-  // A task past the band reloads the band's last task (stage_q skips it): one branch fewer
-  // around loads, whose counts the compiler cannot follow across branches.
   auto load_task = [&](int r, int it) {
     const int band = it - (it / NB) * NB;
     const int t = min(tid + r * 256, band_rows(band) * PAIRS - 1);
     const int y = t / PAIRS, m = t - (t / PAIRS) * PAIRS;
-    const int64_t off = (int64_t)(4 * BR * band + y) * RB + m * 24;
-    const uint32_t* s4 = reinterpret_cast<const uint32_t*>(frame_ptr(src, it / NB) + (off & ~(int64_t)3));
-    const int nbytes = (int)(off & 3) + min(24, RB - m * 24);  // bytes of the aligned window
+    const int off = (4 * BR * band + y) * RB + m * 24;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)frame_ptr(src, it / NB), 0, H * W * 3, 0x00020000);
 #pragma unroll
-    for (int q = 0; q < NDW; ++q) pre[r][q] = 4 * q < nbytes ? s4[q] : 0u;
+    for (int q = 0; q < NDW; ++q) pre[r][q] = __builtin_amdgcn_raw_buffer_load_b32(rs, (off & ~3) + 4 * q, 0, 0);
   };
   auto stage_q = [&](int band) {
 #pragma unroll
     for (int r = 0; r < NT; ++r) {
-      const int t = tid + r * 256;
-      if (t < band_rows(band) * PAIRS) {
+      // a task past the band repeats the band's last task (the same bytes to the same place)
+      const int t = min(tid + r * 256, band_rows(band) * PAIRS - 1);
+      {
         const int y = t / PAIRS, m = t - (t / PAIRS) * PAIRS;
         uint32_t d[6];
         if constexpr (NDW == 6) {
@@ -523,9 +548,8 @@ __global__ __launch_bounds__(256) void conv1_wgrad_x3_kernel(FrameSrc src, int n
       }
     }
   };
-  float zc[8], zn[8];  // steps s and s + 4 in flight
   // group g's 8 pixels of dZ, unconditionally off one address (a group past the band reloads
-  // the band's last group); step() zeroes what is not the group's (z_valid). The last group of
+  // the band's last group); the step zeroes what is not the group's (z_valid). The last group of
   // a row reads up to 7 pixels past the row: the next row, or past the frame the next sample's
   // map or the activation store's next region (dZ is conv1's slice of it) — in bounds, unused.
   auto load_z = [&](float (&z)[8], int f, int oy0, int ng, int s) {
@@ -538,31 +562,43 @@ __global__ __launch_bounds__(256) void conv1_wgrad_x3_kernel(FrameSrc src, int n
     const int g = 2 * s + h, ox0 = 8 * (g - (g / GPR) * GPR);
     return g < ng ? min(8, OW - ox0) : 0;
   };
-  if ((int)blockIdx.x < n_items)
+  auto item_geom = [&](int it, int& f, int& oy0, int& ng) {
+    f = it / NB;
+    const int band = it - (it / NB) * NB;
+    oy0 = BR * band;
+    ng = min(BR, OH - oy0) * GPR;
+  };
+  float zb[2][8];  // dZ of steps i and i + 1 of the wave (step i + 2 is loaded into i's set)
+  if ((int)blockIdx.x < n_items) {
+    int f, oy0, ng;
+    item_geom(blockIdx.x, f, oy0, ng);
 #pragma unroll
     for (int r = 0; r < NT; ++r) load_task(r, blockIdx.x);
+    load_z(zb[0], f, oy0, ng, wave);
+    load_z(zb[1], f, oy0, ng, wave + 4);
+  }
   for (int it = blockIdx.x; it < n_items; it += gridDim.x) {
-    const int f = it / NB, band = it - (it / NB) * NB;
-    const int oy0 = BR * band, nr = min(BR, OH - oy0);
-    const int ng = nr * GPR, KS = (ng + 1) / 2;  // groups, 16-pixel steps of the band
+    int f, oy0, ng;
+    item_geom(it, f, oy0, ng);
+    const int band = it - (it / NB) * NB;
     stage_q(band);
-    if (wave < KS) load_z(zc, f, oy0, ng, wave);
-    if (wave + 4 < KS) load_z(zn, f, oy0, ng, wave + 4);
     __syncthreads();
-    const int inext = it + (int)gridDim.x;
-    // one 16-pixel step (the wave's i-th) from the dZ values in z, which then takes step
-    // s + 8 (the two buffers alternate, no copies)
-    int ns = 0;  // steps this wave has run in the item
-    auto step = [&](int s, float (&z)[8]) {
+    const int inext = min(it + (int)gridDim.x, n_items - 1);
+    int fn, oy0n, ngn;
+    item_geom(inext, fn, oy0n, ngn);
+    static_for<KW>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      const int s = wave + 4 * i;
+      float(&z)[8] = zb[i & 1];
       union { uint16_t u[8]; bf16x8 v; } a0, a1, a2;
       const int nvz = z_valid(ng, s);
 #pragma unroll
       for (int j = 0; j < 8; ++j) split3_bf16(j < nvz ? z[j] : 0.0f, a0.u[j], a1.u[j], a2.u[j]);
-#pragma unroll
-      for (int r = 0; r < NT; ++r)
-        if (ns == r && inext < n_items) load_task(r, inext);
-      ++ns;
-      if (s + 8 < KS) load_z(z, f, oy0, ng, s + 8);
+      if constexpr (i < NT) load_task(i, inext);
+      if constexpr (i + 2 < KW)
+        load_z(z, f, oy0, ng, s + 8);
+      else
+        load_z(z, fn, oy0n, ngn, wave + 4 * (i + 2 - KW));
       const int g = min(2 * s + h, ng - 1);
       const int oy = g / GPR, ox0 = 8 * (g - (g / GPR) * GPR);
       const uint16_t* gb = Q + oy * 4 * RSQ + ox0;
@@ -591,15 +627,7 @@ __global__ __launch_bounds__(256) void conv1_wgrad_x3_kernel(FrameSrc src, int n
       for (int nt = 0; nt < 5; ++nt) acc[nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1.v, b[nt].v, acc[nt], 0, 0, 0);
 #pragma unroll
       for (int nt = 0; nt < 5; ++nt) acc[nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2.v, b[nt].v, acc[nt], 0, 0, 0);
-    };
-    for (int s = wave; s < KS; s += 8) {
-      step(s, zc);
-      if (s + 4 < KS) step(s + 4, zn);
-    }
-    // staging tasks of the next item not issued inside the steps (short bands)
-#pragma unroll
-    for (int r = 0; r < NT; ++r)
-      if (r >= ns && inext < n_items) load_task(r, inext);
+    });
     __syncthreads();
   }
   // fold the four wave sums in LDS (fixed order), one slab per workgroup: D[co][slot]

@@ -267,6 +267,108 @@ __global__ __launch_bounds__(256) void xdb(FA fa, FB fb, EP ep, int M, int N, in
   });
 }
 
+// Loader/MFMA-wave core (gemm_x6pc_kernel) with diagnostic switches: LOAD 0 = the loader waves
+// stage tile 0 once and then only meet the barriers (MFMA + LDS-read + barrier bound);
+// HOIST 1 = the MFMA waves read both 16-k fragment sets of a K tile before its MFMAs.
+template <int BM, int BN, int BK, int LOAD, int HOIST, class FA, class FB, class EP>
+__global__ __launch_bounds__(512, 1) void xpc(FA fa, FB fb, EP ep, int M, int N, int K) {
+  constexpr int LDK = BK + 8;
+  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int NA = (FA::template slots<BM, BK>() + 255) / 256;
+  constexpr int NB = (FB::template slots<BN, BK>() + 255) / 256;
+  constexpr int PA = BM * LDK, PB = BN * LDK;
+  __shared__ __attribute__((aligned(16))) uint16_t As[2][3 * PA];
+  __shared__ __attribute__((aligned(16))) uint16_t Bs[2][3 * PB];
+  typedef float f16v_ __attribute__((ext_vector_type(16)));
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bool loader = wave >= 4;
+  const int ltid = tid - 256;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int kb = 0, ke = K;
+  const int nk = (ke - kb + BK - 1) / BK;
+  f4 pa[2][NA], pb[2][NB];
+  auto fetch = [&](auto R, int j) {
+    fa.template fetch<BM, BK>(pa[decltype(R)::value], m0, kb + j * BK, ke, ltid);
+    fb.template fetch<BN, BK>(pb[decltype(R)::value], n0, kb + j * BK, ke, ltid);
+  };
+  auto commit = [&](auto R, int stage) {
+    commit_x6<BM, BK, LDK, FA>(pa[decltype(R)::value], As[stage], ltid);
+    commit_x6<BN, BK, LDK, FB>(pb[decltype(R)::value], Bs[stage], ltid);
+  };
+  using R0 = std::integral_constant<int, 0>;
+  using R1 = std::integral_constant<int, 1>;
+  if (loader) {
+    fetch(R0{}, 0);
+    if (nk > 1) fetch(R1{}, 1);
+    commit(R0{}, 0);
+    if (!LOAD) commit(R1{}, 1);
+  }
+  __syncthreads();
+  const int wm = wave & 1, wn = (wave >> 1) & 1;
+  f16v_ acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+  const int ra = (wm * TM * 32 + (lane & 31)) * LDK + 8 * (lane >> 5);
+  const int rb = (wn * TN * 32 + (lane & 31)) * LDK + 8 * (lane >> 5);
+  auto iteration = [&](auto R, int it) {
+    constexpr int P = decltype(R)::value;
+    if (loader) {
+      if constexpr (LOAD) {
+        if (it + 2 < nk) fetch(R, it + 2);
+        if (it + 1 < nk) commit(std::integral_constant<int, P ^ 1>{}, P ^ 1);
+      }
+    } else {
+      const uint16_t* as = As[P];
+      const uint16_t* bs = Bs[P];
+      bf16x8_ a[BK / 16][3][TM], b[BK / 16][3][TN];
+      auto rd = [&](int q) {
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+            a[q][t][i] = *reinterpret_cast<const bf16x8_*>(&as[t * PA + ra + i * 32 * LDK + q * 16]);
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            b[q][t][j] = *reinterpret_cast<const bf16x8_*>(&bs[t * PB + rb + j * 32 * LDK + q * 16]);
+        }
+      };
+      if constexpr (HOIST) {
+#pragma unroll
+        for (int q = 0; q < BK / 16; ++q) rd(q);
+      }
+#pragma unroll
+      for (int q = 0; q < BK / 16; ++q) {
+        if constexpr (!HOIST) rd(q);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[q][2][i], b[q][0][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[q][0][i], b[q][2][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[q][1][i], b[q][1][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[q][1][i], b[q][0][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[q][0][i], b[q][1][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[q][0][i], b[q][0][j], acc[i][j], 0, 0, 0);
+          }
+      }
+    }
+    __syncthreads();
+  };
+  for (int it = 0; it < nk; it += 2) {
+    iteration(R0{}, it);
+    if (it + 1 < nk) iteration(R1{}, it + 1);
+  }
+  if (!loader)
+    run_epilogue<TM, TN, 16>(ep, acc, M, N, 0, [&](int i, int j, int r, int& row, int& col) {
+      row = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      col = n0 + wn * TN * 32 + j * 32 + (lane & 31);
+    });
+}
+
 template <int BM, int BN, int WM, int WN>
 static void dh_shape(int M, int N, int K, const char* name) {
   float* a = dalloc((int64_t)M * K, 31, -0.5f);
@@ -320,11 +422,35 @@ int main(int argc, char** argv) {
   };
   rep("library gemm_x6 <128,128,32,2,2>", timeit([&] { launch_gemm_x6<128, 128, 32, 2, 2>(fa, fb, ep, E, N, XC, st); }));
   rep("library gemm_x6 <64,64,32,2,2>", timeit([&] { launch_gemm_x6<64, 64, 32, 2, 2>(fa, fb, ep, E, N, XC, st); }));
+
 #define XK(BM, BN, BK, WM, WN, L, S, P, R)                                                                   \
   rep("xk<" #BM "," #BN "," #BK "> loads" #L " split" #S " pf" #P " prio" #R, timeit([&] {                  \
         hipLaunchKernelGGL((xk<BM, BN, BK, WM, WN, L, S, P, R, DenseRows, DenseRows, EpiBias2>),             \
                            grid_for(E, N, BM, BN), dim3(256), 0, st, fa, fb, ep, E, N, XC);                  \
       }));
+  if (argc > 1 && atoi(argv[1]) == 3) {
+    setenv("VN_GEMM_CLASSIC", "1", 1);
+    rep("classic gemm_x6 <128,128,32,2,2>", timeit([&] { launch_gemm_x6<128, 128, 32, 2, 2>(fa, fb, ep, E, N, XC, st); }));
+    unsetenv("VN_GEMM_CLASSIC");
+    EpiNone en{gt};
+#define XPC(BM, BN, L, H)                                                                                  \
+    rep("xpc<" #BM "," #BN "> load" #L " hoist" #H, timeit([&] {                                           \
+          hipLaunchKernelGGL((xpc<BM, BN, 32, L, H, DenseRows, DenseRows, EpiBias2>), grid_for(E, N, BM, BN), \
+                             dim3(512), 0, st, fa, fb, ep, E, N, XC);                                      \
+        }));
+    XPC(128, 128, 1, 0)
+    XPC(128, 128, 1, 1)
+    XPC(128, 128, 0, 0)
+    XPC(128, 128, 0, 1)
+    rep("xpc<128,128> load0 hoist1 epilogue-none", timeit([&] {
+          hipLaunchKernelGGL((xpc<128, 128, 32, 0, 1, DenseRows, DenseRows, EpiNone>), grid_for(E, N, 128, 128),
+                             dim3(512), 0, st, fa, fb, en, E, N, XC);
+        }));
+    XK(128, 128, 32, 2, 2, 0, 1, 1, 0)
+    XK(128, 128, 32, 2, 2, 1, 1, 1, 0)
+    printf("done\n");
+    return 0;
+  }
   XK(128, 128, 32, 2, 2, 1, 1, 1, 0)
   XK(128, 128, 32, 2, 2, 0, 1, 1, 0)
   {
