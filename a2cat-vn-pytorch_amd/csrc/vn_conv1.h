@@ -229,10 +229,9 @@ __global__ __launch_bounds__(256, 2) void conv1_fwd_x3_kernel(FrameSrc src, int 
     const uint32_t* s4 = reinterpret_cast<const uint32_t*>(frame_ptr(src, f) + (int64_t)4 * BR * band * RB);
     const int nd = band_dwords(band);
 #pragma unroll
-    for (int j = 0; j < NPF; ++j) {
-      const int i = tid + j * 256;
-      if (i < nd) pre[j] = s4[i];
-    }
+    // unconditional (a lane past the band reloads its last dword; past the last item the item
+    // repeats): no branch around the loads for the wait counts to get lost in
+    for (int j = 0; j < NPF; ++j) pre[j] = s4[min(tid + j * 256, nd - 1)];
   };
   if ((int)blockIdx.x < n_items) load_item(blockIdx.x);
   for (int it = blockIdx.x; it < n_items; it += gridDim.x) {
@@ -255,7 +254,7 @@ __global__ __launch_bounds__(256, 2) void conv1_fwd_x3_kernel(FrameSrc src, int 
       }
     }
     __syncthreads();
-    if (it + (int)gridDim.x < n_items) load_item(it + gridDim.x);
+    load_item(min(it + (int)gridDim.x, n_items - 1));
     const int tiles = (npb + 31) / 32;
     for (int t = wave; t < tiles; t += 4) {
       const int px = min(t * 32 + c32, npb - 1);
