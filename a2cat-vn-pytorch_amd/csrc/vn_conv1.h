@@ -491,12 +491,16 @@ __global__ __launch_bounds__(256) void conv1_wgrad_x3_kernel(FrameSrc src, int n
     for (int r = 0; r < 16; ++r) acc[nt][r] = 0.0f;
   const int n_items = n_frames * NB;
   auto band_rows = [&](int band) { return min(BRI, H - 4 * BR * band); };
-  // Every wave runs KW steps of every item (KW even: the two dZ register sets alternate across
+  // Every wave runs KW steps of every item (KW a multiple of D: the D dZ register sets rotate across
   // items too), the ones past the band's KS on zeroed dZ; all loads are unconditional, so the
   // compiler counts every wait (a load behind a branch, or a trip count it cannot see, made
   // the waves wait for vmcnt(0): all loads and stores in flight, once per step).
   constexpr int KS_MAX = (BR * GPR + 1) / 2;
-  constexpr int KW = ((KS_MAX + 3) / 4 + 1) / 2 * 2;
+  constexpr int KW0 = (KS_MAX + 3) / 4;
+  // dZ register sets: step i + D is loaded while steps i + 1 .. i + D - 1 wait; three where KW
+  // allows it without an extra masked step (174x174: 6), else two (84x84: 8)
+  constexpr int D = KW0 % 3 == 0 ? 3 : 2;
+  constexpr int KW = (KW0 + D - 1) / D * D;
   static_assert(NT <= KW, "staging tasks are issued one per step");
   // staging task (band row y, pair m): pixels 8m .. 8m+7 of the row = 24 frame bytes (fewer
   // in the last pair), prefetched into registers one item ahead as NDW aligned dwords through
@@ -567,14 +571,14 @@ __global__ __launch_bounds__(256) void conv1_wgrad_x3_kernel(FrameSrc src, int n
     oy0 = BR * band;
     ng = min(BR, OH - oy0) * GPR;
   };
-  float zb[2][8];  // dZ of steps i and i + 1 of the wave (step i + 2 is loaded into i's set)
+  float zb[D][8];  // dZ of steps i .. i + D - 1 of the wave (step i + D is loaded into i's set)
   if ((int)blockIdx.x < n_items) {
     int f, oy0, ng;
     item_geom(blockIdx.x, f, oy0, ng);
 #pragma unroll
     for (int r = 0; r < NT; ++r) load_task(r, blockIdx.x);
-    load_z(zb[0], f, oy0, ng, wave);
-    load_z(zb[1], f, oy0, ng, wave + 4);
+#pragma unroll
+    for (int d = 0; d < D; ++d) load_z(zb[d], f, oy0, ng, wave + 4 * d);
   }
   for (int it = blockIdx.x; it < n_items; it += gridDim.x) {
     int f, oy0, ng;
@@ -588,16 +592,16 @@ __global__ __launch_bounds__(256) void conv1_wgrad_x3_kernel(FrameSrc src, int n
     static_for<KW>([&](auto I) {
       constexpr int i = decltype(I)::value;
       const int s = wave + 4 * i;
-      float(&z)[8] = zb[i & 1];
+      float(&z)[8] = zb[i % D];
       union { uint16_t u[8]; bf16x8 v; } a0, a1, a2;
       const int nvz = z_valid(ng, s);
 #pragma unroll
       for (int j = 0; j < 8; ++j) split3_bf16(j < nvz ? z[j] : 0.0f, a0.u[j], a1.u[j], a2.u[j]);
       if constexpr (i < NT) load_task(i, inext);
-      if constexpr (i + 2 < KW)
-        load_z(z, f, oy0, ng, s + 8);
+      if constexpr (i + D < KW)
+        load_z(z, f, oy0, ng, s + 4 * D);
       else
-        load_z(z, fn, oy0n, ngn, wave + 4 * (i + 2 - KW));
+        load_z(z, fn, oy0n, ngn, wave + 4 * (i + D - KW));
       const int g = min(2 * s + h, ng - 1);
       const int oy = g / GPR, ox0 = 8 * (g - (g / GPR) * GPR);
       const uint16_t* gb = Q + oy * 4 * RSQ + ox0;
