@@ -228,9 +228,9 @@ __global__ __launch_bounds__(256, 2) void conv1_fwd_x3_kernel(FrameSrc src, int 
     const int f = it / NB, band = it - (it / NB) * NB;
     const uint32_t* s4 = reinterpret_cast<const uint32_t*>(frame_ptr(src, f) + (int64_t)4 * BR * band * RB);
     const int nd = band_dwords(band);
-#pragma unroll
     // unconditional (a lane past the band reloads its last dword; past the last item the item
     // repeats): no branch around the loads for the wait counts to get lost in
+#pragma unroll
     for (int j = 0; j < NPF; ++j) pre[j] = s4[min(tid + j * 256, nd - 1)];
   };
   if ((int)blockIdx.x < n_items) load_item(blockIdx.x);
