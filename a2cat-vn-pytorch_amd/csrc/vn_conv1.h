@@ -1005,18 +1005,15 @@ __global__ __launch_bounds__(NW * 64, 2) void conv2_dgrad_x6_kernel(const float*
   // per launch; with 8 waves (174x174) the pixel-major order measured 3 % faster (coalesced
   // 64-B runs of the dZ2 loads) and is kept.
   auto slot_pc = [](int i) { return NW == 4 ? ((i & 15) + 16 * (i >> 7)) * 8 + ((i >> 4) & 7) : i; };
-  auto load_z = [&](int f) {  // dZ2 and the ReLU words of frame f, into registers
+  // dZ2 and the ReLU words of frame f, into registers; unconditional (slots past the frame
+  // reload its last one, staging skips them; past the last frame the frame repeats): no branch
+  // around the loads for the compiler's wait counts to get lost in
+  auto load_z = [&](int f) {
     const f4* z4 = reinterpret_cast<const f4*>(dZ2 + (int64_t)f * NP * 32);
 #pragma unroll
-    for (int j = 0; j < NZ; ++j) {
-      const int i = slot_pc(tid + j * NT);
-      if (i < NP * 8) zr[j] = z4[i];
-    }
+    for (int j = 0; j < NZ; ++j) zr[j] = z4[min(slot_pc(tid + j * NT), NP * 8 - 1)];
 #pragma unroll
-    for (int j = 0; j < NM; ++j) {
-      const int i = tid + j * NT;
-      if (i < IH * IW) mr[j] = mask[(int64_t)f * IH * IW + i];
-    }
+    for (int j = 0; j < NM; ++j) mr[j] = mask[(int64_t)f * IH * IW + min(tid + j * NT, IH * IW - 1)];
   };
   if ((int)blockIdx.x < n_frames) load_z(blockIdx.x);
   for (int f = blockIdx.x; f < n_frames; f += gridDim.x) {
@@ -1038,7 +1035,7 @@ __global__ __launch_bounds__(NW * 64, 2) void conv2_dgrad_x6_kernel(const float*
       if (i < IH * IW) ms[i] = mr[j];
     }
     __syncthreads();
-    if (f + (int)gridDim.x < n_frames) load_z(f + gridDim.x);
+    load_z(min(f + (int)gridDim.x, n_frames - 1));
 #pragma unroll 1
     for (int t0 = 2 * (wave >> 2); t0 < TILES; t0 += 2 * (NW / 4)) {
       int off[2][4];
