@@ -47,22 +47,54 @@ constexpr int skinny_kc() {  // chunk length: kSkKB * 128 values, as the LDS all
   return (MR * kSkKB * 128 * 4 <= 128 * 1024) ? kSkKB * 128 : (128 * 1024 / (MR * 4)) / 128 * 128;
 }
 
+struct RowsFill {  // dense rows A [M][lda] (16-B aligned, lda % 4 == 0)
+  const float* A;
+  int64_t lda;
+  __device__ __forceinline__ f4 operator()(int m, int k) const {
+    return *reinterpret_cast<const f4*>(A + (int64_t)m * lda + k);
+  }
+};
+
 template <int MR, class FILL>
 __device__ __forceinline__ void skinny_dot(const FILL& fill, const float* __restrict__ B, int M, int K, float* As,
                                            float (&acc)[MR]) {
   constexpr int KC = skinny_kc<MR>(), NB = KC / 128;
   const int tid = threadIdx.x, kl = tid & 31;
+  // every load of a chunk (B, then all of A's staging from dense rows) is issued before the
+  // first use: a staging loop that stored each value as it arrived paid one memory round trip
+  // per 256 values (10 in a row for conv_merge's 4 x 2592)
+  constexpr int NFI = (MR * KC / 4 + 255) / 256;  // staging f4 per thread, at most
   for (int k0 = 0; k0 < K; k0 += KC) {
     const int kc = min(KC, K - k0);
     f4 b[NB];
 #pragma unroll
-    for (int i = 0; i < NB; ++i)
-      if (4 * kl + 128 * i < kc) b[i] = *reinterpret_cast<const f4*>(B + k0 + 4 * kl + 128 * i);
-    __syncthreads();  // the previous chunk's reads are done
-    const int q4 = (kc + 3) / 4;
-    for (int i = tid; i < M * q4; i += 256) {
-      const int m = i / q4, q = i - m * q4;
-      *reinterpret_cast<f4*>(&As[m * KC + 4 * q]) = fill(m, k0 + 4 * q);
+    for (int i = 0; i < NB; ++i)  // clamped (a lane past the chunk reloads its end; unused)
+      b[i] = *reinterpret_cast<const f4*>(B + k0 + min(4 * kl + 128 * i, kc - 4));
+    const int q4 = (kc + 3) / 4, nf = M * q4;
+    if constexpr (std::is_same<FILL, RowsFill>::value) {
+      f4 fr[NFI];
+#pragma unroll
+      for (int j = 0; j < NFI; ++j)
+        if (j * 256 < nf) {  // wave-uniform
+          const int i = min(tid + j * 256, nf - 1);
+          const int m = i / q4, q = i - m * q4;
+          fr[j] = fill(m, k0 + 4 * q);
+        }
+      __syncthreads();  // the previous chunk's reads are done
+#pragma unroll
+      for (int j = 0; j < NFI; ++j) {
+        const int i = tid + j * 256;
+        if (j * 256 < nf && i < nf) {
+          const int m = i / q4, q = i - m * q4;
+          *reinterpret_cast<f4*>(&As[m * KC + 4 * q]) = fr[j];
+        }
+      }
+    } else {  // a gathering fill (the LSTM's xcat: three sources) measured faster value by value
+      __syncthreads();
+      for (int i = tid; i < nf; i += 256) {
+        const int m = i / q4, q = i - m * q4;
+        *reinterpret_cast<f4*>(&As[m * KC + 4 * q]) = fill(m, k0 + 4 * q);
+      }
     }
     __syncthreads();
 #pragma unroll
@@ -88,13 +120,6 @@ __device__ __forceinline__ void skinny_dot(const FILL& fill, const float* __rest
   for (int m = 0; m < MR; ++m) acc[m] = sum32(acc[m]);
 }
 
-struct RowsFill {  // dense rows A [M][lda] (16-B aligned, lda % 4 == 0)
-  const float* A;
-  int64_t lda;
-  __device__ __forceinline__ f4 operator()(int m, int k) const {
-    return *reinterpret_cast<const f4*>(A + (int64_t)m * lda + k);
-  }
-};
 
 // C[m][col] = A[m] . B[col] for m < M <= MR, col < N; then the epilogue.
 template <int MR, class EP>
