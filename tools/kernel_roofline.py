@@ -37,7 +37,7 @@ def table(h, E, T):
     # name regex -> (per-call FLOPs, per-call bytes, MFMA form)
     return [
         (r"conv1_fwd_x3_kernel", fs * p1 * 32 * 147 * 2, fs * (fb + p1 * 32 * f4 + p1 * 4), "x3"),
-        (r"conv2_fwd_x6_kernel|NhwcIm2col<32, 4, 4, 2, %d, %d, %d, %d, 1>, DenseRows, EpiBiasAct" % (o1, o1, o2, o2),
+        (r"conv2_fwd_x6_kernel|conv2_fwd_ring2?_kernel|NhwcIm2col<32, 4, 4, 2, %d, %d, %d, %d, 1>, DenseRows, EpiBiasAct" % (o1, o1, o2, o2),
          fs * p2 * 32 * 512 * 2, fs * (p1 + p2) * 32 * f4, "x6"),
         (r"NhwcIm2col<32, 4, 4, 2, %d, %d, %d, %d, 2>, DenseRows, EpiBiasAct" % (o2, o2, o3, o3),
          E * p3 * 64 * 1024 * 2, E * (2 * p2 * 32 + p3 * 64) * f4, "x6"),
