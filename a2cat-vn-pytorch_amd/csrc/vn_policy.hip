@@ -996,34 +996,35 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_x6_kernel(const float* __re
   f4 dbs = f4zero();  // fp32 column sums of dZ (channels 4 (tid % C4) .. +3), g == 0 only
   const int items = (n + IMG - 1) / IMG * S::NB;
   f4 zr[NZ], xr[NX];
-  auto load = [&](int it) {  // the item's dZ band rows and the X rows under them, into registers
+  // the item's dZ band rows and the X rows under them, into registers: unconditional (a slot
+  // past the item or an image past n reloads a valid one; the split zeroes it), so no branch
+  // hides the loads from the compiler's wait counts
+  auto load = [&](int it) {
     const int img0 = (it / S::NB) * IMG, band = it - (it / S::NB) * S::NB;
 #pragma unroll
     for (int j = 0; j < NZ; ++j) {
-      const int i = tid + j * NT;
-      const int k = i / C4, im = k / BP;
-      zr[j] = (i < KP * C4 && img0 + im < n)
-                  ? reinterpret_cast<const f4*>(dZ)[(((int64_t)(img0 + im) * OH + band * BR) * OW + (k - im * BP)) * C4 + i % C4]
-                  : f4zero();
+      const int i = min(tid + j * NT, KP * C4 - 1);
+      const int k = i / C4, im = k / BP, imc = min(img0 + im, n - 1);
+      zr[j] = reinterpret_cast<const f4*>(dZ)[(((int64_t)imc * OH + band * BR) * OW + (k - im * BP)) * C4 + i % C4];
     }
 #pragma unroll
     for (int j = 0; j < NX; ++j) {
-      const int i = tid + j * NT;
-      const int r = i / X4, im = r / NPX;
-      xr[j] = (i < IMG * NPX * X4 && img0 + im < n)
-                  ? reinterpret_cast<const f4*>(X)[((((int64_t)(img0 + im) * G + g) * IH + 2 * band * BR) * IW + (r - im * NPX)) * X4 + i % X4]
-                  : f4zero();
+      const int i = min(tid + j * NT, IMG * NPX * X4 - 1);
+      const int r = i / X4, im = r / NPX, imc = min(img0 + im, n - 1);
+      xr[j] = reinterpret_cast<const f4*>(X)[((((int64_t)imc * G + g) * IH + 2 * band * BR) * IW + (r - im * NPX)) * X4 + i % X4];
     }
   };
   if ((int)blockIdx.x < items) load(blockIdx.x);
   for (int it = blockIdx.x; it < items; it += gridDim.x) {
+    const int img0 = (it / S::NB) * IMG;
 #pragma unroll
     for (int j = 0; j < NZ; ++j) {  // split into the planes
       const int i = tid + j * NT;
       if (i < KP * C4) {
-        if (S::BIAS && g == 0) dbs += zr[j];
+        const f4 z = img0 + (i / C4) / BP < n ? zr[j] : f4zero();
+        if (S::BIAS && g == 0) dbs += z;
         uint2 t0, t1, t2;
-        split3_pack(zr[j], t0, t1, t2);
+        split3_pack(z, t0, t1, t2);
         uint16_t* d = zs + (i / C4) * PZ + 4 * (i % C4);
         *reinterpret_cast<uint2*>(d) = t0;
         *reinterpret_cast<uint2*>(d + PLZ) = t1;
@@ -1034,8 +1035,9 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_x6_kernel(const float* __re
     for (int j = 0; j < NX; ++j) {
       const int i = tid + j * NT;
       if (i < IMG * NPX * X4) {
+        const f4 x = img0 + (i / X4) / NPX < n ? xr[j] : f4zero();
         uint2 t0, t1, t2;
-        split3_pack(xr[j], t0, t1, t2);
+        split3_pack(x, t0, t1, t2);
         uint16_t* d = xs + (i / X4) * PX + 4 * (i % X4);
         *reinterpret_cast<uint2*>(d) = t0;
         *reinterpret_cast<uint2*>(d + PLX) = t1;
@@ -1043,7 +1045,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_x6_kernel(const float* __re
       }
     }
     __syncthreads();
-    if (it + (int)gridDim.x < items) load(it + gridDim.x);  // next item's loads under this one's MFMAs
+    load(min(it + (int)gridDim.x, items - 1));  // next item's loads under this one's MFMAs
     auto kstep = [&](int ks) {
       // this lane's rows of the two tr reads: with KPERM the MFMA's k slot 8 Gq + 4s + q takes
       // item pixel 32 ks + 16 (Gq >> 1) + 8s + 4 (Gq & 1) + q (any bijection works when A and B
