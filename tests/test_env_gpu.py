@@ -319,8 +319,41 @@ def test_index_only_step_and_masked_reset():
             o.reset(mask)
 
 
+def test_c2_single_scene_1024_envs():
+    """Config C2's shape (cached THOR, 1 scene, 1024 envs, 84x84 frames; BASELINE.json): a
+    synthetic 24x24 scene at full frame size, states / rewards / dones / frame rows bit-exact
+    vs the oracle over 40 steps (auto-resets included), gathered bytes on a sample."""
+    vnav = _vnav()
+    sc = [vnav.synthetic_scene(3)]
+    n = 1024
+    env = vnav.VectorEnv(sc, n, seed=4242)
+    o = oracle_of(sc, n, 4242, max_steps=900)
+    rng = np.random.RandomState(5)
+    sample = np.sort(rng.choice(n, 32, replace=False))
+    idx = torch.as_tensor(sample, device="cuda")
+    done_seen = 0
+    for t in range(40):
+        a = rng.randint(0, 4, size=n).astype(np.int32)
+        (img, goal), reward, done, info = env.step(torch.as_tensor(a, device="cuda"))
+        ob = o.step(a)
+        assert np.array_equal(info["state"].cpu().numpy(), ob["state"]), t
+        assert np.array_equal(done.cpu().numpy(), ob["done"]), t
+        assert np.array_equal(reward.cpu().numpy().view(np.uint32), ob["reward"].view(np.uint32)), t
+        assert np.array_equal(info["img_row"].cpu().numpy(), ob["img_row"]), t
+        assert np.array_equal(info["goal_row"].cpu().numpy(), ob["goal_row"]), t
+        done_seen += int(ob["done"].sum())
+        if t % 8 == 7:
+            im, gl = img[idx].cpu().numpy(), goal[idx].cpu().numpy()
+            for j, e in enumerate(sample):
+                assert np.array_equal(im[j], synth_frames(3, [ob["img_row"][e]], FRAME)[0])
+                assert np.array_equal(gl[j], synth_frames(3, [ob["goal_row"][e]], FRAME)[0])
+    assert done_seen > 0  # episodes ended and were reset inside the window
+    assert env.error_flags() == 0
+
+
 def test_full_size_synthetic_scenes():
-    """4096 envs, 4 synthetic 24x24 scenes, 84x84 frames synthesised on the device."""
+    """Config C3's shape: 4096 envs, 4 synthetic 24x24 scenes, 84x84 frames synthesised on
+    the device."""
     vnav = _vnav()
     sc = [vnav.synthetic_scene(k) for k in range(4)]
     n = 4096
