@@ -60,7 +60,8 @@ def parse():
                    help="skip the 174x174 LSTM + aux-deconv train leg (the reference's logged experiment shape)")
     p.add_argument("--no-train-ref4", action="store_true",
                    help="skip the 4-env (the logged run's batch) 174x174 leg")
-    p.add_argument("--c5", action="store_true", help="add the 300x400 + goal + aux-depth train leg (config C5)")
+    p.add_argument("--no-c5", action="store_true",
+                   help="skip the 300x400 + goal + aux-depth train leg (config C5, 512 envs per GPU)")
     p.add_argument("--num-steps", type=int, default=20, help="A2C rollout length (reference: 20)")
     p.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
     p.add_argument("--dist-backend", default="nccl", help="torch.distributed backend (nccl = RCCL on ROCm)")
@@ -450,7 +451,7 @@ def main():
             train_ref4["reference_log_fps"] = REFERENCE_LOG_FPS
             del sc4
             torch.cuda.empty_cache()
-        if args.c5:
+        if not args.no_c5:
             train_c5 = bench_train(args, aux_scenes(4, (300, 400, 3)), dev, world, rank, recurrent=True,
                                    aux_weight=AUX_WEIGHT_LOGGED, envs=512, updates=3, warmup=1,
                                    model="AuxiliaryBigGoalHouseModel (LSTM + deconv heads), 300x400 (config C5)")

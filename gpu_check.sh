@@ -12,6 +12,6 @@ echo "== smoke" && timeout -k 10 200 python -c "import __graft_entry__ as g; g.s
 fi
 echo "== bench" && timeout -k 10 400 python bench.py ${BENCH_ARGS:-} > $OUT/bench.log 2>&1; rc=$?; tail -3 $OUT/bench.log; [ $rc -eq 0 ] || exit $rc
 if [ "${SKIP_PROF:-0}" != "1" ]; then
-echo "== rocprofv3" && ROOT=$PWD && (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $ROOT/$OUT/prof -o run --output-format csv -- python3 $ROOT/bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-pmc --train-steps 3 --train-warmup 1 > $ROOT/$OUT/bench_prof.log 2>&1); rc=$?; tail -2 $OUT/bench_prof.log; [ $rc -eq 0 ] || exit $rc
+echo "== rocprofv3" && ROOT=$PWD && (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $ROOT/$OUT/prof -o run --output-format csv -- python3 $ROOT/bench.py --no-c5 --steps 100 --warmup 10 --no-cpu-baseline --no-pmc --train-steps 3 --train-warmup 1 > $ROOT/$OUT/bench_prof.log 2>&1); rc=$?; tail -2 $OUT/bench_prof.log; [ $rc -eq 0 ] || exit $rc
 fi
 echo "== done"

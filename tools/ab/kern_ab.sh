@@ -11,7 +11,7 @@ ARGS="--steps 10 --warmup 2 --no-cpu-baseline --no-pmc ${KAB_ARGS:---no-train-re
 for v in new head; do
   if [ $v = new ]; then cp /tmp/new.so $L; else cp tools/ab/libvnav_head.so $L; fi
   (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $ROOT/gpurun_out/kab_$v -o run \
-     -- python3 $ROOT/bench.py $ARGS > $ROOT/gpurun_out/kab_$v.log 2>&1) || exit 1
+     -- python3 $ROOT/bench.py --no-c5 $ARGS > $ROOT/gpurun_out/kab_$v.log 2>&1) || exit 1
 done
 cp /tmp/new.so $L
 python3 tools/ab/kern_diff.py gpurun_out/kab_head/run_kernel_stats.csv gpurun_out/kab_new/run_kernel_stats.csv

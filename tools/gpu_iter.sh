@@ -13,11 +13,11 @@ if [ -n "${TESTS:-}" ]; then
   rc=$?; tail -4 $OUT/pytest_$TAG.log; [ $rc -eq 0 ] || exit $rc
 fi
 if [ -n "${BENCH_ARGS:-}" ]; then
-  timeout -k 10 400 python3 bench.py $BENCH_ARGS > $OUT/bench_$TAG.log 2>&1
+  timeout -k 10 400 python3 bench.py --no-c5 $BENCH_ARGS > $OUT/bench_$TAG.log 2>&1
   rc=$?; tail -1 $OUT/bench_$TAG.log | cut -c1-3000; [ $rc -eq 0 ] || exit $rc
   if [ "${PROF:-1}" = "1" ]; then
     cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $ROOT/$OUT/prof_$TAG -o run \
-      -- python3 $ROOT/bench.py $BENCH_ARGS > $ROOT/$OUT/prof_$TAG.log 2>&1
+      -- python3 $ROOT/bench.py --no-c5 $BENCH_ARGS > $ROOT/$OUT/prof_$TAG.log 2>&1
     rc=$?; [ $rc -eq 0 ] || exit $rc
   fi
 fi

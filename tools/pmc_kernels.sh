@@ -14,6 +14,6 @@ for SET in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
            "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_INSTS_SALU"; do
   i=$((i + 1))
   (cd /tmp && timeout -k 10 300 rocprofv3 --pmc $SET --kernel-include-regex "$REGEX" --output-format csv \
-      -d $OUT/pmc_k$i -o run -- python3 $ROOT/bench.py $ARGS > $OUT/pmc_k$i.log 2>&1) || exit $?
+      -d $OUT/pmc_k$i -o run -- python3 $ROOT/bench.py --no-c5 $ARGS > $OUT/pmc_k$i.log 2>&1) || exit $?
   echo "pass $i done"
 done

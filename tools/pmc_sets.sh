@@ -13,6 +13,6 @@ i=0
 for SET in "${SETS[@]}"; do
   i=$((i + 1))
   (cd /tmp && timeout -k 10 300 rocprofv3 --pmc $SET --kernel-include-regex "$REGEX" --output-format csv \
-      -d $OUT/pmcs_k$i -o run -- python3 $ROOT/bench.py $ARGS > $OUT/pmcs_k$i.log 2>&1) || exit $?
+      -d $OUT/pmcs_k$i -o run -- python3 $ROOT/bench.py --no-c5 $ARGS > $OUT/pmcs_k$i.log 2>&1) || exit $?
   echo "pass $i done: $SET"
 done

@@ -12,6 +12,6 @@ ARGS="--steps 30 --warmup 5 --no-cpu-baseline --train-steps 0"
 for C in FETCH_SIZE WRITE_SIZE; do
   name=$(echo $C | tr 'A-Z' 'a-z' | cut -d_ -f1)
   (cd /tmp && timeout -k 10 300 rocprofv3 --pmc $C --kernel-include-regex env_kernel --output-format csv \
-      -d $OUT/pmc_$name -o run -- python3 $ROOT/bench.py $ARGS > $OUT/pmc_$name.log 2>&1) || exit $?
+      -d $OUT/pmc_$name -o run -- python3 $ROOT/bench.py --no-c5 $ARGS > $OUT/pmc_$name.log 2>&1) || exit $?
   echo "pass $C done"
 done
