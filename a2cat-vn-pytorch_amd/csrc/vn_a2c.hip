@@ -248,6 +248,57 @@ __global__ void a2c_schedule_kernel(int64_t* state, float* lr_out, double lr0, d
   state[1] = total + steps_per_update;
 }
 
+// First launch of a rollout: the device schedule (thread 0: a2c_schedule_kernel's
+// arithmetic), step 0's frame rows copied from the env's current rows, and — recurrent —
+// step 0's mask = the carried m and its [one_hot(a) | r] * m (UnrealEnvBaseWrapper,
+// models/goal.py:63-64), with step_post_kernel's arithmetic. Replaces eight launches
+// (schedule, two row copies, the mask copy and four framework kernels of the one-hot build).
+__global__ __launch_bounds__(256) void rollout_begin_kernel(int64_t* state, float* lr_out, double lr0, double max_steps,
+                                                            int64_t steps_per_update, int T,
+                                                            const int32_t* __restrict__ img_src,
+                                                            const int32_t* __restrict__ goal_src,
+                                                            int32_t* __restrict__ img_dst,
+                                                            int32_t* __restrict__ goal_dst, int E,
+                                                            const int64_t* __restrict__ prev_action,
+                                                            const float* __restrict__ prev_reward,
+                                                            const float* __restrict__ prev_mask, int A,
+                                                            float* __restrict__ mask0, float* __restrict__ lra0) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e == 0) {
+    const int64_t total = state[1];
+    const double frac = max_steps > 0.0 ? fmin((double)total / max_steps, 1.0) : 0.0;
+    *lr_out = (float)(lr0 * (1.0 - frac));
+    state[2] = state[0];
+    state[0] += T;
+    state[1] = total + steps_per_update;
+  }
+  if (e >= E) return;
+  img_dst[e] = img_src[e];
+  goal_dst[e] = goal_src[e];
+  if (mask0) {
+    const float m = prev_mask[e];
+    const int64_t a = prev_action[e];
+    mask0[e] = m;
+    for (int j = 0; j < A; ++j) lra0[(int64_t)e * (A + 1) + j] = j == a ? m : 0.0f;
+    lra0[(int64_t)e * (A + 1) + A] = prev_reward[e] * m;
+  }
+}
+
+// The update's metric vector in one thread (replaces four framework kernels): [stats4 *
+// inv_n (torch's tensor / scalar: times the f32 reciprocal), grad norm, aux loss = the
+// per-head MSEs summed (ai2_auxiliary/trainer.py:51-54), episode stats3].
+__global__ void metrics_kernel(const float* __restrict__ stats4, float inv_n, const float* __restrict__ scalars2,
+                               const float* __restrict__ aux3, const float* __restrict__ aux_numel3,
+                               const float* __restrict__ episode3, float* __restrict__ out9) {
+  if (threadIdx.x != 0) return;
+  for (int i = 0; i < 4; ++i) out9[i] = stats4[i] * inv_n;
+  out9[4] = scalars2[0];
+  // (h0 + h2) + h1: torch's sum of three values (two threads along the reduction, thread 0
+  // takes elements 0 and 2, then one shuffle step)
+  out9[5] = aux3 ? (aux3[0] / aux_numel3[0] + aux3[2] / aux_numel3[2]) + aux3[1] / aux_numel3[1] : 0.0f;
+  for (int i = 0; i < 3; ++i) out9[6 + i] = episode3[i];
+}
+
 // Trace marker: an empty kernel whose grid size (tag workgroups of 64 lanes) a kernel
 // trace records, so a rocprofv3 trace of a test run can be split per test.
 __global__ void trace_marker_kernel() {}
@@ -300,6 +351,32 @@ int vn_a2c_schedule(int64_t* state3, float* lr_out, double lr0, double max_time_
   if (!state3 || !lr_out || T <= 0 || steps_per_update < 0) return fail(VN_EINVAL, "vn_a2c_schedule: bad args");
   hipLaunchKernelGGL(a2c_schedule_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, state3, lr_out, lr0,
                      max_time_steps, steps_per_update, T);
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
+
+int vn_a2c_rollout_begin(int64_t* state3, float* lr_out, double lr0, double max_time_steps, int64_t steps_per_update,
+                         int T, const int32_t* img_row_src, const int32_t* goal_row_src, int32_t* img_row_dst,
+                         int32_t* goal_row_dst, int E, const int64_t* prev_action, const float* prev_reward,
+                         const float* prev_mask, int num_actions, float* mask0, float* lra0, vn_stream_t stream) {
+  if (!state3 || !lr_out || T <= 0 || steps_per_update < 0 || E <= 0 || !img_row_src || !goal_row_src ||
+      !img_row_dst || !goal_row_dst)
+    return fail(VN_EINVAL, "vn_a2c_rollout_begin: bad args");
+  if (mask0 && (!lra0 || !prev_action || !prev_reward || !prev_mask || num_actions <= 0))
+    return fail(VN_EINVAL, "vn_a2c_rollout_begin: mask0 needs lra0, prev_action, prev_reward, prev_mask");
+  hipLaunchKernelGGL(rollout_begin_kernel, dim3((E + 255) / 256), dim3(256), 0, (hipStream_t)stream, state3, lr_out,
+                     lr0, max_time_steps, steps_per_update, T, img_row_src, goal_row_src, img_row_dst, goal_row_dst,
+                     E, prev_action, prev_reward, prev_mask, num_actions, mask0, lra0);
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
+
+int vn_a2c_metrics(const float* stats4, float inv_n, const float* scalars2, const float* aux3,
+                   const float* aux_numel3, const float* episode_stats3, float* out9, vn_stream_t stream) {
+  if (!stats4 || !scalars2 || !episode_stats3 || !out9 || (aux3 && !aux_numel3))
+    return fail(VN_EINVAL, "vn_a2c_metrics: bad args");
+  hipLaunchKernelGGL(metrics_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, stats4, inv_n, scalars2, aux3,
+                     aux_numel3, episode_stats3, out9);
   VN_HIP(hipGetLastError());
   return VN_OK;
 }

@@ -337,6 +337,44 @@ __global__ void transpose_kernel(const float* __restrict__ W, int rows, int cols
   WT[(int64_t)c * rows + r] = W[idx];
 }
 
+// Up to kTSet weight transposes (transpose_kernel's element map) in one launch: thread idx
+// of the concatenated element ranges finds its matrix by a scan of the range starts. A
+// backward transposes its weights once (5 matrices of the trunk, 2 of the LSTM core); one
+// launch each cost a dependent dispatch apiece on the few-env path.
+constexpr int kTSet = 6;
+struct TransposeSet {
+  const float* W[kTSet];
+  float* WT[kTSet];
+  int rows[kTSet], cols[kTSet];
+  int64_t start[kTSet + 1];
+  int n = 0;
+  void add(const float* w, int r, int c, float* wt) {
+    if ((int64_t)r * c == 0) return;
+    if (n == 0) start[0] = 0;
+    W[n] = w;
+    WT[n] = wt;
+    rows[n] = r;
+    cols[n] = c;
+    start[n + 1] = start[n] + (int64_t)r * c;
+    ++n;
+  }
+};
+
+__global__ void transpose_set_kernel(TransposeSet s) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= s.start[s.n]) return;
+  int i = 0;
+  while (i + 1 < s.n && idx >= s.start[i + 1]) ++i;
+  const int64_t l = idx - s.start[i];
+  const int cols = s.cols[i], r = (int)(l / cols), c = (int)(l - (l / cols) * cols);
+  s.WT[i][(int64_t)c * s.rows[i] + r] = s.W[i][l];
+}
+
+inline void launch_transpose_set(const TransposeSet& s, hipStream_t st) {
+  if (s.n == 0) return;
+  hipLaunchKernelGGL(transpose_set_kernel, dim3((unsigned)((s.start[s.n] + 255) / 256)), dim3(256), 0, st, s);
+}
+
 // dst[c][r] = src[r][c] for a rows x cols block (row strides lds / ldd), 64 x 64 tiles
 // through LDS: both the reads and the writes are row-contiguous.
 __global__ __launch_bounds__(256) void tile_transpose_kernel(const float* __restrict__ src, int rows, int cols,
@@ -1432,12 +1470,10 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
   auto T = [&](int i) { return w.wt + L.wt_off[i]; };
   // dz5_in != NULL: the trunk backward of the recurrent policy (heads and LSTM already done)
   const float* dz5 = dz5_in ? dz5_in : w.dz5;
-  // transposed weights for the dgrad products
-  for (int i = 1; i < 6; ++i) {
-    const int rows = L.l[i].cout, cols = L.l[i].kp;
-    if (rows * cols == 0) continue;
-    hipLaunchKernelGGL(transpose_kernel, dim3((rows * cols + 255) / 256), dim3(256), 0, st, P + L.l[i].w, rows, cols,
-                       T(i));
+  {  // transposed weights for the dgrad products, one launch
+    TransposeSet ts;
+    for (int i = 1; i < 6; ++i) ts.add(P + L.l[i].w, L.l[i].cout, L.l[i].kp, T(i));
+    launch_transpose_set(ts, st);
   }
   const int n9 = n * G::OH3 * G::OW3;
   // ---- head: dX5 = dout x Whead, masked by X5 ; dWhead = dout^T x X5
@@ -1650,11 +1686,10 @@ int backward_bignet(const PolicyLayout& L, const float* P, const FrameSrc& src, 
   constexpr int OH3 = OH2 - 2, OW3 = OW2 - 2, FCIN = 32 * OH3 * OW3;
   const int A1 = L.A + 1;
   auto T = [&](int i) { return w.wt + L.wt_off[i]; };
-  for (int i = 1; i < 6; ++i) {
-    const int rows = L.l[i].cout, cols = L.l[i].kp;
-    if (rows * cols == 0) continue;
-    hipLaunchKernelGGL(transpose_kernel, dim3((rows * cols + 255) / 256), dim3(256), 0, st, P + L.l[i].w, rows, cols,
-                       T(i));
+  {
+    TransposeSet ts;
+    for (int i = 1; i < 6; ++i) ts.add(P + L.l[i].w, L.l[i].cout, L.l[i].kp, T(i));
+    launch_transpose_set(ts, st);
   }
   const float* dz5 = dz5_in ? dz5_in : w.dz5;
   if (!dz5_in) {  // heads
@@ -1805,10 +1840,12 @@ inline int lstm_backward(const PolicyLayout& L, const float* P, int T, int E, co
   const int A1 = L.A + 1;
   const int N = T * E;
   const int64_t e512 = (int64_t)E * 512;
-  hipLaunchKernelGGL(transpose_kernel, dim3((2048 * L.xcat + 255) / 256), dim3(256), 0, st, P + L.lw, 2048, L.xcat,
-                     w.wcat_t);
-  hipLaunchKernelGGL(transpose_kernel, dim3((A1 * 512 + 255) / 256), dim3(256), 0, st, P + L.l[5].w, A1, 512,
-                     w.head_t);
+  {
+    TransposeSet ts;
+    ts.add(P + L.lw, 2048, L.xcat, w.wcat_t);
+    ts.add(P + L.l[5].w, A1, 512, w.head_t);
+    launch_transpose_set(ts, st);
+  }
   {  // heads: dh_heads = dout x Whead ; dWhead = dout^T x h
     DenseRows fa{dout, OUT_LD, N};
     DenseRows fb{w.head_t, A1, 512};
@@ -1977,8 +2014,12 @@ int aux_forward_impl(const PolicyLayout& L, const float* P, const float* X4, int
                      const AuxWork& w, hipStream_t st) {
   using G = Geo<H0, W0>;
   constexpr int IH = G::OH3, IW = G::OW3, AH = 2 * IH + 2, AW = 2 * IW + 2, PH = 2 * AH + 2, PW = 2 * AW + 2;
-  hipLaunchKernelGGL(transpose_kernel, dim3((32 * 768 + 255) / 256), dim3(256), 0, st, P + L.aw1, 32, 768, w.w1t);
-  hipLaunchKernelGGL(transpose_kernel, dim3((48 * 128 + 255) / 256), dim3(256), 0, st, P + L.aw2, 48, 128, w.w2t);
+  {
+    TransposeSet ts;
+    ts.add(P + L.aw1, 32, 768, w.w1t);
+    ts.add(P + L.aw2, 48, 128, w.w2t);
+    launch_transpose_set(ts, st);
+  }
   if (const int rc = deconv_all<32, kAuxC1, IH, IW, AH, AW>(X4, w.w1t, A1, P + L.ab1, 1, n, st); rc != VN_OK) return rc;
   if constexpr (aux2_fits<AH, AW>()) {
     launch_aux2<AH, AW, PH, PW, false>(A1, n, P + L.aw2, P + L.ab2, Pout, nullptr, 0.0f, nullptr, nullptr, st);

@@ -145,6 +145,10 @@ SIGNATURES.update({
                                        c_float, c_void_p, c_float, c_float,
                                        c_float, c_void_p]),
     "vn_a2c_schedule": (c_int, [c_void_p, c_void_p, c_double, c_double, c_int64, c_int, c_void_p]),
+    "vn_a2c_metrics": (c_int, [c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "vn_a2c_rollout_begin":(c_int, [c_void_p, c_void_p, c_double, c_double, c_int64, c_int, c_void_p, c_void_p,
+                                     c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
+                                     c_void_p, c_void_p]),
     "vn_policy_sample_dev": (c_int, [c_void_p, c_int, c_int, c_uint64, c_void_p, c_uint64, c_void_p, c_void_p,
                                      c_void_p, c_void_p, c_void_p]),
     "vn_trace_marker": (c_int, [c_int, c_void_p]),

@@ -13,7 +13,7 @@ Everything per step is a device launch: policy forward on frames gathered zero-c
 from the scene cache by row index, categorical sampling, env step (index-only), then
 returns, loss gradient, backward, one flat-buffer all-reduce, norm, clip + RMSprop. No
 host synchronisation inside ``step(sync=False)``. The per-update values (sampling counter,
-learning rate) come from a device-side schedule (``vn_a2c_schedule``), so one update has no
+learning rate) come from a device-side schedule (``vn_a2c_rollout_begin``), so one update has no
 per-call host arguments: with ``cuda_graph=True`` it is captured once in a hipGraph and
 replayed (single process), which removes the per-launch host cost that dominates small
 batches (the reference's own run is 4 envs x 20 steps, ~400 launches per update).
@@ -34,6 +34,7 @@ UnrealTrainer's replay buffer (deep_rl, absent); here it uses the on-policy roll
 import ctypes
 import time
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -277,14 +278,6 @@ class A2CTrainer:
         frac = min(self.total_steps / self.max_time_steps, 1.0) if self.max_time_steps > 0 else 0.0
         return self.learning_rate * (1.0 - frac)
 
-    def _last_reward_action(self, lra, mask):
-        """[one_hot(a_{t-1}) | r_{t-1}] * m_t (goal.py:63: last action, reward)."""
-        A = self.A
-        lra.zero_()
-        lra[:, :A].scatter_(1, self.prev_action[:, None], 1.0)
-        lra[:, A] = self.prev_reward
-        lra.mul_(mask[:, None])
-
     def _policy_step(self, t, frames):
         """Forward of step t of the rollout into self.out[t*E:(t+1)*E]."""
         net, E, N = self.net, self.env.num_envs, self.num_steps * self.env.num_envs
@@ -292,10 +285,9 @@ class A2CTrainer:
         if not self.recurrent:
             net.forward(self.params, frames, E, self.acts, N, t * E, self.out[sl])
             return
+        # step 0's mask / last action-reward come from vn_a2c_rollout_begin, later steps' from
+        # the env step before them
         net.forward(self.params, frames, E, self.acts, N, t * E, None)
-        if t == 0:  # later steps' inputs were written by vn_a2c_step_post after the previous env step
-            self.masks[0].copy_(self.prev_mask)
-            self._last_reward_action(self.lra[0], self.masks[0])
         hp = self.h0 if t == 0 else self.h_all[(t - 1) * E:t * E]
         cp = self.c0 if t == 0 else self.c_all[(t - 1) * E:t * E]
         net.lstm_step(self.params, E, net.x5(self.acts, N)[sl], self.lra[t], self.masks[t], hp, cp, self.xcat[sl],
@@ -320,14 +312,19 @@ class A2CTrainer:
         E, T, A = env.num_envs, self.num_steps, self.A
         N = T * E
         info = env._info
-        _lib.check(lib.vn_a2c_schedule(_lib.ptr(self.sched), _lib.ptr(self.lr_dev), ctypes.c_double(self.learning_rate),
-                                       ctypes.c_double(self.max_time_steps), ctypes.c_int64(N * self.world), T,
-                                       self._stream()), "vn_a2c_schedule")
+        # one launch: the device schedule, step 0's frame rows (later steps' rows are written
+        # into their slots by the env step before them) and, recurrent, step 0's mask and
+        # [one_hot(a) | r] * m from the carried last action / reward / mask
+        rec = self.recurrent
+        _lib.check(lib.vn_a2c_rollout_begin(
+            _lib.ptr(self.sched), _lib.ptr(self.lr_dev), ctypes.c_double(self.learning_rate),
+            ctypes.c_double(self.max_time_steps), ctypes.c_int64(N * self.world), T, _lib.ptr(info["img_row"]),
+            _lib.ptr(info["goal_row"]), _lib.ptr(self.rows_img), _lib.ptr(self.rows_goal), E,
+            _lib.ptr(self.prev_action) if rec else None, _lib.ptr(self.prev_reward) if rec else None,
+            _lib.ptr(self.prev_mask) if rec else None, A, _lib.ptr(self.masks) if rec else None,
+            _lib.ptr(self.lra) if rec else None, self._stream()), "vn_a2c_rollout_begin")
         for t in range(T):
             sl = slice(t * E, (t + 1) * E)
-            if t == 0:  # later steps' rows are written into their slots by the env step before them
-                self.rows_img[sl].copy_(info["img_row"])
-                self.rows_goal[sl].copy_(info["goal_row"])
             self._policy_step(t, self._frames(self.rows_img[sl], self.rows_goal[sl]))
             # the emitted frames' arena rows go straight into step t + 1's slots (the last step's
             # into the env's own info rows: the bootstrap and the next rollout read them there)
@@ -420,11 +417,14 @@ class A2CTrainer:
         batch, _ = self.sample_training_batch()
         self.update(batch)
         N = self.num_steps * self.env.num_envs
-        if self.aux_weight > 0:  # sum of the per-head MSEs (trainer.py:51-54)
-            aux = (self.aux_stats[:3] / self._aux_numel).sum().view(1)
-        else:
-            aux = torch.zeros(1, device=self.device)
-        m = torch.cat([self.stats / N, self.scalars[:1], aux, self.episode_stats])
+        # [stats / N, grad norm, aux loss (sum of the per-head MSEs, trainer.py:51-54),
+        # episode stats] in one launch; / N is torch's tensor / scalar (times the f32 reciprocal)
+        m = torch.empty(9, dtype=torch.float32, device=self.device)
+        aux = self.aux_weight > 0
+        _lib.check(self.lib.vn_a2c_metrics(_lib.ptr(self.stats), ctypes.c_float(np.float32(1.0) / np.float32(N)),
+                                           _lib.ptr(self.scalars), _lib.ptr(self.aux_stats) if aux else None,
+                                           _lib.ptr(self._aux_numel) if aux else None, _lib.ptr(self.episode_stats),
+                                           _lib.ptr(m), self._stream()), "vn_a2c_metrics")
         vdist.reduce_metrics_(m, 6, self.group)
         return m
 

@@ -368,6 +368,20 @@ int vn_rmsprop_step(float* params, const float* grads, float* square_avg, int64_
  * Bit-identical to the host-argument forms fed the same values. */
 int vn_a2c_schedule(int64_t* state3, float* lr_out, double lr0, double max_time_steps,
                     int64_t steps_per_update, int T, vn_stream_t stream);
+/* First launch of a rollout (replaces vn_a2c_schedule + the step-0 input copies):
+ * vn_a2c_schedule's update of state3 / lr_out, img/goal_row_dst[e] = *_src[e] (step 0's
+ * frame rows) and, when mask0 != NULL, mask0[e] = prev_mask[e] and lra0 [E][A+1] =
+ * [one_hot(prev_action[e]) | prev_reward[e]] * prev_mask[e] (vn_a2c_step_post's form). */
+int vn_a2c_rollout_begin(int64_t* state3, float* lr_out, double lr0, double max_time_steps,
+                         int64_t steps_per_update, int T, const int32_t* img_row_src,
+                         const int32_t* goal_row_src, int32_t* img_row_dst, int32_t* goal_row_dst, int E,
+                         const int64_t* prev_action, const float* prev_reward, const float* prev_mask,
+                         int num_actions, float* mask0, float* lra0, vn_stream_t stream);
+/* An update's metric vector out9 = [stats4 * inv_n, scalars2[0] (grad norm), aux loss =
+ * sum over the three heads of aux3[h] / aux_numel3[h] (0 when aux3 == NULL), episode_stats3]
+ * in one launch. */
+int vn_a2c_metrics(const float* stats4, float inv_n, const float* scalars2, const float* aux3,
+                   const float* aux_numel3, const float* episode_stats3, float* out9, vn_stream_t stream);
 int vn_policy_sample_dev(const float* out, int n, int num_actions, uint64_t seed,
                          const int64_t* counter_base_dev, uint64_t counter_offset, int32_t* actions,
                          float* logp, float* entropy, float* value, vn_stream_t stream);
