@@ -640,6 +640,14 @@ class GoalNavPolicy(torch.nn.Module):
         out = out.view(T, B, A + 1).transpose(0, 1)
         return [out[..., :A], out[..., A:A + 1], (hT.view(B, 1, 512), cT.view(B, 1, 512))]
 
+    def value_prediction(self, inputs, masks=None, states=None):
+        """BigGoalHouseModel.value_prediction (goal.py:135-138): the critic over the recurrent
+        features of ``inputs`` -> (value [B,T,1], states). The same HIP forward as ``forward``
+        (the critic is one column of the fused heads product), so the value is bit-identical
+        to forward's and its gradient flows through the same backward."""
+        _logits, value, states = self.forward(inputs, masks, states)
+        return value, states
+
     def forward_deconv(self, inputs, masks=None, states=None):
         """AuxiliaryBigGoalHouseModel.forward_deconv (goal.py:177-189): (depth [B,T,1,h,w],
         mask [B,T,3,h,w], goal mask [B,T,3,h,w]) from conv_base's map, states unchanged."""

@@ -96,6 +96,32 @@ def test_recurrent_policy_float_input_and_defaults():
     _close(s2[0].cpu(), s1[0].cpu(), 1e-5, "h")
 
 
+def test_value_prediction_matches_oracle_critic():
+    """value_prediction (goal.py:135-138): the critic over the recurrent features, with the
+    final states — the oracle's value and (h_T, c_T) at 1e-5, and bitwise forward's value."""
+    pol = _perturbed_policy(2)
+    ref = RecurrentGoalNetOracle((84, 84)).load_reference(pol.reference_state_dict())
+    B, T, A = 3, 5, 4
+    rng = np.random.RandomState(4)
+    img = torch.as_tensor(rng.randint(0, 256, size=(B, T, 84, 84, 3)).astype(np.uint8))
+    gl = torch.as_tensor(rng.randint(0, 256, size=(B, T, 84, 84, 3)).astype(np.uint8))
+    lra = torch.zeros(B, T, A + 1)
+    lra[..., A] = torch.as_tensor(rng.randn(B, T).astype(np.float32))
+    masks = torch.as_tensor((rng.rand(B, T) > 0.3).astype(np.float32))
+    h0 = torch.as_tensor(rng.randn(B, 1, 512).astype(np.float32)) * 0.5
+    c0 = torch.as_tensor(rng.randn(B, 1, 512).astype(np.float32)) * 0.5
+    inputs = ((img.cuda(), gl.cuda()), lra.cuda())
+    with torch.no_grad():
+        value, (hT, cT) = pol.value_prediction(inputs, masks.cuda(), (h0.cuda(), c0.cuda()))
+        _l, v_fwd, _s = pol(inputs, masks.cuda(), (h0.cuda(), c0.cuda()))
+        _rl, rv, (rh, rc) = ref.forward_seq(frames_to_float(img), frames_to_float(gl), lra, masks, (h0, c0))
+    assert tuple(value.shape) == (B, T, 1)
+    assert torch.equal(value, v_fwd)
+    _close(value.cpu(), rv, 1e-5, "value_prediction")
+    _close(hT.cpu(), rh, 1e-5, "h_T")
+    _close(cT.cpu(), rc, 1e-5, "c_T")
+
+
 def _small_env(n_envs=12, seed=21):
     import vnav
     sc = [vnav.synthetic_scene(k) for k in range(2)]
