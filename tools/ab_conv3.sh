@@ -1,7 +1,9 @@
 #!/bin/bash
 # A/B of conv3's forward product tile (VN_C3_CFG, csrc/vn_policy.hip forward): rocprofv3
 # kernel stats of the 84x84 LSTM and 174x174 LSTM + aux bench legs per form; prints each
-# form's conv3 forward calls and average duration.
+# form's conv3 forward calls and average duration. The VN_C3_CFG switch (1: 128x32, 2: 64x64,
+# 3: 128x64, 4: 128x64 with BK 64) was removed from the source after the measurement
+# (profiles/r03/ab_conv3/summary.txt); re-add it to run this again.
 set -o pipefail
 ROOT=${GRAFT_REPO_ROOT:-/root/repo}
 export TMPDIR=/tmp
