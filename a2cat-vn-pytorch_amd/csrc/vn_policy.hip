@@ -316,9 +316,10 @@ struct EpiSlab {
   }
 };
 
-// Split-K slab [splits][M][N] -> dW [M][KP] and, when N == KP + 1, the bias column db [M].
+// Split-K slab [splits][M][N] -> dW [M][KP] and, when N == KP + 1, the bias column db [M]
+// (also into db2 when given: the LSTM's b_ih and b_hh share one gradient).
 __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int M, int N, int KP, float* dW,
-                                    float* db) {
+                                    float* db, float* db2) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= M * N) return;
   const int row = idx / N, col = idx - (idx / N) * N;
@@ -326,8 +327,10 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, int splits, 
   for (int z = 0; z < splits; ++z) s += slab[((int64_t)z * M + row) * N + col];
   if (col < KP)
     dW[(int64_t)row * KP + col] = s;
-  else
+  else {
     db[row] = s;
+    if (db2) db2[row] = s;
+  }
 }
 
 __global__ void transpose_kernel(const float* __restrict__ W, int rows, int cols, float* __restrict__ WT) {
@@ -672,7 +675,7 @@ inline void launch_wgrad(const float* dZ, int64_t ldz, int M, FB fb, int KP, int
   EpiSlab ep{slab, M, N};
   launch_gemm<BM, BN, BK, WM, WN>(fa, fb, ep, M, N, P, st, splits, kchunk);
   const int total = M * N;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, slab, splits, M, N, KP, dW, db);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, slab, splits, M, N, KP, dW, db, nullptr);
 }
 
 // The same split-K wgrad on the x6 core: both operands gathered along the reduction index
@@ -693,7 +696,7 @@ inline void launch_wgrad6(const float* dZ, int64_t ldz, int M, FB fb, int KP, in
   hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, BK, WM, WN, DenseT, FB, EpiSlab>), grid_for(M, N, BM, BN, splits),
                      dim3(256), 0, st, fa, fb, ep, M, N, P, kchunk);
   const int total = M * N;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, slab, splits, M, N, KP, dW, db);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, slab, splits, M, N, KP, dW, db, nullptr);
 }
 
 // Split-K wgrad on the x6 core from transposed operands: dZT [M][P] (rows = output
@@ -701,7 +704,7 @@ inline void launch_wgrad6(const float* dZ, int64_t ldz, int M, FB fb, int KP, in
 // [P][*] tensors are transposed once (tile_transpose) so the reduction runs k-contiguous.
 template <int BM, int BN, int WM, int WN>
 inline void launch_wgrad_x6(const float* dZT, int M, const float* XT, int KP, int P, int64_t ldt, float* slab,
-                            int64_t slab_cap, float* dW, float* db, hipStream_t st) {
+                            int64_t slab_cap, float* dW, float* db, hipStream_t st, float* db2 = nullptr) {
   constexpr int BK = 32;
   const int N = KP + (db ? 1 : 0);  // db == nullptr: no bias column
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
@@ -716,7 +719,7 @@ inline void launch_wgrad_x6(const float* dZT, int M, const float* XT, int KP, in
   hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, BK, WM, WN, DenseRows, RowsOnes, EpiSlab>), grid_for(M, N, BM, BN, splits),
                      dim3(256), 0, st, fa, fb, ep, M, N, P, kchunk);
   const int total = M * N;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, slab, splits, M, N, KP, dW, db);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, slab, splits, M, N, KP, dW, db, db2);
 }
 
 // dgrad of one (group, parity) class of a k4 s2 conv: input pixels (y, x) with
@@ -1192,7 +1195,7 @@ inline int launch_conv_wgrad_x6(const float* dz, const float* X, int n, float* s
     nsrc = kParts;
   }
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((nel + 255) / 256)), dim3(256), 0, st, src, nsrc, S::CO,
-                     S::SLAB_N, S::KW, dW, S::BIAS ? db : nullptr);
+                     S::SLAB_N, S::KW, dW, S::BIAS ? db : nullptr, nullptr);
   return VN_OK;
 }
 
@@ -1917,8 +1920,7 @@ inline int lstm_backward(const PolicyLayout& L, const float* P, int T, int E, co
     tile_transpose(w.dgates, N, 2048, 2048, w.dgates_t, nt, st);
     tile_transpose(xcat_all, N, L.xcat, L.xcat, w.xcat_t, nt, st);
     launch_wgrad_x6<128, 128, 2, 2>(w.dgates_t, 2048, w.xcat_t, L.xcat, N, nt, w.slab, slab_floats(L), Gr + L.lw,
-                                   Gr + L.lbih, st);
-    VN_HIP(hipMemcpyAsync(Gr + L.lbhh, Gr + L.lbih, 2048 * sizeof(float), hipMemcpyDeviceToDevice, st));
+                                   Gr + L.lbih, st, Gr + L.lbhh);
   }
   VN_HIP(hipGetLastError());
   return VN_OK;
