@@ -109,13 +109,15 @@ class A2CTrainer:
             f32 = dict(dtype=torch.float32, **kw)
             self.xcat = torch.zeros((N, X), **f32)
             self.lstm_acts = torch.zeros((N, 2048), **f32)
-            self.c_all = torch.zeros((N, 512), **f32)
-            self.h_all = torch.zeros((N, 512), **f32)
+            # h and c of every step in one [2][T*E][512] buffer, and the carry into the next
+            # rollout in one [2][E][512] buffer: the carry is one strided copy per update
+            self._hc_all = torch.zeros((2, N, 512), **f32)
+            self.h_all, self.c_all = self._hc_all[0], self._hc_all[1]
             self.gates = torch.zeros((E, 2048), **f32)
             self.masks = torch.ones((T, E), **f32)
             self.lra = torch.zeros((T, E, A1), **f32)
-            self.h0 = torch.zeros((E, 512), **f32)    # state entering the rollout
-            self.c0 = torch.zeros((E, 512), **f32)
+            self._hc0 = torch.zeros((2, E, 512), **f32)  # state entering the rollout
+            self.h0, self.c0 = self._hc0[0], self._hc0[1]
             self.prev_action = torch.zeros(E, dtype=torch.int64, **kw)
             self.prev_reward = torch.zeros(E, **f32)
             self.prev_mask = torch.zeros(E, **f32)    # 0: the first step starts every episode
@@ -379,9 +381,8 @@ class A2CTrainer:
             net.lstm_backward(self.params, T, E, self.dout, self.h_all, self.xcat, self.lstm_acts, self.c_all, self.c0,
                               self.masks, net.x5(self.acts, N), self.dz5, self.grads, self.lstm_ws)
             net.backward_ex(self.params, frames, N, self.acts, N, None, self.dz5, dx4, self.grads, self.workspace)
-            # (h, c) after the last step carry into the next rollout
-            self.h0.copy_(self.h_all[(T - 1) * E:])
-            self.c0.copy_(self.c_all[(T - 1) * E:])
+            # (h, c) after the last step carry into the next rollout (one copy launch)
+            self._carry_states()
         else:
             net.backward_ex(self.params, frames, N, self.acts, N, self.dout, None, dx4, self.grads, self.workspace)
         if aux_batch is not None:
@@ -402,6 +403,11 @@ class A2CTrainer:
                                            ctypes.c_float(scale), _lib.ptr(self.scalars), _lib.ptr(self.lr_dev),
                                            ctypes.c_float(self.rms_alpha), ctypes.c_float(self.rms_epsilon), st),
                    "vn_rmsprop_step_dev")
+
+    def _carry_states(self):
+        """(h0, c0) = (h, c) of the rollout's last step, both in one strided copy."""
+        E, T = self.env.num_envs, self.num_steps
+        self._hc0.copy_(self._hc_all.view(2, T, E, 512)[:, T - 1])
 
     def _add_trunk_grads(self, g):
         """grads[trunk] += g[trunk]: the conv / conv_merge layers (the only ones backward_ex
@@ -490,8 +496,7 @@ class A2CTrainer:
         for _ in range(int(max_rollouts)):
             self.rollout()
             if self.recurrent:  # (h, c) after the last step carry on, as update() does
-                self.h0.copy_(self.h_all[(T - 1) * E:])
-                self.c0.copy_(self.c_all[(T - 1) * E:])
+                self._carry_states()
             st = self.episode_stats.to(torch.float64)
             vdist.reduce_metrics_(st, 0, self.group)
             tot += st.cpu()
