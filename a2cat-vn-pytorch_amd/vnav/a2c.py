@@ -51,7 +51,8 @@ class A2CTrainer:
     def __init__(self, env, net=None, params=None, num_steps=20, gamma=0.99, learning_rate=7e-4,
                  max_time_steps=2e6, rms_alpha=0.99, rms_epsilon=1e-5, max_gradient_norm=0.5,
                  value_coefficient=0.5, entropy_coefficient=0.01, seed=0, process_group=None, recurrent=False,
-                 aux_weight=0.0, arch="goal", cuda_graph=False, aux_source="rollout", replay_size=8):
+                 aux_weight=0.0, arch="goal", cuda_graph=False, aux_source="rollout", replay_size=8,
+                 capture_collectives=False, allreduce_buckets=2, time_collectives=False):
         self.env = env
         self.lib = _lib.load()
         self.device = env.device
@@ -67,6 +68,12 @@ class A2CTrainer:
         self.seed = int(seed)
         self.group = process_group
         self.world, self.rank = vdist.world_of(process_group)
+        if allreduce_buckets not in (1, 2):
+            raise ValueError("allreduce_buckets must be 1 or 2")
+        self.allreduce_buckets = int(allreduce_buckets)
+        self.time_collectives = bool(time_collectives)
+        self.collective_events = []
+        self._head_work = None
         self.aux_weight = float(aux_weight)
         self.net = net if net is not None else PolicyNet(env.frame_shape[:2], env.num_actions, self.device,
                                                          recurrent=recurrent, aux=self.aux_weight > 0, arch=arch)
@@ -186,9 +193,15 @@ class A2CTrainer:
         self.num_updates = 0
         self.total_steps = 0
         self.cuda_graph = bool(cuda_graph)
-        if self.cuda_graph and self.world > 1 and not vdist.capturable(process_group):
-            raise ValueError("cuda_graph=True at world > 1 needs the nccl (RCCL) backend: a gloo all-reduce "
-                             "cannot be captured in a hipGraph")
+        if self.cuda_graph and self.world > 1:
+            if not vdist.capturable(process_group):
+                raise ValueError("cuda_graph=True at world > 1 needs the nccl (RCCL) backend: a gloo all-reduce "
+                                 "cannot be captured in a hipGraph")
+            if not capture_collectives:
+                # the captured RCCL all-reduce has not run against eager updates on a multi-GPU
+                # node (DESIGN.md "Multi-GPU"): opt in explicitly
+                raise ValueError("cuda_graph=True at world > 1 captures the RCCL all-reduces in the hipGraph, which "
+                                 "is not yet validated against eager updates: pass capture_collectives=True to opt in")
         self._graph = None
         self._graph_out = None
         self._graph_gen = None
@@ -380,6 +393,9 @@ class A2CTrainer:
         if self.recurrent:
             net.lstm_backward(self.params, T, E, self.dout, self.h_all, self.xcat, self.lstm_acts, self.c_all, self.c0,
                               self.masks, net.x5(self.acts, N), self.dz5, self.grads, self.lstm_ws)
+            # the heads + LSTM (+ aux heads) gradients are final here: their all-reduce runs on
+            # RCCL's stream while the trunk backward runs on this one
+            self._allreduce_head_bucket()
             net.backward_ex(self.params, frames, N, self.acts, N, None, self.dz5, dx4, self.grads, self.workspace)
             # (h, c) after the last step carry into the next rollout (one copy launch)
             self._carry_states()
@@ -393,7 +409,7 @@ class A2CTrainer:
                 g, = torch.autograd.grad(loss, self.model_view().params, allow_unused=True)
                 if g is not None:
                     self.grads.add_(g)
-        scale = vdist.allreduce_gradients_(self.grads, self.group)  # RCCL, one flat bucket
+        scale = self._allreduce_tail()
         P = net.n_params
         _lib.check(lib.vn_grad_norm(_lib.ptr(self.grads), P, ctypes.c_float(scale),
                                     ctypes.c_float(self.max_gradient_norm), _lib.ptr(self.norm_partial),
@@ -403,6 +419,52 @@ class A2CTrainer:
                                            ctypes.c_float(scale), _lib.ptr(self.scalars), _lib.ptr(self.lr_dev),
                                            ctypes.c_float(self.rms_alpha), ctypes.c_float(self.rms_epsilon), st),
                    "vn_rmsprop_step_dev")
+
+    def _buckets_split(self):
+        """Two gradient buckets when the head bucket is final before the trunk backward:
+        [head.w, P) = heads + LSTM + aux heads (flat layout, include/vnav.h), [0, head.w) =
+        the conv / conv_merge trunk. One bucket otherwise (feed-forward nets compute heads and
+        trunk in one call; a compute_auxiliary_loss override may touch every parameter)."""
+        return self.world > 1 and self.allreduce_buckets == 2 and self.recurrent and not self._custom_aux
+
+    def _allreduce_head_bucket(self):
+        self._head_work = None
+        if not self._buckets_split():
+            return
+        hw, _ = self.net.offsets["head"]
+        self._head_work = vdist.allreduce_async_(self.grads[hw:], self.group)
+
+    def _allreduce_tail(self):
+        """The remaining all-reduce (the trunk bucket, or the whole flat gradient) and the
+        wait for the head bucket; returns the 1/world scale. With time_collectives the
+        compute-stream time from here to the all-reduced gradient (the exposed, not
+        overlapped, collective time) is recorded per update."""
+        if self.world == 1:
+            return 1.0
+        ev = None
+        if self.time_collectives:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
+        if getattr(self, "_head_work", None) is not None:
+            hw, _ = self.net.offsets["head"]
+            scale = vdist.allreduce_gradients_(self.grads[:hw], self.group)
+            self._head_work.wait()
+            self._head_work = None
+        else:
+            scale = vdist.allreduce_gradients_(self.grads, self.group)  # RCCL, one flat bucket
+        if ev is not None:
+            ev[1].record()
+            self.collective_events.append(ev)
+        return scale
+
+    def collective_ms(self):
+        """Mean exposed all-reduce time per update (ms) over the recorded updates (syncs)."""
+        if not self.collective_events:
+            return None
+        torch.cuda.synchronize(self.device)
+        ms = [a.elapsed_time(b) for a, b in self.collective_events]
+        self.collective_events = []
+        return sum(ms) / len(ms)
 
     def _carry_states(self):
         """(h0, c0) = (h, c) of the rollout's last step, both in one strided copy."""
@@ -517,7 +579,32 @@ class A2CTrainer:
         if self.recurrent:
             for k in self._RECURRENT_STATE:
                 sd[k] = getattr(self, k).cpu()
+        if self.aux_source == "replay":  # the replay ring and its draw stream resume exactly
+            sd["replay_rows"] = self.replay_rows.cpu()
+            sd["replay_fill_pos"] = torch.tensor([self.replay_filled, self.replay_pos], dtype=torch.int64)
+            sd["replay_rng"] = self._replay_rng.get_state()
         return sd
+
+    def params_state_dict(self):
+        """The world-agnostic part of the state: parameters, RMSprop state and the update /
+        step counters (what a single-process ``test()`` needs after distributed training)."""
+        return {"params": self.params.detach().cpu(), "square_avg": self.square_avg.cpu(),
+                "num_updates": self.num_updates, "total_steps": self.total_steps, "sched": self.sched.cpu(),
+                "seed": self.seed, "world": self.world, "params_only": True}
+
+    def load_params_state_dict(self, sd):
+        """Parameters (and RMSprop state, counters when present) of any world's checkpoint;
+        the env state and recurrent carry of this trainer are left as they are."""
+        if tuple(sd["params"].shape) != tuple(self.params.shape):
+            raise ValueError("checkpoint holds %d parameters, this policy has %d"
+                             % (sd["params"].numel(), self.params.numel()))
+        self.params.copy_(sd["params"].to(self.device))
+        if "square_avg" in sd:
+            self.square_avg.copy_(sd["square_avg"].to(self.device))
+        self.num_updates = int(sd.get("num_updates", self.num_updates))
+        self.total_steps = int(sd.get("total_steps", self.total_steps))
+        if "sched" in sd:
+            self.sched.copy_(sd["sched"].to(self.device))
 
     def load_state_dict(self, sd):
         """Restore a state_dict() of this rank (env shard, running returns, recurrent carry
@@ -541,6 +628,10 @@ class A2CTrainer:
         if self.recurrent:
             for k in self._RECURRENT_STATE:
                 getattr(self, k).copy_(sd[k].to(self.device))
+        if self.aux_source == "replay" and "replay_rows" in sd:
+            self.replay_rows.copy_(sd["replay_rows"].to(self.device))
+            self.replay_filled, self.replay_pos = (int(x) for x in sd["replay_fill_pos"])
+            self._replay_rng.set_state(sd["replay_rng"])
         self.env.observe(gather=False)
 
 

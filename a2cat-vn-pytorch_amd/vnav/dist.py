@@ -1,9 +1,11 @@
 """Data parallelism: one process per GPU, torch.distributed over RCCL ("nccl" on ROCm).
 
 Envs are independent, so each rank owns its own env shard and a full replica of the
-scene cache; the only data-path exchange is ONE all-reduce of the flat
-fp32 gradient buffer per update (0.96 MB for the 84x84 policy: latency-bound on xGMI,
-issued as a single call), plus one tiny all-reduce of the episode/loss statistics.
+scene cache; the only data-path exchange is the all-reduce of the flat
+fp32 gradient buffer per update (0.96 MB for the 84x84 feed-forward policy, one call;
+9.4 MB with the LSTM, in two buckets: heads + LSTM + aux heads as soon as the LSTM
+backward ends, overlapped with the trunk backward, then the trunk), plus one tiny
+all-reduce of the episode/loss statistics.
 The reference has no distributed code at all (it runs 4 SubprocVecEnv processes on
 one GPU, experiments/thor_cached_auxiliary.py:58-71).
 """
@@ -53,6 +55,17 @@ def allreduce_gradients_(flat, group=None):
     return 1.0 / world
 
 
+def allreduce_async_(flat, group=None):
+    """Start a SUM all-reduce of ``flat`` in place and return its work handle (None at world
+    1). With RCCL the collective runs on the communicator's own stream once the current
+    stream reaches this point, so later kernels on the current stream overlap it; ``wait()``
+    makes the current stream wait for it."""
+    world, _ = world_of(group)
+    if world == 1:
+        return None
+    return dist.all_reduce(flat, group=group, async_op=True)
+
+
 def reduce_metrics_(m, n_mean, group=None):
     """m = [mean stats (n_mean entries) | summed counters]: average the first n_mean
     entries over ranks and sum the rest."""
@@ -71,6 +84,23 @@ def broadcast_params_(flat, src=0, group=None):
         gsrc = src if group is None else dist.get_global_rank(group, src)
         dist.broadcast(flat, src=gsrc, group=group)
     return flat
+
+
+def check_ranks_agree(values, what, group=None):
+    """Raise on every rank unless all ranks hold the same integer ``values`` (an all-reduce
+    of [v, -v] with MAX gives max and -min in one call)."""
+    world, rank = world_of(group)
+    if world == 1:
+        return
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
+    v = torch.tensor([float(x) for x in values], dtype=torch.float64, device=dev)
+    t = torch.cat([v, -v])
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    n = len(values)
+    hi, lo = t[:n].cpu(), -t[n:].cpu()
+    if not torch.equal(hi, lo):
+        raise RuntimeError("ranks disagree on %s: min %s, max %s (rank %d has %s)"
+                           % (what, lo.tolist(), hi.tolist(), rank, list(values)))
 
 
 def rank_seed(seed, rank):

@@ -256,10 +256,13 @@ class VectorEnv:
             if a.shape != (self.num_envs,):
                 raise ValueError("actions must have shape [num_envs]")
         if out is not None and gather:
-            # the same caller-owned buffers as the previous call: validated then, pointers cached
+            # the same caller-owned buffers as the previous call: validated then, pointers cached.
+            # The key also holds each buffer's current data_ptr and size, so a tensor that was
+            # resize_()d or set_() to other storage since is validated again
             bufs = (out["image"], out["goal"], out.get("reward"), out.get("done"), out.get("state"))
             c = self._out_cache
-            if c is not None and all(x is y for x, y in zip(bufs, c[0])):
+            if c is not None and all(x is y for x, y in zip(bufs, c[0])) and \
+                    c[2] == tuple((t.data_ptr(), t.numel()) if t is not None else None for t in bufs):
                 P = c[1]
                 _lib.check(self.lib.vn_step(self._ctx, _lib.ptr(a), P[0], P[1], P[2], P[3], P[4], self._stream()),
                            "vn_step")
@@ -282,7 +285,8 @@ class VectorEnv:
             self._check_out("state", state, torch.int32, self.num_envs)
             if gather:
                 bufs = (img, goal, reward, done, state)
-                self._out_cache = (bufs, tuple(_lib.ptr(t) for t in bufs))
+                self._out_cache = (bufs, tuple(_lib.ptr(t) for t in bufs),
+                                   tuple((t.data_ptr(), t.numel()) if t is not None else None for t in bufs))
         _lib.check(self.lib.vn_step(self._ctx, _lib.ptr(a), _lib.ptr(img), _lib.ptr(goal), _lib.ptr(reward),
                                     _lib.ptr(done), _lib.ptr(state), self._stream()), "vn_step")
         info = dict(self._info)

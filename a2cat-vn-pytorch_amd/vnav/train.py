@@ -102,6 +102,8 @@ class Experiment:
     auxiliary_weight = 0.0
     hardness = None
     cuda_graph = False
+    capture_collectives = False  # cuda_graph at world > 1 (captured RCCL): explicit opt-in only
+    aux_source = "rollout"
 
     def __init__(self, env_kwargs=None, model_kwargs=None, save_dir=None, seed=0, device=None, logger=print,
                  **overrides):
@@ -131,7 +133,10 @@ class Experiment:
                           rms_epsilon=self.rms_epsilon, max_gradient_norm=self.max_gradient_norm,
                           value_coefficient=self.value_coefficient, entropy_coefficient=self.entropy_coefficient,
                           seed=self.seed, recurrent=self.recurrent,
-                          aux_weight=self.auxiliary_weight, cuda_graph=self.cuda_graph and vdist.capturable())
+                          aux_weight=self.auxiliary_weight, aux_source=self.aux_source,
+                          # world > 1: only on explicit opt-in (the captured RCCL path is unvalidated)
+                          cuda_graph=self.cuda_graph and (self.world == 1 or self.capture_collectives),
+                          capture_collectives=self.capture_collectives)
 
     def _setup(self):
         if self.trainer is None:
@@ -147,23 +152,96 @@ class Experiment:
 
     @property
     def checkpoint_path(self):
-        """One file per rank when world > 1: the env shard, running returns and recurrent
-        carry are per rank (the parameters and RMSprop state are the same on every rank)."""
-        if self.world > 1:
-            return os.path.join(self.save_dir, "checkpoint.rank%d.pt" % self.rank)
+        """save_dir/checkpoint.pt. One process: the whole trainer state. world > 1: the
+        world-agnostic parameters + RMSprop state that rank 0 writes once every rank's own
+        state is on disk (what ``test()`` in a single process loads); the per-rank states
+        (env shard, running returns, recurrent carry) live in ``rank_checkpoint_path()``."""
         return os.path.join(self.save_dir, "checkpoint.pt")
 
-    def save_checkpoint(self, path=None):
-        path = path or self.checkpoint_path
+    def _generation_dir(self, total_steps):
+        return os.path.join(self.save_dir, "ckpt-%012d" % int(total_steps))
+
+    def rank_checkpoint_path(self, total_steps=None):
+        """This rank's file of the last complete checkpoint set (world > 1), or of the set
+        at ``total_steps``. None when no complete set exists."""
+        if total_steps is None:
+            latest = self._latest()
+            if latest is None:
+                return None
+            total_steps = latest["total_steps"]
+        return os.path.join(self._generation_dir(total_steps), "rank%d.pt" % self.rank)
+
+    def _latest(self):
+        """latest.json: the complete per-rank checkpoint set (written by rank 0 after every
+        rank has saved)."""
+        import json
+        p = os.path.join(self.save_dir, "latest.json")
+        if not os.path.exists(p):
+            return None
+        with open(p) as f:
+            return json.load(f)
+
+    @staticmethod
+    def _atomic_save(obj, path):
         os.makedirs(os.path.dirname(path), exist_ok=True)
         tmp = path + ".tmp"
-        torch.save(self.trainer.state_dict(), tmp)
+        torch.save(obj, tmp)
         os.replace(tmp, path)
-        return path
+
+    def save_checkpoint(self, path=None):
+        """One process: checkpoint.pt. world > 1 (collective: every rank calls it): each rank
+        writes its state into the generation directory ckpt-<total_steps>/rank<r>.pt; after a
+        barrier rank 0 writes the world-agnostic checkpoint.pt and then latest.json (the
+        commit point: a crash before it leaves the previous complete set in force) and drops
+        older generations. Resume therefore never mixes ranks of different updates."""
+        tr = self.trainer
+        if self.world == 1:
+            path = path or self.checkpoint_path
+            self._atomic_save(tr.state_dict(), path)
+            return path
+        step = tr.total_steps
+        self._atomic_save(tr.state_dict(), self.rank_checkpoint_path(step))
+        torch.distributed.barrier()
+        if self.rank == 0:
+            import json
+            import shutil
+            self._atomic_save(tr.params_state_dict(), self.checkpoint_path)
+            tmp = os.path.join(self.save_dir, "latest.json.tmp")
+            with open(tmp, "w") as f:
+                json.dump({"total_steps": step, "num_updates": tr.num_updates, "world": self.world}, f)
+            os.replace(tmp, os.path.join(self.save_dir, "latest.json"))
+            keep = os.path.basename(self._generation_dir(step))
+            for d in os.listdir(self.save_dir):
+                if d.startswith("ckpt-") and d != keep:
+                    shutil.rmtree(os.path.join(self.save_dir, d), ignore_errors=True)
+        torch.distributed.barrier()
+        return self.rank_checkpoint_path(step)
+
+    def has_checkpoint(self):
+        if self.world == 1:
+            return os.path.exists(self.checkpoint_path)
+        latest = self._latest()
+        return latest is not None and os.path.exists(self.rank_checkpoint_path(latest["total_steps"]))
 
     def load_checkpoint(self, path=None):
-        sd = torch.load(path or self.checkpoint_path, map_location="cpu", weights_only=True)
-        self._setup().load_state_dict(sd)
+        """One process: checkpoint.pt (or ``path``). world > 1 (collective): this rank's file
+        of the complete set named by latest.json; then the ranks check that they agree on the
+        update and step counters (all-reduce min / max: a mismatch would leave one rank
+        blocked in the gradient all-reduce) and take rank 0's parameters and RMSprop state."""
+        tr = self._setup()
+        if self.world == 1:
+            tr.load_state_dict(torch.load(path or self.checkpoint_path, map_location="cpu", weights_only=True))
+            return self
+        latest = self._latest()
+        if latest is None:
+            raise FileNotFoundError("no complete checkpoint set in %s (latest.json missing)" % self.save_dir)
+        if int(latest["world"]) != self.world:
+            raise ValueError("checkpoint set of world %d resumed at world %d" % (int(latest["world"]), self.world))
+        tr.load_state_dict(torch.load(path or self.rank_checkpoint_path(latest["total_steps"]), map_location="cpu",
+                                      weights_only=True))
+        vdist.check_ranks_agree([tr.num_updates, tr.total_steps], "checkpoint counters (num_updates, total_steps)")
+        vdist.broadcast_params_(tr.params)
+        vdist.broadcast_params_(tr.square_avg)
         return self
 
     def _log(self, m):
@@ -182,7 +260,7 @@ class Experiment:
         """Train to max_time_steps: deep_rl's Trainer.run() (train.py:25). resume=True
         continues from save_dir's checkpoint when there is one (parameters, RMSprop state,
         per-env state and running returns, recurrent carry, update / step counters)."""
-        if resume and os.path.exists(self.checkpoint_path):
+        if resume and self.has_checkpoint():
             self.load_checkpoint()
         tr = self._setup()
         window = dict(episodes=0.0, rsum=0.0, lsum=0.0)
@@ -219,13 +297,20 @@ class Experiment:
             self.logger("Saving %s (step %d)" % (path, self.trainer.total_steps))  # outputs/output.txt:462
 
     def test(self, episodes=None, checkpoint=None):
-        """deep_rl's Trainer.test() (test-train.py:26): the saved policy (when a checkpoint
-        exists) over ``episodes`` (default validation_episodes, else 100) episodes."""
+        """deep_rl's Trainer.test() (test-train.py:26): the saved policy over ``episodes``
+        (default validation_episodes, else 100) episodes. Reads save_dir/checkpoint.pt (or
+        ``checkpoint``), whichever world wrote it: the policy parameters are world-agnostic,
+        a single-process file also restores its env state. Raises FileNotFoundError when
+        there is no checkpoint (evaluating untrained weights would be silent nonsense)."""
         path = checkpoint or self.checkpoint_path
-        if os.path.exists(path):
-            self.load_checkpoint(path)
+        if not os.path.exists(path):
+            raise FileNotFoundError("no checkpoint to test: %s (train first, or pass checkpoint=)" % path)
+        sd = torch.load(path, map_location="cpu", weights_only=True)
+        tr = self._setup()
+        if sd.get("params_only") or (int(sd.get("world", 1)), int(sd.get("rank", 0))) != (self.world, self.rank):
+            tr.load_params_state_dict(sd)
         else:
-            self._setup()
+            tr.load_state_dict(sd)
         n = episodes or self.validation_episodes or 100
         res = self.trainer.evaluate(episodes=n)
         self._log(dict(step=self.trainer.total_steps, **res))
@@ -271,6 +356,11 @@ class ThorCachedAuxiliary(Experiment):
     # extra step costs ~0.01 of return, the same order as the 0.01 entropy bonus, so the
     # policy settles stochastic). profiles/r03/entropy/, DESIGN.md "End-to-end check".
     entropy_coefficient = 0.001
+    # AuxiliaryTrainer computes the deconv loss on self.replay.sample_sequence()
+    # (experiments/ai2_auxiliary/trainer.py:27-31), not on the on-policy batch: the aux batch
+    # is a stored rollout drawn from the last replay_size rollouts. deep_rl's replay buffer
+    # (its capacity and sequence shape) is absent, so the sequence shape is parity unpinned.
+    aux_source = "replay"
 
     def create_env(self, kwargs):
         goal = tuple(kwargs.get("goal", (10, 14, 0)))

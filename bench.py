@@ -65,6 +65,11 @@ def parse():
     p.add_argument("--num-steps", type=int, default=20, help="A2C rollout length (reference: 20)")
     p.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
     p.add_argument("--dist-backend", default="nccl", help="torch.distributed backend (nccl = RCCL on ROCm)")
+    p.add_argument("--pmc-leg", choices=sorted(LEGS), default=None,
+                   help="(child of the PMC pass) run only this training leg: one warmup update, then exactly one "
+                        "update between two vn_trace_marker launches; no env leg, no JSON line")
+    p.add_argument("--cpu-sweep", default="1,16,all",
+                   help="CPU-baseline process counts (comma list; 'all' = every CPU of this process's affinity)")
     return p.parse_args()
 
 
@@ -113,13 +118,14 @@ def pmc_traffic(envs, scenes):
                                        "source": "live rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes"}
 
 
-def pmc_train_mfma(envs, scenes):
-    """Measured matrix-core utilisation of one 84x84 LSTM training update (rollout + update):
-    a rocprofv3 --pmc pass (SQ_VALU_MFMA_BUSY_CYCLES summed over the SIMDs, GRBM_GUI_ACTIVE
-    summed over the 8 XCDs; no tracing) over a child bench run. Busy fraction =
-    sum(MFMA busy) / (SIMDs x sum(GRBM) / 8) over every dispatch of the run. The split-bf16
-    products issue 3-6 bf16 MFMAs per fp32 product, so this is pipe occupancy, not the
-    algorithmic fraction reported next to it."""
+def pmc_train_mfma(args, leg):
+    """Measured matrix-core utilisation of exactly one training update of ``leg`` (rollout +
+    update): a rocprofv3 --pmc pass (SQ_VALU_MFMA_BUSY_CYCLES summed over the SIMDs,
+    GRBM_GUI_ACTIVE summed over the 8 XCDs; no tracing) over a child run of this script with
+    --pmc-leg, which runs one warmup update and then one update between two vn_trace_marker
+    launches. Only the dispatches between the markers are counted. Busy fraction =
+    sum(MFMA busy) / (SIMDs x sum(GRBM) / 8). The split-bf16 products issue 3-6 bf16 MFMAs
+    per fp32 product, so this is pipe occupancy, not the algorithmic fraction."""
     import csv
     import glob
     import shutil
@@ -127,11 +133,10 @@ def pmc_train_mfma(envs, scenes):
     import tempfile
     if shutil.which("rocprofv3") is None:
         return None
-    d = tempfile.mkdtemp(prefix="vnav_pmc_mfma_", dir="/tmp")
+    d = tempfile.mkdtemp(prefix="vnav_pmc_mfma_%s_" % leg, dir="/tmp")
     cmd = ["rocprofv3", "--pmc", "SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE", "--output-format", "csv", "-d", d,
-           "-o", "run", "--", sys.executable, os.path.abspath(__file__), "--steps", "2", "--warmup", "1",
-           "--no-cpu-baseline", "--no-pmc", "--no-train-ff", "--no-train-ref", "--train-steps", "1",
-           "--train-warmup", "0", "--envs", str(envs), "--scenes", str(scenes)]
+           "-o", "run", "--", sys.executable, os.path.abspath(__file__), "--pmc-leg", leg, "--envs", str(args.envs),
+           "--scenes", str(args.scenes), "--num-steps", str(args.num_steps)]
     env = dict(os.environ, TMPDIR="/tmp")
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
@@ -142,23 +147,24 @@ def pmc_train_mfma(envs, scenes):
         return None
     if r.returncode != 0:
         return None
-    mfma = grbm = 0.0
-    disp = set()
+    rows = {}
     for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(path) as f:
             for row in csv.DictReader(f):
-                name = row.get("Kernel_Name", "")
-                if "env_kernel" in name or "random_actions" in name or "synth_frames" in name:
-                    continue  # the env-only warmup steps and scene synthesis of the child run
-                disp.add(row["Dispatch_Id"])
-                if row["Counter_Name"] == "SQ_VALU_MFMA_BUSY_CYCLES":
-                    mfma += float(row["Counter_Value"])
-                elif row["Counter_Name"] == "GRBM_GUI_ACTIVE":
-                    grbm += float(row["Counter_Value"])
+                rec = rows.setdefault(int(row["Dispatch_Id"]), {"name": row.get("Kernel_Name", "")})
+                rec[row["Counter_Name"]] = rec.get(row["Counter_Name"], 0.0) + float(row["Counter_Value"])
+    marks = sorted(i for i, v in rows.items() if "trace_marker" in v["name"])
+    shutil.rmtree(d, ignore_errors=True)
+    if len(marks) != 2:
+        return None
+    win = [v for i, v in rows.items() if marks[0] < i < marks[1]]
+    mfma = sum(v.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) for v in win)
+    grbm = sum(v.get("GRBM_GUI_ACTIVE", 0.0) for v in win)
     if grbm <= 0:
         return None
-    return {"mfma_busy_cycles": mfma, "grbm_gui_active": grbm, "dispatches": len(disp),
-            "source": "live rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE, one LSTM update"}
+    return {"mfma_busy_cycles": mfma, "grbm_gui_active": grbm, "dispatches": len(win), "updates": 1,
+            "source": "live rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE, the dispatches of exactly one "
+                      "%s update (between two vn_trace_marker launches of a --pmc-leg child)" % leg}
 
 
 def aux_flops_per_sample(o3):
@@ -171,10 +177,20 @@ def aux_flops_per_sample(o3):
     return 2 * 3 * (l1 + l2)
 
 
-def train_flops_per_env_step(h=84, w=84, A=4, T=20, recurrent=False, aux=False):
-    """Algorithmic FLOPs of one A2C env-step: policy forward (kept activations serve the
-    backward), weight gradients of every layer, input gradients of all but conv1, and the
-    bootstrap forward amortised over the rollout."""
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md; no sparsity)
+# fp32-equivalent ceilings of the MFMA forms the kernels issue per exact fp32 product
+# (DESIGN.md "bf16 MFMA with exact operand splits"): x3 = 3 bf16 MFMAs (u8 frame x split
+# weight / split dZ), x6 = 6 (split x split), f32 = the f32 MFMA / VALU rate
+CEIL_TFLOPS = {"x3": BF16_MFMA_PEAK_TFLOPS / 3, "x6": BF16_MFMA_PEAK_TFLOPS / 6, "f32": FP32_MFMA_PEAK_TFLOPS}
+
+
+def train_flops_terms(h=84, w=84, A=4, T=20, recurrent=False, aux=False):
+    """Algorithmic FLOPs of one A2C env-step by (part, MFMA form): policy forward (kept
+    activations serve the backward), weight gradients of every layer, input gradients of
+    all but conv1, the bootstrap forward amortised over the rollout, and the
+    aux deconv heads. The form is the one the kernels issue at these geometries
+    (conv1 forward / weight gradient on u8 frames: x3; the aux heads' second layer: f32
+    VALU forward, f32 MFMA backward; everything else x6)."""
     o1 = ((h - 7) // 4 + 1, (w - 7) // 4 + 1)
     o2 = ((o1[0] - 4) // 2 + 1, (o1[1] - 4) // 2 + 1)
     o3 = ((o2[0] - 4) // 2 + 1, (o2[1] - 4) // 2 + 1)
@@ -182,11 +198,33 @@ def train_flops_per_env_step(h=84, w=84, A=4, T=20, recurrent=False, aux=False):
     macs = [2 * p1 * 32 * 147, 2 * p2 * 32 * 512, p3 * 64 * 1024, p3 * 32 * 64, 512 * 32 * p3, (A + 1) * 512]
     if recurrent:  # LSTM gates GEMM [xcat=512+A+1 padded to 4, +512] x 2048: fwd, dgrad, wgrad
         macs.append(2048 * ((512 + A + 1 + 3) // 4 * 4 + 512))
-    fwd = 2 * sum(macs)
-    total = fwd + fwd + 2 * sum(macs[1:]) + fwd / T
+    f1, frest = 2 * macs[0], 2 * sum(macs[1:])
+    terms = [("forward conv1", "x3", f1 * (1 + 1.0 / T)), ("forward rest", "x6", frest * (1 + 1.0 / T)),
+             ("wgrad conv1", "x3", f1), ("wgrad rest", "x6", frest), ("dgrad", "x6", frest)]
     if aux:
-        total += aux_flops_per_sample(o3)
+        ah, aw = 2 * o3[0] + 2, 2 * o3[1] + 2
+        ph, pw = 2 * ah + 2, 2 * aw + 2
+        l1 = 2 * ah * aw * 48 * 4 * 32
+        l2 = 2 * ph * pw * 7 * 4 * 16
+        terms += [("aux layer 1 (fwd, dX4, dW1)", "x6", 3 * l1), ("aux layer 2 forward", "f32", l2),
+                  ("aux layer 2 backward", "f32", 2 * l2)]
+    return terms
+
+
+def train_flops_per_env_step(h=84, w=84, A=4, T=20, recurrent=False, aux=False):
+    """(total algorithmic FLOPs per env-step, forward FLOPs per sample)."""
+    terms = train_flops_terms(h, w, A, T, recurrent, aux)
+    total = sum(f for _, _, f in terms)
+    fwd = sum(f for name, _, f in terms if name.startswith("forward")) / (1 + 1.0 / T)
     return total, fwd
+
+
+def issued_ceiling_tflops(h=84, w=84, A=4, T=20, recurrent=False, aux=False):
+    """The update's fp32-equivalent ceiling when every part runs at the peak of the MFMA form
+    it issues: total FLOPs / sum(FLOPs_i / ceiling_i)."""
+    terms = train_flops_terms(h, w, A, T, recurrent, aux)
+    total = sum(f for _, _, f in terms)
+    return total / sum(f / CEIL_TFLOPS[form] for _, form, f in terms)
 
 
 def aux_scenes(n, frame, seed=0):
@@ -204,7 +242,7 @@ def aux_scenes(n, frame, seed=0):
 
 
 def bench_train(args, scenes, dev, world, rank, recurrent, aux_weight=0.0, envs=None, updates=None, warmup=None,
-                model=None, cuda_graph=False):
+                model=None, cuda_graph=False, marker=False):
     """A2C training throughput: one step = rollout of num_steps on every local env (policy
     forward + sampling + env step) + backward + one RCCL all-reduce of the flat gradient +
     clip + RMSprop. recurrent: the full BigGoalHouseModel (LSTM core, BPTT over the rollout);
@@ -215,19 +253,26 @@ def bench_train(args, scenes, dev, world, rank, recurrent, aux_weight=0.0, envs=
     warmup = args.train_warmup if warmup is None else warmup
     env = vnav.VectorEnv(scenes, E, seed=2000 + rank, device=dev)
     tr = vnav.A2CTrainer(env, num_steps=T, seed=7, max_time_steps=1e12, recurrent=recurrent, aux_weight=aux_weight,
-                         cuda_graph=cuda_graph)
+                         cuda_graph=cuda_graph, time_collectives=world > 1 and not cuda_graph)
     for _ in range(warmup):
         tr.step(sync=False)
     torch.cuda.synchronize(dev)
+    tr.collective_ms()  # drop the warmup updates' collective timings
+    if marker:  # the PMC child's window: exactly the timed updates between two marker kernels
+        from vnav import _lib
+        _lib.check(_lib.load().vn_trace_marker(1, _lib.stream_ptr(dev)), "vn_trace_marker")
     if world > 1:
         torch.distributed.barrier()
     t0 = time.perf_counter()
     for _ in range(updates):
         tr.step(sync=False)
+    if marker:
+        _lib.check(_lib.load().vn_trace_marker(2, _lib.stream_ptr(dev)), "vn_trace_marker")
     torch.cuda.synchronize(dev)
     if world > 1:
         torch.distributed.barrier()
     el = time.perf_counter() - t0
+    coll_ms = tr.collective_ms() if world > 1 else None
     if world > 1:
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -236,6 +281,7 @@ def bench_train(args, scenes, dev, world, rank, recurrent, aux_weight=0.0, envs=
     h, w = env.frame_shape[:2]
     flops, fwd = train_flops_per_env_step(h, w, T=T, recurrent=recurrent, aux=aux_weight > 0)
     tflops = E * T * updates * flops / el / 1e12
+    ceil = issued_ceiling_tflops(h, w, T=T, recurrent=recurrent, aux=aux_weight > 0)
     if model is None:
         model = "BigGoalHouseModel (LSTM core)" if recurrent else "BigGoalHouseModel trunk + heads (no LSTM)"
     res = {"model": model, "frame": [h, w, 3],
@@ -244,9 +290,85 @@ def bench_train(args, scenes, dev, world, rank, recurrent, aux_weight=0.0, envs=
            "num_steps": T, "ms_per_update": el / updates * 1e3, "dtype": "f32",
            "roofline": {"bound": "mfma", "achieved": tflops, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                         "frac": tflops / FP32_MFMA_PEAK_TFLOPS, "flops_per_env_step": flops,
-                        "scope": "whole update (all kernels), algorithmic FLOPs"}}
+                        "scope": "whole update (all kernels), algorithmic FLOPs",
+                        # the same FLOPs against the ceiling of the MFMA forms the kernels issue
+                        # (x3 / x6 split-bf16, f32): frac_issued = achieved / that ceiling
+                        "issued_ceiling_tflops": ceil, "frac_issued": tflops / ceil,
+                        "issued_ceiling_terms": [[n, f, fl] for n, f, fl in
+                                                 train_flops_terms(h, w, T=T, recurrent=recurrent,
+                                                                   aux=aux_weight > 0)]}}
+    if world > 1:
+        P = tr.net.n_params
+        hw = tr.net.offsets["head"][0]
+        res["dist"] = {"backend": torch.distributed.get_backend(tr.group), "world": world,
+                       "allreduce_bytes": 4 * P,
+                       "buckets": [[4 * (P - hw), "heads + LSTM + aux heads (overlaps the trunk backward)"],
+                                   [4 * hw, "trunk"]] if tr._buckets_split() else [[4 * P, "flat"]],
+                       # compute-stream time from the end of the backward to the all-reduced
+                       # gradient (HIP events): the exposed, not overlapped, collective time
+                       "allreduce_exposed_ms_per_update": coll_ms}
     del tr, env
     return res
+
+
+# training legs: name -> (bench_train keyword arguments, scene geometry, default updates / warmup)
+LEGS = {
+    "84": dict(recurrent=True),
+    "ff": dict(recurrent=False),
+    # thor-cached-auxiliary as logged (outputs/output.txt): 174x174 scenes, LSTM policy, aux
+    # deconv loss with the experiment's weight 0.1 (experiments/thor_cached_auxiliary.py:42
+    # overrides AuxiliaryTrainer's 0.05 default, ai2_auxiliary/trainer.py:25), 4 scenes
+    "174": dict(recurrent=True, aux_weight=AUX_WEIGHT_LOGGED, frame=(174, 174, 3), updates=3, warmup=1,
+                model="AuxiliaryBigGoalHouseModel (LSTM + deconv heads), 174x174"),
+    # the logged run's exact batch: 4 envs x 20 steps per update, one captured hipGraph per update
+    "ref4": dict(recurrent=True, aux_weight=AUX_WEIGHT_LOGGED, frame=(174, 174, 3), envs=4, updates=400, warmup=3,
+                 cuda_graph=True, model="AuxiliaryBigGoalHouseModel (LSTM + deconv heads), 174x174, 4 envs "
+                                        "(the logged run's batch), hipGraph per update"),
+    "c5": dict(recurrent=True, aux_weight=AUX_WEIGHT_LOGGED, frame=(300, 400, 3), envs=512, updates=3, warmup=1,
+               model="AuxiliaryBigGoalHouseModel (LSTM + deconv heads), 300x400 (config C5)"),
+}
+LEG_ORDER = ("84", "ff", "174", "ref4", "c5")
+
+
+def leg_enabled(args, leg, world):
+    return {"84": not args.no_train_84, "ff": not args.no_train_ff, "174": not args.no_train_ref,
+            "ref4": not args.no_train_ref and not args.no_train_ref4 and world == 1, "c5": not args.no_c5}[leg]
+
+
+def run_leg(leg, args, scenes, dev, world, rank, updates=None, warmup=None, marker=False):
+    kw = dict(LEGS[leg])
+    frame = kw.pop("frame", None)
+    sc = aux_scenes(4, frame) if frame else scenes
+    up, wu = kw.pop("updates", None), kw.pop("warmup", None)
+    updates = updates if updates is not None else up
+    warmup = warmup if warmup is not None else wu
+    res = bench_train(args, sc, dev, world, rank, updates=updates, warmup=warmup, marker=marker, **kw)
+    if leg in ("174", "ref4"):
+        # context only, not like for like: the logged run also trained UNREAL pixel-control,
+        # reward-prediction and value-replay heads on replayed sequences (deep_rl, absent)
+        res["reference_log_fps"] = REFERENCE_LOG_FPS
+        res["reference_log_note"] = ("the logged 106 env-steps/s also paid for the UNREAL pc / rp / vr losses on "
+                                     "replayed sequences, which this leg does not run: context, not a like-for-like "
+                                     "comparison")
+    if leg == "ref4" and not marker:
+        eager = bench_train(args, sc, dev, world, rank, updates=100, warmup=3, recurrent=True,
+                            aux_weight=AUX_WEIGHT_LOGGED, envs=4, model="eager")
+        res["eager_value"] = eager["value"]
+        res["eager_ms_per_update"] = eager["ms_per_update"]
+    return res
+
+
+def ranks_seen(dev, world):
+    """Which devices the ranks ran on (all-gather of rank, host, PCI bus / uuid): the first
+    multi-GPU run shows that RCCL saw N ranks on N distinct GPUs."""
+    import socket
+    p = torch.cuda.get_device_properties(dev)
+    ident = "%s:%s" % (socket.gethostname(), getattr(p, "pci_bus_id", None) if hasattr(p, "pci_bus_id")
+                       else str(getattr(p, "uuid", dev.index)))
+    seen = [None] * world
+    torch.distributed.all_gather_object(seen, (int(os.environ.get("RANK", "0")), ident))
+    return {"backend": torch.distributed.get_backend(), "world": world, "ranks_seen": len({r for r, _ in seen}),
+            "distinct_devices": len({i for _, i in seen}), "devices": [i for _, i in sorted(seen)]}
 
 
 def device_copy_rate(dev, nbytes, reps=20):
@@ -309,27 +431,58 @@ def host_cpu_info():
     return {"nproc": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)), "model": model}
 
 
-def cpu_baseline(scenes, seconds, workers):
-    """The oracle ('port') batched VectorEnv in numpy, one process per core (fork, before
-    any GPU initialisation), each stepping 256 envs incl. the two-frame gather."""
+def _cpu_quota():
+    """The cgroup CPU quota of this process (cpu.max 'quota period' -> CPUs), if any."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        return None
+
+
+def _cpu_run(workers, seconds, per, fb):
     import multiprocessing as mp
+    ctx = mp.get_context("fork")
+    t0 = time.perf_counter()
+    with ctx.Pool(workers) as pool:
+        res = pool.map(_cpu_worker, [(per, seconds, 100 + i, fb) for i in range(workers)])
+    wall = time.perf_counter() - t0
+    return sum(r[0] / r[1] for r in res), sum(r[0] for r in res), wall
+
+
+def cpu_baseline(scenes, seconds, sweep="1,16,all"):
+    """The oracle ('port') batched VectorEnv in numpy, one process per core (fork, before
+    any GPU initialisation), each stepping 256 envs incl. the two-frame gather, at each
+    process count of ``sweep`` ('all' = every CPU of this process's affinity). ``value`` /
+    ``cores`` are the largest count; ``sweep`` holds every point (and the cgroup quota, when
+    one limits the CPUs the box gives this job)."""
     fb = int(np.prod(scenes[0].frame_shape))
     rows = sum(s.n_states for s in scenes)
     _CPU_SHARED["scenes"] = [(s.graph, s.spd) for s in scenes]
     # frame contents do not change the cost of a gather; fill (not hash) the arena
     _CPU_SHARED["arena"] = np.full((rows, fb), 7, dtype=np.uint8)
     per = 256
-    ctx = mp.get_context("fork")
-    t0 = time.perf_counter()
-    with ctx.Pool(workers) as pool:
-        res = pool.map(_cpu_worker, [(per, seconds, 100 + i, fb) for i in range(workers)])
+    ncpu = len(os.sched_getaffinity(0))
+    counts = []
+    for tok in str(sweep).split(","):
+        n = ncpu if tok.strip() == "all" else int(tok)
+        n = max(1, min(n, ncpu))
+        if n not in counts:
+            counts.append(n)
+    points = []
+    for n in counts:
+        rate, total, wall = _cpu_run(n, seconds, per, fb)
+        points.append({"procs": n, "value": rate, "env_steps": total, "wall_s": wall})
     _CPU_SHARED.clear()
-    wall = time.perf_counter() - t0
-    total = sum(r[0] for r in res)
-    rate = sum(r[0] / r[1] for r in res)
-    return dict(value=rate, unit="env-steps/s", cores=workers, kind="port", host=host_cpu_info(),
-                sample="oracle VectorEnvOracle (numpy) %d procs x %d envs, %.0f s each, %d env-steps incl. "
-                       "2-frame gather from a %d-row arena (wall %.1f s)" % (workers, per, seconds, total, rows, wall))
+    top = points[-1]
+    host = host_cpu_info()
+    host["cgroup_cpu_quota"] = _cpu_quota()
+    return dict(value=top["value"], unit="env-steps/s", cores=top["procs"], kind="port", host=host,
+                sweep=points,
+                sample="oracle VectorEnvOracle (numpy), %s processes x %d envs, %.0f s each (incl. 2-frame gather "
+                       "from a %d-row arena); value = %d processes" % ("/".join(str(c) for c in counts), per, seconds,
+                                                                      rows, top["procs"]))
 
 
 # ---------------------------------------------------------------- GPU bench
@@ -342,16 +495,21 @@ def main():
     import vnav
 
     scenes = [vnav.synthetic_scene(k) for k in range(args.scenes)]
+    if args.pmc_leg:  # child of pmc_train_mfma: one leg, one warmup + one marked update
+        torch.cuda.set_device(0)
+        run_leg(args.pmc_leg, args, scenes, torch.device("cuda", 0), 1, 0, updates=1, warmup=1, marker=True)
+        return
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        workers = max(1, min(16, len(os.sched_getaffinity(0))))
-        cpu = cpu_baseline(scenes, args.cpu_seconds, workers)
+        cpu = cpu_baseline(scenes, args.cpu_seconds, args.cpu_sweep)
     traffic, traffic_info = None, None
-    mfma_pmc = None
+    mfma_pmc = {}
     if rank == 0 and world == 1 and not args.no_pmc:  # child rocprofv3 runs, before this process touches the GPU
         traffic, traffic_info = pmc_traffic(args.envs, args.scenes)
-        if args.train_steps > 0 and not args.no_train_84:
-            mfma_pmc = pmc_train_mfma(args.envs, args.scenes)
+        if args.train_steps > 0:
+            for leg in ("84", "174", "c5"):
+                if leg_enabled(args, leg, world):
+                    mfma_pmc[leg] = pmc_train_mfma(args, leg)
 
     ndev = torch.cuda.device_count()
     dev = torch.device("cuda", local % max(ndev, 1))
@@ -418,50 +576,26 @@ def main():
         elapsed, kern_ms = float(t[0]), float(t[1])
     flags = env.error_flags()
     del env, out
-    train = train_ff = train_ref = train_ref4 = train_c5 = None
+    legs = {}
     if args.train_steps > 0:
         torch.cuda.empty_cache()
-        if not args.no_train_84:
-            train = bench_train(args, scenes, dev, world, rank, recurrent=True)
+        for leg in LEG_ORDER:
+            if not leg_enabled(args, leg, world):
+                continue
+            legs[leg] = run_leg(leg, args, scenes, dev, world, rank)
             torch.cuda.empty_cache()
-        if not args.no_train_ff:
-            train_ff = bench_train(args, scenes, dev, world, rank, recurrent=False)
-            torch.cuda.empty_cache()
-        if not args.no_train_ref:
-            # thor-cached-auxiliary as logged (outputs/output.txt): 174x174 scenes, LSTM policy,
-            # aux deconv loss with the experiment's weight 0.1 (experiments/thor_cached_auxiliary.py:42
-            # overrides AuxiliaryTrainer's 0.05 default, ai2_auxiliary/trainer.py:25), 4 scenes
-            train_ref = bench_train(args, aux_scenes(4, (174, 174, 3)), dev, world, rank, recurrent=True,
-                                    aux_weight=AUX_WEIGHT_LOGGED, updates=3, warmup=1,
-                                    model="AuxiliaryBigGoalHouseModel (LSTM + deconv heads), 174x174")
-            train_ref["reference_log_fps"] = REFERENCE_LOG_FPS
-            torch.cuda.empty_cache()
-        if not args.no_train_ref and not args.no_train_ref4 and world == 1:
-            # the logged run's exact shape: 4 envs x 20 steps per update (outputs/output.txt), where
-            # ~400 launches per update make it launch-bound: eager vs one captured hipGraph per update
-            sc4 = aux_scenes(4, (174, 174, 3))
-            eager = bench_train(args, sc4, dev, world, rank, recurrent=True, aux_weight=AUX_WEIGHT_LOGGED, envs=4,
-                                updates=100, warmup=3, model="AuxiliaryBigGoalHouseModel, 174x174, 4 envs (eager)")
-            train_ref4 = bench_train(args, sc4, dev, world, rank, recurrent=True, aux_weight=AUX_WEIGHT_LOGGED,
-                                     envs=4, updates=400, warmup=3, cuda_graph=True,
-                                     model="AuxiliaryBigGoalHouseModel (LSTM + deconv heads), 174x174, 4 envs "
-                                           "(the logged run's batch), hipGraph per update")
-            train_ref4["eager_value"] = eager["value"]
-            train_ref4["eager_ms_per_update"] = eager["ms_per_update"]
-            train_ref4["reference_log_fps"] = REFERENCE_LOG_FPS
-            del sc4
-            torch.cuda.empty_cache()
-        if not args.no_c5:
-            train_c5 = bench_train(args, aux_scenes(4, (300, 400, 3)), dev, world, rank, recurrent=True,
-                                   aux_weight=AUX_WEIGHT_LOGGED, envs=512, updates=3, warmup=1,
-                                   model="AuxiliaryBigGoalHouseModel (LSTM + deconv heads), 300x400 (config C5)")
-            torch.cuda.empty_cache()
+    train, train_ff, train_ref, train_ref4, train_c5 = (legs.get(k) for k in ("84", "ff", "174", "ref4", "c5"))
+    dist_info = None
+    if world > 1:
+        dist_info = ranks_seen(dev, world)
     if rank == 0:
-        if train is not None and mfma_pmc is not None:
-            simds = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
-            mfma_pmc["simds"] = simds
-            mfma_pmc["busy_frac"] = mfma_pmc["mfma_busy_cycles"] / (simds * mfma_pmc["grbm_gui_active"] / 8.0)
-            train["roofline"]["mfma_busy_measured"] = mfma_pmc
+        simds = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
+        for leg, pm in mfma_pmc.items():
+            if pm is None or legs.get(leg) is None:
+                continue
+            pm["simds"] = simds
+            pm["busy_frac"] = pm["mfma_busy_cycles"] / (simds * pm["grbm_gui_active"] / 8.0)
+            legs[leg]["roofline"]["mfma_busy_measured"] = pm
         env_steps = E * K * world
         value = env_steps / elapsed
         bpe = alg_bytes_per_env_step(fb)
@@ -500,6 +634,7 @@ def main():
             "train_174_lstm_aux": train_ref,
             "train_174_lstm_aux_4env": train_ref4,
             **({"train_c5_300x400": train_c5} if train_c5 else {}),
+            **({"dist": dist_info} if dist_info else {}),
             "error_flags": flags,
         }
         print(json.dumps(line))

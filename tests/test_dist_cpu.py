@@ -138,3 +138,113 @@ def test_gloo_subgroup_broadcast_uses_group_rank():
     assert np.all(res[0][1] == 0.0)            # rank 0 is not in the group: untouched
     assert np.all(res[1][1] == 1.0) and np.all(res[2][1] == 1.0)
     assert res[1][2] == (2, 0) and res[2][2] == (2, 1)
+
+
+class _StubTrainer:
+    """The parts of A2CTrainer the checkpoint protocol uses (CPU tensors, no GPU)."""
+
+    def __init__(self, rank, world):
+        self.rank, self.world = rank, world
+        self.params = torch.zeros(6)
+        self.square_avg = torch.zeros(6)
+        self.env_state = torch.zeros(3)
+        self.num_updates = self.total_steps = 0
+
+    def advance(self, n, rank_value):
+        self.num_updates += n
+        self.total_steps += 10 * n
+        self.params.fill_(float(self.num_updates))
+        self.square_avg.fill_(2.0 * self.num_updates)
+        self.env_state.fill_(rank_value)
+
+    def state_dict(self):
+        return {"params": self.params.clone(), "square_avg": self.square_avg.clone(), "env": self.env_state.clone(),
+                "num_updates": self.num_updates, "total_steps": self.total_steps, "rank": self.rank,
+                "world": self.world}
+
+    def params_state_dict(self):
+        return {"params": self.params.clone(), "square_avg": self.square_avg.clone(), "num_updates": self.num_updates,
+                "total_steps": self.total_steps, "world": self.world, "params_only": True}
+
+    def load_state_dict(self, sd):
+        self.params.copy_(sd["params"])
+        self.square_avg.copy_(sd["square_avg"])
+        self.env_state.copy_(sd["env"])
+        self.num_updates, self.total_steps = int(sd["num_updates"]), int(sd["total_steps"])
+
+
+def _ckpt_worker(rank, world, port, save_dir, q):
+    import sys
+    for p in (REPO, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import json
+    import torch.distributed as dist
+    from vnav import dist as vdist
+    from vnav import train
+    vdist.init_distributed(backend="gloo")
+    out = {}
+    exp = train.make_trainer("cached-thor", save_dir=save_dir, device="cpu", logger=None)
+    exp.trainer = _StubTrainer(rank, world)
+    exp.trainer.advance(10, 100 + rank)
+    exp.save_checkpoint()                                    # set at step 100
+    exp.trainer.advance(10, 200 + rank)
+    exp.save_checkpoint()                                    # set at step 200 (replaces 100)
+    out["gens"] = sorted(d for d in os.listdir(save_dir) if d.startswith("ckpt-"))
+    out["latest"] = json.load(open(os.path.join(save_dir, "latest.json")))
+    # a crash after rank 0 (only) wrote the next generation: latest.json still names step 200
+    exp.trainer.advance(10, 300 + rank)
+    if rank == 0:
+        exp._atomic_save(exp.trainer.state_dict(), exp.rank_checkpoint_path(exp.trainer.total_steps))
+    dist.barrier()
+    fresh = train.make_trainer("cached-thor", save_dir=save_dir, device="cpu", logger=None)
+    fresh.trainer = _StubTrainer(rank, world)
+    fresh.load_checkpoint()
+    out["resumed"] = (fresh.trainer.num_updates, fresh.trainer.total_steps, float(fresh.trainer.env_state[0]),
+                      float(fresh.trainer.params[0]))
+    # rank 1's file of the complete set disagrees (a hand-edited / foreign file): every rank refuses
+    dist.barrier()
+    if rank == 1:
+        p = fresh.rank_checkpoint_path()
+        sd = torch.load(p, weights_only=True)
+        sd["num_updates"] += 1
+        sd["params"].fill_(-1.0)
+        torch.save(sd, p)
+    dist.barrier()
+    bad = train.make_trainer("cached-thor", save_dir=save_dir, device="cpu", logger=None)
+    bad.trainer = _StubTrainer(rank, world)
+    try:
+        bad.load_checkpoint()
+        out["mismatch"] = "loaded"
+    except RuntimeError as e:
+        out["mismatch"] = "refused" if "disagree" in str(e) else str(e)
+    q.put((rank, out))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_checkpoint_sets_are_complete_and_consistent(tmp_path):
+    """world > 1 checkpoints (vnav/train.py): per-rank files in a generation directory
+    committed by rank 0's latest.json after a barrier, a world-agnostic checkpoint.pt for a
+    single-process test(), resume from the last complete set after a partial save, and a
+    refusal on every rank when the ranks' counters disagree."""
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_ckpt_worker, args=(r, world, port, str(tmp_path), q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        o = res[r]
+        assert o["latest"] == {"total_steps": 200, "num_updates": 20, "world": 2}
+        assert o["resumed"] == (20, 200, 200.0 + r, 20.0)   # own env state, rank 0's params
+        assert o["mismatch"] == "refused"
+    assert res[0]["gens"] == ["ckpt-%012d" % 200]
+    sd = torch.load(os.path.join(str(tmp_path), "checkpoint.pt"), weights_only=True)
+    assert sd["params_only"] and sd["num_updates"] == 20 and float(sd["params"][0]) == 20.0

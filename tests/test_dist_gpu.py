@@ -6,7 +6,9 @@ vn_rmsprop_step_dev (vnav/a2c.py update, vnav/dist.py). Two checks:
   equal the update over the concatenated batch (params and square_avg);
 * world 2 (gloo, both ranks on cuda:0 — the box has one GPU; RCCL refuses two ranks on
   one device): A2CTrainer.update() on identical rollouts on both ranks gives exactly the
-  single-process update, and per-rank checkpoints restore each rank's own shard.
+  single-process update, the two-bucket all-reduce (heads + LSTM + aux heads issued after
+  the LSTM backward, overlapped with the trunk backward) equals the one-bucket update
+  bitwise, and per-rank checkpoints restore each rank's own shard.
 """
 import ctypes
 import os
@@ -104,16 +106,28 @@ def _worker(rank, world, port, tmp, q):
         # (1) identical rollouts on both ranks (same env seed, sampling seed of rank 0)
         vdist.rank_seed = lambda seed, r: orig_seed(seed, 0)
 
-        def make(group, env_seed=4, recurrent=True):
-            env = vnav.VectorEnv(sc, 16, seed=env_seed, max_episode_steps=10)
+        def make(group, env_seed=4, recurrent=True, buckets=2, aux=0.0):
+            scn = aux_sc if aux else sc
+            env = vnav.VectorEnv(scn, 16, seed=env_seed, max_episode_steps=10)
             return vnav.A2CTrainer(env, num_steps=5, seed=2, max_time_steps=0, process_group=group,
-                                   recurrent=recurrent)
-        a = make(None)
+                                   recurrent=recurrent, allreduce_buckets=buckets, time_collectives=True,
+                                   aux_weight=aux)
+        from bench import aux_scenes
+        aux_sc = aux_scenes(2, (84, 84, 3))
+        a = make(None)                       # two buckets: heads + LSTM overlapped with the trunk backward
+        a1 = make(None, buckets=1)           # one flat bucket after the whole backward
+        ax = make(None, aux=0.1)             # + the aux heads in the first bucket
+        ax1 = make(None, aux=0.1, buckets=1)
         b = make(solo) if rank == 0 else None
         for _ in range(3):
-            a.step(sync=True)
+            for t in (a, a1, ax, ax1):
+                t.step(sync=True)
             if b is not None:
                 b.step(sync=True)
+        res["buckets_equal"] = bool(torch.equal(a.params, a1.params) and torch.equal(a.square_avg, a1.square_avg))
+        res["buckets_equal_aux"] = bool(torch.equal(ax.params, ax1.params))
+        res["split"] = (a._buckets_split(), a1._buckets_split())
+        res["collective_ms"] = a.collective_ms()
         if rank == 0:
             res["world"] = a.world
             res["same_params"] = bool(torch.equal(a.params, b.params))
@@ -170,5 +184,10 @@ def test_world2_trainer_update_and_per_rank_checkpoints(tmp_path):
     for r in range(world):
         assert "error" not in res[r], res[r]["error"]
         assert res[r]["resume_exact"] and res[r]["refused_other"] and res[r]["shards_differ"], res[r]
+        # the bucketed all-reduce (heads + LSTM first, overlapped with the trunk backward)
+        # equals the single flat bucket bitwise, with and without the aux heads
+        assert res[r]["split"] == (True, False), res[r]
+        assert res[r]["buckets_equal"] and res[r]["buckets_equal_aux"], res[r]
+        assert res[r]["collective_ms"] is not None and res[r]["collective_ms"] >= 0.0
     assert res[0]["world"] == 2
     assert res[0]["same_params"] and res[0]["same_sq"], res[0]

@@ -18,6 +18,9 @@ activation store the kernels wrote; every mask bit that disagrees with the sign 
 oracle's own pre-activation is asserted to be a tie (|z| <= 1e-5 of the layer's scale).
 
 Tolerances (north star): outputs 1e-5, parameter gradients 1e-4 of each tensor's scale.
+Logits and values are also checked element by element: |gpu - fp64| <= 1e-5 |fp64| + a floor
+of 1e-6 of the tensor's scale (a logit near zero is a sum of cancelling terms whose fp32
+rounding is set by the terms, not by the sum: the floor states that absolute bound).
 """
 import ctypes
 
@@ -40,6 +43,25 @@ def _err(a, b):
     a = np.asarray(a, dtype=np.float64)
     b = np.asarray(b, dtype=np.float64)
     return np.abs(a - b).max() / max(np.abs(b).max(), 1e-30)
+
+
+ELEM_RTOL, ELEM_FLOOR = 1e-5, 1e-6
+
+
+def _elementwise(a, b, rtol=ELEM_RTOL, floor=ELEM_FLOOR):
+    """max over elements of |a - b| / (rtol |b| + floor max|b|): <= 1 passes."""
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    return float((np.abs(a - b) / (rtol * np.abs(b) + floor * max(np.abs(b).max(), 1e-30))).max())
+
+
+def _check_outputs(o_logits, o_value, logits, value):
+    """Logits / values: normwise 1e-5 of scale and the elementwise bound above."""
+    assert _err(o_logits, logits) <= 1e-5
+    assert _err(o_value, value) <= 1e-5
+    e = (_elementwise(o_logits, logits), _elementwise(o_value, value))
+    assert max(e) <= 1.0, "elementwise logits / values: %.3g / %.3g of the bound" % e
+    return e
 
 
 def _acts_views(net, acts, n):
@@ -165,8 +187,7 @@ def test_84_batch4096_forward_backward_vs_fp64_oracle():
     logits, value, _, pre = ref.forward_masked(fi, fg, masks)
     flips = _check_masks_are_signs(masks, pre)
     o = out.cpu().numpy()
-    assert _err(o[:, :4], logits.detach().numpy()) <= 1e-5
-    assert _err(o[:, 4], value.detach().numpy().ravel()) <= 1e-5
+    _check_outputs(o[:, :4], o[:, 4], logits.detach().numpy(), value.detach().numpy().ravel())
     assert _err(x5.numpy(), (pre["z5"] * masks["m5"]).detach().numpy()) <= 1e-5
     loss, _ = oa2c.loss(logits, value.view(-1), actions.cpu().long(), rets.cpu().double())
     loss.backward()
@@ -174,14 +195,15 @@ def test_84_batch4096_forward_backward_vs_fp64_oracle():
     print("84x84 n=4096: worst gradient error %.3g of scale; tie flips %s" % (worst, flips))
 
 
-def _aux_scene_174():
+def _aux_scene(hw=(174, 174), X=6):
     import vnav
     rng = np.random.RandomState(3)
-    X = Y = 6
+    Y = X
+    h, w = hw
     maze = np.ones((X, Y), dtype=bool)
-    obs = rng.randint(0, 256, size=(X, Y, 4, 174, 174, 3)).astype(np.uint8)
-    dep = rng.randint(0, 256, size=(X, Y, 4, 174, 174, 1)).astype(np.uint8)
-    seg = rng.randint(0, 256, size=(X, Y, 4, 174, 174, 3)).astype(np.uint8)
+    obs = rng.randint(0, 256, size=(X, Y, 4, h, w, 3)).astype(np.uint8)
+    dep = rng.randint(0, 256, size=(X, Y, 4, h, w, 1)).astype(np.uint8)
+    seg = rng.randint(0, 256, size=(X, Y, 4, h, w, 3)).astype(np.uint8)
     return vnav.oriented_scene(maze, obs, [(0, 0, 1)], depths=dep, segmentations=seg)
 
 
@@ -194,18 +216,22 @@ def _gather(env, rows):
     return dst
 
 
-def test_174_batch512_rows_aux_vs_fp64_oracle():
-    """174x174 (the reference topology), 512 samples gathered from the scene cache by row,
-    as the trainer's update runs them: trunk + heads forward, the aux heads' fused loss
+@pytest.mark.parametrize("hw,n", [((174, 174), 512), ((300, 400), 512)], ids=["174x174", "c5_300x400"])
+def test_batch_rows_aux_vs_fp64_oracle(hw, n):
+    """174x174 (the reference topology) and config C5's 300x400 (the size-adaptive trunk:
+    74x99 -> 36x48 -> 17x23, conv_merge over 12,512 features, heads to 74x98), 512 samples
+    gathered from the scene cache by row, as the trainer's update runs them (the C5 leg's
+    rollout forward runs 512 envs per step): trunk + heads forward, the aux heads' fused loss
     (vn_aux_forward_loss_grad), the aux backward into dL/dX4 and the trunk backward of the
-    A2C loss + 0.1 x the deconv loss — outputs, predictions and every gradient vs fp64."""
+    A2C loss + 0.1 x the deconv loss — outputs, predictions and every gradient vs fp64, with
+    the GPU's ReLU masks (no tie search)."""
     import vnav
     from vnav.policy import AuxTargets, frames_from_rows
-    pol = _noisy_policy((174, 174), 8, aux=True)
+    pol = _noisy_policy(hw, 8, aux=True)
     net, params = pol.net, pol.params.data
-    env = vnav.VectorEnv([_aux_scene_174()], 8, seed=1)
+    env = vnav.VectorEnv([_aux_scene(hw, 6 if hw == (174, 174) else 4)], 8, seed=1)
     arena, fb, rows_total, _ = env.frame_arena()
-    n, w = 512, 0.1
+    w = 0.1
     g = torch.Generator(device="cuda").manual_seed(9)
     rows_i = torch.randint(0, rows_total, (n,), dtype=torch.int32, device="cuda", generator=g)
     rows_g = torch.randint(0, rows_total, (n,), dtype=torch.int32, device="cuda", generator=g)
@@ -237,7 +263,7 @@ def test_174_batch512_rows_aux_vs_fp64_oracle():
     torch.cuda.synchronize()
 
     sd = pol.reference_state_dict()
-    ref = GoalNetOracle((174, 174)).load_reference(sd).double()
+    ref = GoalNetOracle(hw).load_reference(sd).double()
     heads = AuxHeadsOracle().load_reference(sd).double()
     logits, value, x4, pre = ref.forward_masked(frames_to_float(img).double(), frames_to_float(gl).double(), masks)
     flips = _check_masks_are_signs(masks, pre)
@@ -247,8 +273,7 @@ def test_174_batch512_rows_aux_vs_fp64_oracle():
         if bad.any():
             assert float(z.detach()[bad].abs().max() / z.detach().abs().max()) <= 1e-5
     o = out.cpu().numpy()
-    assert _err(o[:, :4], logits.detach().numpy()) <= 1e-5
-    assert _err(o[:, 4], value.detach().numpy().ravel()) <= 1e-5
+    _check_outputs(o[:, :4], o[:, 4], logits.detach().numpy(), value.detach().numpy().ravel())
     ph, pw = net.aux_layout["p_hw"]
     tgt = [t.double() for t in aux_targets(dd[ri], ss[ri], ss[rg], 4, (ph, pw))]
     mse = [torch.nn.functional.mse_loss(p, t) for p, t in zip(preds, tgt)]
@@ -257,12 +282,14 @@ def test_174_batch512_rows_aux_vs_fp64_oracle():
     loss, _ = oa2c.loss(logits, value.view(-1), actions.cpu().long(), rets.cpu().double())
     (loss + w * sum(mse)).backward()
     worst = _grads_vs_oracle(net, grads, ref, heads)
-    print("174x174 n=512 + aux: worst gradient error %.3g of scale; tie flips %s" % (worst, flips))
+    print("%dx%d n=%d + aux: worst gradient error %.3g of scale; tie flips %s" % (hw[0], hw[1], n, worst, flips))
 
 
-@pytest.mark.parametrize("E", [1024, 16, 5])
+@pytest.mark.parametrize("E", [2048, 1024, 16, 5])
 def test_lstm_core_vs_fp64_torch_lstm(E):
-    """The recurrent core at 1024 envs x 3 steps (gates / dh products past the split-K
+    """The recurrent core at 2048 envs x 3 steps (6144 rows: the trunk-feature gradient
+    dz5 = dgates x W_ih takes the unsplit 128 x 128 EpiMask product the training update runs at
+    >= 4096 rows), at 1024 envs x 3 steps (gates / dh products past the split-K
     threshold, the weight gradient over 3072 rows) and at 16 / 5 envs (the fused VALU
     steps of vn_skinny.h: xcat + gates + cell, dh product + next cell backward): per-step
     (h, c), the heads on h, and the gradients of W_ih, W_hh, both biases, the heads and
@@ -329,8 +356,7 @@ def test_lstm_core_vs_fp64_torch_lstm(E):
     assert _err(c_all.cpu().numpy(), torch.cat(cs).detach().numpy()) <= 1e-5
     logits, value = pl(y), cr(y)
     o = out.cpu().numpy()
-    assert _err(o[:, :4], logits.detach().numpy()) <= 1e-5
-    assert _err(o[:, 4], value.detach().numpy().ravel()) <= 1e-5
+    _check_outputs(o[:, :4], o[:, 4], logits.detach().numpy(), value.detach().numpy().ravel())
     loss, _ = oa2c.loss(logits, value.view(-1), actions.cpu().long(), rets.cpu().double())
     loss.backward()
     mine = net.to_reference(grads)
@@ -447,9 +473,9 @@ def test_logged_run_shape_trainer_update_vs_fp64_oracle():
     y = torch.cat(ys)
     logits, value = ref.policy_logits(y), ref.critic(y).view(-1)
     vboot = ref.critic(yb[:, 0]).view(-1)
-    assert _err(out[:, :A].numpy(), logits.detach().numpy()) <= 1e-5
-    assert _err(out[:, A].numpy(), value.detach().numpy()) <= 1e-5
+    _check_outputs(out[:, :A].numpy(), out[:, A].numpy(), logits.detach().numpy(), value.detach().numpy())
     assert _err(boot[:, A].numpy(), vboot.detach().numpy()) <= 1e-5
+    assert _elementwise(boot[:, A].numpy(), vboot.detach().numpy()) <= 1.0
     vext = torch.cat([value.detach().view(T, E), vboot.detach().view(1, E)])
     R = oa2c.returns(rewards.double(), dones, vext, 0.99)
     loss, _ = oa2c.loss(logits, value, actions, R.view(-1))

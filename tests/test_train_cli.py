@@ -86,15 +86,28 @@ def test_resume_continues_exactly(tmp_path):
     assert torch.equal(rest.trainer.params, full.trainer.params)
 
 
-def test_checkpoint_file_per_rank(tmp_path, monkeypatch):
-    """world > 1: each rank writes and reads its own checkpoint (the env shard, running
-    returns and recurrent carry are per rank); one process keeps checkpoint.pt."""
+def test_checkpoint_paths_per_rank(tmp_path, monkeypatch):
+    """checkpoint.pt is the single-process state (world 1) or the world-agnostic policy
+    state (world > 1); the per-rank files (env shard, running returns, recurrent carry) sit
+    in the generation directory of the last complete set (tests/test_dist_cpu.py covers the
+    protocol at world 2)."""
     train = _train()
     exp = train.make_trainer("cached-thor", save_dir=str(tmp_path))
     assert exp.checkpoint_path == os.path.join(str(tmp_path), "checkpoint.pt")
+    assert not exp.has_checkpoint()
     for r in range(2):
         monkeypatch.setenv("RANK", str(r))
         monkeypatch.setenv("WORLD_SIZE", "2")
         monkeypatch.setenv("LOCAL_RANK", str(r))
         exp = train.make_trainer("cached-thor", save_dir=str(tmp_path))
-        assert exp.checkpoint_path == os.path.join(str(tmp_path), "checkpoint.rank%d.pt" % r)
+        assert exp.checkpoint_path == os.path.join(str(tmp_path), "checkpoint.pt")
+        assert exp.rank_checkpoint_path() is None
+        assert exp.rank_checkpoint_path(4800) == os.path.join(str(tmp_path), "ckpt-%012d" % 4800, "rank%d.pt" % r)
+
+
+def test_test_without_checkpoint_raises(tmp_path):
+    """test() refuses to evaluate when there is no checkpoint (no silent random policy)."""
+    train = _train()
+    exp = train.make_trainer("cached-thor", save_dir=str(tmp_path))
+    with pytest.raises(FileNotFoundError):
+        exp.test(episodes=1)
