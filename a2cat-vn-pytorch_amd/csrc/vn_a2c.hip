@@ -299,6 +299,73 @@ __global__ void metrics_kernel(const float* __restrict__ stats4, float inv_n, co
   for (int i = 0; i < 3; ++i) out9[6 + i] = episode3[i];
 }
 
+// ---- goal runs (vn_goal_runs, include/vnav.h) ----------------------------------------
+// One workgroup of kGoalThreads: thread i takes a contiguous chunk of the items, counts its
+// flagged ones, an inclusive scan over the threads gives each chunk its base, and the chunk
+// writes its flagged items in order — the list is ascending (deterministic).
+constexpr int kGoalThreads = 1024;
+
+__device__ __forceinline__ int block_scan_incl(int v, int* sh) {
+  const int tid = threadIdx.x;
+  sh[tid] = v;
+  __syncthreads();
+  for (int d = 1; d < kGoalThreads; d <<= 1) {
+    const int add = tid >= d ? sh[tid - d] : 0;
+    __syncthreads();
+    sh[tid] += add;
+    __syncthreads();
+  }
+  return sh[tid];
+}
+
+__global__ __launch_bounds__(kGoalThreads) void goal_runs_step_kernel(const uint8_t* __restrict__ done_prev,
+                                                                      const int32_t* __restrict__ delta_prev, int E,
+                                                                      int32_t* __restrict__ delta,
+                                                                      int32_t* __restrict__ list,
+                                                                      int32_t* __restrict__ count) {
+  __shared__ int sh[kGoalThreads];
+  const int tid = threadIdx.x, per = (E + kGoalThreads - 1) / kGoalThreads;
+  const int e0 = min(tid * per, E), e1 = min(e0 + per, E);
+  int c = 0;
+  for (int e = e0; e < e1; ++e) {
+    const bool nw = !done_prev || done_prev[e];
+    delta[e] = nw ? 0 : delta_prev[e] - E;
+    c += nw;
+  }
+  const int incl = block_scan_incl(c, sh);
+  int o = incl - c;
+  for (int e = e0; e < e1; ++e)
+    if (!done_prev || done_prev[e]) list[o++] = e;
+  if (tid == kGoalThreads - 1) *count = incl;
+}
+
+__global__ __launch_bounds__(kGoalThreads) void goal_runs_rollout_kernel(const uint8_t* __restrict__ dones, int T,
+                                                                         int E, int32_t* __restrict__ list,
+                                                                         int32_t* __restrict__ run_length,
+                                                                         int32_t* __restrict__ count) {
+  __shared__ int sh[kGoalThreads];
+  const int tid = threadIdx.x;
+  // run lengths, per env from the last step back: a run ends at its env's next done (that
+  // step still has the run's goal) or at the rollout's last step
+  for (int e = tid; e < E; e += kGoalThreads) {
+    int end = T - 1;
+    for (int t = T - 1; t >= 0; --t) {
+      if (dones[(int64_t)t * E + e]) end = t;
+      if (t == 0 || dones[(int64_t)(t - 1) * E + e]) run_length[(int64_t)t * E + e] = end - t + 1;
+    }
+  }
+  const int64_t N = (int64_t)T * E, per = (N + kGoalThreads - 1) / kGoalThreads;
+  const int64_t s0 = min((int64_t)tid * per, N), s1 = min(s0 + per, N);
+  auto start = [&](int64_t s) { return s < E || dones[s - E] != 0; };
+  int c = 0;
+  for (int64_t s = s0; s < s1; ++s) c += start(s);
+  const int incl = block_scan_incl(c, sh);
+  int o = incl - c;
+  for (int64_t s = s0; s < s1; ++s)
+    if (start(s)) list[o++] = (int32_t)s;
+  if (tid == kGoalThreads - 1) *count = incl;
+}
+
 // Trace marker: an empty kernel whose grid size (tag workgroups of 64 lanes) a kernel
 // trace records, so a rocprofv3 trace of a test run can be split per test.
 __global__ void trace_marker_kernel() {}
@@ -313,6 +380,26 @@ int vn_a2c_episode_stats(float* episode_stats_env, int E, float* stats3, vn_stre
   if (!episode_stats_env || !stats3 || E <= 0) return fail(VN_EINVAL, "vn_a2c_episode_stats: bad args");
   hipLaunchKernelGGL(episode_stats_kernel, dim3(1), dim3(kPostThreads), 0, (hipStream_t)stream, episode_stats_env, E,
                      stats3);
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
+
+int vn_goal_runs_step(const uint8_t* done_prev, const int32_t* delta_prev, int E, int32_t* delta, int32_t* list,
+                      int32_t* count, vn_stream_t stream) {
+  if (E <= 0 || !delta || !list || !count || (done_prev && !delta_prev))
+    return fail(VN_EINVAL, "vn_goal_runs_step: bad args");
+  hipLaunchKernelGGL(goal_runs_step_kernel, dim3(1), dim3(kGoalThreads), 0, (hipStream_t)stream, done_prev, delta_prev,
+                     E, delta, list, count);
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
+
+int vn_goal_runs_rollout(const uint8_t* dones, int T, int E, int32_t* list, int32_t* run_length, int32_t* count,
+                         vn_stream_t stream) {
+  if (!dones || T <= 0 || E <= 0 || !list || !run_length || !count || (int64_t)T * E > INT32_MAX)
+    return fail(VN_EINVAL, "vn_goal_runs_rollout: bad args");
+  hipLaunchKernelGGL(goal_runs_rollout_kernel, dim3(1), dim3(kGoalThreads), 0, (hipStream_t)stream, dones, T, E, list,
+                     run_length, count);
   VN_HIP(hipGetLastError());
   return VN_OK;
 }

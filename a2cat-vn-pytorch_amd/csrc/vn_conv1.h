@@ -184,7 +184,8 @@ __device__ __forceinline__ uint32_t u8x2_bf16(uint32_t v) {  // two low bytes ->
 }
 
 template <int H, int W, int OH, int OW>
-__global__ __launch_bounds__(256, 2) void conv1_fwd_x3_kernel(FrameSrc src, int n_frames, const float* __restrict__ Wt,
+__global__ __launch_bounds__(256, 2) void conv1_fwd_x3_kernel(FrameSrc src, int n_frames, FrameList fl,
+                                                           const float* __restrict__ Wt,
                                                            const float* __restrict__ bias, float* __restrict__ Y,
                                                            uint32_t* __restrict__ mask) {
   using B = Conv1X3Band<H, W>;
@@ -220,12 +221,12 @@ __global__ __launch_bounds__(256, 2) void conv1_fwd_x3_kernel(FrameSrc src, int 
   // cannot tell it from the next item's prefetch in flight and waits for vmcnt(0) each tile
 #pragma unroll
   for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(bs[j][0]), "v"(bs[j][1]), "v"(bs[j][2]), "v"(bs[j][3]));
-  const int n_items = n_frames * NB;
+  const int n_items = fl_count(fl, n_frames) * NB;
   // dwords of item it's band: rows 4*BR*band .. (clamped to the frame)
   auto band_dwords = [&](int band) { return min(BRI, H - 4 * BR * band) * RB / 4; };
   uint32_t pre[NPF];  // next item's bytes, in flight while the current item computes
   auto load_item = [&](int it) {
-    const int f = it / NB, band = it - (it / NB) * NB;
+    const int f = fl_frame(fl, it / NB), band = it - (it / NB) * NB;
     const uint32_t* s4 = reinterpret_cast<const uint32_t*>(frame_ptr(src, f) + (int64_t)4 * BR * band * RB);
     const int nd = band_dwords(band);
     // unconditional (a lane past the band reloads its last dword; past the last item the item
@@ -235,7 +236,7 @@ __global__ __launch_bounds__(256, 2) void conv1_fwd_x3_kernel(FrameSrc src, int 
   };
   if ((int)blockIdx.x < n_items) load_item(blockIdx.x);
   for (int it = blockIdx.x; it < n_items; it += gridDim.x) {
-    const int f = it / NB, band = it - (it / NB) * NB;
+    const int f = fl_frame(fl, it / NB), band = it - (it / NB) * NB;
     const int oy0 = BR * band, nr = min(BR, OH - oy0), npb = nr * OW;
     const int nd = band_dwords(band);
 #pragma unroll
@@ -449,8 +450,8 @@ constexpr bool conv1_wgrad_x3_fits() {
 }
 
 template <int H, int W, int OH, int OW>
-__global__ __launch_bounds__(256) void conv1_wgrad_x3_kernel(FrameSrc src, int n_frames, const float* __restrict__ dZ,
-                                                             float* __restrict__ slab) {
+__global__ __launch_bounds__(256) void conv1_wgrad_x3_kernel(FrameSrc src, int n_frames, FrameList fl,
+                                                             const float* __restrict__ dZ, float* __restrict__ slab) {
   using Bd = Conv1WgBand<H, W>;
   using QL = typename Bd::Q;
   constexpr int PC = QL::PC, PX = QL::PX, RSQ = QL::RSQ;
@@ -489,7 +490,7 @@ __global__ __launch_bounds__(256) void conv1_wgrad_x3_kernel(FrameSrc src, int n
   for (int nt = 0; nt < 5; ++nt)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[nt][r] = 0.0f;
-  const int n_items = n_frames * NB;
+  const int n_items = fl_count(fl, n_frames) * NB;
   auto band_rows = [&](int band) { return min(BRI, H - 4 * BR * band); };
   // Every wave runs KW steps of every item (KW a multiple of D: the D dZ register sets rotate across
   // items too), the ones past the band's KS on zeroed dZ; all loads are unconditional, so the
@@ -508,13 +509,14 @@ __global__ __launch_bounds__(256) void conv1_wgrad_x3_kernel(FrameSrc src, int n
   // read as zero instead of needing a branch. A task past the band reloads the band's last
   // task (stage_q skips it).
   uint32_t pre[NT][NDW];
-  auto load_task = [&](int r, int it) {
+  // f: item it's frame (resolved once per item by item_geom)
+  auto load_task = [&](int r, int it, int f) {
     const int band = it - (it / NB) * NB;
     const int t = min(tid + r * 256, band_rows(band) * PAIRS - 1);
     const int y = t / PAIRS, m = t - (t / PAIRS) * PAIRS;
     const int off = (4 * BR * band + y) * RB + m * 24;
     const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)frame_ptr(src, it / NB), 0, H * W * 3, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void*)frame_ptr(src, f), 0, H * W * 3, 0x00020000);
 #pragma unroll
     for (int q = 0; q < NDW; ++q) pre[r][q] = __builtin_amdgcn_raw_buffer_load_b32(rs, (off & ~3) + 4 * q, 0, 0);
   };
@@ -566,7 +568,7 @@ __global__ __launch_bounds__(256) void conv1_wgrad_x3_kernel(FrameSrc src, int n
     return g < ng ? min(8, OW - ox0) : 0;
   };
   auto item_geom = [&](int it, int& f, int& oy0, int& ng) {
-    f = it / NB;
+    f = fl_frame(fl, it / NB);
     const int band = it - (it / NB) * NB;
     oy0 = BR * band;
     ng = min(BR, OH - oy0) * GPR;
@@ -576,7 +578,7 @@ __global__ __launch_bounds__(256) void conv1_wgrad_x3_kernel(FrameSrc src, int n
     int f, oy0, ng;
     item_geom(blockIdx.x, f, oy0, ng);
 #pragma unroll
-    for (int r = 0; r < NT; ++r) load_task(r, blockIdx.x);
+    for (int r = 0; r < NT; ++r) load_task(r, blockIdx.x, f);
 #pragma unroll
     for (int d = 0; d < D; ++d) load_z(zb[d], f, oy0, ng, wave + 4 * d);
   }
@@ -597,7 +599,7 @@ __global__ __launch_bounds__(256) void conv1_wgrad_x3_kernel(FrameSrc src, int n
       const int nvz = z_valid(ng, s);
 #pragma unroll
       for (int j = 0; j < 8; ++j) split3_bf16(j < nvz ? z[j] : 0.0f, a0.u[j], a1.u[j], a2.u[j]);
-      if constexpr (i < NT) load_task(i, inext);
+      if constexpr (i < NT) load_task(i, inext, fn);
       if constexpr (i + D < KW)
         load_z(z, f, oy0, ng, s + 4 * D);
       else
@@ -961,7 +963,7 @@ template <int IH, int IW, int OH, int OW, int NW>
 __global__ __launch_bounds__(NW * 64, 2) void conv2_dgrad_x6_kernel(const float* __restrict__ dZ2,
                                                                 const float* __restrict__ WT,
                                                                 const uint32_t* __restrict__ mask,
-                                                                float* __restrict__ dX1, int n_frames) {
+                                                                float* __restrict__ dX1, int n_frames, FrameList fl) {
   constexpr int NP = OH * OW;
   constexpr int HYC = IH / 2, WXC = IW / 2, NPC = HYC * WXC;
   constexpr int TILES = (NPC + 15) / 16;
@@ -1008,15 +1010,19 @@ __global__ __launch_bounds__(NW * 64, 2) void conv2_dgrad_x6_kernel(const float*
   // dZ2 and the ReLU words of frame f, into registers; unconditional (slots past the frame
   // reload its last one, staging skips them; past the last frame the frame repeats): no branch
   // around the loads for the compiler's wait counts to get lost in
-  auto load_z = [&](int f) {
+  // item i (list position) -> frame fl_frame(fl, i)
+  auto load_z = [&](int i) {
+    const int f = fl_frame(fl, i);
     const f4* z4 = reinterpret_cast<const f4*>(dZ2 + (int64_t)f * NP * 32);
 #pragma unroll
     for (int j = 0; j < NZ; ++j) zr[j] = z4[min(slot_pc(tid + j * NT), NP * 8 - 1)];
 #pragma unroll
     for (int j = 0; j < NM; ++j) mr[j] = mask[(int64_t)f * IH * IW + min(tid + j * NT, IH * IW - 1)];
   };
+  n_frames = fl_count(fl, n_frames);
   if ((int)blockIdx.x < n_frames) load_z(blockIdx.x);
-  for (int f = blockIdx.x; f < n_frames; f += gridDim.x) {
+  for (int fi = blockIdx.x; fi < n_frames; fi += gridDim.x) {
+    const int f = fl_frame(fl, fi);
 #pragma unroll
     for (int j = 0; j < NZ; ++j) {
       const int i = slot_pc(tid + j * NT);
@@ -1035,7 +1041,7 @@ __global__ __launch_bounds__(NW * 64, 2) void conv2_dgrad_x6_kernel(const float*
       if (i < IH * IW) ms[i] = mr[j];
     }
     __syncthreads();
-    load_z(min(f + (int)gridDim.x, n_frames - 1));
+    load_z(min(fi + (int)gridDim.x, n_frames - 1));
 #pragma unroll 1
     for (int t0 = 2 * (wave >> 2); t0 < TILES; t0 += 2 * (NW / 4)) {
       int off[2][4];
@@ -1153,7 +1159,7 @@ template <int IH, int IW, int OH, int OW>
 __global__ __launch_bounds__(512, 2) void conv2_fwd_x6_kernel(const float* __restrict__ X1,
                                                               const float* __restrict__ W2,
                                                               const float* __restrict__ bias,
-                                                              float* __restrict__ X2, int n_frames) {
+                                                              float* __restrict__ X2, int n_frames, FrameList fl) {
   using Bd = Conv2FwdBand<IH, IW, OH, OW>;
   constexpr int BR = Bd::BR, NB = Bd::NB, PSX = Bd::PSX, RSP = Bd::RSP, PO = Bd::PO;
   constexpr bool kTiled = Bd::kTiled;
@@ -1203,13 +1209,13 @@ __global__ __launch_bounds__(512, 2) void conv2_fwd_x6_kernel(const float* __res
   // here: a first use inside the loop would wait on the item prefetches in flight as well
   const f4 b4 = *reinterpret_cast<const f4*>(bias + 4 * (tid & 7));
   asm volatile("" ::"v"(b4[0]), "v"(b4[1]), "v"(b4[2]), "v"(b4[3]));
-  const int n_items = n_frames * NB;
+  const int n_items = fl_count(fl, n_frames) * NB;
   auto band_f4 = [&](int band) { return min(BRI, IH - 2 * BR * band) * IW * 8; };
   // two items' X1 in flight: item it + 2 * gridDim.x is loaded into the registers item it
   // just split into LDS (one item of MFMA work was shorter than the load under full load)
   f4 pre[2][NV];
   auto load_item = [&](f4 (&pr)[NV], int it) {
-    const int f = it / NB, band = it - (it / NB) * NB;
+    const int f = fl_frame(fl, it / NB), band = it - (it / NB) * NB;
     const f4* s4 = reinterpret_cast<const f4*>(X1 + ((int64_t)f * IH + 2 * BR * band) * IW * 32);
     const int nv = band_f4(band);
 #pragma unroll
@@ -1219,7 +1225,7 @@ __global__ __launch_bounds__(512, 2) void conv2_fwd_x6_kernel(const float* __res
   if ((int)(blockIdx.x + gridDim.x) < n_items) load_item(pre[1], blockIdx.x + gridDim.x);
   auto item = [&](auto stage, int it) {
     constexpr int S = decltype(stage)::value;
-    const int f = it / NB, band = it - (it / NB) * NB;
+    const int f = fl_frame(fl, it / NB), band = it - (it / NB) * NB;
     const int oy0 = BR * band, nr = min(BR, OH - oy0), npb = nr * OW;
     {  // split the band's X1 rows into the three planes
       const int nv = band_f4(band);
@@ -1336,7 +1342,7 @@ constexpr bool conv2_fwd_ring_fits() {
 __global__ __launch_bounds__(512, 1) void conv2_fwd_ring_kernel(const float* __restrict__ X1,
                                                                 const float* __restrict__ W2,
                                                                 const float* __restrict__ bias,
-                                                                float* __restrict__ X2, int n_frames) {
+                                                                float* __restrict__ X2, int n_frames, FrameList fl) {
   using R = Conv2Ring42;
   constexpr int IW = R::IW, OW = R::OW, NB = R::NB, WH = R::WH, PSX = R::PSX, RSP = R::RSP, PL = R::PL;
   constexpr int NV = R::NV, PP = R::PP, TP = R::TP, NP = R::OH * R::OW;
@@ -1361,10 +1367,11 @@ __global__ __launch_bounds__(512, 1) void conv2_fwd_ring_kernel(const float* __r
   // make the bias land here: its first use sits in the loop's epilogue, where the compiler
   // cannot tell it from the band prefetches in flight and would wait for vmcnt(0)
   asm volatile("" ::"v"(b4[0]), "v"(b4[1]), "v"(b4[2]), "v"(b4[3]));
-  // this workgroup's items: k -> (frame blockIdx.x + (k / NB) * gridDim.x, band k % NB)
+  // this workgroup's items: k -> (frame of list item blockIdx.x + (k / NB) * gridDim.x, band k % NB)
+  n_frames = fl_count(fl, n_frames);
   const int my_frames = (int)blockIdx.x < n_frames ? (n_frames - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
   const int n_items = my_frames * NB;
-  auto frame_of = [&](int k) { return (int)blockIdx.x + (k / NB) * (int)gridDim.x; };
+  auto frame_of = [&](int k) { return fl_frame(fl, (int)blockIdx.x + (k / NB) * (int)gridDim.x); };
   f4 pre[2][NV];
   auto load_item = [&](f4 (&pr)[NV], int k) {
     const int b = k % NB, lo = R::new_lo(b);
@@ -1523,7 +1530,7 @@ struct Conv2Ring42x2 {
 __global__ __launch_bounds__(256, 2) void conv2_fwd_ring2_kernel(const float* __restrict__ X1,
                                                                  const float* __restrict__ W2,
                                                                  const float* __restrict__ bias,
-                                                                 float* __restrict__ X2, int n_frames) {
+                                                                 float* __restrict__ X2, int n_frames, FrameList fl) {
   using R = Conv2Ring42;
   using Q = Conv2Ring42x2;
   constexpr int IW = R::IW, OW = R::OW, NB = R::NB, WH = R::WH, PSX = R::PSX, RSP = R::RSP, PL = Q::PL;
@@ -1547,9 +1554,10 @@ __global__ __launch_bounds__(256, 2) void conv2_fwd_ring2_kernel(const float* __
   }
   const f4 b4 = *reinterpret_cast<const f4*>(bias + ct * 16 + 4 * q);
   asm volatile("" ::"v"(b4[0]), "v"(b4[1]), "v"(b4[2]), "v"(b4[3]));  // landed before the loop
+  n_frames = fl_count(fl, n_frames);
   const int my_frames = (int)blockIdx.x < n_frames ? (n_frames - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
   const int n_items = my_frames * NB;
-  auto frame_of = [&](int k) { return (int)blockIdx.x + (k / NB) * (int)gridDim.x; };
+  auto frame_of = [&](int k) { return fl_frame(fl, (int)blockIdx.x + (k / NB) * (int)gridDim.x); };
   // ring slot of X1 row y of item k's frame: rows of consecutive frames continue the count
   // (42 per frame), so a band's 8 rows and the next band's new rows (which replace the band's
   // six oldest once its MFMAs are done) never collide
@@ -1588,6 +1596,7 @@ __global__ __launch_bounds__(256, 2) void conv2_fwd_ring2_kernel(const float* __
   f4 acc[4];
   for (int k = 0; k < n_items; ++k) {
     const int b = k % NB, oy0 = R::BR * b, nr = min(R::BR, R::OH - oy0);
+    const int fk = frame_of(k);  // resolved here, where no LDS access is in flight
     // tile t < 3: band row t, ox = i16; tile 3: row i16 >> 2, ox = 16 + (i16 & 3); lanes past the
     // band take row 0 at their ox (see conv2_fwd_ring_kernel)
 #pragma unroll
@@ -1646,7 +1655,7 @@ __global__ __launch_bounds__(256, 2) void conv2_fwd_ring2_kernel(const float* __
     }
     __syncthreads();  // MFMA(k) and the partials done: band k's oldest slots are free
     if (kh == 0) {
-      const int64_t out0 = ((int64_t)frame_of(k) * NP + oy0 * OW) * 32 + ct * 16 + 4 * q;
+      const int64_t out0 = ((int64_t)fk * NP + oy0 * OW) * 32 + ct * 16 + 4 * q;
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         int r = t < 3 ? t : (i16 >> 2);

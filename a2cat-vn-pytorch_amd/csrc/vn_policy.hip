@@ -94,6 +94,29 @@ struct NhwcIm2col {
   VN_ROWS_LOADER
 };
 
+// conv3's im2col over concat(image, goal) X2 with goal-frame deduplication: group 1 (the goal
+// map) of sample n is read from sample n + gd[n] (the start of its goal run, vn_goal_runs).
+template <int C, int KH, int KW, int S, int H, int W, int OH, int OW>
+struct NhwcIm2colGoal {
+  const float* X;
+  int M;  // samples * OH * OW
+  const int32_t* gd;
+  __device__ __forceinline__ f4 load4(int m, int k, int kend) const {
+    if (m >= M || k >= kend) return f4zero();
+    const int n = m / (OH * OW);
+    const int r = m - n * (OH * OW);
+    const int oy = r / OW, ox = r - (r / OW) * OW;
+    const int c = k % C;
+    int t = k / C;
+    const int g = t & 1;
+    t >>= 1;
+    const int ky = t / KW, kx = t % KW;
+    const int64_t ns = (int64_t)n + (g ? gd[n] : 0);
+    return *reinterpret_cast<const f4*>(X + (((ns * 2 + g) * H + oy * S + ky) * W + ox * S + kx) * C + c);
+  }
+  VN_ROWS_LOADER
+};
+
 // BigHouseModel conv1 (Conv2d(3, 32, k8, s4), bignet.py:29) im2col over the image frame
 // only: row m = (sample, oy, ox), k = (ky*8 + kx)*3 + c, K = 192; u8 frames as x/255
 // (ScaledFloatFrame) or dense float NCHW frames.
@@ -918,10 +941,13 @@ __global__ __launch_bounds__(S::NT, S::NT >= 512 ? 1 : 2) void parity_dgrad_x6_k
 
 // conv3's input gradient: column c is channel c % 32 of input group c / 32 (X2 layout
 // [n][2][IH][IW][32]), masked by the ReLU that produced X2 (as EpiMaskParityG).
+// mask_goal == 0 (goal-frame deduplication): group 1 is left unmasked — a sample's goal map
+// lives at its run start, where goal_dz2_reduce_kernel sums the run and applies the mask.
 template <int IH, int IW>
 struct EpiDgMaskG2 {
   const float* X;
   float* out;
+  int mask_goal = 1;
   __device__ __forceinline__ int64_t index(int img, int y, int x, int col) const {
     return ((((int64_t)img * 2 + (col >> 5)) * IH + y) * IW + x) * 32 + (col & 31);
   }
@@ -929,11 +955,35 @@ struct EpiDgMaskG2 {
     return *reinterpret_cast<const f4*>(X + index(img, y, x, col));
   }
   __device__ __forceinline__ void post(int img, int y, int x, int col, f4 v, f4 xm) const {
+    const bool m = mask_goal || col < 32;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = xm[e] > 0.0f ? v[e] : 0.0f;
+    for (int e = 0; e < 4; ++e) v[e] = (!m || xm[e] > 0.0f) ? v[e] : 0.0f;
     *reinterpret_cast<f4*>(out + index(img, y, x, col)) = v;
   }
 };
+
+// Goal-frame deduplication, backward: the goal map gradient of a run = the sum of its
+// samples' (conv3's unmasked input gradient, group 1) in step order, under the ReLU of the
+// run's goal map: dZ2[2r+1] = [X2[2r+1] > 0] * sum_{i < len} dX2[2(r + iE) + 1] for every run
+// start r. One thread per (run, channel quad of a pixel); the run count is on the device.
+__global__ __launch_bounds__(256) void goal_dz2_reduce_kernel(float* __restrict__ dz2, const float* __restrict__ X2,
+                                                              int64_t frame_f4, const int32_t* __restrict__ list,
+                                                              const int32_t* __restrict__ count,
+                                                              const int32_t* __restrict__ run_length, int E) {
+  const int64_t total = (int64_t)(*count) * frame_f4;
+  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * 256) {
+    const int64_t j = idx / frame_f4, c = idx - j * frame_f4;
+    const int64_t r = list[j];
+    const int len = run_length[r];
+    f4* d = reinterpret_cast<f4*>(dz2) + (2 * r + 1) * frame_f4 + c;
+    f4 acc = *d;
+    for (int i = 1; i < len; ++i) acc += reinterpret_cast<const f4*>(dz2)[(2 * (r + (int64_t)i * E) + 1) * frame_f4 + c];
+    const f4 x = reinterpret_cast<const f4*>(X2)[(2 * r + 1) * frame_f4 + c];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc[e] = x[e] > 0.0f ? acc[e] : 0.0f;
+    *d = acc;
+  }
+}
 
 // Transposed conv output: bias (+ ReLU), NHWC with C channels (as EpiDeconv).
 template <int OH, int OW, int C>
@@ -1006,8 +1056,12 @@ __device__ __forceinline__ s16x4_ lds_tr(const uint16_t* p) {
 }
 
 template <class S>
+// fl: the images (frames) to reduce over (conv2 with goal-frame deduplication; identity
+// else). gdelta (conv3 with deduplication): input group 1 (the goal half of X2) of sample s is
+// read from sample s + gdelta[s], the sample whose goal frame holds its goal's map.
 __global__ __launch_bounds__(512, 1) void conv_wgrad_x6_kernel(const float* __restrict__ dZ, const float* __restrict__ X,
-                                                            float* __restrict__ slab, int n) {
+                                                            float* __restrict__ slab, int n, FrameList fl,
+                                                            const int32_t* __restrict__ gdelta) {
   constexpr int IH = S::IH, IW = S::IW, OH = S::OH, OW = S::OW, CO = S::CO, G = S::G, BR = S::BR, IMG = S::IMG;
   constexpr int NPX = S::NPX, KP = S::KP, PZ = S::PZ, PX = S::PX, MT = S::MT, C4 = S::C4;
   constexpr int CX = S::CX, X4 = CX / 4, NTW = S::NTW, NTT = 2 * NTW;
@@ -1035,23 +1089,37 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_x6_kernel(const float* __re
 #pragma unroll
     for (int nt = 0; nt < NTT; ++nt) acc[mt][nt] = f4zero();
   f4 dbs = f4zero();  // fp32 column sums of dZ (channels 4 (tid % C4) .. +3), g == 0 only
+  n = fl_count(fl, n);
   const int items = (n + IMG - 1) / IMG * S::NB;
   f4 zr[NZ], xr[NX];
   // the item's dZ band rows and the X rows under them, into registers: unconditional (a slot
   // past the item or an image past n reloads a valid one; the split zeroes it), so no branch
-  // hides the loads from the compiler's wait counts
+  // hides the loads from the compiler's wait counts. The item's image indices (list entries,
+  // goal redirection) are resolved first with scalar loads.
   auto load = [&](int it) {
     const int img0 = (it / S::NB) * IMG, band = it - (it / S::NB) * S::NB;
+    int zi[IMG], xi[IMG];
+#pragma unroll
+    for (int im = 0; im < IMG; ++im) {
+      zi[im] = fl_frame(fl, min(img0 + im, n - 1));
+      xi[im] = zi[im] + ((gdelta && g == 1) ? fl_sload(gdelta + zi[im]) : 0);
+    }
 #pragma unroll
     for (int j = 0; j < NZ; ++j) {
       const int i = min(tid + j * NT, KP * C4 - 1);
-      const int k = i / C4, im = k / BP, imc = min(img0 + im, n - 1);
+      const int k = i / C4, im = k / BP;
+      int imc = zi[0];  // select chain over the item's images (registers, no indexed array)
+#pragma unroll
+      for (int m = 1; m < IMG; ++m) imc = im == m ? zi[m] : imc;
       zr[j] = reinterpret_cast<const f4*>(dZ)[(((int64_t)imc * OH + band * BR) * OW + (k - im * BP)) * C4 + i % C4];
     }
 #pragma unroll
     for (int j = 0; j < NX; ++j) {
       const int i = min(tid + j * NT, IMG * NPX * X4 - 1);
-      const int r = i / X4, im = r / NPX, imc = min(img0 + im, n - 1);
+      const int r = i / X4, im = r / NPX;
+      int imc = xi[0];
+#pragma unroll
+      for (int m = 1; m < IMG; ++m) imc = im == m ? xi[m] : imc;
       xr[j] = reinterpret_cast<const f4*>(X)[((((int64_t)imc * G + g) * IH + 2 * band * BR) * IW + (r - im * NPX)) * X4 + i % X4];
     }
   };
@@ -1176,7 +1244,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_x6_kernel(const float* __re
 
 template <class S>
 inline int launch_conv_wgrad_x6(const float* dz, const float* X, int n, float* slab, int64_t slab_cap, float* dW,
-                                float* db, hipStream_t st) {
+                                float* db, hipStream_t st, FrameList fl = FrameList{}, const int32_t* gdelta = nullptr) {
   const void* kfn = (const void*)conv_wgrad_x6_kernel<S>;
   VN_HIP(ensure_dyn_lds(kfn, S::LDS));
   const int items = (n + S::IMG - 1) / S::IMG * S::NB;
@@ -1184,7 +1252,7 @@ inline int launch_conv_wgrad_x6(const float* dz, const float* X, int n, float* s
   const int64_t nel = (int64_t)S::CO * S::SLAB_N;
   int bx = std::max(1, std::min(items, resident_blocks(kfn, 512, S::LDS) / S::G));
   bx = (int)std::max<int64_t>(1, std::min<int64_t>(bx, slab_cap / nel - kParts));
-  hipLaunchKernelGGL((conv_wgrad_x6_kernel<S>), dim3(bx, S::G), dim3(512), S::LDS, st, dz, X, slab, n);
+  hipLaunchKernelGGL((conv_wgrad_x6_kernel<S>), dim3(bx, S::G), dim3(512), S::LDS, st, dz, X, slab, n, fl, gdelta);
   const float* src = slab;
   int nsrc = bx;
   if (bx >= 2 * kParts) {  // two-stage fixed-order reduce: one pass over hundreds of slabs is latency-bound
@@ -1224,7 +1292,7 @@ inline void dgrad_class_groups(const float* dz, const float* WT, float* out, con
 
 template <int COUT, int CIN, int H, int W, int OH, int OW>
 inline int dgrad_all_classes_groups(const float* dz, const float* WT, float* out, const float* X, int nimg, int G,
-                                     hipStream_t st) {
+                                     hipStream_t st, int mask_goal = 1) {
   constexpr int CH = k4s2_covered<H, OH>(), CW = k4s2_covered<W, OW>();
   // the covered class pixels (CH/2 x CW/2 per class when even) over the dZ3 map
   using S = ParityDg<OH, OW, CH / 2, CW / 2, COUT, 2 * CIN, 2>;
@@ -1233,10 +1301,11 @@ inline int dgrad_all_classes_groups(const float* dz, const float* WT, float* out
   const bool generic = getenv("VN_DGRAD_GENERIC") != nullptr;
   if (CH % 2 == 0 && CW % 2 == 0 && S::fits && COUT == 64 && CIN == 32 && G == 2 && !generic) {
     if constexpr (CH % 2 == 0 && CW % 2 == 0 && S::fits) {
-      const int rc = launch_parity_dgrad_x6<S>(dz, WT, EpiDgMaskG2<H, W>{X, out}, nimg, st);
+      const int rc = launch_parity_dgrad_x6<S>(dz, WT, EpiDgMaskG2<H, W>{X, out, mask_goal}, nimg, st);
       if (rc != VN_OK) return rc;
     }
   } else {
+    if (!mask_goal) return fail(VN_EINVAL, "goal runs need the parity-class dgrad kernel");
     dgrad_class_groups<COUT, CIN, H, W, OH, OW, 0, 0>(dz, WT, out, X, nimg, G, st);
     dgrad_class_groups<COUT, CIN, H, W, OH, OW, 0, 1>(dz, WT, out, X, nimg, G, st);
     dgrad_class_groups<COUT, CIN, H, W, OH, OW, 1, 0>(dz, WT, out, X, nimg, G, st);
@@ -1289,11 +1358,28 @@ inline Acts acts_at(const PolicyLayout& L, float* base, int64_t cap, int64_t off
   return a;
 }
 
+// Goal-frame deduplication (vn_goal_runs) needs every frame-level kernel of the geometry to
+// take a frame list: the u8 conv1 x3 kernels, the x6 / ring conv2 forward, the conv2 x6
+// input gradient and weight gradient, conv3's parity-class input gradient (84x84, 174x174).
+template <int H0, int W0>
+constexpr bool kGoalRunsGeo = (H0 == 84 && W0 == 84) || (H0 == 174 && W0 == 174);
+
+inline bool goal_runs_ok(const PolicyLayout& L, int n) {
+  if (L.arch != 0 || n <= kSkinnyRows) return false;
+  if (!((L.H == 84 && L.W == 84) || (L.H == 174 && L.W == 174))) return false;
+  // the A/B overrides select kernels without frame lists (read per call)
+  for (const char* v : {"VN_WGRAD_GENERIC", "VN_DGRAD_GENERIC", "VN_CONV2F_GENERIC", "VN_CONV2F_RING1"})
+    if (getenv(v)) return false;
+  return true;
+}
+
 template <int H0, int W0>
 int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int n, const Acts& a, float* out,
-                 hipStream_t st) {
+                 hipStream_t st, const vn_goal_runs* gr = nullptr) {
   using G = Geo<H0, W0>;
   const int A1 = L.A + 1;
+  // goal runs: the goal frames of run starts only (checked by the caller: goal_runs_ok, u8 frames)
+  const FrameList fl = gr ? FrameList{gr->goal_list, gr->goal_count, n} : FrameList{};
   // conv1 (frames -> X1), 2n frames. u8 frames take the split-bf16 kernel (bands of
   // output rows staged in LDS), else the f32 LDS-frame kernel; dense float frames take the
   // generic im2col path.
@@ -1307,7 +1393,7 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
       const int blocks =
           std::min(frames * B::NB, resident_blocks((const void*)conv1_fwd_x3_kernel<H0, W0, G::OH1, G::OW1>, 256, 0));
       hipLaunchKernelGGL((conv1_fwd_x3_kernel<H0, W0, G::OH1, G::OW1>), dim3(blocks), dim3(256), 0, st, src, frames,
-                         P + L.l[0].w, P + L.l[0].b, a.X[0], a.M1);
+                         fl, P + L.l[0].w, P + L.l[0].b, a.X[0], a.M1);
       conv1_done = true;
     }
   } else if constexpr (kConv1Lds) {
@@ -1333,7 +1419,7 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
     VN_HIP(ensure_dyn_lds(kfn, Bd::LDS));  // > 64 KiB dynamic LDS: opt-in
     const int blocks = std::min(frames * Bd::NB, resident_blocks(kfn, 512, Bd::LDS));
     hipLaunchKernelGGL((conv2_fwd_x6_kernel<G::OH1, G::OW1, G::OH2, G::OW2>), dim3(blocks), dim3(512), Bd::LDS, st,
-                       a.X[0], P + L.l[1].w, P + L.l[1].b, a.X[1], frames);
+                       a.X[0], P + L.l[1].w, P + L.l[1].b, a.X[1], frames, fl);
   } else {
     using Bd = Conv2FwdBand<G::OH1, G::OW1, G::OH2, G::OW2>;
     bool done = false;
@@ -1347,13 +1433,13 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
           VN_HIP(ensure_dyn_lds(kfn, Conv2Ring42::LDS));
           const int blocks = std::min(frames, resident_blocks(kfn, 512, Conv2Ring42::LDS));
           hipLaunchKernelGGL(conv2_fwd_ring_kernel, dim3(blocks), dim3(512), Conv2Ring42::LDS, st, a.X[0],
-                             P + L.l[1].w, P + L.l[1].b, a.X[1], frames);
+                             P + L.l[1].w, P + L.l[1].b, a.X[1], frames, fl);
         } else {
           const void* kfn = (const void*)conv2_fwd_ring2_kernel;
           VN_HIP(ensure_dyn_lds(kfn, Conv2Ring42x2::LDS));
           const int blocks = std::min(frames, resident_blocks(kfn, 256, Conv2Ring42x2::LDS));
           hipLaunchKernelGGL(conv2_fwd_ring2_kernel, dim3(blocks), dim3(256), Conv2Ring42x2::LDS, st, a.X[0],
-                             P + L.l[1].w, P + L.l[1].b, a.X[1], frames);
+                             P + L.l[1].w, P + L.l[1].b, a.X[1], frames, fl);
         }
         done = true;
       }
@@ -1366,7 +1452,7 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
         VN_HIP(ensure_dyn_lds(kfn, Bd::LDS));
         const int blocks = std::min(frames * Bd::NB, resident_blocks(kfn, 512, Bd::LDS));
         hipLaunchKernelGGL((conv2_fwd_x6_kernel<G::OH1, G::OW1, G::OH2, G::OW2>), dim3(blocks), dim3(512), Bd::LDS, st,
-                           a.X[0], P + L.l[1].w, P + L.l[1].b, a.X[1], frames);
+                           a.X[0], P + L.l[1].w, P + L.l[1].b, a.X[1], frames, FrameList{});
         done = true;
       }
     }
@@ -1385,15 +1471,23 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
                        dim3(1024), 0, st, a.X[1], M, P + L.l[2].w, P + L.l[2].b, P + L.l[3].w, P + L.l[3].b, a.X[2],
                        a.X[3]);
   }
-  // conv3 over concat(image, goal) (X2 -> X3)
+  // conv3 over concat(image, goal) (X2 -> X3); with goal runs the goal half of a sample is
+  // read from its run start
   if (!small34) {
-    NhwcIm2col<32, 4, 4, 2, G::OH2, G::OW2, G::OH3, G::OW3, 2> fa{a.X[1], n * G::OH3 * G::OW3};
     DenseRows fb{P + L.l[2].w, 1024, 64};
     EpiBiasAct ep{a.X[2], 64, P + L.l[2].b, 1};
-    if constexpr (G::OH3 * G::OW3 >= 64)  // 174x174, 300x400: 128-row tiles (A split over more MFMAs)
-      launch_gemm_x6_sk<128, 64, 32, 2, 2>(fa, fb, ep, fa.M, 64, 1024, st, L);
-    else  // 84x84: 3x3 maps, 64-row tiles keep >= 2 tiles per CU
-      launch_gemm_x6_sk<64, 64, 32, 2, 2>(fa, fb, ep, fa.M, 64, 1024, st, L);
+    auto conv3 = [&](auto fa) {
+      if constexpr (G::OH3 * G::OW3 >= 64)  // 174x174, 300x400: 128-row tiles (A split over more MFMAs)
+        launch_gemm_x6_sk<128, 64, 32, 2, 2>(fa, fb, ep, fa.M, 64, 1024, st, L);
+      else  // 84x84: 3x3 maps, 64-row tiles keep >= 2 tiles per CU
+        launch_gemm_x6_sk<64, 64, 32, 2, 2>(fa, fb, ep, fa.M, 64, 1024, st, L);
+    };
+    if (gr) {
+      if constexpr (kGoalRunsGeo<H0, W0>)
+        conv3(NhwcIm2colGoal<32, 4, 4, 2, G::OH2, G::OW2, G::OH3, G::OW3>{a.X[1], n * G::OH3 * G::OW3, gr->goal_delta});
+    } else {
+      conv3(NhwcIm2col<32, 4, 4, 2, G::OH2, G::OW2, G::OH3, G::OW3, 2>{a.X[1], n * G::OH3 * G::OW3});
+    }
   }
   // conv4 1x1 (X3 -> X4)
   if (!small34) {
@@ -1467,9 +1561,11 @@ inline BwdWork carve(const PolicyLayout& L, float* ws, int64_t n) {
 template <int H0, int W0>
 int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int n, const Acts& a,
                   const float* dout, const float* dz5_in, const float* dx4_extra, float* Gr, const BwdWork& w,
-                  hipStream_t st) {
+                  hipStream_t st, const vn_goal_runs* gr = nullptr) {
   using G = Geo<H0, W0>;
   const int A1 = L.A + 1;
+  // goal runs: the image frames and the goal frames of run starts (ascending)
+  const FrameList fl = gr ? FrameList{gr->goal_list, gr->goal_count, n} : FrameList{};
   auto T = [&](int i) { return w.wt + L.wt_off[i]; };
   // dz5_in != NULL: the trunk backward of the recurrent policy (heads and LSTM already done)
   const float* dz5 = dz5_in ? dz5_in : w.dz5;
@@ -1519,14 +1615,22 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
     using Wg = Conv3Wg<G::OH2, G::OW2, G::OH3, G::OW3>;
     if (Wg::fits && !getenv("VN_WGRAD_GENERIC")) {  // read per call (A/B and parity checks)
       if constexpr (Wg::fits) {
-        const int rc = launch_conv_wgrad_x6<Wg>(w.dz3, a.X[1], n, w.slab, w.slab_cap, Gr + L.l[2].w, Gr + L.l[2].b, st);
+        const int rc = launch_conv_wgrad_x6<Wg>(w.dz3, a.X[1], n, w.slab, w.slab_cap, Gr + L.l[2].w, Gr + L.l[2].b, st,
+                                                FrameList{}, gr ? gr->goal_delta : nullptr);
         if (rc != VN_OK) return rc;
       }
     } else {
       launch_wgrad6<64, 128, 2, 2>(w.dz3, 64, 64, fbw, 1024, n9, w.slab, w.slab_cap, Gr + L.l[2].w, Gr + L.l[2].b, st);
     }
-    const int rc = dgrad_all_classes_groups<64, 32, G::OH2, G::OW2, G::OH3, G::OW3>(w.dz3, T(2), w.dz2, a.X[1], n, 2, st);
+    const int rc =
+        dgrad_all_classes_groups<64, 32, G::OH2, G::OW2, G::OH3, G::OW3>(w.dz3, T(2), w.dz2, a.X[1], n, 2, st, gr ? 0 : 1);
     if (rc != VN_OK) return rc;
+    if (gr) {  // each run's goal-map gradient: summed over the run at its start, masked there
+      constexpr int64_t frame_f4 = (int64_t)G::OH2 * G::OW2 * 8;
+      const int blocks = (int)std::min<int64_t>((n * frame_f4 + 255) / 256, 4096);
+      hipLaunchKernelGGL(goal_dz2_reduce_kernel, dim3(blocks), dim3(256), 0, st, w.dz2, a.X[1], frame_f4, gr->goal_list,
+                         gr->goal_count, gr->run_length, gr->num_envs);
+    }
   }
   // ---- conv2 (k4 s2): wgrad (needs X1), then dgrad into dz1 written over X1
   {
@@ -1538,7 +1642,7 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
     if (Wg2::fits && !getenv("VN_WGRAD_GENERIC")) {  // x6 form; read per call (A/B and parity checks)
       if constexpr (Wg2::fits) {
         const int rc = launch_conv_wgrad_x6<Wg2>(w.dz2, a.X[0], frames, w.slab, w.slab_cap, Gr + L.l[1].w, Gr + L.l[1].b,
-                                                 st);
+                                                 st, fl);
         if (rc != VN_OK) return rc;
       }
     } else if constexpr (lds <= 80 * 1024) {  // f32 MFMA, two workgroups per CU (bands of output rows)
@@ -1575,7 +1679,7 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
           VN_HIP(ensure_dyn_lds(kfn, lds));  // > 64 KiB dynamic LDS: opt-in
           const int blocks = std::min(frames, resident_blocks(kfn, NW * 64, lds));
           hipLaunchKernelGGL((conv2_dgrad_x6_kernel<G::OH1, G::OW1, G::OH2, G::OW2, NW>), dim3(blocks), dim3(NW * 64), lds,
-                             st, w.dz2, T(1), a.M1, a.X[0], frames);
+                             st, w.dz2, T(1), a.M1, a.X[0], frames, fl);
           done = true;
         }
       }
@@ -1606,7 +1710,7 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
       const void* kfn = (const void*)conv1_wgrad_x3_kernel<H0, W0, G::OH1, G::OW1>;
       const int blocks = std::min(frames * Bd::NB, resident_blocks(kfn, 256, Bd::LDS));
       hipLaunchKernelGGL((conv1_wgrad_x3_kernel<H0, W0, G::OH1, G::OW1>), dim3(blocks), dim3(256), Bd::LDS, st, src,
-                         frames, a.X[0], w.slab);
+                         frames, fl, a.X[0], w.slab);
       constexpr int kParts = 32;
       float* part = w.slab + (int64_t)blocks * 32 * 160;
       hipLaunchKernelGGL(slab_partial_kernel, dim3((32 * 160 + 255) / 256, kParts), dim3(256), 0, st, w.slab, blocks,
@@ -2224,8 +2328,34 @@ int vn_policy_workspace_floats(vn_policy* p, int64_t n, int64_t* floats) {
   return VN_OK;
 }
 
+namespace {
+int check_goal_runs(const vn_policy* p, const FrameSrc& src, int n, const vn_goal_runs* g, bool backward,
+                    const char* who) {
+  if (!g) return VN_OK;
+  if (!goal_runs_ok(p->L, n) || src.f32[0] || src.f32[1])
+    return fail(VN_EINVAL, std::string(who) + ": goal runs are not supported here (see vn_policy_goal_runs_supported)");
+  if (!g->goal_list || !g->goal_count || !g->goal_delta)
+    return fail(VN_EINVAL, std::string(who) + ": incomplete goal runs");
+  if (backward && (!g->run_length || g->num_envs <= 0 || n % g->num_envs != 0))
+    return fail(VN_EINVAL, std::string(who) + ": goal runs need run_length and num_envs dividing n");
+  return VN_OK;
+}
+}  // namespace
+
+int vn_policy_goal_runs_supported(vn_policy* p, int n, int* supported) {
+  if (!p || !supported) return fail(VN_EINVAL, "vn_policy_goal_runs_supported: bad args");
+  *supported = goal_runs_ok(p->L, n) ? 1 : 0;
+  return VN_OK;
+}
+
 int vn_policy_forward(vn_policy* p, const float* params, const vn_frames* frames, int n, float* acts,
                       int64_t act_capacity, int64_t act_offset, float* out, vn_stream_t stream) {
+  return vn_policy_forward_goals(p, params, frames, n, acts, act_capacity, act_offset, out, nullptr, stream);
+}
+
+int vn_policy_forward_goals(vn_policy* p, const float* params, const vn_frames* frames, int n, float* acts,
+                            int64_t act_capacity, int64_t act_offset, float* out, const vn_goal_runs* goals,
+                            vn_stream_t stream) {
   if (!p || !params || !frames || !acts || n <= 0) return fail(VN_EINVAL, "vn_policy_forward: bad args");
   if (!out && !p->L.lstm) return fail(VN_EINVAL, "vn_policy_forward: out is NULL");
   if (act_offset < 0 || act_offset + n > act_capacity)
@@ -2233,21 +2363,32 @@ int vn_policy_forward(vn_policy* p, const float* params, const vn_frames* frames
   const FrameSrc src = to_src(frames);
   if ((!src.base[0] && !src.f32[0]) || (!src.base[1] && !src.f32[1]))
     return fail(VN_EINVAL, "vn_policy_forward: missing frames");
+  const int rc = check_goal_runs(p, src, n, goals, false, "vn_policy_forward");
+  if (rc != VN_OK) return rc;
   const Acts a = acts_at(p->L, acts, act_capacity, act_offset);
   hipStream_t st = (hipStream_t)stream;
   if (p->L.arch == 1) return forward_bignet<84, 84>(p->L, params, src, n, a, out, st);
   return dispatch_geo(p->L, [&](auto g) {
-    return forward_impl<decltype(g)::H, decltype(g)::W>(p->L, params, src, n, a, out, st);
+    return forward_impl<decltype(g)::H, decltype(g)::W>(p->L, params, src, n, a, out, st, goals);
   });
 }
 
 int vn_policy_backward_ex(vn_policy* p, const float* params, const vn_frames* frames, int n, float* acts,
                           int64_t act_capacity, const float* dout, const float* dz5, const float* dx4_extra,
                           float* grads, float* workspace, vn_stream_t stream) {
+  return vn_policy_backward_goals(p, params, frames, n, acts, act_capacity, dout, dz5, dx4_extra, grads, workspace,
+                                  nullptr, stream);
+}
+
+int vn_policy_backward_goals(vn_policy* p, const float* params, const vn_frames* frames, int n, float* acts,
+                             int64_t act_capacity, const float* dout, const float* dz5, const float* dx4_extra,
+                             float* grads, float* workspace, const vn_goal_runs* goals, vn_stream_t stream) {
   if (!p || !params || !frames || !acts || !grads || !workspace || n <= 0 || (!dout && !dz5))
     return fail(VN_EINVAL, "vn_policy_backward: bad args");
   if (n > act_capacity) return fail(VN_EINVAL, "vn_policy_backward: n exceeds the activation capacity");
   const FrameSrc src = to_src(frames);
+  const int rc = check_goal_runs(p, src, n, goals, true, "vn_policy_backward");
+  if (rc != VN_OK) return rc;
   const Acts a = acts_at(p->L, acts, act_capacity, 0);
   const BwdWork w = carve(p->L, workspace, n);
   hipStream_t st = (hipStream_t)stream;
@@ -2257,7 +2398,8 @@ int vn_policy_backward_ex(vn_policy* p, const float* params, const vn_frames* fr
     return backward_bignet<84, 84>(p->L, params, src, n, a, d, dz5, grads, w, st);
   }
   return dispatch_geo(p->L, [&](auto g) {
-    return backward_impl<decltype(g)::H, decltype(g)::W>(p->L, params, src, n, a, d, dz5, dx4_extra, grads, w, st);
+    return backward_impl<decltype(g)::H, decltype(g)::W>(p->L, params, src, n, a, d, dz5, dx4_extra, grads, w, st,
+                                                         goals);
   });
 }
 

@@ -65,6 +65,17 @@ class A2CStep(ctypes.Structure):
     ]
 
 
+class GoalRuns(ctypes.Structure):
+    """vn_goal_runs (include/vnav.h)."""
+    _fields_ = [
+        ("goal_list", c_void_p),
+        ("goal_count", c_void_p),
+        ("goal_delta", c_void_p),
+        ("run_length", c_void_p),
+        ("num_envs", c_int),
+    ]
+
+
 # name -> (restype, argtypes). Every symbol here is declared in include/vnav.h.
 SIGNATURES = {
     "vn_version": (ctypes.c_char_p, []),
@@ -152,6 +163,13 @@ SIGNATURES.update({
     "vn_policy_sample_dev": (c_int, [c_void_p, c_int, c_int, c_uint64, c_void_p, c_uint64, c_void_p, c_void_p,
                                      c_void_p, c_void_p, c_void_p]),
     "vn_trace_marker": (c_int, [c_int, c_void_p]),
+    "vn_policy_goal_runs_supported": (c_int, [c_void_p, c_int, P(c_int)]),
+    "vn_policy_forward_goals": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int64, c_int64, c_void_p,
+                                        P(GoalRuns), c_void_p]),
+    "vn_policy_backward_goals": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int64, c_void_p, c_void_p,
+                                         c_void_p, c_void_p, c_void_p, P(GoalRuns), c_void_p]),
+    "vn_goal_runs_step": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "vn_goal_runs_rollout": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "vn_a2c_episode_stats": (c_int, [c_void_p, c_int, c_void_p, c_void_p]),
     "vn_rmsprop_step_dev": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_float, c_void_p, c_void_p, c_float,
                                     c_float, c_void_p]),

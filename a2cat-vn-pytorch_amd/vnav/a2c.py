@@ -52,7 +52,7 @@ class A2CTrainer:
                  max_time_steps=2e6, rms_alpha=0.99, rms_epsilon=1e-5, max_gradient_norm=0.5,
                  value_coefficient=0.5, entropy_coefficient=0.01, seed=0, process_group=None, recurrent=False,
                  aux_weight=0.0, arch="goal", cuda_graph=False, aux_source="rollout", replay_size=8,
-                 capture_collectives=False, allreduce_buckets=2, time_collectives=False):
+                 capture_collectives=False, allreduce_buckets=2, time_collectives=False, dedup_goals=True):
         self.env = env
         self.lib = _lib.load()
         self.device = env.device
@@ -181,6 +181,34 @@ class A2CTrainer:
         self._model_view = None
         arena, fb, _, _ = env.frame_arena()
         self._arena, self._fb = arena, fb
+        # goal-frame deduplication (vn_goal_runs): an env's goal frame is constant within an
+        # episode, so shared_base runs on it once per goal run — at the rollout's first step and
+        # after each done — and the backward sums a run's goal-map gradients before conv2 /
+        # conv1 (same outputs, gradients up to summation order). Runs where the policy's
+        # kernels take frame lists (84x84 / 174x174, more than 16 envs).
+        self.dedup_goals = bool(dedup_goals) and self.net.arch == "goal" and self.net.goal_runs_supported(E)
+        if self.dedup_goals:
+            i32 = dict(dtype=torch.int32, **kw)
+            self.goal_delta = torch.zeros((T, E), **i32)
+            self.goal_list_step = torch.zeros((T, E), **i32)
+            self.goal_count = torch.zeros(T + 1, **i32)  # per step, then the update's
+            self.goal_list = torch.zeros(N, **i32)
+            self.goal_run_length = torch.zeros(N, **i32)
+            self._goal_runs_step = []
+            for t in range(T):
+                g = _lib.GoalRuns()
+                g.goal_list = self.goal_list_step[t].data_ptr()
+                g.goal_count = self.goal_count[t:t + 1].data_ptr()
+                g.goal_delta = self.goal_delta[t].data_ptr()
+                g.num_envs = E
+                self._goal_runs_step.append(g)
+            g = _lib.GoalRuns()
+            g.goal_list = self.goal_list.data_ptr()
+            g.goal_count = self.goal_count[T:T + 1].data_ptr()
+            g.goal_delta = self.goal_delta.data_ptr()
+            g.run_length = self.goal_run_length.data_ptr()
+            g.num_envs = E
+            self._goal_runs_update = g
         # the rollout's fused env steps (vn_step_a2c): sampling + step + bookkeeping, one launch
         # per step; per-env episode statistics reduced once per rollout (vn_a2c_episode_stats)
         self.stats_env = torch.zeros((3, E), dtype=torch.float32, **kw)
@@ -297,12 +325,20 @@ class A2CTrainer:
         """Forward of step t of the rollout into self.out[t*E:(t+1)*E]."""
         net, E, N = self.net, self.env.num_envs, self.num_steps * self.env.num_envs
         sl = slice(t * E, (t + 1) * E)
+        goals = None
+        if self.dedup_goals:  # step t's new goals: all at t = 0, else the envs done at t - 1
+            P = _lib.ptr
+            _lib.check(self.lib.vn_goal_runs_step(P(self.dones[t - 1]) if t else None,
+                                                  P(self.goal_delta[t - 1]) if t else None, E,
+                                                  P(self.goal_delta[t]), P(self.goal_list_step[t]),
+                                                  P(self.goal_count[t:t + 1]), self._stream()), "vn_goal_runs_step")
+            goals = self._goal_runs_step[t]
         if not self.recurrent:
-            net.forward(self.params, frames, E, self.acts, N, t * E, self.out[sl])
+            net.forward(self.params, frames, E, self.acts, N, t * E, self.out[sl], goals=goals)
             return
         # step 0's mask / last action-reward come from vn_a2c_rollout_begin, later steps' from
         # the env step before them
-        net.forward(self.params, frames, E, self.acts, N, t * E, None)
+        net.forward(self.params, frames, E, self.acts, N, t * E, None, goals=goals)
         hp = self.h0 if t == 0 else self.h_all[(t - 1) * E:t * E]
         cp = self.c0 if t == 0 else self.c_all[(t - 1) * E:t * E]
         net.lstm_step(self.params, E, net.x5(self.acts, N)[sl], self.lra[t], self.masks[t], hp, cp, self.xcat[sl],
@@ -390,17 +426,25 @@ class A2CTrainer:
             net.aux_backward(self.params, self.acts, N, N, self.a1, self.dpred, self.grads, self.dx4, self.aux_ws)
             dx4 = self.dx4
         frames = self._frames(self.rows_img, self.rows_goal)
+        goals = None
+        if self.dedup_goals:  # the rollout's goal runs: starts ascending, run lengths
+            P = _lib.ptr
+            _lib.check(lib.vn_goal_runs_rollout(P(self.dones), T, E, P(self.goal_list), P(self.goal_run_length),
+                                                P(self.goal_count[T:T + 1]), st), "vn_goal_runs_rollout")
+            goals = self._goal_runs_update
         if self.recurrent:
             net.lstm_backward(self.params, T, E, self.dout, self.h_all, self.xcat, self.lstm_acts, self.c_all, self.c0,
                               self.masks, net.x5(self.acts, N), self.dz5, self.grads, self.lstm_ws)
             # the heads + LSTM (+ aux heads) gradients are final here: their all-reduce runs on
             # RCCL's stream while the trunk backward runs on this one
             self._allreduce_head_bucket()
-            net.backward_ex(self.params, frames, N, self.acts, N, None, self.dz5, dx4, self.grads, self.workspace)
+            net.backward_ex(self.params, frames, N, self.acts, N, None, self.dz5, dx4, self.grads, self.workspace,
+                            goals=goals)
             # (h, c) after the last step carry into the next rollout (one copy launch)
             self._carry_states()
         else:
-            net.backward_ex(self.params, frames, N, self.acts, N, self.dout, None, dx4, self.grads, self.workspace)
+            net.backward_ex(self.params, frames, N, self.acts, N, self.dout, None, dx4, self.grads, self.workspace,
+                            goals=goals)
         if aux_batch is not None:
             self._add_trunk_grads(self.aux_grads)
         if self._custom_aux:

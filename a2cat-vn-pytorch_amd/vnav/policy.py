@@ -306,22 +306,42 @@ class PolicyNet:
         c = int(capacity)
         return acts[c * (self.act_floats - 512):c * self.act_floats].view(c, 512)
 
-    def forward(self, params, frames, n, acts, capacity, offset, out):
-        """out=None (recurrent nets only): trunk only, features kept in acts."""
-        _lib.check(self.lib.vn_policy_forward(self._h, _lib.ptr(params), ctypes.byref(frames), int(n), _lib.ptr(acts),
-                                              int(capacity), int(offset), _lib.ptr(out),
-                                              _lib.stream_ptr(self.device)), "vn_policy_forward")
+    def forward(self, params, frames, n, acts, capacity, offset, out, goals=None):
+        """out=None (recurrent nets only): trunk only, features kept in acts. goals: a
+        _lib.GoalRuns of this call's samples (goal-frame deduplication, vn_goal_runs)."""
+        if goals is None:
+            _lib.check(self.lib.vn_policy_forward(self._h, _lib.ptr(params), ctypes.byref(frames), int(n),
+                                                  _lib.ptr(acts), int(capacity), int(offset), _lib.ptr(out),
+                                                  _lib.stream_ptr(self.device)), "vn_policy_forward")
+            return
+        _lib.check(self.lib.vn_policy_forward_goals(self._h, _lib.ptr(params), ctypes.byref(frames), int(n),
+                                                    _lib.ptr(acts), int(capacity), int(offset), _lib.ptr(out),
+                                                    ctypes.byref(goals), _lib.stream_ptr(self.device)),
+                   "vn_policy_forward_goals")
+
+    def goal_runs_supported(self, n):
+        """Whether forward / backward take goal runs for calls of n samples (84x84 / 174x174)."""
+        ok = ctypes.c_int()
+        _lib.check(self.lib.vn_policy_goal_runs_supported(self._h, int(n), ctypes.byref(ok)),
+                   "vn_policy_goal_runs_supported")
+        return bool(ok.value)
 
     def backward(self, params, frames, n, acts, capacity, dout, grads, workspace):
         _lib.check(self.lib.vn_policy_backward(self._h, _lib.ptr(params), ctypes.byref(frames), int(n), _lib.ptr(acts),
                                                int(capacity), _lib.ptr(dout), _lib.ptr(grads), _lib.ptr(workspace),
                                                _lib.stream_ptr(self.device)), "vn_policy_backward")
 
-    def backward_ex(self, params, frames, n, acts, capacity, dout, dz5, dx4, grads, workspace):
+    def backward_ex(self, params, frames, n, acts, capacity, dout, dz5, dx4, grads, workspace, goals=None):
         P = _lib.ptr
-        _lib.check(self.lib.vn_policy_backward_ex(self._h, P(params), ctypes.byref(frames), int(n), P(acts),
-                                                  int(capacity), P(dout), P(dz5), P(dx4), P(grads), P(workspace),
-                                                  _lib.stream_ptr(self.device)), "vn_policy_backward_ex")
+        if goals is None:
+            _lib.check(self.lib.vn_policy_backward_ex(self._h, P(params), ctypes.byref(frames), int(n), P(acts),
+                                                      int(capacity), P(dout), P(dz5), P(dx4), P(grads), P(workspace),
+                                                      _lib.stream_ptr(self.device)), "vn_policy_backward_ex")
+            return
+        _lib.check(self.lib.vn_policy_backward_goals(self._h, P(params), ctypes.byref(frames), int(n), P(acts),
+                                                     int(capacity), P(dout), P(dz5), P(dx4), P(grads), P(workspace),
+                                                     ctypes.byref(goals), _lib.stream_ptr(self.device)),
+                   "vn_policy_backward_goals")
 
     # -- aux deconv heads ------------------------------------------------------------
     def aux_workspace_floats(self):

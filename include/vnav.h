@@ -328,6 +328,46 @@ int vn_policy_backward_ex(vn_policy* p, const float* params, const vn_frames* fr
                           int64_t act_capacity, const float* dout, const float* dz5, const float* dx4_extra,
                           float* grads, float* workspace, vn_stream_t stream);
 
+/* ---- goal-frame deduplication: shared_base on the goal frame once per episode ----
+ * BigGoalHouseModel runs shared_base on the goal frame at every step (models/goal.py:88), but
+ * an env's goal frame does not change within an episode. A goal run is a sample whose goal is
+ * new — the first step of a rollout, or the step after a done (the env auto-reset) — followed
+ * by the same env's later steps up to its next done. With goal runs the policy computes conv1 /
+ * conv2 of a goal frame only at the run's first sample, conv_base reads every sample's goal
+ * map from its run start, and the backward sums a run's goal-map gradients before conv2's
+ * weight / input gradient and conv1's weight gradient: the same outputs (bitwise: the
+ * kernels are batch-independent) and the same gradients up to summation order. Samples are
+ * time-major (t*E + e). */
+typedef struct vn_goal_runs {
+  const int32_t* goal_list;   /* samples (of the call) that start a goal run, ascending */
+  const int32_t* goal_count;  /* device scalar: entries of goal_list */
+  const int32_t* goal_delta;  /* [n] offset (<= 0, in samples) to the sample holding this sample's goal maps */
+  const int32_t* run_length;  /* backward: [n] steps of the run starting at each listed sample */
+  int num_envs;               /* backward: E, the sample stride between an env's steps */
+} vn_goal_runs;
+/* *supported = 1 when the policy takes goal runs for calls of n samples (84x84 / 174x174
+ * uint8 frames, n > 16, no VN_*_GENERIC override set); else 0. */
+int vn_policy_goal_runs_supported(vn_policy* p, int n, int* supported);
+/* vn_policy_forward with the goal runs of this call's n samples (goals != NULL; an unsupported
+ * configuration is an error, not a silent fallback). */
+int vn_policy_forward_goals(vn_policy* p, const float* params, const vn_frames* frames, int n, float* acts,
+                            int64_t act_capacity, int64_t act_offset, float* out, const vn_goal_runs* goals,
+                            vn_stream_t stream);
+/* vn_policy_backward_ex over samples whose forward ran with these goal runs (the goal maps
+ * of non-start samples were never computed: a backward without the runs would read them). */
+int vn_policy_backward_goals(vn_policy* p, const float* params, const vn_frames* frames, int n, float* acts,
+                             int64_t act_capacity, const float* dout, const float* dz5, const float* dx4_extra,
+                             float* grads, float* workspace, const vn_goal_runs* goals, vn_stream_t stream);
+/* Rollout step t's goal runs (before its forward): new[e] = done_prev == NULL || done_prev[e]
+ * (done_prev = step t - 1's dones; NULL at t = 0); delta[e] = new ? 0 : delta_prev[e] - E;
+ * list = the envs with new goals, ascending; *count = their number. One workgroup. */
+int vn_goal_runs_step(const uint8_t* done_prev, const int32_t* delta_prev, int E, int32_t* delta, int32_t* list,
+                      int32_t* count, vn_stream_t stream);
+/* The update's goal runs over the rollout's T*E samples (dones [T][E]): list = the run starts
+ * ascending, run_length [T*E] at each start, *count. One workgroup. */
+int vn_goal_runs_rollout(const uint8_t* dones, int T, int E, int32_t* list, int32_t* run_length, int32_t* count,
+                         vn_stream_t stream);
+
 /* ---- A2C (the deep_rl trainer contract; DESIGN.md "A2C contract") ---- */
 int vn_policy_sample(const float* out, int n, int num_actions, uint64_t seed, uint64_t counter,
                      int32_t* actions, float* logp, float* entropy, float* value, vn_stream_t stream);

@@ -54,9 +54,9 @@ int main(int argc, char** argv) {
   for (int grid : {512, 768, 1024}) {
     auto run = [&]() {
       if (which[0] == 'w')
-        hipLaunchKernelGGL((conv1_wgrad_x3_kernel<84, 84, 20, 20>), dim3(grid), dim3(256), (Conv1WgBand<84, 84>::LDS), 0, src, frames, dz, slab);
+        hipLaunchKernelGGL((conv1_wgrad_x3_kernel<84, 84, 20, 20>), dim3(grid), dim3(256), (Conv1WgBand<84, 84>::LDS), 0, src, frames, FrameList{}, dz, slab);
       else if (which[0] == 'd')
-        hipLaunchKernelGGL((conv2_dgrad_x6_kernel<20, 20, 9, 9, 4>), dim3(grid), dim3(256), dlds, 0, dz2, wt, msk, dx1, frames);
+        hipLaunchKernelGGL((conv2_dgrad_x6_kernel<20, 20, 9, 9, 4>), dim3(grid), dim3(256), dlds, 0, dz2, wt, msk, dx1, frames, FrameList{});
       else
         hipLaunchKernelGGL((conv2_dgrad_kernel<20, 20, 9, 9, true>), dim3(grid), dim3(256), 0, 0, dz2, wt, dx1, msk, dx1, frames);
     };
