@@ -715,7 +715,7 @@ constexpr size_t conv2_wgrad_lds() {
 template <int IH, int IW, int OH, int OW>
 __global__ __launch_bounds__(256) void conv2_wgrad_kernel(const float* __restrict__ X1, const float* __restrict__ dZ2,
                                                           int n_frames, float* __restrict__ slab,
-                                                          float* __restrict__ bias_slab) {
+                                                          float* __restrict__ bias_slab, FrameList fl) {
   using Bd = Conv2WgBand<IH, IW, OH, OW>;
   constexpr int BR = Bd::BR, NB = Bd::NB;
   constexpr int NX = Bd::rows_of(BR) * IW * 32, NP = OH * OW;
@@ -730,13 +730,13 @@ __global__ __launch_bounds__(256) void conv2_wgrad_kernel(const float* __restric
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[j][r] = 0.0f;
   float bacc = 0.0f;  // bias gradient: column sums of dZ2 (wave 0 only)
-  const int n_items = n_frames * NB;
+  const int n_items = fl_count(fl, n_frames) * NB;
   // The next item's band is loaded into registers while this one computes (the load and
   // the MFMA phases of the two workgroups on a CU otherwise ran in lockstep, unoverlapped).
   constexpr int NVX = (NX / 4 + 255) / 256, NVD = ((BR * OW + 1) / 2 * 2 * 8 + 255) / 256;
   f4 px4[NVX], pd4[NVD];
   auto load_item = [&](int it) {
-    const int f = it / NB, band = it - (it / NB) * NB;
+    const int f = fl_frame(fl, it / NB), band = it - (it / NB) * NB;
     const int oy0 = BR * band, nr = min(BR, OH - oy0), npb = nr * OW, npe = (npb + 1) / 2 * 2;
     const int y0 = 2 * oy0, nx = min(2 * nr + 2, IH - y0) * IW * 32;
     const f4* s4 = reinterpret_cast<const f4*>(X1 + ((int64_t)f * IH + y0) * IW * 32);
@@ -1104,6 +1104,179 @@ __global__ __launch_bounds__(NW * 64, 2) void conv2_dgrad_x6_kernel(const float*
     }
     __syncthreads();
   }
+}
+
+// ---- conv2 input gradient, banded (maps too large to stage whole: 300x400) ------------
+// The product of conv2_dgrad_x6_kernel over a band of BY rows of the conv1 map: a work item is
+// (frame, band); the dZ2 rows its pixels' taps reach (BY/2 + 1 of them) are split once into
+// three bf16 planes (pixel stride 40, a zero row for out-of-range taps), the band's conv1 ReLU
+// words staged beside them, the next item's rows prefetched into registers. Wave w owns
+// parity class (py, px) = (w >> 1, w & 1) with its split weights in registers; a class's
+// width is (IW - px + 1) / 2, so odd maps (99 columns) work. 74x99 conv1 map, BY = 8: 61 KB of
+// LDS, two workgroups per CU; dZ2 is staged 1.25x (a row shared by neighbouring bands).
+constexpr size_t conv2_dgband_lds(int IW, int OW, int BY) {  // 3 planes of BY/2 + 1 dZ2 rows + 1, ReLU words
+  return (size_t)3 * ((BY / 2 + 1) * OW + 1) * 40 * 2 + (size_t)BY * IW * 4;
+}
+
+template <int IH, int IW, int OH, int OW, int BY>
+struct Conv2DgBand {
+  static_assert(BY % 2 == 0, "bands of whole parity rows");
+  static constexpr int NB = (IH + BY - 1) / BY;  // bands per frame
+  static constexpr int ZR = BY / 2 + 1;          // staged dZ2 rows
+  static constexpr int PS = 40;                  // plane row stride (bf16)
+  static constexpr int PL = (ZR * OW + 1) * PS;  // plane size (bf16), + the zero row
+  static constexpr size_t LDS = conv2_dgband_lds(IW, OW, BY);
+};
+
+template <int IW, int OW>
+constexpr int conv2_dgrad_band_rows() {  // the largest even band whose LDS keeps 2 workgroups per CU
+  int by = 16;
+  while (by > 2 && conv2_dgband_lds(IW, OW, by) > 80 * 1024) by -= 2;
+  return by;
+}
+
+template <int IH, int IW, int OH, int OW, int BY>
+__global__ __launch_bounds__(256, 2) void conv2_dgrad_band_x6_kernel(const float* __restrict__ dZ2,
+                                                                     const float* __restrict__ WT,
+                                                                     const uint32_t* __restrict__ mask,
+                                                                     float* __restrict__ dX1, int n_frames,
+                                                                     FrameList fl) {
+  using B = Conv2DgBand<IH, IW, OH, OW, BY>;
+  constexpr int NB = B::NB, ZR = B::ZR, PS = B::PS, PL = B::PL, NT = 256;
+  constexpr int NP = OH * OW;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem_db[];
+  uint16_t* zs = reinterpret_cast<uint16_t*>(smem_db);
+  uint32_t* ms = reinterpret_cast<uint32_t*>(smem_db + (size_t)3 * PL * 2);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int py = wave >> 1, px = wave & 1;
+  const int xc = (IW - px + 1) / 2;  // class width
+  const int i16 = lane & 15, q = lane >> 4;
+  bf16x8_t bw[4][2][3];  // [tap][ci tile][term]: B[k = co 8q + j][ci]
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int ky = py + 2 * (t >> 1), kx = px + 2 * (t & 1);
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      union { uint16_t u[8]; bf16x8_t v; } b0, b1, b2;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        split3_bf16(WT[((ky * 4 + kx) * 32 + nt * 16 + i16) * 32 + 8 * q + j], b0.u[j], b1.u[j], b2.u[j]);
+      bw[t][nt][0] = b0.v;
+      bw[t][nt][1] = b1.v;
+      bw[t][nt][2] = b2.v;
+    }
+  }
+  for (int i = tid; i < 3 * PS / 2; i += NT) {  // zero rows
+    const int pl = i / (PS / 2), e = i - pl * (PS / 2);
+    reinterpret_cast<uint32_t*>(zs + pl * PL + ZR * OW * PS)[e] = 0u;
+  }
+  constexpr int NZ = (ZR * OW * 8 + NT - 1) / NT, NM = (BY * IW + NT - 1) / NT;
+  f4 zr[NZ];
+  uint32_t mr[NM];
+  auto z_lo = [](int band) { return max(BY / 2 * band - 1, 0); };
+  auto z_rows = [&](int band) { return min(BY / 2 * band + BY / 2, OH) - z_lo(band); };
+  auto b_rows = [](int band) { return min(BY, IH - BY * band); };
+  // item it = (list item it / NB, band it % NB): its dZ2 rows and ReLU words into registers,
+  // unconditional (clamped: slots past the band reload its last one; staging skips them)
+  auto load = [&](int it) {
+    const int f = fl_frame(fl, it / NB), band = it - (it / NB) * NB;
+    const int nz = z_rows(band) * OW * 8, nm = b_rows(band) * IW;
+    const f4* z4 = reinterpret_cast<const f4*>(dZ2 + ((int64_t)f * OH + z_lo(band)) * OW * 32);
+#pragma unroll
+    for (int j = 0; j < NZ; ++j) zr[j] = z4[min(tid + j * NT, nz - 1)];
+    const uint32_t* m = mask + ((int64_t)f * IH + BY * band) * IW;
+#pragma unroll
+    for (int j = 0; j < NM; ++j) mr[j] = m[min(tid + j * NT, nm - 1)];
+  };
+  const int n_items = fl_count(fl, n_frames) * NB;
+  if ((int)blockIdx.x < n_items) load(blockIdx.x);
+  for (int it = blockIdx.x; it < n_items; it += gridDim.x) {
+    const int f = fl_frame(fl, it / NB), band = it - (it / NB) * NB;
+    const int zlo = z_lo(band), nz = z_rows(band) * OW * 8, by = b_rows(band);
+#pragma unroll
+    for (int j = 0; j < NZ; ++j) {
+      const int i = tid + j * NT;
+      if (i < nz) {
+        uint2 t0, t1, t2;
+        split3_pack(zr[j], t0, t1, t2);
+        uint16_t* d = zs + (i >> 3) * PS + 4 * (i & 7);
+        *reinterpret_cast<uint2*>(d) = t0;
+        *reinterpret_cast<uint2*>(d + PL) = t1;
+        *reinterpret_cast<uint2*>(d + 2 * PL) = t2;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NM; ++j) {
+      const int i = tid + j * NT;
+      if (i < by * IW) ms[i] = mr[j];
+    }
+    __syncthreads();
+    load(min(it + (int)gridDim.x, n_items - 1));
+    const int yy0 = BY / 2 * band;             // first class row of the band (both py: y0 even)
+    const int ncy = (by - py + 1) / 2;         // class rows of this class in the band
+    const int npc = ncy * xc, tiles = (npc + 15) / 16;
+#pragma unroll 1
+    for (int t0 = 0; t0 < tiles; t0 += 2) {
+      int off[2][4];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int pc = (t0 + u) * 16 + i16;  // this lane's class pixel (A row)
+        const int yl = pc / xc, xx = pc - (pc / xc) * xc;
+#pragma unroll
+        for (int tap = 0; tap < 4; ++tap) {
+          const int oy = yy0 + yl - (tap >> 1), ox = xx - (tap & 1);
+          const bool ok = pc < npc && oy >= 0 && oy < OH && ox >= 0 && ox < OW;
+          off[u][tap] = (ok ? (oy - zlo) * OW + ox : ZR * OW) * PS + 8 * q;
+        }
+      }
+      f4 acc[2][2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) acc[u][nt] = f4zero();
+#pragma unroll
+      for (int tap = 0; tap < 4; ++tap) {
+        bf16x8_t a[2][3];
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int tm = 0; tm < 3; ++tm) a[u][tm] = *reinterpret_cast<const bf16x8_t*>(zs + tm * PL + off[u][tap]);
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) {  // small terms first (conv2_dgrad_x6_kernel's order)
+            f4 c = acc[u][nt];
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[tap][nt][0], a[u][2], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[tap][nt][2], a[u][0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[tap][nt][1], a[u][1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[tap][nt][0], a[u][1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[tap][nt][1], a[u][0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[tap][nt][0], a[u][0], c, 0, 0, 0);
+            acc[u][nt] = c;
+          }
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int pc = (t0 + u) * 16 + i16;
+        if (pc < npc) {
+          const int yl = pc / xc, xx = pc - (pc / xc) * xc;
+          const int y = 2 * (yy0 + yl) + py, x = 2 * xx + px;
+          const int64_t pix = ((int64_t)f * IH + y) * IW + x;
+          const uint32_t mw = ms[(y - BY * band) * IW + x];
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) {
+            const uint32_t m4 = mw >> (nt * 16 + 4 * q);
+            f4 v = acc[u][nt];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = (m4 >> r) & 1u ? v[r] : 0.0f;
+            *reinterpret_cast<f4*>(dX1 + pix * 32 + nt * 16 + 4 * q) = v;
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  (void)NP;
 }
 
 // ---- conv2 forward on bf16 MFMA (split operands) -----------------------------------

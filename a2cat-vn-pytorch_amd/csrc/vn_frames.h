@@ -49,6 +49,12 @@ __device__ __forceinline__ int fl_frame(const FrameList& fl, int i) {
   const int g = fl_sload(fl.goals + (j > 0 ? j : 0));
   return j >= 0 ? 2 * g + 1 : 2 * i;
 }
+
+// Per-lane form (i differs between lanes: an im2col row's frame), plain vector loads.
+__device__ __forceinline__ int fl_frame_v(const FrameList& fl, int i) {
+  if (!fl.goals) return i;
+  return i < fl.nimg ? 2 * i : 2 * fl.goals[i - fl.nimg] + 1;
+}
 #endif
 
 }  // namespace vn

@@ -45,6 +45,13 @@ template <class E, class = void>
 struct has_pre_row : std::false_type {};
 template <class E>
 struct has_pre_row<E, std::void_t<decltype(&E::pre_row)>> : std::true_type {};
+// A loader whose valid rows end at a device-side count (row_limit(), wave-uniform): tiles at
+// or past it return at once and the epilogue stores no row at or past it (the grid is sized
+// for the host's upper bound — goal-frame deduplication's device-side frame counts).
+template <class L, class = void>
+struct has_row_limit : std::false_type {};
+template <class L>
+struct has_row_limit<L, std::void_t<decltype(&L::row_limit)>> : std::true_type {};
 
 // Epilogue over an accumulator tile: NR values per (i, j) whose (row, col) come from rc; the
 // column of a value depends on j (and the lane) only, its row on i and r only.
@@ -372,6 +379,11 @@ __global__ __launch_bounds__(256) void gemm_x6_kernel(FA fa, FB fb, EP ep, int M
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WM, wn = wave / WM;
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  if constexpr (has_row_limit<FA>::value) {  // uniform: the whole workgroup leaves together
+    const int lim = fa.row_limit();
+    if (m0 >= lim) return;
+    M = min(M, lim);
+  }
   const int kb = blockIdx.z * kchunk;
   const int ke = min(K, kb + kchunk);
   f16v_ acc[TM][TN];

@@ -117,6 +117,40 @@ struct NhwcIm2colGoal {
   VN_ROWS_LOADER
 };
 
+// conv2's im2col (one 32-channel input, k4 s2) over the frames of a FrameList (goal-frame
+// deduplication on maps without a persistent conv2 kernel, 300x400): row m = (list item
+// m / (OH*OW), output pixel); rows end at the list's device-side count (row_limit).
+template <int H, int W, int OH, int OW>
+struct FrameListIm2col {
+  const float* X;
+  int M;  // host upper bound: 2 * samples * OH * OW
+  FrameList fl;
+  __device__ __forceinline__ int row_limit() const { return fl_count(fl, 0) * (OH * OW); }
+  __device__ __forceinline__ f4 load4(int m, int k, int kend) const {
+    if (m >= M || k >= kend) return f4zero();
+    const int i = m / (OH * OW);
+    const int r = m - i * (OH * OW);
+    const int oy = r / OW, ox = r - (r / OW) * OW;
+    const int c = k & 31, t = k >> 5, ky = t >> 2, kx = t & 3;
+    const int64_t f = fl_frame_v(fl, i);
+    return *reinterpret_cast<const f4*>(X + ((f * H + oy * 2 + ky) * W + ox * 2 + kx) * 32 + c);
+  }
+  VN_ROWS_LOADER
+};
+
+// Bias + ReLU into the listed frames' maps (row m of FrameListIm2col -> its frame's pixel).
+template <int OH, int OW>
+struct EpiBiasActFrames {
+  float* Y;
+  const float* bias;
+  FrameList fl;
+  __device__ __forceinline__ float pre_col(int col) const { return bias[col]; }
+  __device__ __forceinline__ void post(int row, int col, float v, float b, int) const {
+    const int i = row / (OH * OW), r = row - i * (OH * OW);
+    Y[((int64_t)fl_frame_v(fl, i) * (OH * OW) + r) * 32 + col] = fmaxf(v + b, 0.0f);
+  }
+};
+
 // BigHouseModel conv1 (Conv2d(3, 32, k8, s4), bignet.py:29) im2col over the image frame
 // only: row m = (sample, oy, ox), k = (ky*8 + kx)*3 + c, K = 192; u8 frames as x/255
 // (ScaledFloatFrame) or dense float NCHW frames.
@@ -318,6 +352,7 @@ struct EpiMaskParityG {
   float* out;
   const float* X;
   int G;
+  int mask_goal = 1;  // 0: group 1 unmasked (goal runs: masked at the run start by goal_dz2_reduce_kernel)
   __device__ __forceinline__ int64_t index(int row, int col) const {
     constexpr int per = HYC * WXC;
     const int n = row / per;
@@ -327,7 +362,7 @@ struct EpiMaskParityG {
   }
   __device__ __forceinline__ float pre(int row, int col) const { return X[index(row, col)]; }
   __device__ __forceinline__ void post(int row, int col, float v, float x, int) const {
-    out[index(row, col)] = x > 0.0f ? v : 0.0f;
+    out[index(row, col)] = (x > 0.0f || (!mask_goal && col >= CIN)) ? v : 0.0f;
   }
 };
 
@@ -1277,7 +1312,7 @@ using Conv2Wg = WgSpec<IH, IW, OH, OW, 32, 1, (OH % 4 == 0 && OH > 9 ? 4 : OH), 
 
 template <int COUT, int CIN, int H, int W, int OH, int OW, int PY, int PX>
 inline void dgrad_class_groups(const float* dz, const float* WT, float* out, const float* X, int nimg, int G,
-                               hipStream_t st) {
+                               hipStream_t st, int mask_goal = 1) {
   // only the covered pixels: at 84x84 the 5x5 / 5x4 classes of conv3's 9x9 input shrink to
   // 4x4 (64 of 81 rows per image; the uncovered 17 are zeroed by dgrad_all_classes_groups)
   constexpr int CH = k4s2_covered<H, OH>(), CW = k4s2_covered<W, OW>();
@@ -1286,7 +1321,7 @@ inline void dgrad_class_groups(const float* dz, const float* WT, float* out, con
   DgradA<COUT, 4, 2, OH, OW, HYC, WXC> fa{dz, M};
   static_assert(CIN == 32, "conv3: two groups of 32 channels (W^T rows of 64)");
   DgradB<COUT, 4, 2, 2 * CIN> fb{WT, G * CIN, 0, PY, PX};
-  EpiMaskParityG<H, W, 2, PY, PX, HYC, WXC, CIN> ep{out, X, G};
+  EpiMaskParityG<H, W, 2, PY, PX, HYC, WXC, CIN> ep{out, X, G, mask_goal};
   launch_gemm_x6<128, 64, 32, 2, 2>(fa, fb, ep, M, G * CIN, 4 * COUT, st);
 }
 
@@ -1305,11 +1340,10 @@ inline int dgrad_all_classes_groups(const float* dz, const float* WT, float* out
       if (rc != VN_OK) return rc;
     }
   } else {
-    if (!mask_goal) return fail(VN_EINVAL, "goal runs need the parity-class dgrad kernel");
-    dgrad_class_groups<COUT, CIN, H, W, OH, OW, 0, 0>(dz, WT, out, X, nimg, G, st);
-    dgrad_class_groups<COUT, CIN, H, W, OH, OW, 0, 1>(dz, WT, out, X, nimg, G, st);
-    dgrad_class_groups<COUT, CIN, H, W, OH, OW, 1, 0>(dz, WT, out, X, nimg, G, st);
-    dgrad_class_groups<COUT, CIN, H, W, OH, OW, 1, 1>(dz, WT, out, X, nimg, G, st);
+    dgrad_class_groups<COUT, CIN, H, W, OH, OW, 0, 0>(dz, WT, out, X, nimg, G, st, mask_goal);
+    dgrad_class_groups<COUT, CIN, H, W, OH, OW, 0, 1>(dz, WT, out, X, nimg, G, st, mask_goal);
+    dgrad_class_groups<COUT, CIN, H, W, OH, OW, 1, 0>(dz, WT, out, X, nimg, G, st, mask_goal);
+    dgrad_class_groups<COUT, CIN, H, W, OH, OW, 1, 1>(dz, WT, out, X, nimg, G, st, mask_goal);
   }
   if constexpr (CH < H || CW < W) {
     const int64_t total = (int64_t)nimg * G * (H * W - CH * CW) * (CIN / 4);
@@ -1362,11 +1396,11 @@ inline Acts acts_at(const PolicyLayout& L, float* base, int64_t cap, int64_t off
 // take a frame list: the u8 conv1 x3 kernels, the x6 / ring conv2 forward, the conv2 x6
 // input gradient and weight gradient, conv3's parity-class input gradient (84x84, 174x174).
 template <int H0, int W0>
-constexpr bool kGoalRunsGeo = (H0 == 84 && W0 == 84) || (H0 == 174 && W0 == 174);
+constexpr bool kGoalRunsGeo = (H0 == 84 && W0 == 84) || (H0 == 174 && W0 == 174) || (H0 == 300 && W0 == 400);
 
 inline bool goal_runs_ok(const PolicyLayout& L, int n) {
   if (L.arch != 0 || n <= kSkinnyRows) return false;
-  if (!((L.H == 84 && L.W == 84) || (L.H == 174 && L.W == 174))) return false;
+  if (!((L.H == 84 && L.W == 84) || (L.H == 174 && L.W == 174) || (L.H == 300 && L.W == 400))) return false;
   // the A/B overrides select kernels without frame lists (read per call)
   for (const char* v : {"VN_WGRAD_GENERIC", "VN_DGRAD_GENERIC", "VN_CONV2F_GENERIC", "VN_CONV2F_RING1"})
     if (getenv(v)) return false;
@@ -1456,7 +1490,12 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
         done = true;
       }
     }
-    if (!done) {
+    if (!done && gr) {  // goal runs: the listed frames only (tiles past the device count return)
+      FrameListIm2col<G::OH1, G::OW1, G::OH2, G::OW2> fa{a.X[0], 2 * n * G::OH2 * G::OW2, fl};
+      DenseRows fb{P + L.l[1].w, 512, 32};
+      EpiBiasActFrames<G::OH2, G::OW2> ep{a.X[1], P + L.l[1].b, fl};
+      launch_gemm_x6<128, 32, 32, 4, 1>(fa, fb, ep, fa.M, 32, 512, st);
+    } else if (!done) {
       NhwcIm2col<32, 4, 4, 2, G::OH1, G::OW1, G::OH2, G::OW2, 1> fa{a.X[0], 2 * n * G::OH2 * G::OW2};
       DenseRows fb{P + L.l[1].w, 512, 32};
       EpiBiasAct ep{a.X[1], 32, P + L.l[1].b, 1};
@@ -1619,6 +1658,13 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
                                                 FrameList{}, gr ? gr->goal_delta : nullptr);
         if (rc != VN_OK) return rc;
       }
+    } else if (gr) {  // goal runs: the goal half of a sample's X2 at its run start
+      if constexpr (kGoalRunsGeo<H0, W0>) {
+        using ImG = NhwcIm2colGoal<32, 4, 4, 2, G::OH2, G::OW2, G::OH3, G::OW3>;
+        Im2colT<ImG> fbg{ImG{a.X[1], n9, gr->goal_delta}, 1024};
+        launch_wgrad6<64, 128, 2, 2>(w.dz3, 64, 64, fbg, 1024, n9, w.slab, w.slab_cap, Gr + L.l[2].w, Gr + L.l[2].b,
+                                     st);
+      }
     } else {
       launch_wgrad6<64, 128, 2, 2>(w.dz3, 64, 64, fbw, 1024, n9, w.slab, w.slab_cap, Gr + L.l[2].w, Gr + L.l[2].b, st);
     }
@@ -1649,7 +1695,7 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
       VN_HIP(ensure_dyn_lds((const void*)conv2_wgrad_kernel<G::OH1, G::OW1, G::OH2, G::OW2>, lds));  // > 64 KiB dynamic LDS: opt-in
       float* bias_slab = w.slab + (int64_t)blocks * 32 * 512;
       hipLaunchKernelGGL((conv2_wgrad_kernel<G::OH1, G::OW1, G::OH2, G::OW2>), dim3(blocks), dim3(256), lds, st,
-                         a.X[0], w.dz2, frames, w.slab, bias_slab);
+                         a.X[0], w.dz2, frames, w.slab, bias_slab, fl);
       // two-stage fixed-order reduce of the per-workgroup slabs (one pass over 512 slabs per
       // element ran 118 us, latency-bound)
       constexpr int kParts = 32;
@@ -1696,7 +1742,20 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
                            w.dz2, T(1), a.X[0], a.M1, a.X[0], frames);
       }
     } else {
-      dgrad_all_classes<32, 32, G::OH1, G::OW1, G::OH2, G::OW2>(w.dz2, T(1), a.X[0], a.X[0], 2 * n, 0, 1, 32, st);
+      // odd conv1 maps (300x400: 74x99): the banded x6 kernel over the u8 conv1 bitmask; the
+      // four class products for float frames or under VN_DGRAD_GENERIC (A/B, parity tests)
+      const bool bits = conv1_x3_fits<H0, W0>() && !(src.f32[0] || src.f32[1]) && !getenv("VN_DGRAD_GENERIC");
+      if (bits) {
+        constexpr int BY = conv2_dgrad_band_rows<G::OW1, G::OW2>();
+        using Bd = Conv2DgBand<G::OH1, G::OW1, G::OH2, G::OW2, BY>;
+        const void* kfn = (const void*)conv2_dgrad_band_x6_kernel<G::OH1, G::OW1, G::OH2, G::OW2, BY>;
+        VN_HIP(ensure_dyn_lds(kfn, Bd::LDS));
+        const int blocks = std::min(frames * Bd::NB, resident_blocks(kfn, 256, Bd::LDS));
+        hipLaunchKernelGGL((conv2_dgrad_band_x6_kernel<G::OH1, G::OW1, G::OH2, G::OW2, BY>), dim3(blocks), dim3(256),
+                           Bd::LDS, st, w.dz2, T(1), a.M1, a.X[0], frames, fl);
+      } else {
+        dgrad_all_classes<32, 32, G::OH1, G::OW1, G::OH2, G::OW2>(w.dz2, T(1), a.X[0], a.X[0], 2 * n, 0, 1, 32, st);
+      }
     }
   }
   // ---- conv1: wgrad from dz1 (in X1's storage) and the frames

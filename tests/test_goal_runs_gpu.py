@@ -12,6 +12,8 @@ conv1 backward.
   env transitions) and the same update gradients to 1e-5 of scale (LSTM + aux heads, 174x174;
   LSTM, 84x84);
 * configurations without frame-list kernels refuse goal runs instead of ignoring them.
+C5's 300x400 geometry takes goal runs through the banded conv2 input gradient, the f32 conv2
+weight gradient and the row-limited generic conv2 forward product.
 """
 import ctypes
 
@@ -103,7 +105,8 @@ def _rollout_batch(hw, T, E, seed, p_done=0.3):
     return img, gl, dones
 
 
-@pytest.mark.parametrize("hw,T,E", [((84, 84), 4, 64), ((174, 174), 3, 24)], ids=["84x84", "174x174"])
+@pytest.mark.parametrize("hw,T,E", [((84, 84), 4, 64), ((174, 174), 3, 24), ((300, 400), 3, 20)],
+                         ids=["84x84", "174x174", "c5_300x400"])
 def test_dedup_forward_bitwise_and_backward_vs_fp64_oracle(hw, T, E):
     from vnav import _lib
     from vnav.policy import frames_from_batch
@@ -178,7 +181,8 @@ def _trainer_pair(hw, E, aux, T=5, seed=4):
     return out
 
 
-@pytest.mark.parametrize("hw,E,aux", [((174, 174), 32, True), ((84, 84), 96, False)], ids=["174_lstm_aux", "84_lstm"])
+@pytest.mark.parametrize("hw,E,aux", [((174, 174), 32, True), ((84, 84), 96, False), ((300, 400), 24, True)],
+                         ids=["174_lstm_aux", "84_lstm", "c5_lstm_aux"])
 def test_trainer_dedup_equals_full(hw, E, aux):
     a, b = _trainer_pair(hw, E, aux)
     assert a.dedup_goals and not b.dedup_goals
@@ -205,19 +209,26 @@ def test_trainer_dedup_equals_full(hw, E, aux):
 
 
 def test_goal_runs_refused_where_unsupported():
-    """C5 (300x400: generic conv2 products) and a few envs (skinny paths) have no frame-list
-    kernels: goal runs are an error there, never a silent fallback."""
+    """A few envs (the skinny paths), BigHouseModel (no goal branch) and the A/B overrides
+    that select kernels without frame lists take no goal runs: an error, never a silent
+    fallback."""
+    import os
     from vnav import _lib
     from vnav.policy import PolicyNet, frames_from_batch
-    net = PolicyNet((300, 400), 4)
-    assert not net.goal_runs_supported(512)
-    n = 32
-    img = torch.zeros((n, 300, 400, 3), dtype=torch.uint8, device="cuda")
+    net = PolicyNet((84, 84), 4)
+    assert not net.goal_runs_supported(16) and net.goal_runs_supported(17)
+    n = 16
+    img = torch.zeros((n, 84, 84, 3), dtype=torch.uint8, device="cuda")
     z = torch.zeros(n, dtype=torch.int32, device="cuda")
     gr = _lib.GoalRuns()
     gr.goal_list, gr.goal_count, gr.goal_delta = z.data_ptr(), z.data_ptr(), z.data_ptr()
     with pytest.raises(_lib.VnavError, match="goal runs"):
         net.forward(net.init_params(0), frames_from_batch(img, img), n, net.new_acts(n), n, 0,
                     torch.zeros((n, 8), device="cuda"), goals=gr)
-    small = PolicyNet((84, 84), 4)
-    assert not small.goal_runs_supported(16) and small.goal_runs_supported(17)
+    assert not PolicyNet((84, 84), 4, recurrent=True, arch="bighouse").goal_runs_supported(512)
+    os.environ["VN_WGRAD_GENERIC"] = "1"
+    try:
+        assert not net.goal_runs_supported(512)
+    finally:
+        os.environ.pop("VN_WGRAD_GENERIC")
+    assert PolicyNet((300, 400), 4).goal_runs_supported(512)

@@ -206,3 +206,32 @@ def test_conv34_small_matches_generic_products(hw, N):
         if e > 1e-5:
             bad[k] = "%.3g" % e
     assert not bad, bad
+
+
+@pytest.mark.parametrize("N", [3, 300])
+def test_conv2_band_dgrad_matches_class_products(N):
+    """300x400 (74x99 conv1 map, odd width): conv2's input gradient on the banded x6 kernel
+    (`conv2_dgrad_band_x6_kernel`: bands of 10 conv1 rows, the last one 4, class widths 50 / 49)
+    against the four parity-class products (VN_DGRAD_GENERIC). It feeds conv1's weight
+    gradient, which must agree to 1e-5 of scale; N = 300 wraps the persistent grid."""
+    from vnav.policy import GoalNavPolicy
+    torch.manual_seed(13)
+    hw = (300, 400)
+    pol = GoalNavPolicy(3, 4, hw)
+    with torch.no_grad():
+        pol.params.add_(torch.randn_like(pol.params) * 0.01)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    img = torch.randint(0, 256, (N, 1) + hw + (3,), dtype=torch.uint8, device="cuda", generator=g)
+    gl = torch.randint(0, 256, (N, 1) + hw + (3,), dtype=torch.uint8, device="cuda", generator=g)
+    cl = torch.randn((N, 1, 4), device="cuda", generator=g)
+    cv = torch.randn((N, 1, 1), device="cuda", generator=g)
+    fast = pol.net.to_reference(_grads(pol, img, gl, cl, cv, generic=None))
+    gen = pol.net.to_reference(_grads(pol, img, gl, cl, cv, generic="VN_DGRAD_GENERIC"))
+    bad = {}
+    for k in gen:
+        b = gen[k].numpy().astype(np.float64)
+        e = np.abs(fast[k].numpy() - b).max() / max(np.abs(b).max(), 1e-30)
+        if e > 1e-5:
+            bad[k] = "%.3g" % e
+    assert not bad, bad
+    assert np.abs(fast["shared_base.0.0.weight"].numpy()).max() > 0

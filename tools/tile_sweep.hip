@@ -209,7 +209,7 @@ int main(int argc, char** argv) {
                         (int)lds);
     float ms = timeit([&] {
       hipLaunchKernelGGL((conv2_wgrad_kernel<20, 20, 9, 9>), dim3(blocks), dim3(256), lds, st, X1, dz2, frames, slab,
-                         slab + (int64_t)blocks * 32 * 512);
+                         slab + (int64_t)blocks * 32 * 512, FrameList{});
     });
     printf("conv2 wgrad specialised   %8.3f ms %7.1f TF\n", ms, f2 * 2 * n / ms / 1e9);
   }
