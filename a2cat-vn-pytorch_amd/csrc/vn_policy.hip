@@ -96,12 +96,21 @@ struct NhwcIm2col {
 
 // conv3's im2col over concat(image, goal) X2 with goal-frame deduplication: group 1 (the goal
 // map) of sample n is read from sample n + gd[n] (the start of its goal run, vn_goal_runs).
+//
+// As the A operand (conv3's forward) a thread's fetch slots keep their rows across the K loop,
+// so the redirected sample of each slot is loaded once, at the first fetch, and kept in
+// registers (a per-element gd load put a dependent load in front of every K tile's gather:
+// +23 % per 174x174 call); as a transposed wgrad operand (rows = pixels, changing every K tile)
+// load4 looks gd up per element.
 template <int C, int KH, int KW, int S, int H, int W, int OH, int OW>
 struct NhwcIm2colGoal {
+  static constexpr int kMaxSlots = 8;
   const float* X;
   int M;  // samples * OH * OW
   const int32_t* gd;
-  __device__ __forceinline__ f4 load4(int m, int k, int kend) const {
+  mutable int gsm[kMaxSlots];  // slot j's goal sample (first fetch)
+  mutable bool ready;
+  __device__ __forceinline__ f4 load_at(int m, int k, int kend, int64_t ngoal) const {
     if (m >= M || k >= kend) return f4zero();
     const int n = m / (OH * OW);
     const int r = m - n * (OH * OW);
@@ -111,10 +120,42 @@ struct NhwcIm2colGoal {
     const int g = t & 1;
     t >>= 1;
     const int ky = t / KW, kx = t % KW;
-    const int64_t ns = (int64_t)n + (g ? gd[n] : 0);
+    const int64_t ns = g ? ngoal : (int64_t)n;
     return *reinterpret_cast<const f4*>(X + (((ns * 2 + g) * H + oy * S + ky) * W + ox * S + kx) * C + c);
   }
-  VN_ROWS_LOADER
+  __device__ __forceinline__ f4 load4(int m, int k, int kend) const {
+    const int n = m < M ? m / (OH * OW) : 0;
+    return load_at(m, k, kend, (int64_t)n + gd[n]);
+  }
+  static constexpr bool kTrans = false;
+  template <int ROWS, int BK>
+  static constexpr int slots() { return ROWS * (BK / 4); }
+  template <int ROWS, int BK>
+  __device__ __forceinline__ void fetch(f4* r, int row0, int k0, int kend, int tid) const {
+    constexpr int Q = BK / 4, T = ROWS * Q, NS = (T + 255) / 256;
+    static_assert(NS <= kMaxSlots, "fetch slots");
+    if (!ready) {
+#pragma unroll
+      for (int j = 0; j < NS; ++j) {
+        const int m = row0 + (tid + j * 256) / Q;
+        const int n = m < M ? m / (OH * OW) : 0;
+        gsm[j] = n + gd[n];
+      }
+      ready = true;
+    }
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+      const int i = tid + j * 256;
+      if (T % 256 == 0 || i < T) {
+        const int rr = i / Q, q = i - (i / Q) * Q;
+        r[j] = load_at(row0 + rr, k0 + 4 * q, kend, gsm[j]);
+      }
+    }
+  }
+  template <int ROWS, int BK, int LD>
+  __device__ __forceinline__ static void commit(const f4* r, float* s, int tid) {
+    commit_rows<ROWS, BK, LD>(r, s, tid);
+  }
 };
 
 // conv2's im2col (one 32-channel input, k4 s2) over the frames of a FrameList (goal-frame
