@@ -27,6 +27,7 @@
 #include "vn_gemm.h"
 #include "vn_lstm.h"
 #include "vn_aux.h"
+#include "vn_unreal.h"
 #include "vn_skinny.h"
 
 #include "vn_frames.h"
@@ -524,6 +525,10 @@ struct PolicyLayout {
   // W2 [48][4][4][8] (block diagonal), b2 [8]; maps X4 [h3][w3] -> A1 [AH][AW] -> P [PH][PW]
   int aux, AH, AW, PH, PW;
   int64_t aw1, ab1, aw2, ab2;
+  // UNREAL heads (goal.py:94-133, vn_unreal.h): pc_base W [2592][512] (rows (y, x, c)), b [2592];
+  // pc W1 [32][4][4][64], b1 [64]; pc W2 [64][4][4][8] (block diagonal), b2 [8]; rp W [3][3 FCIN], b [4]
+  int unreal;
+  int64_t upw, upb, uw1, ub1, uw2, ub2, urw, urb;
   // split-K scratch on the policy's device (vn_policy_create_ex): slabs of the products whose
   // tiles alone cannot fill the chip (small batches), see launch_gemm_x6_sk
   float* sk;
@@ -531,7 +536,7 @@ struct PolicyLayout {
   int sk_dev;
 };
 
-inline PolicyLayout make_layout(int H, int W, int A, int lstm = 0, int aux = 0, int arch = 0) {
+inline PolicyLayout make_layout(int H, int W, int A, int lstm = 0, int aux = 0, int arch = 0, int unreal = 0) {
   PolicyLayout L{};
   L.arch = arch;
   L.H = H;
@@ -596,6 +601,26 @@ inline PolicyLayout make_layout(int H, int W, int A, int lstm = 0, int aux = 0, 
     off += (int64_t)kAuxC1 * 16 * kAuxC2;
     L.ab2 = off;
     off += kAuxC2;
+  }
+  L.unreal = unreal;
+  if (unreal) {
+    off = (off + 3) / 4 * 4;  // float4 rows for the products
+    L.upw = off;
+    off += (int64_t)kPcBase * 512;
+    L.upb = off;
+    off += kPcBase;
+    L.uw1 = off;
+    off += 32ll * 16 * kPcC1;
+    L.ub1 = off;
+    off += kPcC1;
+    L.uw2 = off;
+    off += (int64_t)kPcC1 * 16 * kPcC2;
+    L.ub2 = off;
+    off += kPcC2;
+    L.urw = off;
+    off += 3ll * 3 * L.FCIN;
+    L.urb = off;
+    off += 4;
   }
   L.n_params = off;
   L.wt_total = wt;
@@ -2043,7 +2068,7 @@ inline LstmWork lstm_carve(const PolicyLayout& L, float* ws, int64_t T, int64_t 
 inline int lstm_backward(const PolicyLayout& L, const float* P, int T, int E, const float* dout, const float* h_all,
                          const float* xcat_all, const float* acts_all, const float* c_all, const float* c_init,
                          const float* mask_all, const float* x5_all, float* dz5, float* Gr, const LstmWork& w,
-                         hipStream_t st) {
+                         hipStream_t st, const float* dh_extra = nullptr, int extra_envs = 0) {
   const int A1 = L.A + 1;
   const int N = T * E;
   const int64_t e512 = (int64_t)E * 512;
@@ -2061,6 +2086,11 @@ inline int lstm_backward(const PolicyLayout& L, const float* P, int T, int E, co
     Im2colT<DenseRows> fbw{DenseRows{h_all, 512, N}, 512};
     launch_wgrad<32, 64, 2, 2>(dout, OUT_LD, A1, fbw, 512, N, w.slab, slab_floats(L), Gr + L.l[5].w, Gr + L.l[5].b,
                                st);
+  }
+  if (dh_extra) {  // the output gradient of other heads on the first extra_envs envs (pixel control)
+    const int64_t total = (int64_t)T * extra_envs * 128;
+    hipLaunchKernelGGL(add_env_rows_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, dh_extra, T, E,
+                       extra_envs, 512, w.dh_heads);
   }
   const unsigned cb = (unsigned)((e512 + 255) / 256);
   if (E <= kSkinnyRows) {
@@ -2325,6 +2355,135 @@ int aux_backward_impl(const PolicyLayout& L, const float* P, const float* X4, in
   return VN_OK;
 }
 
+
+// ---- UNREAL heads (vn_unreal.h) -------------------------------------------------------
+struct PcWork {
+  float* w1t;     // [16*64][32]
+  float* w2t;     // [16*8][64]
+  float* wpct;    // [512][2592]
+  float* slab;
+  float* colsum;  // [kColsumBlocks][64]
+};
+
+inline int64_t pc_workspace_floats(const PolicyLayout& L) {
+  return 1024ll * 32 + 128ll * 64 + 512ll * kPcBase + slab_floats(L) + (int64_t)kColsumBlocks * 64 + 64;
+}
+
+inline PcWork pc_carve(const PolicyLayout& L, float* ws) {
+  PcWork w;
+  float* p = ws;
+  w.w1t = p;
+  p += 1024ll * 32;
+  w.w2t = p;
+  p += 128ll * 64;
+  w.wpct = p;
+  p += 512ll * kPcBase;
+  w.slab = p;
+  p += slab_floats(L);
+  w.colsum = p;
+  return w;
+}
+
+// pixel_control (goal.py:131-137) on feature rows h [n][512]: pc_base (x6 product, bias,
+// ReLU), the two first deconvs as one 32 -> 64 deconv, the two second deconvs as one
+// block-diagonal 64 -> 8 deconv (ReLU on both), then the value/action combination.
+int pc_forward_impl(const PolicyLayout& L, const float* P, const float* h, int n, float* pcb, float* A1, float* P2,
+                    float* q, const PcWork& w, hipStream_t st) {
+  {
+    DenseRows fa{h, 512, n};
+    DenseRows fb{P + L.upw, 512, kPcBase};
+    EpiBiasAct ep{pcb, kPcBase, P + L.upb, 1};
+    launch_gemm_x6_sk<64, 64, 32, 2, 2>(fa, fb, ep, n, kPcBase, 512, st, L);
+  }
+  {
+    TransposeSet ts;
+    ts.add(P + L.uw1, 32, 16 * kPcC1, w.w1t);
+    ts.add(P + L.uw2, kPcC1, 16 * kPcC2, w.w2t);
+    launch_transpose_set(ts, st);
+  }
+  if (const int rc = deconv_all<32, kPcC1, kPcMap, kPcMap, kPcA1, kPcA1>(pcb, w.w1t, A1, P + L.ub1, 1, n, st); rc != VN_OK)
+    return rc;
+  if (const int rc = deconv_all<kPcC1, kPcC2, kPcA1, kPcA1, kPcP, kPcP>(A1, w.w2t, P2, P + L.ub2, 1, n, st); rc != VN_OK)
+    return rc;
+  const int64_t npix = (int64_t)n * kPcP * kPcP;
+  hipLaunchKernelGGL(pc_combine_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, st, P2, npix, L.A, q);
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
+
+// Gradients of the pixel-control parameters and dh [n][512] (stored, or added when
+// accumulate) from dq [n][42][42][A]. Consumes P2 (-> dP2), A1 (-> dA1) and pcb (-> dpcb).
+int pc_backward_impl(const PolicyLayout& L, const float* P, const float* h, int n, float* pcb, float* A1, float* P2,
+                     const float* dq, float* Gr, float* dh, int accumulate, const PcWork& w, hipStream_t st) {
+  const int64_t npix = (int64_t)n * kPcP * kPcP;
+  hipLaunchKernelGGL(pc_dq_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, st, P2, dq, npix, L.A);
+  // second layer: dW2 = A1^T x im2col(dP2) (block-diagonal mask), db2, dA1 masked in place, db1
+  const int P1 = n * kPcA1 * kPcA1;
+  using Im2 = NhwcIm2col<kPcC2, 4, 4, 2, kPcP, kPcP, kPcA1, kPcA1, 1>;  // dP2 windows per A1 pixel
+  launch_wgrad6<64, 128, 2, 2>(A1, kPcC1, kPcC1, Im2colT<Im2>{Im2{P2, P1}, 16 * kPcC2}, 16 * kPcC2, P1, w.slab,
+                               slab_floats(L), Gr + L.uw2, nullptr, st);
+  hipLaunchKernelGGL(pc_blockdiag_mask_kernel, dim3((kPcC1 * 16 * kPcC2 + 255) / 256), dim3(256), 0, st, Gr + L.uw2,
+                     L.A);
+  colsum(P2, npix, kPcC2, w.colsum, Gr + L.ub2, st);
+  {
+    DenseRows fb{P + L.uw2, 16 * kPcC2, kPcC1};
+    EpiMask ep{A1, A1, kPcC1};
+    launch_gemm_x6<64, 64, 32, 2, 2>(Im2{P2, P1}, fb, ep, P1, kPcC1, 16 * kPcC2, st);
+  }
+  colsum(A1, (int64_t)P1, kPcC1, w.colsum, Gr + L.ub1, st);
+  // first layer: dW1[ci][tap][co] = sum pcb[iy][ix][ci] dA1[2iy + ky][2ix + kx][co]; dpcb =
+  // conv(dA1, W1) under pc_base's ReLU, over pcb
+  const int P0 = n * kPcMap * kPcMap;
+  using Im1 = NhwcIm2col<kPcC1, 4, 4, 2, kPcA1, kPcA1, kPcMap, kPcMap, 1>;  // dA1 windows per pcb pixel
+  launch_wgrad6<32, 128, 1, 4>(pcb, 32, 32, Im2colT<Im1>{Im1{A1, P0}, 16 * kPcC1}, 16 * kPcC1, P0, w.slab,
+                               slab_floats(L), Gr + L.uw1, nullptr, st);
+  {
+    DenseRows fb{P + L.uw1, 16 * kPcC1, 32};
+    EpiMask ep{pcb, pcb, 32};
+    launch_gemm_x6<128, 32, 32, 4, 1>(Im1{A1, P0}, fb, ep, P0, 32, 16 * kPcC1, st);
+  }
+  // pc_base: dW = dpcb^T x h (+ bias column), dh = dpcb x W
+  {
+    Im2colT<DenseRows> fbw{DenseRows{h, 512, n}, 512};
+    launch_wgrad6<128, 128, 2, 2>(pcb, kPcBase, kPcBase, fbw, 512, n, w.slab, slab_floats(L), Gr + L.upw, Gr + L.upb,
+                                  st);
+  }
+  tile_transpose(P + L.upw, kPcBase, 512, 512, w.wpct, kPcBase, st);
+  {
+    DenseRows fa{pcb, kPcBase, n};
+    DenseRows fb{w.wpct, kPcBase, 512};
+    EpiAcc ep{dh, 512, accumulate};
+    launch_gemm_x6_sk<64, 64, 32, 2, 2>(fa, fb, ep, n, 512, kPcBase, st, L);
+  }
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
+
+// reward_prediction (goal.py:121-129): logits [n][4] (3 + pad) of x [n][3 FCIN] (three
+// frames' conv_base maps, NHWC each; the rows of W are permuted to match).
+int rp_forward_impl(const PolicyLayout& L, const float* P, const float* x, int n, float* out, hipStream_t st) {
+  const int K = 3 * L.FCIN;
+  DenseRows fa{x, K, n};
+  DenseRows fb{P + L.urw, K, 3};
+  EpiBiasAct ep{out, 4, P + L.urb, 0};
+  launch_gemm_sk<64, 16, 32, 4, 1>(fa, fb, ep, n, 3, K, st, L);
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
+
+int rp_backward_impl(const PolicyLayout& L, const float* P, const float* x, int n, const float* dout, float* Gr,
+                     float* dx, float* slab, hipStream_t st) {
+  const int K = 3 * L.FCIN;
+  Im2colT<DenseRows> fbw{DenseRows{x, K, n}, K};
+  launch_wgrad<32, 64, 2, 2>(dout, 4, 3, fbw, K, n, slab, slab_floats(L), Gr + L.urw, Gr + L.urb, st);
+  if (dx) {
+    const int64_t total = (int64_t)n * (K / 4);
+    hipLaunchKernelGGL(rp_dx_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, dout, P + L.urw, n, K, dx);
+  }
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
+
 }  // namespace vn
 
 using namespace vn;
@@ -2373,8 +2532,10 @@ int vn_policy_create(int frame_h, int frame_w, int num_actions, vn_policy** out)
 
 int vn_policy_create_ex(int frame_h, int frame_w, int num_actions, int flags, vn_policy** out) {
   if (!out) return fail(VN_EINVAL, "vn_policy_create: out is NULL");
-  if (flags & ~(VN_POLICY_LSTM | VN_POLICY_AUX | VN_POLICY_BIGHOUSE))
+  if (flags & ~(VN_POLICY_LSTM | VN_POLICY_AUX | VN_POLICY_BIGHOUSE | VN_POLICY_UNREAL))
     return fail(VN_EINVAL, "vn_policy_create: unknown flags");
+  if ((flags & VN_POLICY_BIGHOUSE) && (flags & VN_POLICY_UNREAL))
+    return fail(VN_EINVAL, "vn_policy_create: the UNREAL heads are BigGoalHouseModel's (goal.py:94-133)");
   if ((flags & VN_POLICY_BIGHOUSE) && (frame_h != 84 || frame_w != 84 || (flags & VN_POLICY_AUX)))
     return fail(VN_EINVAL, "vn_policy_create: BigHouseModel takes 84x84 frames (Linear(7*7*32)) and no aux heads");
   *out = nullptr;
@@ -2384,7 +2545,7 @@ int vn_policy_create_ex(int frame_h, int frame_w, int num_actions, int flags, vn
   vn_policy* p = new (std::nothrow) vn_policy();
   if (!p) return fail(VN_ENOMEM, "vn_policy_create: host allocation");
   p->L = make_layout(frame_h, frame_w, num_actions, (flags & VN_POLICY_LSTM) ? 1 : 0, (flags & VN_POLICY_AUX) ? 1 : 0,
-                     (flags & VN_POLICY_BIGHOUSE) ? 1 : 0);
+                     (flags & VN_POLICY_BIGHOUSE) ? 1 : 0, (flags & VN_POLICY_UNREAL) ? 1 : 0);
   // split-K scratch on the current device (16 MB; without it small batches run unsplit)
   p->L.sk = nullptr;
   p->L.sk_cap = 0;
@@ -2519,6 +2680,48 @@ int vn_policy_backward_trunk(vn_policy* p, const float* params, const vn_frames*
                                stream);
 }
 
+int vn_policy_unreal_info(vn_policy* p, int64_t* info8) {
+  if (!p || !info8) return fail(VN_EINVAL, "vn_policy_unreal_info: bad args");
+  if (!p->L.unreal) return fail(VN_EINVAL, "vn_policy_unreal_info: policy has no UNREAL heads");
+  const PolicyLayout& L = p->L;
+  const int64_t v[8] = {L.upw, L.upb, L.uw1, L.ub1, L.uw2, L.ub2, L.urw, L.urb};
+  for (int i = 0; i < 8; ++i) info8[i] = v[i];
+  return VN_OK;
+}
+
+int vn_pc_workspace_floats(vn_policy* p, int64_t* floats) {
+  if (!p || !floats || !p->L.unreal) return fail(VN_EINVAL, "vn_pc_workspace_floats: bad args");
+  *floats = pc_workspace_floats(p->L);
+  return VN_OK;
+}
+
+int vn_pc_forward(vn_policy* p, const float* params, const float* h, int n, float* pcb, float* a1, float* p2, float* q,
+                  float* workspace, vn_stream_t stream) {
+  if (!p || !p->L.unreal || !params || !h || !pcb || !a1 || !p2 || !q || !workspace || n <= 0)
+    return fail(VN_EINVAL, "vn_pc_forward: bad args");
+  return pc_forward_impl(p->L, params, h, n, pcb, a1, p2, q, pc_carve(p->L, workspace), (hipStream_t)stream);
+}
+
+int vn_pc_backward(vn_policy* p, const float* params, const float* h, int n, float* pcb, float* a1, float* p2,
+                   const float* dq, float* grads, float* dh, int accumulate, float* workspace, vn_stream_t stream) {
+  if (!p || !p->L.unreal || !params || !h || !pcb || !a1 || !p2 || !dq || !grads || !dh || !workspace || n <= 0)
+    return fail(VN_EINVAL, "vn_pc_backward: bad args");
+  return pc_backward_impl(p->L, params, h, n, pcb, a1, p2, dq, grads, dh, accumulate, pc_carve(p->L, workspace),
+                          (hipStream_t)stream);
+}
+
+int vn_rp_forward(vn_policy* p, const float* params, const float* x, int n, float* out, vn_stream_t stream) {
+  if (!p || !p->L.unreal || !params || !x || !out || n <= 0) return fail(VN_EINVAL, "vn_rp_forward: bad args");
+  return rp_forward_impl(p->L, params, x, n, out, (hipStream_t)stream);
+}
+
+int vn_rp_backward(vn_policy* p, const float* params, const float* x, int n, const float* dout, float* grads,
+                   float* dx, float* workspace, vn_stream_t stream) {
+  if (!p || !p->L.unreal || !params || !x || !dout || !grads || !workspace || n <= 0)
+    return fail(VN_EINVAL, "vn_rp_backward: bad args");
+  return rp_backward_impl(p->L, params, x, n, dout, grads, dx, pc_carve(p->L, workspace).slab, (hipStream_t)stream);
+}
+
 int vn_policy_aux_info(vn_policy* p, int64_t* info8) {
   if (!p || !info8) return fail(VN_EINVAL, "vn_policy_aux_info: bad args");
   if (!p->L.aux) return fail(VN_EINVAL, "vn_policy_aux_info: policy has no aux heads");
@@ -2643,6 +2846,21 @@ int vn_lstm_backward(vn_policy* p, const float* params, int T, int E, const floa
   const LstmWork w = lstm_carve(p->L, workspace, T, E);
   return lstm_backward(p->L, params, T, E, dout, h_all, xcat_all, acts_all, c_all, c_init, mask_all, x5_all, dz5_all,
                        grads, w, (hipStream_t)stream);
+}
+
+int vn_lstm_backward_ex(vn_policy* p, const float* params, int T, int E, const float* dout, const float* h_all,
+                        const float* xcat_all, const float* acts_all, const float* c_all, const float* c_init,
+                        const float* mask_all, const float* x5_all, const float* dh_extra, int extra_envs,
+                        float* dz5_all, float* grads, float* workspace, vn_stream_t stream) {
+  if (dh_extra && (extra_envs <= 0 || extra_envs > E))
+    return fail(VN_EINVAL, "vn_lstm_backward_ex: extra_envs must be 1..E with dh_extra");
+  if (!p || !p->L.lstm || !params || T <= 0 || E <= 0 || !dout || !h_all || !xcat_all || !acts_all || !c_all ||
+      !x5_all || !dz5_all || !grads || !workspace)
+    return fail(VN_EINVAL, "vn_lstm_backward_ex: bad args");
+  if ((int64_t)T * E > (int64_t)1 << 30) return fail(VN_EINVAL, "vn_lstm_backward_ex: T*E too large");
+  const LstmWork w = lstm_carve(p->L, workspace, T, E);
+  return lstm_backward(p->L, params, T, E, dout, h_all, xcat_all, acts_all, c_all, c_init, mask_all, x5_all, dz5_all,
+                       grads, w, (hipStream_t)stream, dh_extra, dh_extra ? extra_envs : 0);
 }
 
 }  // extern "C"

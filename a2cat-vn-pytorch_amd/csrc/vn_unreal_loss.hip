@@ -1,0 +1,226 @@
+// vn_unreal_loss.hip — the UNREAL auxiliary losses of the trainer on gfx950: pixel control
+// (n-step Q-learning on pixel-change pseudo-rewards), reward prediction (3-class
+// cross-entropy on three consecutive frames) and value replay, with the weights of
+// experiments/thor_cached_auxiliary.py:39-41 (rp 1.0, pc 0.05, vr 1.0).
+//
+// The loss formulas live in deep_rl's UnrealTrainer (deep-rl==0.2.9, absent from the image):
+// parity unpinned. The restatement follows the published UNREAL algorithm (Jaderberg et al.
+// 2016) as deep_rl's call sites use it: the pseudo-reward of step t is the mean over each
+// 4x4 cell (pc_cell_size, goal.py:72) and the 3 channels of |obs_{t+1} - obs_t| on the
+// centre crop of 42 x 4 pixels of the image observation (_get_input_for_pixel_control,
+// thor_cached_auxiliary.py:47-48; obs scaled to [0,1] by ScaledFloatFrame), Q targets
+// R_T = max_a Q(s_T), R_t = r_t + gamma_pc (1 - done_t) R_{t+1}, loss mean (Q(s_t, a_t) - R_t)^2;
+// reward prediction classes (r = 0, r > 0, r < 0) of the reward after frame t from frames
+// t-2, t-1, t of one episode; value replay mean (V - R)^2 against the n-step returns. The
+// oracle is oracle/unreal.py.
+#include <hip/hip_runtime.h>
+
+#include "vn_common.h"
+
+namespace vn {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+constexpr int kPcCells = 42;  // the pixel-control map (goal.py:103-112)
+constexpr int kPcCellPx = 4;
+
+// Mean |f1 - f0| / 255 over cell (cy, cx)'s 4 x 4 pixels and 3 channels (u8 HWC frames).
+__device__ __forceinline__ float pc_cell_change(const uint8_t* __restrict__ f0, const uint8_t* __restrict__ f1, int W,
+                                                int top, int left, int cy, int cx) {
+  int s = 0;
+#pragma unroll
+  for (int dy = 0; dy < kPcCellPx; ++dy) {
+    const int64_t o = ((int64_t)(top + cy * kPcCellPx + dy) * W + left + cx * kPcCellPx) * 3;
+#pragma unroll
+    for (int j = 0; j < 3 * kPcCellPx; ++j) s += abs((int)f1[o + j] - (int)f0[o + j]);
+  }
+  return (float)s * (1.0f / (255.0f * 3 * kPcCellPx * kPcCellPx));
+}
+
+template <int NT>
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) red[wave] = v;
+  __syncthreads();
+  float t = 0.0f;
+#pragma unroll
+  for (int w = 0; w < NT / 64; ++w) t += red[w];
+  __syncthreads();
+  return t;
+}
+
+// One thread per (env e < S, cell): the Q targets backwards over the rollout and dq of
+// rows t*S + e (row T*S + e, the bootstrap, gets 0: its max is a detached target).
+__global__ __launch_bounds__(256) void unreal_pc_loss_kernel(const float* __restrict__ q, const int32_t* __restrict__ actions,
+                                                             const uint8_t* __restrict__ dones,
+                                                             const uint8_t* __restrict__ arena, int64_t frame_bytes,
+                                                             int H, int W, const int32_t* __restrict__ rows_img,
+                                                             const int32_t* __restrict__ rows_last, int T, int E, int S,
+                                                             int A, float gamma, float coef, float* __restrict__ dq,
+                                                             float* __restrict__ stats) {
+  __shared__ float red[4];
+  constexpr int PP = kPcCells * kPcCells;
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  float sq = 0.0f;
+  if (idx < S * PP) {
+    const int e = idx / PP, pix = idx - e * PP, cy = pix / kPcCells, cx = pix - cy * kPcCells;
+    const int top = (H - kPcCells * kPcCellPx) / 2, left = (W - kPcCells * kPcCellPx) / 2;
+    const int64_t ob = ((int64_t)(T * S + e) * PP + pix) * A;
+    float R = q[ob];
+    for (int a = 1; a < A; ++a) R = fmaxf(R, q[ob + a]);
+    for (int a = 0; a < A; ++a) dq[ob + a] = 0.0f;
+    const uint8_t* fn = arena + (int64_t)rows_last[e] * frame_bytes;
+    for (int t = T - 1; t >= 0; --t) {
+      const int64_t r = (int64_t)t * E + e;
+      const uint8_t* f = arena + (int64_t)rows_img[r] * frame_bytes;
+      const float rew = pc_cell_change(f, fn, W, top, left, cy, cx);
+      R = rew + (dones[r] ? 0.0f : gamma * R);
+      const int act = actions[r];
+      const int64_t o = ((int64_t)(t * S + e) * PP + pix) * A;
+      const float d = q[o + act] - R;
+      sq += d * d;
+      for (int a = 0; a < A; ++a) dq[o + a] = a == act ? 2.0f * coef * d : 0.0f;
+      fn = f;
+    }
+  }
+  const float t = block_sum<256>(sq, red);
+  if (threadIdx.x == 0 && t != 0.0f) atomicAdd(stats, t);
+}
+
+// Reward prediction, one workgroup: sample j = (ts - 2) S + e (frames ts-2, ts-1, ts of env
+// e, 2 <= ts < T) is used when no episode ends at ts-2 or ts-1; dlogits of the mean
+// cross-entropy over the used samples, times the weight; stats[0] = the mean CE, stats[1] =
+// the sample count.
+constexpr int kRpThreads = 1024;
+__global__ __launch_bounds__(kRpThreads) void unreal_rp_loss_kernel(const float* __restrict__ logits,
+                                                                    const float* __restrict__ rewards,
+                                                                    const uint8_t* __restrict__ dones, int T, int E, int S,
+                                                                    float weight, float* __restrict__ dlogits,
+                                                                    float* __restrict__ stats) {
+  __shared__ float red[kRpThreads / 64];
+  const int n = (T - 2) * S;
+  float cnt = 0.0f;
+  for (int j = threadIdx.x; j < n; j += kRpThreads) {
+    const int ts = 2 + j / S, e = j % S;
+    cnt += (dones[(int64_t)(ts - 2) * E + e] || dones[(int64_t)(ts - 1) * E + e]) ? 0.0f : 1.0f;
+  }
+  const float count = block_sum<kRpThreads>(cnt, red);
+  const float inv = count > 0.0f ? 1.0f / count : 0.0f;
+  float ce = 0.0f;
+  for (int j = threadIdx.x; j < n; j += kRpThreads) {
+    const int ts = 2 + j / S, e = j % S;
+    const bool used = !(dones[(int64_t)(ts - 2) * E + e] || dones[(int64_t)(ts - 1) * E + e]);
+    const float r = rewards[(int64_t)ts * E + e];
+    const int cls = r == 0.0f ? 0 : (r > 0.0f ? 1 : 2);
+    const float* l = logits + (int64_t)j * 4;
+    const float m = fmaxf(l[0], fmaxf(l[1], l[2]));
+    const float ex[3] = {expf(l[0] - m), expf(l[1] - m), expf(l[2] - m)};
+    const float z = ex[0] + ex[1] + ex[2];
+    float* g = dlogits + (int64_t)j * 4;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) g[c] = used ? (ex[c] / z - (c == cls ? 1.0f : 0.0f)) * weight * inv : 0.0f;
+    g[3] = 0.0f;
+    if (used) ce += logf(z) + m - l[cls];
+  }
+  const float total = block_sum<kRpThreads>(ce, red);
+  if (threadIdx.x == 0) {
+    stats[0] = total * inv;
+    stats[1] = count;
+  }
+}
+
+// dX4 rows t*E + e (e < S) from the rp input gradient dx [(T-2) S][3][F]: frame t is slot
+// 2 - k of sample ts = t + k (k = 0..2, 2 <= ts < T), summed in that order.
+__global__ __launch_bounds__(256) void unreal_rp_scatter_kernel(const float* __restrict__ dx, int T, int E, int S, int F,
+                                                                float* __restrict__ dx4, int accumulate) {
+  const int F4 = F / 4;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)T * S * F4) return;
+  const int q4 = (int)(i % F4);
+  const int te = (int)(i / F4), t = te / S, e = te - (te / S) * S;
+  f4 v = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const int ts = t + k;
+    if (ts < 2 || ts >= T) continue;
+    v += reinterpret_cast<const f4*>(dx + (((int64_t)(ts - 2) * S + e) * 3 + (2 - k)) * F)[q4];
+  }
+  f4* d = reinterpret_cast<f4*>(dx4 + ((int64_t)t * E + e) * F) + q4;
+  *d = accumulate ? *d + v : v;
+}
+
+// Value replay on rows t*E + e (e < S): dout[.][A] += coef (V - R), stats += (V - R)^2.
+__global__ __launch_bounds__(256) void unreal_vr_kernel(const float* __restrict__ out, const float* __restrict__ returns,
+                                                        int T, int E, int S, int A, float coef,
+                                                        float* __restrict__ dout, float* __restrict__ stats) {
+  __shared__ float red[4];
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  float sq = 0.0f;
+  if (i < T * S) {
+    const int t = i / S, e = i - t * S;
+    const int64_t r = (int64_t)t * E + e;
+    const float d = out[r * 8 + A] - returns[r];
+    dout[r * 8 + A] += coef * d;
+    sq = d * d;
+  }
+  const float t = block_sum<256>(sq, red);
+  if (threadIdx.x == 0 && t != 0.0f) atomicAdd(stats, t);
+}
+
+}  // namespace vn
+
+using namespace vn;
+
+extern "C" {
+
+int vn_unreal_pc_loss_grad(const float* q, const int32_t* actions, const uint8_t* dones, const uint8_t* arena,
+                           int64_t frame_bytes, int height, int width, const int32_t* rows_img,
+                           const int32_t* rows_last, int T, int E, int S, int num_actions, float gamma, float weight,
+                           float* dq, float* stats, vn_stream_t stream) {
+  if (!q || !actions || !dones || !arena || !rows_img || !rows_last || !dq || !stats || T <= 0 || S <= 0 || S > E ||
+      num_actions < 1 || num_actions > 7 || height < kPcCells * kPcCellPx || width < kPcCells * kPcCellPx ||
+      frame_bytes < (int64_t)height * width * 3)
+    return fail(VN_EINVAL, "vn_unreal_pc_loss_grad: bad args");
+  const int n = S * kPcCells * kPcCells;
+  const float coef = weight / ((float)T * n);
+  hipLaunchKernelGGL(unreal_pc_loss_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, q, actions, dones,
+                     arena, frame_bytes, height, width, rows_img, rows_last, T, E, S, num_actions, gamma, coef, dq,
+                     stats);
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
+
+int vn_unreal_rp_loss_grad(const float* logits, const float* rewards, const uint8_t* dones, int T, int E, int S,
+                           float weight, float* dlogits, float* stats2, vn_stream_t stream) {
+  if (!logits || !rewards || !dones || !dlogits || !stats2 || T < 3 || S <= 0 || S > E)
+    return fail(VN_EINVAL, "vn_unreal_rp_loss_grad: bad args (needs T >= 3)");
+  hipLaunchKernelGGL(unreal_rp_loss_kernel, dim3(1), dim3(kRpThreads), 0, (hipStream_t)stream, logits, rewards, dones,
+                     T, E, S, weight, dlogits, stats2);
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
+
+int vn_unreal_rp_scatter(const float* dx, int T, int E, int S, int fcin, float* dx4, int accumulate,
+                         vn_stream_t stream) {
+  if (!dx || !dx4 || T < 3 || S <= 0 || S > E || fcin <= 0 || fcin % 4)
+    return fail(VN_EINVAL, "vn_unreal_rp_scatter: bad args");
+  const int64_t total = (int64_t)T * S * (fcin / 4);
+  hipLaunchKernelGGL(unreal_rp_scatter_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     dx, T, E, S, fcin, dx4, accumulate);
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
+
+int vn_unreal_vr_grad(const float* out, const float* returns, int T, int E, int S, int num_actions, float weight,
+                      float* dout, float* stats, vn_stream_t stream) {
+  if (!out || !returns || !dout || !stats || T <= 0 || S <= 0 || S > E || num_actions < 1 || num_actions > 7)
+    return fail(VN_EINVAL, "vn_unreal_vr_grad: bad args");
+  const float coef = 2.0f * weight / ((float)T * S);
+  hipLaunchKernelGGL(unreal_vr_kernel, dim3((T * S + 255) / 256), dim3(256), 0, (hipStream_t)stream, out, returns, T, E,
+                     S, num_actions, coef, dout, stats);
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
+
+}  // extern "C"

@@ -136,6 +136,22 @@ SIGNATURES.update({
                                          c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
     "vn_aux_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p,
                                 c_void_p, c_void_p, c_void_p]),
+    "vn_policy_unreal_info": (c_int, [c_void_p, P(c_int64)]),
+    "vn_pc_workspace_floats": (c_int, [c_void_p, P(c_int64)]),
+    "vn_pc_forward": (c_int, [c_void_p] * 3 + [c_int] + [c_void_p] * 6),
+    "vn_pc_backward": (c_int, [c_void_p] * 3 + [c_int] + [c_void_p] * 6 + [c_int, c_void_p, c_void_p]),
+    "vn_rp_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "vn_rp_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                               c_void_p]),
+    "vn_lstm_backward_ex": (c_int, [c_void_p, c_void_p, c_int, c_int] + [c_void_p] * 9 + [c_int] + [c_void_p] * 4),
+    "vn_unreal_pc_loss_grad": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p,
+                                       c_void_p, c_int, c_int, c_int, c_int, c_float, c_float, c_void_p, c_void_p,
+                                       c_void_p]),
+    "vn_unreal_rp_loss_grad": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p,
+                                       c_void_p, c_void_p]),
+    "vn_unreal_rp_scatter": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
+    "vn_unreal_vr_grad": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_void_p, c_void_p,
+                                  c_void_p]),
     "vn_policy_backward_ex": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int64, c_void_p, c_void_p,
                                       c_void_p, c_void_p, c_void_p, c_void_p]),
     "vn_policy_sample": (c_int, [c_void_p, c_int, c_int, c_uint64, c_uint64,

@@ -30,6 +30,17 @@ depth / segmentation / goal-segmentation heads against avg-pooled targets gather
 the env's aux arena by row. The reference computes it on a sequence sampled from
 UnrealTrainer's replay buffer (deep_rl, absent); here it uses the on-policy rollout batch
 (documented deviation, parity unpinned at the trainer level).
+
+With ``unreal=True`` (BigGoalHouseModel's pixel-control and reward-prediction heads,
+models/goal.py:94-137; UnrealTrainer's losses with the weights pc 0.05, rp 1.0, vr 1.0 of
+experiments/thor_cached_auxiliary.py:39-41) each update also runs, on the rollout sequences
+of the first ``unreal_envs`` envs: pixel control (n-step Q-learning on the pixel change of
+the image frames, gamma_pc 0.9, on the LSTM features, bootstrap from the last observation),
+reward prediction (the sign class of the reward after three consecutive frames of one
+episode, from their conv_base maps) and value replay (the critic against the n-step
+returns). deep_rl draws these sequences from its replay buffer (absent): here they are the
+on-policy sequences, and the loss formulas are the published algorithm's (parity unpinned,
+csrc/vn_unreal_loss.hip, oracle/unreal.py).
 """
 import ctypes
 import time
@@ -52,7 +63,8 @@ class A2CTrainer:
                  max_time_steps=2e6, rms_alpha=0.99, rms_epsilon=1e-5, max_gradient_norm=0.5,
                  value_coefficient=0.5, entropy_coefficient=0.01, seed=0, process_group=None, recurrent=False,
                  aux_weight=0.0, arch="goal", cuda_graph=False, aux_source="rollout", replay_size=8,
-                 capture_collectives=False, allreduce_buckets=2, time_collectives=False, dedup_goals=True):
+                 capture_collectives=False, allreduce_buckets=2, time_collectives=False, dedup_goals=True,
+                 unreal=False, pc_weight=0.05, rp_weight=1.0, vr_weight=1.0, pc_gamma=0.9, unreal_envs=16):
         self.env = env
         self.lib = _lib.load()
         self.device = env.device
@@ -76,7 +88,8 @@ class A2CTrainer:
         self._head_work = None
         self.aux_weight = float(aux_weight)
         self.net = net if net is not None else PolicyNet(env.frame_shape[:2], env.num_actions, self.device,
-                                                         recurrent=recurrent, aux=self.aux_weight > 0, arch=arch)
+                                                         recurrent=recurrent, aux=self.aux_weight > 0, arch=arch,
+                                                         unreal=unreal)
         self.recurrent = self.net.recurrent
         if self.aux_weight > 0 and (not self.net.aux or getattr(env, "aux_arena", None) is None):
             raise ValueError("aux_weight > 0 needs an aux policy (aux=True) and scenes with depth + segmentation")
@@ -174,6 +187,7 @@ class A2CTrainer:
                                                   self.aux_rows[1].data_ptr())
         # compute_auxiliary_loss overridden by a subclass: called every update (autograd on a
         # GoalNavPolicy view of the flat parameters), its gradient added before the all-reduce
+        self._setup_unreal(unreal, pc_weight, rp_weight, vr_weight, pc_gamma, unreal_envs)
         self._custom_aux = type(self).compute_auxiliary_loss is not A2CTrainer.compute_auxiliary_loss
         if self._custom_aux and cuda_graph:
             raise ValueError("a compute_auxiliary_loss override runs torch autograd per update: use cuda_graph=False")
@@ -233,6 +247,86 @@ class A2CTrainer:
         self._graph = None
         self._graph_out = None
         self._graph_gen = None
+
+    def _setup_unreal(self, unreal, pc_weight, rp_weight, vr_weight, pc_gamma, unreal_envs):
+        """Buffers of the UNREAL losses: the first S envs' T + 1 LSTM features (the last row
+        the bootstrap's) through the pixel-control heads, their T - 2 three-frame conv_base
+        samples through reward prediction."""
+        self.unreal = bool(unreal)
+        if not self.unreal:
+            return
+        net, E, T = self.net, self.env.num_envs, self.num_steps
+        if not (net.unreal and net.recurrent and net.arch == "goal"):
+            raise ValueError("unreal=True needs a recurrent BigGoalHouseModel policy with the UNREAL heads")
+        H, W = self.env.frame_shape[:2]
+        if H < 168 or W < 168:
+            raise ValueError("pixel control crops 42 cells of 4 px (goal.py:72, 112): frames need >= 168 px")
+        if T < 3:
+            raise ValueError("reward prediction needs num_steps >= 3")
+        self.pc_weight, self.rp_weight, self.vr_weight = float(pc_weight), float(rp_weight), float(vr_weight)
+        self.pc_gamma = float(pc_gamma)
+        S = self.unreal_S = max(1, min(int(unreal_envs), E))
+        kw = dict(dtype=torch.float32, device=self.device)
+        n_pc = (T + 1) * S
+        self.h_pc = torch.zeros((n_pc, 512), **kw)
+        self.pcb, self.pc_a1, self.pc_p2, self.pc_q = net.pc_buffers(n_pc)
+        self.pc_dq = torch.zeros_like(self.pc_q)
+        self.dh_pc = torch.zeros((n_pc, 512), **kw)
+        self.pc_ws = torch.empty(net.pc_workspace_floats(), **kw)
+        F = net.fc_in
+        n_rp = (T - 2) * S
+        self.rp_x = torch.zeros((n_rp, 3 * F), **kw)
+        self.rp_dx = torch.zeros((n_rp, 3 * F), **kw)
+        self.rp_out = torch.zeros((n_rp, 4), **kw)
+        self.rp_dout = torch.zeros((n_rp, 4), **kw)
+        # rp's gradient w.r.t. conv_base's map: into the aux heads' dX4 when those run on the
+        # rollout, else into its own buffer (rows of envs >= S stay zero)
+        self.rp_into_aux = self.aux_weight > 0 and self.aux_source == "rollout"
+        self.unreal_dx4 = None if self.rp_into_aux else torch.zeros((T * E, F), **kw)
+        self.unreal_stats = torch.zeros(4, **kw)  # pc sum sq, rp mean CE, rp samples, vr sum sq
+        self._unreal_norm = torch.tensor([1.0 / (T * S * 42 * 42), 1.0, 1.0 / (T * S)], **kw)
+
+    def _unreal_forward_losses(self):
+        """UNREAL losses of this rollout: vr into dout, pc and rp head gradients into grads;
+        returns (dh_extra [T, S, 512], dX4 target). Runs after vn_a2c_loss_grad."""
+        lib, net = self.lib, self.net
+        E, T, A, S = self.env.num_envs, self.num_steps, self.A, self.unreal_S
+        N = T * E
+        P, st = _lib.ptr, self._stream()
+        self.unreal_stats.zero_()
+        if self.vr_weight > 0:
+            _lib.check(lib.vn_unreal_vr_grad(P(self.out), P(self.returns), T, E, S, A, ctypes.c_float(self.vr_weight),
+                                             P(self.dout), P(self.unreal_stats[3:]), st), "vn_unreal_vr_grad")
+        # pixel control on h of the first S envs (+ the bootstrap's)
+        self.h_pc[:T * S].view(T, S, 512).copy_(self.h_all.view(T, E, 512)[:, :S])
+        self.h_pc[T * S:].copy_(self.boot_h[:S])
+        n_pc = (T + 1) * S
+        net.pc_forward(self.params, self.h_pc, n_pc, self.pcb, self.pc_a1, self.pc_p2, self.pc_q, self.pc_ws)
+        H, W = self.env.frame_shape[:2]
+        info = self.env._info
+        _lib.check(lib.vn_unreal_pc_loss_grad(P(self.pc_q), P(self.actions), P(self.dones), ctypes.c_void_p(self._arena),
+                                              ctypes.c_int64(self._fb), H, W, P(self.rows_img), P(info["img_row"]),
+                                              T, E, S, A, ctypes.c_float(self.pc_gamma),
+                                              ctypes.c_float(self.pc_weight), P(self.pc_dq), P(self.unreal_stats),
+                                              st), "vn_unreal_pc_loss_grad")
+        net.pc_backward(self.params, self.h_pc, n_pc, self.pcb, self.pc_a1, self.pc_p2, self.pc_dq, self.grads,
+                        self.dh_pc, self.pc_ws)
+        # reward prediction on three consecutive conv_base maps of the first S envs
+        F = net.fc_in
+        x4 = net.x4(self.acts, N).view(T, E, F)
+        xv = self.rp_x.view(T - 2, S, 3, F)
+        for k in range(3):
+            xv[:, :, k].copy_(x4[k:k + T - 2, :S])
+        n_rp = (T - 2) * S
+        net.rp_forward(self.params, self.rp_x, n_rp, self.rp_out)
+        _lib.check(lib.vn_unreal_rp_loss_grad(P(self.rp_out), P(self.rewards), P(self.dones), T, E, S,
+                                              ctypes.c_float(self.rp_weight), P(self.rp_dout),
+                                              P(self.unreal_stats[1:3]), st), "vn_unreal_rp_loss_grad")
+        net.rp_backward(self.params, self.rp_x, n_rp, self.rp_dout, self.grads, self.rp_dx, self.pc_ws)
+        dx4 = self.dx4 if self.rp_into_aux else self.unreal_dx4
+        _lib.check(lib.vn_unreal_rp_scatter(P(self.rp_dx), T, E, S, F, P(dx4), int(self.rp_into_aux), st),
+                   "vn_unreal_rp_scatter")
+        return self.dh_pc[:T * S], dx4
 
     # deep_rl hook names (experiments/thor_cached_auxiliary.py:50-56)
     def create_env(self, kwargs):
@@ -408,6 +502,7 @@ class A2CTrainer:
                                         ctypes.c_float(self.entropy_coefficient), _lib.ptr(self.dout),
                                         _lib.ptr(self.stats), st), "vn_a2c_loss_grad")
         dx4 = None
+        unreal_dh = None
         if self.aux_weight > 0 and aux_batch is not None:
             # replayed sequence: its own trunk forward, the heads' loss and backward, and the
             # trunk backward of dL/dX4 alone into aux_grads (added after the main backward)
@@ -425,6 +520,8 @@ class A2CTrainer:
                                       self.aux_weight, self.dpred, self.aux_stats, self.aux_ws)
             net.aux_backward(self.params, self.acts, N, N, self.a1, self.dpred, self.grads, self.dx4, self.aux_ws)
             dx4 = self.dx4
+        if self.unreal:  # after the aux heads: reward prediction adds to their dX4
+            unreal_dh, dx4 = self._unreal_forward_losses()
         frames = self._frames(self.rows_img, self.rows_goal)
         goals = None
         if self.dedup_goals:  # the rollout's goal runs: starts ascending, run lengths
@@ -434,7 +531,8 @@ class A2CTrainer:
             goals = self._goal_runs_update
         if self.recurrent:
             net.lstm_backward(self.params, T, E, self.dout, self.h_all, self.xcat, self.lstm_acts, self.c_all, self.c0,
-                              self.masks, net.x5(self.acts, N), self.dz5, self.grads, self.lstm_ws)
+                              self.masks, net.x5(self.acts, N), self.dz5, self.grads, self.lstm_ws,
+                              dh_extra=unreal_dh, extra_envs=self.unreal_S if self.unreal else 0)
             # the heads + LSTM (+ aux heads) gradients are final here: their all-reduce runs on
             # RCCL's stream while the trunk backward runs on this one
             self._allreduce_head_bucket()
@@ -537,7 +635,12 @@ class A2CTrainer:
                                            _lib.ptr(self.scalars), _lib.ptr(self.aux_stats) if aux else None,
                                            _lib.ptr(self._aux_numel) if aux else None, _lib.ptr(self.episode_stats),
                                            _lib.ptr(m), self._stream()), "vn_a2c_metrics")
+        if self.unreal:  # + [pc loss, rp loss, vr loss] (means: averaged over ranks too)
+            u = torch.stack((self.unreal_stats[0], self.unreal_stats[1], self.unreal_stats[3])) * self._unreal_norm
+            m = torch.cat((m, u))
         vdist.reduce_metrics_(m, 6, self.group)
+        if self.unreal and self.world > 1:
+            m[9:] /= self.world
         return m
 
     def _graph_update(self):
@@ -571,16 +674,22 @@ class A2CTrainer:
             # a graph replay writes the same static tensor every update: hand out a copy
             return {"raw": m.clone() if self.cuda_graph else m}
         vals = m.tolist()
-        vl, al, ent, ret_mean, gnorm, aux_loss, eps, rsum, lsum = vals
+        vl, al, ent, ret_mean, gnorm, aux_loss, eps, rsum, lsum = vals[:9]
+        unreal = {}
+        if self.unreal:
+            unreal = {"pc_loss": vals[9], "rp_loss": vals[10], "vr_loss": vals[11]}
         dt = time.perf_counter() - t0
         return {
             "step": self.total_steps, "updates": self.num_updates,
             "value_loss": vl, "action_loss": al, "entropy": ent,
-            "loss": self.value_coefficient * vl + al - self.entropy_coefficient * ent,
+            "loss": self.value_coefficient * vl + al - self.entropy_coefficient * ent + (
+                self.pc_weight * unreal["pc_loss"] + self.rp_weight * unreal["rp_loss"] +
+                self.vr_weight * unreal["vr_loss"] if unreal else 0.0),
             "episodes": eps, "reward": rsum / eps if eps else float("nan"),
             "episode_length": lsum / eps if eps else float("nan"),
             "grad_norm": gnorm, "return_mean": ret_mean, "fps": N * self.world / dt,
             **({"aux_loss": aux_loss} if self.aux_weight > 0 else {}),
+            **unreal,
         }
 
     def run(self, log_every=10, logger=print):

@@ -23,6 +23,8 @@ from . import _lib
 
 LAYERS = ("conv1", "conv2", "conv3", "conv4", "fc", "head")
 OUT_LD = 8
+PC_MAP, PC_A1, PC_P = 9, 20, 42  # pixel-control maps (goal.py:96-112)
+PC_BASE = 32 * PC_MAP * PC_MAP
 
 
 
@@ -71,22 +73,25 @@ AUX_HEADS = (("deconv_depth", 1, 0), ("deconv_mask", 3, 1), ("deconv_mask_goal",
 class PolicyNet:
     """Handle on a vn_policy: flat parameter layout, forward/backward launches."""
 
-    def __init__(self, frame_hw=(84, 84), num_actions=4, device=None, recurrent=False, aux=False, arch="goal"):
+    def __init__(self, frame_hw=(84, 84), num_actions=4, device=None, recurrent=False, aux=False, arch="goal",
+                 unreal=False):
         """arch "goal": BigGoalHouseModel (models/goal.py); "bighouse": BigHouseModel
-        (models/bignet.py, image only, 84x84)."""
+        (models/bignet.py, image only, 84x84). unreal: BigGoalHouseModel's pixel-control and
+        reward-prediction heads (goal.py:94-133, VN_POLICY_UNREAL)."""
         self.lib = _lib.load()
         if arch not in ("goal", "bighouse"):
             raise ValueError("arch must be 'goal' or 'bighouse'")
         self.arch = arch
         self.recurrent = bool(recurrent)
         self.aux = bool(aux)
+        self.unreal = bool(unreal)
         self.frame_hw = tuple(frame_hw)
         self.num_actions = int(num_actions)
         self.device = torch.device("cuda", torch.cuda.current_device() if device is None else
                                    torch.device(device).index or 0)
         h = ctypes.c_void_p()
         # VN_POLICY_LSTM | VN_POLICY_AUX | VN_POLICY_BIGHOUSE
-        flags = (1 if recurrent else 0) | (2 if aux else 0) | (4 if arch == "bighouse" else 0)
+        flags = (1 if recurrent else 0) | (2 if aux else 0) | (4 if arch == "bighouse" else 0) | (8 if unreal else 0)
         with torch.cuda.device(self.device):  # the policy's split-K scratch lives on its device
             _lib.check(self.lib.vn_policy_create_ex(frame_hw[0], frame_hw[1], num_actions, flags, ctypes.byref(h)),
                        "vn_policy_create_ex")
@@ -121,6 +126,11 @@ class PolicyNet:
             _lib.check(self.lib.vn_policy_aux_info(h, info), "vn_policy_aux_info")
             self.aux_layout = dict(w1=info[0], b1=info[1], w2=info[2], b2=info[3], a_hw=(info[4], info[5]),
                                    p_hw=(info[6], info[7]))
+        self.unreal_layout = None
+        if self.unreal:
+            info = (ctypes.c_int64 * 8)()
+            _lib.check(self.lib.vn_policy_unreal_info(h, info), "vn_policy_unreal_info")
+            self.unreal_layout = dict(zip(("pc_w", "pc_b", "w1", "b1", "w2", "b2", "rp_w", "rp_b"), info[:8]))
 
     def check_frames(self, image, goal):
         """Dense frame batches are read by the kernels through raw pointers at this net's
@@ -160,6 +170,14 @@ class PolicyNet:
             X = self.aux_layout
             out["aux"] = (flat[X["w1"]:X["w1"] + 32 * 16 * 48].view(32, 4, 4, 48), flat[X["b1"]:X["b1"] + 48],
                           flat[X["w2"]:X["w2"] + 48 * 16 * 8].view(48, 4, 4, 8), flat[X["b2"]:X["b2"] + 8])
+        if self.unreal_layout:
+            U = self.unreal_layout
+            k = 3 * self.fc_in
+            out["unreal"] = dict(
+                pc_w=flat[U["pc_w"]:U["pc_w"] + PC_BASE * 512].view(PC_BASE, 512), pc_b=flat[U["pc_b"]:U["pc_b"] + PC_BASE],
+                w1=flat[U["w1"]:U["w1"] + 32 * 16 * 64].view(32, 4, 4, 64), b1=flat[U["b1"]:U["b1"] + 64],
+                w2=flat[U["w2"]:U["w2"] + 64 * 16 * 8].view(64, 4, 4, 8), b2=flat[U["b2"]:U["b2"] + 8],
+                rp_w=flat[U["rp_w"]:U["rp_w"] + 3 * k].view(3, k), rp_b=flat[U["rp_b"]:U["rp_b"] + 4])
         return out
 
     def new_params(self):
@@ -192,6 +210,15 @@ class PolicyNet:
                 d1, d2 = 1.0 / math.sqrt(16 * 16), 1.0 / math.sqrt(c * 16)
                 w1[:, :, :, 16 * hd:16 * hd + 16].uniform_(-d1, d1, generator=g)
                 w2[16 * hd:16 * hd + 16, :, :, o:o + c].uniform_(-d2, d2, generator=g)
+        if self.unreal_layout:  # goal.py:26-30 on pc_base, the four ConvTranspose2d and rp
+            u, A = v["unreal"], self.num_actions
+            d = 1.0 / math.sqrt(512)
+            u["pc_w"].uniform_(-d, d, generator=g)
+            u["w1"].uniform_(-d, d, generator=g)  # fan_in = 32 out channels x 16
+            u["w2"][:32, :, :, :A].uniform_(-1.0 / math.sqrt(16 * A), 1.0 / math.sqrt(16 * A), generator=g)
+            u["w2"][32:, :, :, A].uniform_(-0.25, 0.25, generator=g)
+            d = 1.0 / math.sqrt(u["rp_w"].shape[1])
+            u["rp_w"].uniform_(-d, d, generator=g)
         return flat.to(self.device)
 
     def from_reference(self, sd):
@@ -242,6 +269,23 @@ class PolicyNet:
                 b1[16 * hd:16 * hd + 16] = t(sd["%s.0.1.bias" % name])
                 w2[16 * hd:16 * hd + 16, :, :, o:o + c] = t(sd["%s.0.3.weight" % name]).permute(0, 2, 3, 1)
                 b2[o:o + c] = t(sd["%s.0.3.bias" % name])
+        if self.unreal_layout:
+            u, A, m = v["unreal"], self.num_actions, PC_MAP
+            u["pc_w"][:] = t(pick("pc_base", 0, "weight")).view(32, m, m, 512).permute(1, 2, 0, 3).reshape(PC_BASE, 512)
+            u["pc_b"][:] = t(pick("pc_base", 0, "bias")).view(32, m, m).permute(1, 2, 0).reshape(-1)
+            u["w1"][:, :, :, :32] = t(pick("pc_value", 0, "weight")).permute(0, 2, 3, 1)
+            u["w1"][:, :, :, 32:] = t(pick("pc_action", 0, "weight")).permute(0, 2, 3, 1)
+            u["b1"][:32] = t(pick("pc_value", 0, "bias"))
+            u["b1"][32:] = t(pick("pc_action", 0, "bias"))
+            u["w2"][:32, :, :, :A] = t(pick("pc_value", 1, "weight")).permute(0, 2, 3, 1)
+            u["w2"][32:, :, :, A:A + 1] = t(pick("pc_action", 1, "weight")).permute(0, 2, 3, 1)
+            u["b2"][:A] = t(pick("pc_value", 1, "bias"))
+            u["b2"][A] = t(pick("pc_action", 1, "bias")).view(())
+            rw = t(pick("rp", 0, "weight"))
+            if rw.shape[1] != u["rp_w"].shape[1]:
+                raise ValueError("rp weight takes %d inputs, this frame size gives %d" % (rw.shape[1], u["rp_w"].shape[1]))
+            u["rp_w"][:] = rw.view(3, 3, 32, o3[0], o3[1]).permute(0, 1, 3, 4, 2).reshape(3, -1)
+            u["rp_b"][:3] = t(pick("rp", 0, "bias"))
         return flat.to(self.device)
 
     def to_reference(self, flat):
@@ -290,6 +334,20 @@ class PolicyNet:
                 out["%s.0.1.bias" % name] = b1[16 * hd:16 * hd + 16].clone()
                 out["%s.0.3.weight" % name] = w2[16 * hd:16 * hd + 16, :, :, o:o + c].permute(0, 3, 1, 2).contiguous()
                 out["%s.0.3.bias" % name] = b2[o:o + c].clone()
+        if self.unreal_layout:
+            u, m = v["unreal"], PC_MAP
+            out["pc_base.0.0.weight"] = u["pc_w"].view(m, m, 32, 512).permute(2, 0, 1, 3).reshape(PC_BASE, 512).clone()
+            out["pc_base.0.0.bias"] = u["pc_b"].view(m, m, 32).permute(2, 0, 1).reshape(-1).clone()
+            out["pc_value.0.0.weight"] = u["w1"][:, :, :, :32].permute(0, 3, 1, 2).contiguous()
+            out["pc_value.0.0.bias"] = u["b1"][:32].clone()
+            out["pc_action.0.0.weight"] = u["w1"][:, :, :, 32:].permute(0, 3, 1, 2).contiguous()
+            out["pc_action.0.0.bias"] = u["b1"][32:].clone()
+            out["pc_value.0.2.weight"] = u["w2"][:32, :, :, :A].permute(0, 3, 1, 2).contiguous()
+            out["pc_value.0.2.bias"] = u["b2"][:A].clone()
+            out["pc_action.0.2.weight"] = u["w2"][32:, :, :, A:A + 1].permute(0, 3, 1, 2).contiguous()
+            out["pc_action.0.2.bias"] = u["b2"][A:A + 1].clone()
+            out["rp.1.weight"] = u["rp_w"].view(3, 3, o3[0], o3[1], 32).permute(0, 1, 4, 2, 3).reshape(3, -1).clone()
+            out["rp.1.bias"] = u["rp_b"][:3].clone()
         return out
 
     # -- launches -------------------------------------------------------------------
@@ -390,6 +448,39 @@ class PolicyNet:
                                             P(grads), P(dx4), P(workspace), _lib.stream_ptr(self.device)),
                    "vn_aux_backward")
 
+    # -- UNREAL heads (goal.py:94-133) ------------------------------------------------
+    def pc_workspace_floats(self):
+        f = ctypes.c_int64()
+        _lib.check(self.lib.vn_pc_workspace_floats(self._h, ctypes.byref(f)), "vn_pc_workspace_floats")
+        return f.value
+
+    def pc_buffers(self, n):
+        """pcb [n,9,9,32], a1 [n,20,20,64], p2 [n,42,42,8], q [n,42,42,A]."""
+        kw = dict(dtype=torch.float32, device=self.device)
+        return (torch.empty((n, PC_MAP, PC_MAP, 32), **kw), torch.empty((n, PC_A1, PC_A1, 64), **kw),
+                torch.empty((n, PC_P, PC_P, 8), **kw), torch.empty((n, PC_P, PC_P, self.num_actions), **kw))
+
+    def pc_forward(self, params, h, n, pcb, a1, p2, q, workspace):
+        P = _lib.ptr
+        _lib.check(self.lib.vn_pc_forward(self._h, P(params), P(h), int(n), P(pcb), P(a1), P(p2), P(q), P(workspace),
+                                          _lib.stream_ptr(self.device)), "vn_pc_forward")
+
+    def pc_backward(self, params, h, n, pcb, a1, p2, dq, grads, dh, workspace, accumulate=False):
+        P = _lib.ptr
+        _lib.check(self.lib.vn_pc_backward(self._h, P(params), P(h), int(n), P(pcb), P(a1), P(p2), P(dq), P(grads),
+                                           P(dh), int(bool(accumulate)), P(workspace), _lib.stream_ptr(self.device)),
+                   "vn_pc_backward")
+
+    def rp_forward(self, params, x, n, out):
+        P = _lib.ptr
+        _lib.check(self.lib.vn_rp_forward(self._h, P(params), P(x), int(n), P(out), _lib.stream_ptr(self.device)),
+                   "vn_rp_forward")
+
+    def rp_backward(self, params, x, n, dout, grads, dx, workspace):
+        P = _lib.ptr
+        _lib.check(self.lib.vn_rp_backward(self._h, P(params), P(x), int(n), P(dout), P(grads), P(dx), P(workspace),
+                                           _lib.stream_ptr(self.device)), "vn_rp_backward")
+
     def x4(self, acts, capacity):
         """[capacity, h3*w3*32] view of conv_base's output (X4) in an activation store."""
         c = int(capacity)
@@ -421,12 +512,20 @@ class PolicyNet:
                                             _lib.stream_ptr(self.device)), "vn_policy_heads")
 
     def lstm_backward(self, params, T, E, dout, h_all, xcat_all, acts_all, c_all, c_init, mask_all, x5_all, dz5_all,
-                      grads, workspace):
+                      grads, workspace, dh_extra=None, extra_envs=0):
+        """dh_extra [T, extra_envs, 512]: another head's gradient w.r.t. h of the first
+        extra_envs envs (pixel control), added to the policy heads' (vn_lstm_backward_ex)."""
         P = _lib.ptr
-        _lib.check(self.lib.vn_lstm_backward(self._h, P(params), int(T), int(E), P(dout), P(h_all), P(xcat_all),
-                                             P(acts_all), P(c_all), P(c_init), P(mask_all), P(x5_all), P(dz5_all),
-                                             P(grads), P(workspace), _lib.stream_ptr(self.device)),
-                   "vn_lstm_backward")
+        if dh_extra is None:
+            _lib.check(self.lib.vn_lstm_backward(self._h, P(params), int(T), int(E), P(dout), P(h_all), P(xcat_all),
+                                                 P(acts_all), P(c_all), P(c_init), P(mask_all), P(x5_all), P(dz5_all),
+                                                 P(grads), P(workspace), _lib.stream_ptr(self.device)),
+                       "vn_lstm_backward")
+            return
+        _lib.check(self.lib.vn_lstm_backward_ex(self._h, P(params), int(T), int(E), P(dout), P(h_all), P(xcat_all),
+                                                P(acts_all), P(c_all), P(c_init), P(mask_all), P(x5_all), P(dh_extra),
+                                                int(extra_envs), P(dz5_all), P(grads), P(workspace),
+                                                _lib.stream_ptr(self.device)), "vn_lstm_backward_ex")
 
 
 def _lstm_param(sd, suffix):
@@ -572,17 +671,134 @@ class _AuxDeconvFunction(torch.autograd.Function):
         return grads, None, None, None
 
 
+class _RecurrentFeaturesFunction(torch.autograd.Function):
+    """_forward_base (goal.py:83-92) with the recurrent core: the LSTM outputs h [T*B, 512]
+    (time-major rows) of the trunk + LSTM; the backward takes dL/dh into the LSTM backward
+    (vn_lstm_backward_ex, no policy-head gradient) and the trunk backward."""
+
+    @staticmethod
+    def forward(ctx, params, image, goal, lra, masks, h0, c0, net, T, B):
+        net.check_frames(image, goal)
+        n = T * B
+        dev = params.device
+        acts = net.new_acts(n)
+        frames = frames_from_batch(image, goal)
+        net.forward(params, frames, n, acts, n, 0, None)
+        x5 = net.x5(acts, n)
+        L = net.lstm
+        xcat = torch.empty((n, L["xcat"]), dtype=torch.float32, device=dev)
+        gates = torch.empty((B, 2048), dtype=torch.float32, device=dev)
+        la = torch.empty((n, 2048), dtype=torch.float32, device=dev)
+        c_all = torch.empty((n, 512), dtype=torch.float32, device=dev)
+        h_all = torch.empty((n, 512), dtype=torch.float32, device=dev)
+        hp, cp = h0, c0
+        for t in range(T):
+            sl = slice(t * B, (t + 1) * B)
+            net.lstm_step(params, B, x5[sl], lra[sl], masks[t], hp, cp, xcat[sl], gates, la[sl], c_all[sl], h_all[sl])
+            hp, cp = h_all[sl], c_all[sl]
+        ctx.save_for_backward(params, image, goal, acts, xcat, la, c_all, h_all, c0, masks)
+        ctx.net, ctx.T, ctx.B = net, T, B
+        hT, cT = h_all[(T - 1) * B:].clone(), c_all[(T - 1) * B:].clone()
+        ctx.mark_non_differentiable(hT, cT)
+        return h_all.clone(), hT, cT
+
+    @staticmethod
+    def backward(ctx, dh, _dh, _dc):
+        params, image, goal, acts, xcat, la, c_all, h_all, c0, masks = ctx.saved_tensors
+        net, T, B = ctx.net, ctx.T, ctx.B
+        n = T * B
+        dev = params.device
+        grads = torch.zeros_like(params)
+        dz5 = torch.empty((n, 512), dtype=torch.float32, device=dev)
+        zero_out = torch.zeros((n, OUT_LD), dtype=torch.float32, device=dev)
+        ws = torch.empty(net.lstm_workspace_floats(T, B), dtype=torch.float32, device=dev)
+        net.lstm_backward(params, T, B, zero_out, h_all, xcat, la, c_all, c0, masks, net.x5(acts, n), dz5, grads, ws,
+                          dh_extra=dh.contiguous(), extra_envs=B)
+        del ws
+        ws = torch.empty(net.workspace_floats(n), dtype=torch.float32, device=dev)
+        net.backward_trunk(params, frames_from_batch(image, goal), n, acts, n, dz5, grads, ws)
+        return (grads,) + (None,) * 9
+
+
+class _PixelControlFunction(torch.autograd.Function):
+    """pc_base + pc_value / pc_action + combination (goal.py:133-136) on feature rows h."""
+
+    @staticmethod
+    def forward(ctx, params, h, net):
+        n = h.shape[0]
+        h = h.contiguous()
+        pcb, a1, p2, q = net.pc_buffers(n)
+        ws = torch.empty(net.pc_workspace_floats(), dtype=torch.float32, device=params.device)
+        net.pc_forward(params, h, n, pcb, a1, p2, q, ws)
+        ctx.save_for_backward(params, h, pcb, a1, p2)
+        ctx.net = net
+        return q
+
+    @staticmethod
+    def backward(ctx, dq):
+        params, h, pcb, a1, p2 = ctx.saved_tensors
+        net = ctx.net
+        n = h.shape[0]
+        grads = torch.zeros_like(params)
+        dh = torch.empty_like(h)
+        ws = torch.empty(net.pc_workspace_floats(), dtype=torch.float32, device=params.device)
+        net.pc_backward(params, h, n, pcb.clone(), a1.clone(), p2.clone(), dq.contiguous(), grads, dh, ws)
+        return grads, dh, None
+
+
+class _RewardPredictionFunction(torch.autograd.Function):
+    """reward_prediction (goal.py:121-129): the trunk to conv_base on the 3 frames of each
+    sample (rows b*3 + k), rp on their concatenated maps; gradients reach the parameters."""
+
+    @staticmethod
+    def forward(ctx, params, image, goal, net):
+        net.check_frames(image, goal)
+        n = image.shape[0]
+        R = n // 3
+        dev = params.device
+        acts = net.new_acts(n)
+        frames = frames_from_batch(image, goal)
+        out = None if net.recurrent else torch.empty((n, OUT_LD), dtype=torch.float32, device=dev)
+        net.forward(params, frames, n, acts, n, 0, out)
+        x = net.x4(acts, n).reshape(R, 3 * net.fc_in)
+        logits = torch.empty((R, 4), dtype=torch.float32, device=dev)
+        net.rp_forward(params, x, R, logits)
+        ctx.save_for_backward(params, image, goal, acts)
+        ctx.net = net
+        return logits[:, :3]
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        params, image, goal, acts = ctx.saved_tensors
+        net = ctx.net
+        n = image.shape[0]
+        R = n // 3
+        dev = params.device
+        grads = torch.zeros_like(params)
+        dout = torch.zeros((R, 4), dtype=torch.float32, device=dev)
+        dout[:, :3] = dlogits
+        dx = torch.empty((R, 3 * net.fc_in), dtype=torch.float32, device=dev)
+        ws = torch.empty(net.pc_workspace_floats(), dtype=torch.float32, device=dev)
+        net.rp_backward(params, net.x4(acts, n).reshape(R, -1), R, dout, grads, dx, ws)
+        dz5 = torch.zeros((n, 512), dtype=torch.float32, device=dev)  # heads / LSTM take no gradient here
+        ws = torch.empty(net.workspace_floats(n), dtype=torch.float32, device=dev)
+        net.backward_ex(params, frames_from_batch(image, goal), n, acts, n, None, dz5, dx.view(n, net.fc_in), grads, ws)
+        return grads, None, None, None
+
+
 class GoalNavPolicy(torch.nn.Module):
     """Drop-in for BigGoalHouseModel's trunk + heads (see module docstring)."""
 
     _ARCH = "goal"
 
     def __init__(self, num_inputs=3, num_outputs=4, frame_hw=(84, 84), device=None, seed=0, recurrent=False,
-                 aux=False):
+                 aux=False, unreal=False):
         super().__init__()
         if num_inputs != 3:
             raise ValueError("frames are RGB (num_inputs=3)")
-        self.net = PolicyNet(frame_hw, num_outputs, device, recurrent=recurrent, aux=aux, arch=self._ARCH)
+        self.net = PolicyNet(frame_hw, num_outputs, device, recurrent=recurrent, aux=aux, arch=self._ARCH,
+                             unreal=unreal)
+        self.pc_cell_size = 4  # goal.py:72
         self.deconv_cell_size = 4  # goal.py:70,148
         self.params = torch.nn.Parameter(self.net.init_params(seed))
         self.lstm_layers, self.lstm_hidden_size = 1, 512  # goal.py:61-62 (state shape contract)
@@ -667,6 +883,57 @@ class GoalNavPolicy(torch.nn.Module):
         to forward's and its gradient flows through the same backward."""
         _logits, value, states = self.forward(inputs, masks, states)
         return value, states
+
+    def _time_major_inputs(self, inputs, masks, states):
+        observations, lra = inputs
+        image, goal = observations[0], observations[1]
+        B, T = image.shape[:2]
+        dev = self.params.device
+        A = self.net.num_actions
+
+        def time_major(x, dtype=None):
+            x = x.to(dev).transpose(0, 1)
+            return x.reshape(T * B, *x.shape[2:]).to(dtype or x.dtype).contiguous()
+
+        fdt = None if image.dtype == torch.uint8 else torch.float32
+        img, gl = time_major(image, fdt), time_major(goal, fdt)
+        if lra is None:
+            lra = torch.zeros((B, T, A + 1), dtype=torch.float32, device=dev)
+        lr = time_major(lra, torch.float32)
+        m = torch.ones((B, T), dtype=torch.float32, device=dev) if masks is None else masks
+        m = m.to(dev).reshape(B, T).to(torch.float32).t().contiguous()
+        if states is None:
+            states = self.initial_states(B)
+        h0 = states[0].to(dev, torch.float32).reshape(B, 512).contiguous()
+        c0 = states[1].to(dev, torch.float32).reshape(B, 512).contiguous()
+        return img, gl, lr, m, h0, c0, T, B
+
+    def pixel_control(self, inputs, masks=None, states=None):
+        """BigGoalHouseModel.pixel_control (goal.py:131-137): Q maps [B,T,A,42,42] =
+        pc_value + pc_action - mean(pc_action) over the recurrent features, and the states."""
+        if not (self.net.unreal and self.net.recurrent):
+            raise ValueError("pixel_control needs GoalNavPolicy(recurrent=True, unreal=True)")
+        img, gl, lr, m, h0, c0, T, B = self._time_major_inputs(inputs, masks, states)
+        h, hT, cT = _RecurrentFeaturesFunction.apply(self.params, img, gl, lr, m, h0, c0, self.net, T, B)
+        q = _PixelControlFunction.apply(self.params, h, self.net)  # [T*B, 42, 42, A]
+        q = q.view(T, B, *q.shape[1:]).permute(1, 0, 4, 2, 3)
+        return q, (hT.view(B, 1, 512), cT.view(B, 1, 512))
+
+    def reward_prediction(self, inputs):
+        """BigGoalHouseModel.reward_prediction (goal.py:121-129): logits [B,3] from the
+        conv_base maps of the B samples' 3 frames (observations [B,3,...])."""
+        if not self.net.unreal:
+            raise ValueError("reward_prediction needs GoalNavPolicy(unreal=True)")
+        observations = inputs[0] if isinstance(inputs, tuple) and len(inputs) == 2 and \
+            isinstance(inputs[0], (tuple, list)) else inputs
+        image, goal = observations[0], observations[1]
+        if image.shape[1] != 3:
+            raise ValueError("reward_prediction takes 3 frames per sample ([B,3,...])")
+        dev = self.params.device
+        fdt = None if image.dtype == torch.uint8 else torch.float32
+        img = image.to(dev).reshape(-1, *image.shape[2:]).to(fdt or image.dtype).contiguous()
+        gl = goal.to(dev).reshape(-1, *goal.shape[2:]).to(fdt or goal.dtype).contiguous()
+        return _RewardPredictionFunction.apply(self.params, img, gl, self.net)
 
     def forward_deconv(self, inputs, masks=None, states=None):
         """AuxiliaryBigGoalHouseModel.forward_deconv (goal.py:177-189): (depth [B,T,1,h,w],

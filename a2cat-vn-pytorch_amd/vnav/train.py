@@ -104,6 +104,12 @@ class Experiment:
     cuda_graph = False
     capture_collectives = False  # cuda_graph at world > 1 (captured RCCL): explicit opt-in only
     aux_source = "rollout"
+    # UnrealTrainer's pixel-control / reward-prediction / value-replay losses (deep_rl, absent:
+    # parity unpinned) on the UNREAL heads of BigGoalHouseModel (goal.py:94-137)
+    unreal = False
+    rp_weight = 1.0
+    pc_weight = 0.05
+    vr_weight = 1.0
 
     def __init__(self, env_kwargs=None, model_kwargs=None, save_dir=None, seed=0, device=None, logger=print,
                  **overrides):
@@ -134,6 +140,11 @@ class Experiment:
                           value_coefficient=self.value_coefficient, entropy_coefficient=self.entropy_coefficient,
                           seed=self.seed, recurrent=self.recurrent,
                           aux_weight=self.auxiliary_weight, aux_source=self.aux_source,
+                          # the 42x42 pixel-control map crops 168 px (goal.py:72, 112): smaller
+                          # stand-in frames train without the UNREAL losses
+                          unreal=self.unreal and min(self.env.frame_shape[:2]) >= 168,
+                          pc_weight=self.pc_weight, rp_weight=self.rp_weight,
+                          vr_weight=self.vr_weight,
                           # world > 1: only on explicit opt-in (the captured RCCL path is unvalidated)
                           cuda_graph=self.cuda_graph and (self.world == 1 or self.capture_collectives),
                           capture_collectives=self.capture_collectives)
@@ -343,8 +354,8 @@ class ThorCachedAuxiliary(Experiment):
     fixed goal (10, 14, 0), 4 envs, hardness 0.01, LSTM policy + deconv heads with
     auxiliary_weight 0.1 (:42), frames 174x174 (screen_size is not forwarded).
     env_kwargs: scene (a ThorGridWorld pickle path) or grid / frame / goal of the synthetic
-    stand-in. The UNREAL replay losses (rp / pc / vr weights, :39-41) are deep_rl's and not
-    part of this path."""
+    stand-in. The UNREAL losses run with the weights of :39-41 (rp 1.0, pc 0.05, vr 1.0) on
+    the on-policy sequences (deep_rl samples them from its replay buffer, absent)."""
 
     num_processes = 4
     auxiliary_weight = 0.1
@@ -361,6 +372,7 @@ class ThorCachedAuxiliary(Experiment):
     # is a stored rollout drawn from the last replay_size rollouts. deep_rl's replay buffer
     # (its capacity and sequence shape) is absent, so the sequence shape is parity unpinned.
     aux_source = "replay"
+    unreal = True
 
     def create_env(self, kwargs):
         goal = tuple(kwargs.get("goal", (10, 14, 0)))

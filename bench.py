@@ -184,7 +184,7 @@ BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md; no spars
 CEIL_TFLOPS = {"x3": BF16_MFMA_PEAK_TFLOPS / 3, "x6": BF16_MFMA_PEAK_TFLOPS / 6, "f32": FP32_MFMA_PEAK_TFLOPS}
 
 
-def train_flops_terms(h=84, w=84, A=4, T=20, recurrent=False, aux=False, goal_fwd=1.0, goal_bwd=1.0):
+def train_flops_terms(h=84, w=84, A=4, T=20, recurrent=False, aux=False, goal_fwd=1.0, goal_bwd=1.0, unreal=0.0):
     """FLOPs of one A2C env-step by (part, MFMA form): policy forward (kept activations serve
     the backward), weight gradients of every layer, input gradients of all but conv1, the
     bootstrap forward amortised over the rollout, and the aux deconv heads.
@@ -193,7 +193,10 @@ def train_flops_terms(h=84, w=84, A=4, T=20, recurrent=False, aux=False, goal_fw
     everything else x6). goal_fwd / goal_bwd: the fraction of the goal frames whose
     shared_base (conv1, conv2) the rollout forward / the update's backward computes — 1 is
     the reference's algorithm (goal.py:88 runs it on every goal frame); with goal-frame
-    deduplication the measured fractions give the executed FLOPs."""
+    deduplication the measured fractions give the executed FLOPs. unreal: the fraction S / E of
+    the envs whose sequences the UNREAL losses use (pixel control on their T + 1 LSTM rows,
+    reward prediction on their T - 2 three-frame samples), amortised per env-step; the pixel
+    control's second layer counts its A + 1 live channels."""
     o1 = ((h - 7) // 4 + 1, (w - 7) // 4 + 1)
     o2 = ((o1[0] - 4) // 2 + 1, (o1[1] - 4) // 2 + 1)
     o3 = ((o2[0] - 4) // 2 + 1, (o2[1] - 4) // 2 + 1)
@@ -216,21 +219,28 @@ def train_flops_terms(h=84, w=84, A=4, T=20, recurrent=False, aux=False, goal_fw
         l2 = 2 * ph * pw * 7 * 4 * 16
         terms += [("aux layer 1 (fwd, dX4, dW1)", "x6", 3 * l1), ("aux layer 2 forward", "f32", l2),
                   ("aux layer 2 backward", "f32", 2 * l2)]
+    if unreal:
+        rows, samples = unreal * (T + 1) / T, unreal * (T - 2) / T
+        base, d1, d2 = 2 * 512 * 2592, 2 * 20 * 20 * 64 * 4 * 32, 2 * 42 * 42 * (A + 1) * 4 * 32
+        rp = 2 * 3 * 3 * 32 * p3
+        terms += [("unreal pc forward", "x6", (base + d1) * rows), ("unreal pc layer 2 forward", "f32", d2 * rows),
+                  ("unreal pc backward", "x6", 2 * (base + d1 + d2) * rows), ("unreal rp", "f32", 3 * rp * samples)]
     return terms
 
 
-def train_flops_per_env_step(h=84, w=84, A=4, T=20, recurrent=False, aux=False, goal_fwd=1.0, goal_bwd=1.0):
+def train_flops_per_env_step(h=84, w=84, A=4, T=20, recurrent=False, aux=False, goal_fwd=1.0, goal_bwd=1.0,
+                             unreal=0.0):
     """(total FLOPs per env-step, forward FLOPs per sample)."""
-    terms = train_flops_terms(h, w, A, T, recurrent, aux, goal_fwd, goal_bwd)
+    terms = train_flops_terms(h, w, A, T, recurrent, aux, goal_fwd, goal_bwd, unreal)
     total = sum(f for _, _, f in terms)
     fwd = sum(f for name, _, f in terms if name.startswith("forward")) / (1 + 1.0 / T)
     return total, fwd
 
 
-def issued_ceiling_tflops(h=84, w=84, A=4, T=20, recurrent=False, aux=False, goal_fwd=1.0, goal_bwd=1.0):
+def issued_ceiling_tflops(h=84, w=84, A=4, T=20, recurrent=False, aux=False, goal_fwd=1.0, goal_bwd=1.0, unreal=0.0):
     """The update's fp32-equivalent ceiling when every part runs at the peak of the MFMA form
     it issues: total FLOPs / sum(FLOPs_i / ceiling_i)."""
-    terms = train_flops_terms(h, w, A, T, recurrent, aux, goal_fwd, goal_bwd)
+    terms = train_flops_terms(h, w, A, T, recurrent, aux, goal_fwd, goal_bwd, unreal)
     total = sum(f for _, _, f in terms)
     return total / sum(f / CEIL_TFLOPS[form] for _, form, f in terms)
 
@@ -250,18 +260,19 @@ def aux_scenes(n, frame, seed=0):
 
 
 def bench_train(args, scenes, dev, world, rank, recurrent, aux_weight=0.0, envs=None, updates=None, warmup=None,
-                model=None, cuda_graph=False, marker=False):
+                model=None, cuda_graph=False, marker=False, unreal=False):
     """A2C training throughput: one step = rollout of num_steps on every local env (policy
     forward + sampling + env step) + backward + one RCCL all-reduce of the flat gradient +
     clip + RMSprop. recurrent: the full BigGoalHouseModel (LSTM core, BPTT over the rollout);
-    else the feed-forward trunk + heads. aux_weight > 0 adds the deconv heads + aux loss."""
+    else the feed-forward trunk + heads. aux_weight > 0 adds the deconv heads + aux loss;
+    unreal the pixel-control / reward-prediction / value-replay losses (UnrealTrainer)."""
     import vnav
     E, T = envs or args.envs, args.num_steps
     updates = updates or args.train_steps
     warmup = args.train_warmup if warmup is None else warmup
     env = vnav.VectorEnv(scenes, E, seed=2000 + rank, device=dev)
     tr = vnav.A2CTrainer(env, num_steps=T, seed=7, max_time_steps=1e12, recurrent=recurrent, aux_weight=aux_weight,
-                         cuda_graph=cuda_graph, time_collectives=world > 1 and not cuda_graph)
+                         cuda_graph=cuda_graph, time_collectives=world > 1 and not cuda_graph, unreal=unreal)
     for _ in range(warmup):
         tr.step(sync=False)
     torch.cuda.synchronize(dev)
@@ -293,10 +304,11 @@ def bench_train(args, scenes, dev, world, rank, recurrent, aux_weight=0.0, envs=
     if tr.dedup_goals:
         cnt = tr.goal_count.cpu().tolist()
         gf, gb = sum(cnt[:T]) / (E * T), cnt[T] / (E * T)
-    alg, fwd = train_flops_per_env_step(h, w, T=T, recurrent=recurrent, aux=ax)
-    flops, _ = train_flops_per_env_step(h, w, T=T, recurrent=recurrent, aux=ax, goal_fwd=gf, goal_bwd=gb)
+    un = tr.unreal_S / E if tr.unreal else 0.0
+    alg, fwd = train_flops_per_env_step(h, w, T=T, recurrent=recurrent, aux=ax, unreal=un)
+    flops, _ = train_flops_per_env_step(h, w, T=T, recurrent=recurrent, aux=ax, goal_fwd=gf, goal_bwd=gb, unreal=un)
     tflops = E * T * updates * flops / el / 1e12
-    ceil = issued_ceiling_tflops(h, w, T=T, recurrent=recurrent, aux=ax, goal_fwd=gf, goal_bwd=gb)
+    ceil = issued_ceiling_tflops(h, w, T=T, recurrent=recurrent, aux=ax, goal_fwd=gf, goal_bwd=gb, unreal=un)
     if model is None:
         model = "BigGoalHouseModel (LSTM core)" if recurrent else "BigGoalHouseModel trunk + heads (no LSTM)"
     res = {"model": model, "frame": [h, w, 3],
@@ -315,7 +327,11 @@ def bench_train(args, scenes, dev, world, rank, recurrent, aux_weight=0.0, envs=
                         "issued_ceiling_tflops": ceil, "frac_issued": tflops / ceil,
                         "issued_ceiling_terms": [[n, f, fl] for n, f, fl in
                                                  train_flops_terms(h, w, T=T, recurrent=recurrent, aux=ax,
-                                                                   goal_fwd=gf, goal_bwd=gb)]}}
+                                                                   goal_fwd=gf, goal_bwd=gb, unreal=un)]}}
+    if tr.unreal:
+        res["unreal"] = {"sequences_per_update": tr.unreal_S, "pc_weight": tr.pc_weight, "rp_weight": tr.rp_weight,
+                         "vr_weight": tr.vr_weight, "source": "the first S envs' on-policy sequences (deep_rl samples "
+                                                             "replayed ones; parity unpinned)"}
     if world > 1:
         P = tr.net.n_params
         hw = tr.net.offsets["head"][0]
@@ -337,14 +353,17 @@ LEGS = {
     # thor-cached-auxiliary as logged (outputs/output.txt): 174x174 scenes, LSTM policy, aux
     # deconv loss with the experiment's weight 0.1 (experiments/thor_cached_auxiliary.py:42
     # overrides AuxiliaryTrainer's 0.05 default, ai2_auxiliary/trainer.py:25), 4 scenes
-    "174": dict(recurrent=True, aux_weight=AUX_WEIGHT_LOGGED, frame=(174, 174, 3), updates=3, warmup=1,
-                model="AuxiliaryBigGoalHouseModel (LSTM + deconv heads), 174x174"),
+    # (AuxiliaryTrainer is an UnrealTrainer: the pixel-control / reward-prediction / value-replay
+    # losses with the weights of :39-41 run too, on the first 16 envs' sequences)
+    "174": dict(recurrent=True, aux_weight=AUX_WEIGHT_LOGGED, frame=(174, 174, 3), updates=3, warmup=1, unreal=True,
+                model="AuxiliaryBigGoalHouseModel (LSTM + deconv + UNREAL heads), 174x174"),
     # the logged run's exact batch: 4 envs x 20 steps per update, one captured hipGraph per update
     "ref4": dict(recurrent=True, aux_weight=AUX_WEIGHT_LOGGED, frame=(174, 174, 3), envs=4, updates=400, warmup=3,
-                 cuda_graph=True, model="AuxiliaryBigGoalHouseModel (LSTM + deconv heads), 174x174, 4 envs "
-                                        "(the logged run's batch), hipGraph per update"),
+                 cuda_graph=True, unreal=True,
+                 model="AuxiliaryBigGoalHouseModel (LSTM + deconv + UNREAL heads), 174x174, 4 envs (the logged "
+                       "run's batch), hipGraph per update"),
     "c5": dict(recurrent=True, aux_weight=AUX_WEIGHT_LOGGED, frame=(300, 400, 3), envs=512, updates=3, warmup=1,
-               model="AuxiliaryBigGoalHouseModel (LSTM + deconv heads), 300x400 (config C5)"),
+               unreal=True, model="AuxiliaryBigGoalHouseModel (LSTM + deconv + UNREAL heads), 300x400 (config C5)"),
 }
 LEG_ORDER = ("84", "ff", "174", "ref4", "c5")
 
@@ -363,15 +382,16 @@ def run_leg(leg, args, scenes, dev, world, rank, updates=None, warmup=None, mark
     warmup = warmup if warmup is not None else wu
     res = bench_train(args, sc, dev, world, rank, updates=updates, warmup=warmup, marker=marker, **kw)
     if leg in ("174", "ref4"):
-        # context only, not like for like: the logged run also trained UNREAL pixel-control,
-        # reward-prediction and value-replay heads on replayed sequences (deep_rl, absent)
+        # the same losses as the logged run (A2C + aux deconv + UNREAL pc / rp / vr), but deep_rl
+        # ran the aux and UNREAL losses on sequences drawn from its replay buffer (extra trunk /
+        # LSTM passes over them), this leg on the rollout's own sequences
         res["reference_log_fps"] = REFERENCE_LOG_FPS
-        res["reference_log_note"] = ("the logged 106 env-steps/s also paid for the UNREAL pc / rp / vr losses on "
-                                     "replayed sequences, which this leg does not run: context, not a like-for-like "
-                                     "comparison")
+        res["reference_log_note"] = ("the logged 106 env-steps/s ran the same losses (A2C + aux deconv + UNREAL pc / "
+                                     "rp / vr) with the aux and UNREAL batches drawn from deep_rl's replay buffer; "
+                                     "this leg computes them on the rollout's own sequences (no extra trunk passes)")
     if leg == "ref4" and not marker:
         eager = bench_train(args, sc, dev, world, rank, updates=100, warmup=3, recurrent=True,
-                            aux_weight=AUX_WEIGHT_LOGGED, envs=4, model="eager")
+                            aux_weight=AUX_WEIGHT_LOGGED, envs=4, model="eager", unreal=True)
         res["eager_value"] = eager["value"]
         res["eager_ms_per_update"] = eager["ms_per_update"]
     return res

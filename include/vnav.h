@@ -272,6 +272,12 @@ int vn_lstm_backward(vn_policy* p, const float* params, int T, int E, const floa
                      const float* xcat_all, const float* acts_all, const float* c_all, const float* c_init,
                      const float* mask_all, const float* x5_all, float* dz5_all, float* grads, float* workspace,
                      vn_stream_t stream);
+/* vn_lstm_backward plus dh_extra [T][extra_envs][512]: another head's gradient w.r.t. h_t of
+ * envs 0..extra_envs-1 (pixel control, vn_pc_backward), added to the policy heads'. */
+int vn_lstm_backward_ex(vn_policy* p, const float* params, int T, int E, const float* dout, const float* h_all,
+                        const float* xcat_all, const float* acts_all, const float* c_all, const float* c_init,
+                        const float* mask_all, const float* x5_all, const float* dh_extra, int extra_envs,
+                        float* dz5_all, float* grads, float* workspace, vn_stream_t stream);
 /* Trunk gradients (conv1..conv_merge) of the n stored samples from dz5 [n][512]. */
 int vn_policy_backward_trunk(vn_policy* p, const float* params, const vn_frames* frames, int n, float* acts,
                              int64_t act_capacity, const float* dz5, float* grads, float* workspace,
@@ -321,6 +327,63 @@ int vn_aux_forward_loss_grad(vn_policy* p, const float* params, float* acts, int
  * dx4; consumes a1. */
 int vn_aux_backward(vn_policy* p, const float* params, float* acts, int64_t act_capacity, int n, float* a1,
                     const float* dpred, float* grads, float* dx4, float* workspace, vn_stream_t stream);
+/* ---- UNREAL heads: pixel control and reward prediction (models/goal.py:94-133) ----
+ * A policy created with VN_POLICY_UNREAL (BigGoalHouseModel only) appends, 16-byte aligned:
+ *   pc_base W [2592][512] (rows in (y, x, c) order of the reference's (32, 9, 9) view), b [2592];
+ *   pc W1 [32][4][4][64], b1 [64]: pc_value's ConvTranspose2d(32,32,4,2) -> channels 0-31,
+ *     pc_action's -> 32-63;
+ *   pc W2 [64][4][4][8], b2 [8]: block diagonal, pc_value's ConvTranspose2d(32,A,4,2) ->
+ *     channels 0..A-1 from rows 0-31, pc_action's ConvTranspose2d(32,1,4,2) -> channel A from
+ *     rows 32-63, the rest padding;
+ *   rp W [3][3 * FCIN] (FCIN = h3 * w3 * 32; the three frames' conv_base maps, NHWC each:
+ *     the reference's Linear(9*9*32*3, 3) at 174x174), b [4] (3 + pad).
+ * info8 = (pc_base W, pc_base b, W1, b1, W2, b2, rp W, rp b offsets). */
+#define VN_POLICY_UNREAL 8
+int vn_policy_unreal_info(vn_policy* p, int64_t* info8);
+int vn_pc_workspace_floats(vn_policy* p, int64_t* floats);
+/* pixel_control (goal.py:131-137) on feature rows h [n][512] (the LSTM outputs): writes
+ * pcb [n][9][9][32], a1 [n][20][20][64], p2 [n][42][42][8] (kept for the backward) and
+ * q [n][42][42][A] = (pc_value + pc_action) - mean_c(pc_action). */
+int vn_pc_forward(vn_policy* p, const float* params, const float* h, int n, float* pcb, float* a1, float* p2,
+                  float* q, float* workspace, vn_stream_t stream);
+/* From dL/dq [n][42][42][A]: the pixel-control parameter gradients into grads (overwritten)
+ * and dL/dh [n][512] into dh (stored, or added to dh when accumulate != 0). Consumes pcb, a1
+ * and p2 (overwritten by their gradients). */
+int vn_pc_backward(vn_policy* p, const float* params, const float* h, int n, float* pcb, float* a1, float* p2,
+                   const float* dq, float* grads, float* dh, int accumulate, float* workspace, vn_stream_t stream);
+/* reward_prediction (goal.py:121-129): out [n][4] = logits of x [n][3 * FCIN] (column 3 unused). */
+int vn_rp_forward(vn_policy* p, const float* params, const float* x, int n, float* out, vn_stream_t stream);
+/* rp gradients into grads (overwritten) from dL/dout [n][4] (column 3 ignored); dx [n][3 * FCIN]
+ * (may be NULL) = dout x W. workspace: vn_pc_workspace_floats. */
+int vn_rp_backward(vn_policy* p, const float* params, const float* x, int n, const float* dout, float* grads,
+                   float* dx, float* workspace, vn_stream_t stream);
+/* ---- UNREAL losses of the trainer (deep_rl's UnrealTrainer, absent: parity unpinned; the
+ * published algorithm, csrc/vn_unreal_loss.hip, weights experiments/thor_cached_auxiliary.py:39-41) ----
+ * Sequences are the first S envs of a rollout of T steps x E envs (rows t*E + e).
+ * Pixel control: q [(T+1)*S][42][42][A] from vn_pc_forward on rows t*S + e (row T*S + e: the
+ * bootstrap observation); pseudo-reward r_t = mean over each 4x4 cell and 3 channels of
+ * |obs_{t+1} - obs_t| / 255 on the centre 168x168 crop of the u8 image frames (arena rows
+ * rows_img[t*E + e], rows_last[e] for obs_T); R_T = max_a q_T, R_t = r_t + gamma (1 - done_t)
+ * R_{t+1}; dq = weight * d mean((q_t[a_t] - R_t)^2) / dq (0 on the bootstrap rows);
+ * stats[0] += sum of squared errors. */
+int vn_unreal_pc_loss_grad(const float* q, const int32_t* actions, const uint8_t* dones, const uint8_t* arena,
+                           int64_t frame_bytes, int height, int width, const int32_t* rows_img,
+                           const int32_t* rows_last, int T, int E, int S, int num_actions, float gamma, float weight,
+                           float* dq, float* stats, vn_stream_t stream);
+/* Reward prediction: logits [(T-2)*S][4] of samples j = (ts-2)*S + e (frames ts-2..ts of env
+ * e); class of rewards[ts][e]: 0 (r = 0), 1 (r > 0), 2 (r < 0); samples with a done at ts-2
+ * or ts-1 are skipped. dlogits = weight * d mean CE / dlogits; stats2 = (mean CE, count). */
+int vn_unreal_rp_loss_grad(const float* logits, const float* rewards, const uint8_t* dones, int T, int E, int S,
+                           float weight, float* dlogits, float* stats2, vn_stream_t stream);
+/* dx [(T-2)*S][3][fcin] (vn_rp_backward's input gradient) onto dx4 rows t*E + e, e < S
+ * (stored, or added when accumulate != 0; other rows untouched). */
+int vn_unreal_rp_scatter(const float* dx, int T, int E, int S, int fcin, float* dx4, int accumulate,
+                         vn_stream_t stream);
+/* Value replay on rows t*E + e, e < S: dout[.][A] += weight * d mean((V - R)^2) / dV;
+ * stats[0] += sum of squared errors. */
+int vn_unreal_vr_grad(const float* out, const float* returns, int T, int E, int S, int num_actions, float weight,
+                      float* dout, float* stats, vn_stream_t stream);
+
 /* General backward: from dL/d(out) [n][8] (dz5 == NULL) or from dz5 [n][512] (recurrent
  * policies, heads and LSTM done by vn_lstm_backward); dx4_extra [n][h3][w3][32] (aux heads,
  * may be NULL) is added to conv_base's output gradient under its ReLU mask. */

@@ -298,3 +298,64 @@ def seeded_reference_state(frame_hw, seed, aux=False):
             v = rng.uniform(-d, d, size=shape)
         out[name] = v.astype(np.float32)
     return out
+
+
+UNREAL_PARAM_ORDER = (  # BigGoalHouseModel.named_parameters() order of pc_base, pc_action, pc_value, rp
+    "pc_base.0.0.weight", "pc_base.0.0.bias", "pc_action.0.0.weight", "pc_action.0.0.bias",
+    "pc_action.0.2.weight", "pc_action.0.2.bias", "pc_value.0.0.weight", "pc_value.0.0.bias",
+    "pc_value.0.2.weight", "pc_value.0.2.bias", "rp.1.weight", "rp.1.bias",
+)
+
+
+def unreal_shapes(frame_hw=(174, 174), num_outputs=4):
+    """goal.py:94-119; rp's in_features derived from the frame (the reference fixes 9*9*32*3,
+    the 174x174 value)."""
+    _, _, o3 = trunk_sizes(*frame_hw)
+    return {"pc_base.0.0.weight": (32 * 9 * 9, 512), "pc_base.0.0.bias": (32 * 9 * 9,),
+            "pc_action.0.0.weight": (32, 32, 4, 4), "pc_action.0.0.bias": (32,),
+            "pc_action.0.2.weight": (32, 1, 4, 4), "pc_action.0.2.bias": (1,),
+            "pc_value.0.0.weight": (32, 32, 4, 4), "pc_value.0.0.bias": (32,),
+            "pc_value.0.2.weight": (32, num_outputs, 4, 4), "pc_value.0.2.bias": (num_outputs,),
+            "rp.1.weight": (3, 3 * 32 * o3[0] * o3[1]), "rp.1.bias": (3,)}
+
+
+def seeded_unreal_state(frame_hw, seed, num_outputs=4):
+    """gen_model_goldens.py:seeded_weights over the four UNREAL modules alone (PCG64)."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    shapes = unreal_shapes(frame_hw, num_outputs)
+    out = {}
+    for name in UNREAL_PARAM_ORDER:
+        shape = shapes[name]
+        if name.endswith("bias"):
+            v = rng.uniform(-0.05, 0.05, size=shape)
+        else:
+            d = 1.0 / np.sqrt(int(np.prod(shape[1:])))
+            v = rng.uniform(-d, d, size=shape)
+        out[name] = v.astype(np.float32)
+    return out
+
+
+def pixel_control(sd, h, masks=None):
+    """goal.py:131-137 after _forward_base: q [N, A, 42, 42] of features h [N, 512], in the
+    dtype of h (float64 for the parity tests); sd tensors in that dtype. masks (optional):
+    the ReLU masks of a run under test ({"pc_base": [N, 32, 9, 9], "pc_value.0" / "pc_action.0"
+    [N, 32, 20, 20], "pc_value.2" [N, A, 42, 42], "pc_action.2" [N, 1, 42, 42]}) replace the
+    oracle's own, so a pre-activation within rounding of zero cannot flip a mask between them."""
+    def act(x, key):
+        return F.relu(x) if masks is None else x * masks[key].to(x.dtype)
+
+    f = act(F.linear(h, sd["pc_base.0.0.weight"], sd["pc_base.0.0.bias"]).view(-1, 32, 9, 9), "pc_base")
+
+    def branch(name):
+        x = act(F.conv_transpose2d(f, sd[name + ".0.0.weight"], sd[name + ".0.0.bias"], stride=2), name + ".0")
+        return act(F.conv_transpose2d(x, sd[name + ".0.2.weight"], sd[name + ".0.2.bias"], stride=2), name + ".2")
+
+    a = branch("pc_action")
+    return branch("pc_value") + a - a.mean(1, keepdim=True)
+
+
+def reward_prediction(sd, feats):
+    """goal.py:121-129 after conv_base: logits [R, 3] of feats [R, 3, 32, h3, w3] (Flatten =
+    view(R, -1))."""
+    return F.linear(feats.reshape(feats.shape[0], -1), sd["rp.1.weight"], sd["rp.1.bias"])

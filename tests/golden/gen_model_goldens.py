@@ -9,6 +9,7 @@ Cases
          Linear(288, 512) (the 84x84 trunk ends at 3x3x32) and re-initialised with the
          reference's own init_weights; biases then perturbed so bias paths are exercised.
   174x174 the unmodified reference topology (Linear(2592, 512)).
+  unreal174 the pixel-control and reward-prediction heads (goal.py:94-137) at 174x174.
 For each: weights (reference state-dict names), uint8 frame inputs, trunk features,
 logits and value from the reference modules, and the gradients of the engine's A2C
 loss (oracle/a2c.py, parity unpinned at the trainer level) through the reference
@@ -178,11 +179,58 @@ def bighouse_case(B, T, seed):
     return out
 
 
+UNREAL = ("pc_base", "pc_action", "pc_value", "rp")
+
+
+def unreal_case(B, T, R, seed):
+    """BigGoalHouseModel's UNREAL heads (models/goal.py:94-137) at 174x174, the reference
+    topology (pc_base 512 -> 32x9x9, rp Linear(9*9*32*3, 3)). Weights from the seed (PCG64,
+    the four modules only, named_parameters order; the trunk from seed + 1, used only to make
+    the rp inputs). pixel_control runs on stored LSTM features h [B,T,512] (its _forward_base is
+    replaced by one returning h: MaskedRNN's semantics are absent) and reward_prediction on R
+    samples of 3 frames; both losses are sums against stored random weights (dq, drp), so the
+    stored gradients are those of the heads' outputs contracted with them."""
+    torch.manual_seed(seed)
+    model = BigGoalHouseModel(3, 4)
+    seeded_weights(model, seed, UNREAL)
+    seeded_weights(model, seed + 1, ("shared_base", "conv_base"))
+    rng = np.random.RandomState(seed)
+    h = torch.as_tensor((rng.rand(B, T, 512) * 2.0 - 0.5).astype(np.float32)).requires_grad_()
+    f = model.pc_base(h).view(B, T, 32, 9, 9)
+    a = model.pc_action(f)
+    q = model.pc_value(f) + a - a.mean(2, keepdim=True)
+    model._forward_base = lambda inputs, masks, states: (h, None)
+    with torch.no_grad():
+        q_ref, _ = model.pixel_control(None, None, None)
+    assert torch.equal(q, q_ref)
+    dq = torch.as_tensor(rng.randn(*q.shape).astype(np.float32))
+    image = torch.as_tensor(rng.randint(0, 256, size=(R, 3, 174, 174, 3)).astype(np.uint8))
+    goal = torch.as_tensor(rng.randint(0, 256, size=(R, 3, 174, 174, 3)).astype(np.uint8))
+    img = image.permute(0, 1, 4, 2, 3).float() / 255.0
+    gl = goal.permute(0, 1, 4, 2, 3).float() / 255.0
+    feats = model.conv_base(torch.cat((model.shared_base(img), model.shared_base(gl)), 2)).detach().requires_grad_()
+    logits = model.rp(feats)
+    with torch.no_grad():
+        assert torch.equal(logits, model.reward_prediction(((img, gl), None)))
+    drp = torch.as_tensor(rng.randn(R, 3).astype(np.float32))
+    model.zero_grad()
+    ((q * dq).sum() + (logits * drp).sum()).backward()
+    out = {"seed": np.array([seed]), "h": h.detach().numpy(), "q": q.detach().numpy(), "dq": dq.numpy(),
+           "dh": h.grad.numpy(), "rp_features": feats.detach().numpy(), "rp_logits": logits.detach().numpy(),
+           "drp": drp.numpy(), "d_rp_features": feats.grad.numpy()}
+    for name, p in model.named_parameters():
+        if name.split(".")[0] in UNREAL:
+            out["g:" + name] = p.grad.numpy()
+    out["g:pc_base.0.0.weight"] = out["g:pc_base.0.0.weight"][::16].copy()  # every 16th row (size)
+    return out
+
+
 def main():
     np.savez_compressed(os.path.join(HERE, "policy84.npz"), **case(84, 3, 2, 11))
     np.savez_compressed(os.path.join(HERE, "policy174.npz"), **case(174, 2, 1, 12, store_weights=False))
     np.savez_compressed(os.path.join(HERE, "aux174.npz"), **aux_case(174, 2, 1, 13))
     np.savez_compressed(os.path.join(HERE, "bighouse84.npz"), **bighouse_case(2, 2, 14))
+    np.savez_compressed(os.path.join(HERE, "unreal174.npz"), **unreal_case(2, 3, 3, 15))
     n_params = sum(p.numel() for n, p in build(84, 0).named_parameters() if n.split(".")[0] in USED)
     print("84x84 trunk+heads parameters:", n_params)
 

@@ -58,7 +58,34 @@ def test_recurrent_policy_layout(built_lib):
     assert lib.vn_policy_info(h, ctypes.byref(n), None, None) == 0
     assert n.value == base + 2048 * xcat + 4096
     lib.vn_policy_destroy(h)
-    assert lib.vn_policy_create_ex(84, 84, 4, 8, ctypes.byref(h)) != 0  # unknown flag
+    assert lib.vn_policy_create_ex(84, 84, 4, 16, ctypes.byref(h)) != 0  # unknown flag
+
+
+def test_unreal_policy_layout(built_lib):
+    """VN_POLICY_UNREAL appends, 16-byte aligned, pc_base W [2592][512], b [2592], W1 [32][4][4][64],
+    b1 [64], W2 [64][4][4][8], b2 [8], rp W [3][3 FCIN], b [4] (goal.py:94-119); refused with
+    VN_POLICY_BIGHOUSE (bignet.py's heads differ)."""
+    from vnav import _lib
+    lib = _lib.load()
+    for hw, fcin in ((84, 288), (174, 2592)):
+        h = ctypes.c_void_p()
+        n = ctypes.c_int64()
+        assert lib.vn_policy_create_ex(hw, hw, 4, 1, ctypes.byref(h)) == 0
+        assert lib.vn_policy_info(h, ctypes.byref(n), None, None) == 0
+        base = n.value
+        assert lib.vn_policy_unreal_info(h, (ctypes.c_int64 * 8)()) != 0
+        lib.vn_policy_destroy(h)
+        assert lib.vn_policy_create_ex(hw, hw, 4, 1 | 8, ctypes.byref(h)) == 0
+        info = (ctypes.c_int64 * 8)()
+        assert lib.vn_policy_unreal_info(h, info) == 0
+        o = (base + 3) // 4 * 4
+        sizes = (2592 * 512, 2592, 32 * 16 * 64, 64, 64 * 16 * 8, 8, 3 * 3 * fcin, 4)
+        want = [o + sum(sizes[:i]) for i in range(8)]
+        assert list(info) == want and all(v % 4 == 0 for v in info)
+        assert lib.vn_policy_info(h, ctypes.byref(n), None, None) == 0
+        assert n.value == want[-1] + 4
+        lib.vn_policy_destroy(h)
+    assert lib.vn_policy_create_ex(84, 84, 4, 4 | 8, ctypes.byref(h)) != 0
 
 
 def test_aux_policy_layout(built_lib):

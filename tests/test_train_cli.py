@@ -23,6 +23,7 @@ def test_registry_and_hyperparameters():
     assert (cls.rms_alpha, cls.rms_epsilon, cls.max_gradient_norm) == (0.99, 1e-5, 0.5)
     assert (cls.value_coefficient, cls.entropy_coefficient) == (0.5, 0.001)
     assert (cls.auxiliary_weight, cls.hardness, cls.recurrent) == (0.1, 0.01, True)
+    assert (cls.unreal, cls.rp_weight, cls.pc_weight, cls.vr_weight) == (True, 1.0, 0.05, 1.0)  # :39-41
     with pytest.raises(KeyError):
         train.make_trainer("no-such-experiment")
     with pytest.raises(TypeError):
