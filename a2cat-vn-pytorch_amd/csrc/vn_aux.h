@@ -88,12 +88,14 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __rest
   }
 }
 
+// One wave per column (grid = cols): lane l sums partials b = l (mod 64) in order, then a
+// fixed xor tree (the one-thread-per-column form walked up to 512 dependent loads: ~100 us).
 __global__ void colsum_final_kernel(const float* __restrict__ partial, int blocks, int cols, float* __restrict__ out) {
-  const int c = threadIdx.x;
-  if (c >= cols) return;
+  const int c = blockIdx.x, l = threadIdx.x;
   float t = 0.0f;
-  for (int b = 0; b < blocks; ++b) t += partial[(int64_t)b * cols + c];
-  out[c] = t;
+  for (int b = l; b < blocks; b += 64) t += partial[(int64_t)b * cols + c];
+  for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
+  if (l == 0) out[c] = t;
 }
 
 // Per-state target table (built once per scene cache): for every arena row and prediction

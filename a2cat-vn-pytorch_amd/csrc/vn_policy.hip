@@ -433,6 +433,51 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, int splits, 
   }
 }
 
+// The same sum with G lanes per output (few outputs, many slabs: the one-thread form above ran
+// 100-230 dependent loads per thread on 10-40 workgroups, 30-60 us): lane j of output idx sums
+// slabs z = j (mod G) in order, then a fixed xor tree over the G lanes. Deterministic.
+template <int G>
+__global__ __launch_bounds__(256) void wgrad_reduce_g_kernel(const float* __restrict__ slab, int splits, int M, int N,
+                                                             int KP, float* dW, float* db, float* db2) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t MN = (int64_t)M * N;
+  const int64_t idx = t / G;
+  const int j = (int)(t - idx * G);
+  float s = 0.0f;
+  if (idx < MN)
+    for (int z = j; z < splits; z += G) s += slab[(int64_t)z * MN + idx];
+#pragma unroll
+  for (int o = G / 2; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (j != 0 || idx >= MN) return;
+  const int row = (int)(idx / N), col = (int)(idx - (int64_t)row * N);
+  if (col < KP)
+    dW[(int64_t)row * KP + col] = s;
+  else {
+    db[row] = s;
+    if (db2) db2[row] = s;
+  }
+}
+
+// Launch the reduce of `splits` slabs of M x N partials: one thread per output while that
+// fills the chip, else G lanes per output (about 8 slabs per lane).
+inline void launch_wgrad_reduce(const float* slab, int splits, int M, int N, int KP, float* dW, float* db, float* db2,
+                                hipStream_t st) {
+  const int64_t MN = (int64_t)M * N;
+  int G = 1;
+  if (MN < 65536)
+    while (G < 64 && G * 8 < splits) G *= 2;
+  const unsigned blocks = (unsigned)((MN * G + 255) / 256);
+  switch (G) {
+    case 1: hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, slab, splits, M, N, KP, dW, db, db2); break;
+    case 2: hipLaunchKernelGGL(wgrad_reduce_g_kernel<2>, dim3(blocks), dim3(256), 0, st, slab, splits, M, N, KP, dW, db, db2); break;
+    case 4: hipLaunchKernelGGL(wgrad_reduce_g_kernel<4>, dim3(blocks), dim3(256), 0, st, slab, splits, M, N, KP, dW, db, db2); break;
+    case 8: hipLaunchKernelGGL(wgrad_reduce_g_kernel<8>, dim3(blocks), dim3(256), 0, st, slab, splits, M, N, KP, dW, db, db2); break;
+    case 16: hipLaunchKernelGGL(wgrad_reduce_g_kernel<16>, dim3(blocks), dim3(256), 0, st, slab, splits, M, N, KP, dW, db, db2); break;
+    case 32: hipLaunchKernelGGL(wgrad_reduce_g_kernel<32>, dim3(blocks), dim3(256), 0, st, slab, splits, M, N, KP, dW, db, db2); break;
+    default: hipLaunchKernelGGL(wgrad_reduce_g_kernel<64>, dim3(blocks), dim3(256), 0, st, slab, splits, M, N, KP, dW, db, db2); break;
+  }
+}
+
 __global__ void transpose_kernel(const float* __restrict__ W, int rows, int cols, float* __restrict__ WT) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= rows * cols) return;
@@ -714,15 +759,25 @@ inline void launch_gemm32(FA fa, FB fb, EP ep, int M, int N, int K, hipStream_t 
 
 // Epilogue of a split-K product: element (row, col) = the fixed-order sum of its `splits`
 // slab partials, then the product's own epilogue functor (any of its three forms).
-template <class EP>
+// G > 1 (few outputs, many splits): G lanes per element, lane j summing splits z = j (mod G)
+// in order, then a fixed xor tree (as wgrad_reduce_g_kernel).
+template <class EP, int G = 1>
 __global__ __launch_bounds__(256) void splitk_epilogue_kernel(const float* __restrict__ slab, int splits, int M, int N,
                                                               EP ep) {
-  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t idx = t / G;
+  const int j = (int)(t - idx * G);
   const int64_t MN = (int64_t)M * N;
+  float v = 0.0f;
+  if (idx < MN)
+    for (int z = j; z < splits; z += G) v += slab[z * MN + idx];
+  if constexpr (G > 1) {
+#pragma unroll
+    for (int o = G / 2; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if (j != 0) return;
+  }
   if (idx >= MN) return;
   const int row = (int)(idx / N), col = (int)(idx - (idx / N) * N);
-  float v = 0.0f;
-  for (int z = 0; z < splits; ++z) v += slab[z * MN + idx];
   if constexpr (has_pre_col<EP>::value)
     ep.post(row, col, v, ep.pre_col(col), 0);
   else if constexpr (has_pre_row<EP>::value)
@@ -731,6 +786,24 @@ __global__ __launch_bounds__(256) void splitk_epilogue_kernel(const float* __res
     ep.post(row, col, v, ep.pre(row, col), 0);
   else
     ep(row, col, v, 0);
+}
+
+template <class EP>
+inline void launch_splitk_epilogue(const float* slab, int splits, int M, int N, EP ep, hipStream_t st) {
+  const int64_t MN = (int64_t)M * N;
+  int G = 1;
+  if (MN < 65536)
+    while (G < 64 && G * 8 < splits) G *= 2;
+  const unsigned blocks = (unsigned)((MN * G + 255) / 256);
+  switch (G) {
+    case 1: hipLaunchKernelGGL((splitk_epilogue_kernel<EP, 1>), dim3(blocks), dim3(256), 0, st, slab, splits, M, N, ep); break;
+    case 2: hipLaunchKernelGGL((splitk_epilogue_kernel<EP, 2>), dim3(blocks), dim3(256), 0, st, slab, splits, M, N, ep); break;
+    case 4: hipLaunchKernelGGL((splitk_epilogue_kernel<EP, 4>), dim3(blocks), dim3(256), 0, st, slab, splits, M, N, ep); break;
+    case 8: hipLaunchKernelGGL((splitk_epilogue_kernel<EP, 8>), dim3(blocks), dim3(256), 0, st, slab, splits, M, N, ep); break;
+    case 16: hipLaunchKernelGGL((splitk_epilogue_kernel<EP, 16>), dim3(blocks), dim3(256), 0, st, slab, splits, M, N, ep); break;
+    case 32: hipLaunchKernelGGL((splitk_epilogue_kernel<EP, 32>), dim3(blocks), dim3(256), 0, st, slab, splits, M, N, ep); break;
+    default: hipLaunchKernelGGL((splitk_epilogue_kernel<EP, 64>), dim3(blocks), dim3(256), 0, st, slab, splits, M, N, ep); break;
+  }
 }
 
 // Splits of a product whose BM x BN tiles alone leave most of the chip idle (a 4-env rollout
@@ -760,9 +833,7 @@ inline void launch_gemm_x6_sk(FA fa, FB fb, EP ep, int M, int N, int K, hipStrea
   EpiSlab es{L.sk, M, N};
   hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, BK, WM, WN, FA, FB, EpiSlab>), grid_for(M, N, BM, BN, splits), dim3(256),
                      0, st, fa, fb, es, M, N, K, kchunk);
-  const int64_t MN = (int64_t)M * N;
-  hipLaunchKernelGGL(splitk_epilogue_kernel<EP>, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, st, L.sk, splits, M,
-                     N, ep);
+  launch_splitk_epilogue(L.sk, splits, M, N, ep, st);
 }
 
 // The f32 MFMA core's form (the heads: N = actions + 1, K = 512).
@@ -778,9 +849,7 @@ inline void launch_gemm_sk(FA fa, FB fb, EP ep, int M, int N, int K, hipStream_t
   splits = (K + kchunk - 1) / kchunk;
   EpiSlab es{L.sk, M, N};
   launch_gemm<BM, BN, BK, WM, WN>(fa, fb, es, M, N, K, st, splits, kchunk);
-  const int64_t MN = (int64_t)M * N;
-  hipLaunchKernelGGL(splitk_epilogue_kernel<EP>, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, st, L.sk, splits, M,
-                     N, ep);
+  launch_splitk_epilogue(L.sk, splits, M, N, ep, st);
 }
 
 // Split-K wgrad: dW [M][KP] and db [M] of a layer from A^T (dZ [P][M]) x B (im2col [P][KP]).
@@ -798,8 +867,7 @@ inline void launch_wgrad(const float* dZ, int64_t ldz, int M, FB fb, int KP, int
   DenseT fa{dZ, ldz, M};
   EpiSlab ep{slab, M, N};
   launch_gemm<BM, BN, BK, WM, WN>(fa, fb, ep, M, N, P, st, splits, kchunk);
-  const int total = M * N;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, slab, splits, M, N, KP, dW, db, nullptr);
+  launch_wgrad_reduce(slab, splits, M, N, KP, dW, db, nullptr, st);
 }
 
 // The same split-K wgrad on the x6 core: both operands gathered along the reduction index
@@ -819,8 +887,7 @@ inline void launch_wgrad6(const float* dZ, int64_t ldz, int M, FB fb, int KP, in
   EpiSlab ep{slab, M, N};
   hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, BK, WM, WN, DenseT, FB, EpiSlab>), grid_for(M, N, BM, BN, splits),
                      dim3(256), 0, st, fa, fb, ep, M, N, P, kchunk);
-  const int total = M * N;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, slab, splits, M, N, KP, dW, db, nullptr);
+  launch_wgrad_reduce(slab, splits, M, N, KP, dW, db, nullptr, st);
 }
 
 // Split-K wgrad on the x6 core from transposed operands: dZT [M][P] (rows = output
@@ -842,8 +909,7 @@ inline void launch_wgrad_x6(const float* dZT, int M, const float* XT, int KP, in
   EpiSlab ep{slab, M, N};
   hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, BK, WM, WN, DenseRows, RowsOnes, EpiSlab>), grid_for(M, N, BM, BN, splits),
                      dim3(256), 0, st, fa, fb, ep, M, N, P, kchunk);
-  const int total = M * N;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, slab, splits, M, N, KP, dW, db, db2);
+  launch_wgrad_reduce(slab, splits, M, N, KP, dW, db, db2, st);
 }
 
 // dgrad of one (group, parity) class of a k4 s2 conv: input pixels (y, x) with
@@ -2229,7 +2295,7 @@ inline void colsum(const float* src, int64_t rows, int cols, float* partial, flo
   const int lanes = 256 / cols;
   const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(kColsumBlocks, (rows + lanes - 1) / lanes));
   hipLaunchKernelGGL(colsum_partial_kernel, dim3(blocks), dim3(256), 0, st, src, rows, cols, partial);
-  hipLaunchKernelGGL(colsum_final_kernel, dim3(1), dim3(64), 0, st, partial, blocks, cols, out);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3(cols), dim3(64), 0, st, partial, blocks, cols, out);
 }
 
 template <int AH, int AW, int PH, int PW, bool LOSS>
@@ -2405,8 +2471,10 @@ int pc_forward_impl(const PolicyLayout& L, const float* P, const float* h, int n
     return rc;
   if (const int rc = deconv_all<kPcC1, kPcC2, kPcA1, kPcA1, kPcP, kPcP>(A1, w.w2t, P2, P + L.ub2, 1, n, st); rc != VN_OK)
     return rc;
-  const int64_t npix = (int64_t)n * kPcP * kPcP;
-  hipLaunchKernelGGL(pc_combine_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, st, P2, npix, L.A, q);
+  if (q) {  // the trainer's pixel-control loss forms q from P2 itself
+    const int64_t npix = (int64_t)n * kPcP * kPcP;
+    hipLaunchKernelGGL(pc_combine_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, st, P2, npix, L.A, q);
+  }
   VN_HIP(hipGetLastError());
   return VN_OK;
 }
@@ -2416,7 +2484,8 @@ int pc_forward_impl(const PolicyLayout& L, const float* P, const float* h, int n
 int pc_backward_impl(const PolicyLayout& L, const float* P, const float* h, int n, float* pcb, float* A1, float* P2,
                      const float* dq, float* Gr, float* dh, int accumulate, const PcWork& w, hipStream_t st) {
   const int64_t npix = (int64_t)n * kPcP * kPcP;
-  hipLaunchKernelGGL(pc_dq_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, st, P2, dq, npix, L.A);
+  if (dq)  // else P2 already holds dL/dP2 (vn_unreal_pc_loss_grad)
+    hipLaunchKernelGGL(pc_dq_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, st, P2, dq, npix, L.A);
   // second layer: dW2 = A1^T x im2col(dP2) (block-diagonal mask), db2, dA1 masked in place, db1
   const int P1 = n * kPcA1 * kPcA1;
   using Im2 = NhwcIm2col<kPcC2, 4, 4, 2, kPcP, kPcP, kPcA1, kPcA1, 1>;  // dP2 windows per A1 pixel
@@ -2697,14 +2766,14 @@ int vn_pc_workspace_floats(vn_policy* p, int64_t* floats) {
 
 int vn_pc_forward(vn_policy* p, const float* params, const float* h, int n, float* pcb, float* a1, float* p2, float* q,
                   float* workspace, vn_stream_t stream) {
-  if (!p || !p->L.unreal || !params || !h || !pcb || !a1 || !p2 || !q || !workspace || n <= 0)
+  if (!p || !p->L.unreal || !params || !h || !pcb || !a1 || !p2 || !workspace || n <= 0)
     return fail(VN_EINVAL, "vn_pc_forward: bad args");
   return pc_forward_impl(p->L, params, h, n, pcb, a1, p2, q, pc_carve(p->L, workspace), (hipStream_t)stream);
 }
 
 int vn_pc_backward(vn_policy* p, const float* params, const float* h, int n, float* pcb, float* a1, float* p2,
                    const float* dq, float* grads, float* dh, int accumulate, float* workspace, vn_stream_t stream) {
-  if (!p || !p->L.unreal || !params || !h || !pcb || !a1 || !p2 || !dq || !grads || !dh || !workspace || n <= 0)
+  if (!p || !p->L.unreal || !params || !h || !pcb || !a1 || !p2 || !grads || !dh || !workspace || n <= 0)
     return fail(VN_EINVAL, "vn_pc_backward: bad args");
   return pc_backward_impl(p->L, params, h, n, pcb, a1, p2, dq, grads, dh, accumulate, pc_carve(p->L, workspace),
                           (hipStream_t)stream);

@@ -50,15 +50,26 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return t;
 }
 
-// One thread per (env e < S, cell): the Q targets backwards over the rollout and dq of
-// rows t*S + e (row T*S + e, the bootstrap, gets 0: its max is a detached target).
-__global__ __launch_bounds__(256) void unreal_pc_loss_kernel(const float* __restrict__ q, const int32_t* __restrict__ actions,
+// One thread per (env e < S, cell): the Q targets backwards over the rollout. Reads the
+// heads' maps p2 [(T+1) S][42][42][8] of vn_pc_forward (value channels 0..A-1, action channel A,
+// after their ReLUs) and forms q_c = (v_c + a) - a on the fly (goal.py:136); overwrites p2 with
+// dL/dp2: the TD gradient of the taken action's value channel under its ReLU, 0 elsewhere (the
+// action channel's gradient is exactly 0, pc_dq_kernel) and on the bootstrap rows T S + e.
+__device__ __forceinline__ void pc_load8(const float* p, float (&v)[8]) {
+  const f4 lo = reinterpret_cast<const f4*>(p)[0], hi = reinterpret_cast<const f4*>(p)[1];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    v[c] = lo[c];
+    v[4 + c] = hi[c];
+  }
+}
+
+__global__ __launch_bounds__(256) void unreal_pc_loss_kernel(float* __restrict__ p2, const int32_t* __restrict__ actions,
                                                              const uint8_t* __restrict__ dones,
                                                              const uint8_t* __restrict__ arena, int64_t frame_bytes,
                                                              int H, int W, const int32_t* __restrict__ rows_img,
                                                              const int32_t* __restrict__ rows_last, int T, int E, int S,
-                                                             int A, float gamma, float coef, float* __restrict__ dq,
-                                                             float* __restrict__ stats) {
+                                                             int A, float gamma, float coef, float* __restrict__ stats) {
   __shared__ float red[4];
   constexpr int PP = kPcCells * kPcCells;
   const int idx = blockIdx.x * 256 + threadIdx.x;
@@ -66,10 +77,19 @@ __global__ __launch_bounds__(256) void unreal_pc_loss_kernel(const float* __rest
   if (idx < S * PP) {
     const int e = idx / PP, pix = idx - e * PP, cy = pix / kPcCells, cx = pix - cy * kPcCells;
     const int top = (H - kPcCells * kPcCellPx) / 2, left = (W - kPcCells * kPcCellPx) / 2;
-    const int64_t ob = ((int64_t)(T * S + e) * PP + pix) * A;
-    float R = q[ob];
-    for (int a = 1; a < A; ++a) R = fmaxf(R, q[ob + a]);
-    for (int a = 0; a < A; ++a) dq[ob + a] = 0.0f;
+    float v[8];
+    float* pb = p2 + ((int64_t)(T * S + e) * PP + pix) * 8;
+    pc_load8(pb, v);
+    float a = v[0];
+#pragma unroll
+    for (int c = 1; c < 8; ++c)
+      if (c == A) a = v[c];
+    float R = -INFINITY;
+#pragma unroll
+    for (int c = 0; c < 7; ++c)
+      if (c < A) R = fmaxf(R, (v[c] + a) - a);
+    reinterpret_cast<f4*>(pb)[0] = f4{0.f, 0.f, 0.f, 0.f};
+    reinterpret_cast<f4*>(pb)[1] = f4{0.f, 0.f, 0.f, 0.f};
     const uint8_t* fn = arena + (int64_t)rows_last[e] * frame_bytes;
     for (int t = T - 1; t >= 0; --t) {
       const int64_t r = (int64_t)t * E + e;
@@ -77,10 +97,22 @@ __global__ __launch_bounds__(256) void unreal_pc_loss_kernel(const float* __rest
       const float rew = pc_cell_change(f, fn, W, top, left, cy, cx);
       R = rew + (dones[r] ? 0.0f : gamma * R);
       const int act = actions[r];
-      const int64_t o = ((int64_t)(t * S + e) * PP + pix) * A;
-      const float d = q[o + act] - R;
+      float* pt = p2 + ((int64_t)(t * S + e) * PP + pix) * 8;
+      pc_load8(pt, v);
+      float at = v[0], va = v[0];
+#pragma unroll
+      for (int c = 1; c < 8; ++c) {
+        if (c == A) at = v[c];
+        if (c == act) va = v[c];
+      }
+      const float d = ((va + at) - at) - R;
       sq += d * d;
-      for (int a = 0; a < A; ++a) dq[o + a] = a == act ? 2.0f * coef * d : 0.0f;
+      const float g = va > 0.0f ? 2.0f * coef * d : 0.0f;
+      float o[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) o[c] = c == act ? g : 0.0f;
+      reinterpret_cast<f4*>(pt)[0] = f4{o[0], o[1], o[2], o[3]};
+      reinterpret_cast<f4*>(pt)[1] = f4{o[4], o[5], o[6], o[7]};
       fn = f;
     }
   }
@@ -174,18 +206,18 @@ using namespace vn;
 
 extern "C" {
 
-int vn_unreal_pc_loss_grad(const float* q, const int32_t* actions, const uint8_t* dones, const uint8_t* arena,
+int vn_unreal_pc_loss_grad(float* p2, const int32_t* actions, const uint8_t* dones, const uint8_t* arena,
                            int64_t frame_bytes, int height, int width, const int32_t* rows_img,
                            const int32_t* rows_last, int T, int E, int S, int num_actions, float gamma, float weight,
-                           float* dq, float* stats, vn_stream_t stream) {
-  if (!q || !actions || !dones || !arena || !rows_img || !rows_last || !dq || !stats || T <= 0 || S <= 0 || S > E ||
+                           float* stats, vn_stream_t stream) {
+  if (!p2 || !actions || !dones || !arena || !rows_img || !rows_last || !stats || T <= 0 || S <= 0 || S > E ||
       num_actions < 1 || num_actions > 7 || height < kPcCells * kPcCellPx || width < kPcCells * kPcCellPx ||
       frame_bytes < (int64_t)height * width * 3)
     return fail(VN_EINVAL, "vn_unreal_pc_loss_grad: bad args");
   const int n = S * kPcCells * kPcCells;
   const float coef = weight / ((float)T * n);
-  hipLaunchKernelGGL(unreal_pc_loss_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, q, actions, dones,
-                     arena, frame_bytes, height, width, rows_img, rows_last, T, E, S, num_actions, gamma, coef, dq,
+  hipLaunchKernelGGL(unreal_pc_loss_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, p2, actions,
+                     dones, arena, frame_bytes, height, width, rows_img, rows_last, T, E, S, num_actions, gamma, coef,
                      stats);
   VN_HIP(hipGetLastError());
   return VN_OK;

@@ -269,8 +269,7 @@ class A2CTrainer:
         kw = dict(dtype=torch.float32, device=self.device)
         n_pc = (T + 1) * S
         self.h_pc = torch.zeros((n_pc, 512), **kw)
-        self.pcb, self.pc_a1, self.pc_p2, self.pc_q = net.pc_buffers(n_pc)
-        self.pc_dq = torch.zeros_like(self.pc_q)
+        self.pcb, self.pc_a1, self.pc_p2, _ = net.pc_buffers(n_pc, with_q=False)
         self.dh_pc = torch.zeros((n_pc, 512), **kw)
         self.pc_ws = torch.empty(net.pc_workspace_floats(), **kw)
         F = net.fc_in
@@ -301,16 +300,17 @@ class A2CTrainer:
         self.h_pc[:T * S].view(T, S, 512).copy_(self.h_all.view(T, E, 512)[:, :S])
         self.h_pc[T * S:].copy_(self.boot_h[:S])
         n_pc = (T + 1) * S
-        net.pc_forward(self.params, self.h_pc, n_pc, self.pcb, self.pc_a1, self.pc_p2, self.pc_q, self.pc_ws)
+        net.pc_forward(self.params, self.h_pc, n_pc, self.pcb, self.pc_a1, self.pc_p2, None, self.pc_ws)
         H, W = self.env.frame_shape[:2]
         info = self.env._info
-        _lib.check(lib.vn_unreal_pc_loss_grad(P(self.pc_q), P(self.actions), P(self.dones), ctypes.c_void_p(self._arena),
+        # q formed from p2 in the loss kernel, which leaves dL/dp2 in p2 for the backward
+        _lib.check(lib.vn_unreal_pc_loss_grad(P(self.pc_p2), P(self.actions), P(self.dones), ctypes.c_void_p(self._arena),
                                               ctypes.c_int64(self._fb), H, W, P(self.rows_img), P(info["img_row"]),
                                               T, E, S, A, ctypes.c_float(self.pc_gamma),
-                                              ctypes.c_float(self.pc_weight), P(self.pc_dq), P(self.unreal_stats),
-                                              st), "vn_unreal_pc_loss_grad")
-        net.pc_backward(self.params, self.h_pc, n_pc, self.pcb, self.pc_a1, self.pc_p2, self.pc_dq, self.grads,
-                        self.dh_pc, self.pc_ws)
+                                              ctypes.c_float(self.pc_weight), P(self.unreal_stats), st),
+                   "vn_unreal_pc_loss_grad")
+        net.pc_backward(self.params, self.h_pc, n_pc, self.pcb, self.pc_a1, self.pc_p2, None, self.grads, self.dh_pc,
+                        self.pc_ws)
         # reward prediction on three consecutive conv_base maps of the first S envs
         F = net.fc_in
         x4 = net.x4(self.acts, N).view(T, E, F)

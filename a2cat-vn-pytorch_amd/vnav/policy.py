@@ -454,11 +454,12 @@ class PolicyNet:
         _lib.check(self.lib.vn_pc_workspace_floats(self._h, ctypes.byref(f)), "vn_pc_workspace_floats")
         return f.value
 
-    def pc_buffers(self, n):
-        """pcb [n,9,9,32], a1 [n,20,20,64], p2 [n,42,42,8], q [n,42,42,A]."""
+    def pc_buffers(self, n, with_q=True):
+        """pcb [n,9,9,32], a1 [n,20,20,64], p2 [n,42,42,8], q [n,42,42,A] (None without q)."""
         kw = dict(dtype=torch.float32, device=self.device)
         return (torch.empty((n, PC_MAP, PC_MAP, 32), **kw), torch.empty((n, PC_A1, PC_A1, 64), **kw),
-                torch.empty((n, PC_P, PC_P, 8), **kw), torch.empty((n, PC_P, PC_P, self.num_actions), **kw))
+                torch.empty((n, PC_P, PC_P, 8), **kw),
+                torch.empty((n, PC_P, PC_P, self.num_actions), **kw) if with_q else None)
 
     def pc_forward(self, params, h, n, pcb, a1, p2, q, workspace):
         P = _lib.ptr

@@ -60,6 +60,8 @@ def parse():
                    help="skip the 174x174 LSTM + aux-deconv train leg (the reference's logged experiment shape)")
     p.add_argument("--no-train-ref4", action="store_true",
                    help="skip the 4-env (the logged run's batch) 174x174 leg")
+    p.add_argument("--no-train-174", action="store_true",
+                   help="skip the 4096-env 174x174 leg only (the 4-env leg still runs)")
     p.add_argument("--no-c5", action="store_true",
                    help="skip the 300x400 + goal + aux-depth train leg (config C5, 512 envs per GPU)")
     p.add_argument("--num-steps", type=int, default=20, help="A2C rollout length (reference: 20)")
@@ -369,7 +371,7 @@ LEG_ORDER = ("84", "ff", "174", "ref4", "c5")
 
 
 def leg_enabled(args, leg, world):
-    return {"84": not args.no_train_84, "ff": not args.no_train_ff, "174": not args.no_train_ref,
+    return {"84": not args.no_train_84, "ff": not args.no_train_ff, "174": not args.no_train_ref and not args.no_train_174,
             "ref4": not args.no_train_ref and not args.no_train_ref4 and world == 1, "c5": not args.no_c5}[leg]
 
 

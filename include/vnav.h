@@ -343,12 +343,13 @@ int vn_policy_unreal_info(vn_policy* p, int64_t* info8);
 int vn_pc_workspace_floats(vn_policy* p, int64_t* floats);
 /* pixel_control (goal.py:131-137) on feature rows h [n][512] (the LSTM outputs): writes
  * pcb [n][9][9][32], a1 [n][20][20][64], p2 [n][42][42][8] (kept for the backward) and
- * q [n][42][42][A] = (pc_value + pc_action) - mean_c(pc_action). */
+ * q [n][42][42][A] = (pc_value + pc_action) - mean_c(pc_action) (q may be NULL: not formed). */
 int vn_pc_forward(vn_policy* p, const float* params, const float* h, int n, float* pcb, float* a1, float* p2,
                   float* q, float* workspace, vn_stream_t stream);
-/* From dL/dq [n][42][42][A]: the pixel-control parameter gradients into grads (overwritten)
- * and dL/dh [n][512] into dh (stored, or added to dh when accumulate != 0). Consumes pcb, a1
- * and p2 (overwritten by their gradients). */
+/* From dL/dq [n][42][42][A] (or dq == NULL: p2 already holds dL/dp2, as
+ * vn_unreal_pc_loss_grad leaves it): the pixel-control parameter gradients into grads
+ * (overwritten) and dL/dh [n][512] into dh (stored, or added to dh when accumulate != 0).
+ * Consumes pcb, a1 and p2 (overwritten by their gradients). */
 int vn_pc_backward(vn_policy* p, const float* params, const float* h, int n, float* pcb, float* a1, float* p2,
                    const float* dq, float* grads, float* dh, int accumulate, float* workspace, vn_stream_t stream);
 /* reward_prediction (goal.py:121-129): out [n][4] = logits of x [n][3 * FCIN] (column 3 unused). */
@@ -360,16 +361,17 @@ int vn_rp_backward(vn_policy* p, const float* params, const float* x, int n, con
 /* ---- UNREAL losses of the trainer (deep_rl's UnrealTrainer, absent: parity unpinned; the
  * published algorithm, csrc/vn_unreal_loss.hip, weights experiments/thor_cached_auxiliary.py:39-41) ----
  * Sequences are the first S envs of a rollout of T steps x E envs (rows t*E + e).
- * Pixel control: q [(T+1)*S][42][42][A] from vn_pc_forward on rows t*S + e (row T*S + e: the
- * bootstrap observation); pseudo-reward r_t = mean over each 4x4 cell and 3 channels of
- * |obs_{t+1} - obs_t| / 255 on the centre 168x168 crop of the u8 image frames (arena rows
- * rows_img[t*E + e], rows_last[e] for obs_T); R_T = max_a q_T, R_t = r_t + gamma (1 - done_t)
- * R_{t+1}; dq = weight * d mean((q_t[a_t] - R_t)^2) / dq (0 on the bootstrap rows);
- * stats[0] += sum of squared errors. */
-int vn_unreal_pc_loss_grad(const float* q, const int32_t* actions, const uint8_t* dones, const uint8_t* arena,
+ * Pixel control: p2 [(T+1)*S][42][42][8] from vn_pc_forward on rows t*S + e (row T*S + e: the
+ * bootstrap observation), q = (v + a) - a formed from it; pseudo-reward r_t = mean over each
+ * 4x4 cell and 3 channels of |obs_{t+1} - obs_t| / 255 on the centre 168x168 crop of the u8
+ * image frames (arena rows rows_img[t*E + e], rows_last[e] for obs_T); R_T = max_a q_T,
+ * R_t = r_t + gamma (1 - done_t) R_{t+1}; p2 is overwritten by dL/dp2 of weight *
+ * mean((q_t[a_t] - R_t)^2) (under the value ReLU; 0 on the bootstrap rows), ready for
+ * vn_pc_backward with dq == NULL; stats[0] += sum of squared errors. */
+int vn_unreal_pc_loss_grad(float* p2, const int32_t* actions, const uint8_t* dones, const uint8_t* arena,
                            int64_t frame_bytes, int height, int width, const int32_t* rows_img,
                            const int32_t* rows_last, int T, int E, int S, int num_actions, float gamma, float weight,
-                           float* dq, float* stats, vn_stream_t stream);
+                           float* stats, vn_stream_t stream);
 /* Reward prediction: logits [(T-2)*S][4] of samples j = (ts-2)*S + e (frames ts-2..ts of env
  * e); class of rewards[ts][e]: 0 (r = 0), 1 (r > 0), 2 (r < 0); samples with a done at ts-2
  * or ts-1 are skipped. dlogits = weight * d mean CE / dlogits; stats2 = (mean CE, count). */

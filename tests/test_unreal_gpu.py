@@ -159,22 +159,28 @@ def test_pc_loss_kernel_vs_oracle(hw):
     lib = _lib.load()
     c = _loss_case(H=hw[0], W=hw[1])
     T, E, S, A = c["T"], c["E"], c["S"], c["A"]
-    q = torch.rand(((T + 1) * S, 42, 42, A), generator=c["g"]) * 0.3
+    # the heads' maps after their ReLUs: value channels 0..A-1, action channel A, padding
+    p2 = torch.relu(torch.randn(((T + 1) * S, 42, 42, 8), generator=c["g"]) * 0.3)
+    p2[..., A + 1:] = 0.0
+    q = (p2[..., :A] + p2[..., A:A + 1]) - p2[..., A:A + 1]
     P = _lib.ptr
     d = {k: c[k].cuda() for k in ("arena", "rows_img", "rows_last", "actions", "dones")}
-    qd, dq = q.cuda(), torch.full_like(q, 7.0).cuda()
+    dp2 = p2.cuda()
     stats = torch.zeros(1, device="cuda")
     w = 0.05
-    _lib.check(lib.vn_unreal_pc_loss_grad(P(qd), P(d["actions"]), P(d["dones"]), P(d["arena"]),
+    _lib.check(lib.vn_unreal_pc_loss_grad(P(dp2), P(d["actions"]), P(d["dones"]), P(d["arena"]),
                                           hw[0] * hw[1] * 3, hw[0], hw[1], P(d["rows_img"]), P(d["rows_last"]), T, E, S,
-                                          A, ctypes_float(0.9), ctypes_float(w), P(dq), P(stats), None), "pc loss")
+                                          A, ctypes_float(0.9), ctypes_float(w), P(stats), None), "pc loss")
     torch.cuda.synchronize()
     # oracle on the first S envs: frames t = 0..T-1 from the rollout rows, t = T the last obs
     rows = torch.cat((c["rows_img"].view(T, E)[:, :S], c["rows_last"][None, :S])).long()
     frames = c["arena"][rows]
     loss, grad = unreal.pc_loss(q.view(T + 1, S, 42, 42, A), frames, c["actions"].view(T, E)[:, :S],
                                 c["dones"][:, :S])
-    _close(dq.cpu().view(T + 1, S, 42, 42, A).numpy() / w, grad.numpy(), 1e-5, "dq")
+    # dL/dp2: the q gradient under the value channels' ReLU, 0 on the action channel and padding
+    want = torch.zeros((T + 1, S, 42, 42, 8), dtype=torch.float64)
+    want[..., :A] = grad * (p2.view(T + 1, S, 42, 42, 8)[..., :A] > 0)
+    _close(dp2.cpu().view(T + 1, S, 42, 42, 8).numpy() / w, want.numpy(), 1e-5, "dp2")
     np.testing.assert_allclose(stats.item() / (T * S * 42 * 42), loss.item(), rtol=1e-5)
 
 
