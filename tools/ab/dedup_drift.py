@@ -42,8 +42,8 @@ for u in range(U):
     same_actions = same_actions and bool(torch.equal(a.actions, b.actions))
     scale = float(b.params.abs().max())
     d = float((a.params - b.params).abs().max()) / scale
-    g = a.goal_count.cpu().numpy()
     T = a.num_steps
+    g = a.goal_count.cpu().numpy() if a.dedup_goals else np.full(T + 1, E)
     if u < 5 or u % 5 == 4:
         print("update %3d  param diff %.3g of scale  actions identical so far: %s  ep.len %.2f / %.2f  "
               "goal frames computed %.3f" % (u + 1, d, same_actions, ma["episode_length"], mb["episode_length"],
