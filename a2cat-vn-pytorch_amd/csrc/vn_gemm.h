@@ -335,34 +335,9 @@ __device__ __forceinline__ void commit_trans_x6(const f4* r, uint16_t* s, int ti
   }
 }
 
-// A loader whose rows arrive already split (kPreSplit: the three bf16 planes of a weight
-// matrix, split once per call by the same truncation chain): its fetch fills three f4 (8 k
-// of each plane) per slot of 8 k, and commit copies them into the planes without VALU work.
-template <class L, class = void>
-struct has_presplit : std::false_type {};
-template <class L>
-struct has_presplit<L, std::void_t<decltype(L::kPreSplit)>> : std::bool_constant<L::kPreSplit> {};
-
-template <int ROWS, int BK, int LDK>
-__device__ __forceinline__ void commit_presplit_x6(const f4* r, uint16_t* s, int tid) {
-  constexpr int Q = BK / 8, T = ROWS * Q, NS = (T + 255) / 256, PLANE = ROWS * LDK;
-#pragma unroll
-  for (int j = 0; j < NS; ++j) {
-    const int i = tid + j * 256;
-    if (T % 256 == 0 || i < T) {
-      const int rr = i / Q, q = i - (i / Q) * Q;
-      uint16_t* d = s + rr * LDK + 8 * q;
-#pragma unroll
-      for (int t = 0; t < 3; ++t) *reinterpret_cast<f4*>(d + t * PLANE) = r[3 * j + t];
-    }
-  }
-}
-
 template <int ROWS, int BK, int LDK, class L>
 __device__ __forceinline__ void commit_x6(const f4* r, uint16_t* s, int tid) {
-  if constexpr (has_presplit<L>::value)
-    commit_presplit_x6<ROWS, BK, LDK>(r, s, tid);
-  else if constexpr (L::kTrans)
+  if constexpr (L::kTrans)
     commit_trans_x6<ROWS, BK>(r, s, tid);
   else
     commit_rows_x6<ROWS, BK, LDK>(r, s, tid);
@@ -393,8 +368,8 @@ __global__ __launch_bounds__(256) void gemm_x6_kernel(FA fa, FB fb, EP ep, int M
   constexpr int LDK = BK + 8;
   constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
   static_assert(TM >= 1 && TN >= 1, "tile too small for the wave layout");
-  constexpr int NA = (FA::template slots<BM, BK>() + 255) / 256 * (has_presplit<FA>::value ? 3 : 1);
-  constexpr int NB = (FB::template slots<BN, BK>() + 255) / 256 * (has_presplit<FB>::value ? 3 : 1);
+  constexpr int NA = (FA::template slots<BM, BK>() + 255) / 256;
+  constexpr int NB = (FB::template slots<BN, BK>() + 255) / 256;
   // row-major planes [term][row][LDK], or k-major [term][k][trans_ld(rows)] for a transposing loader
   constexpr int LTA = trans_ld(BM), LTB = trans_ld(BN);
   constexpr int PA = FA::kTrans ? BK * LTA : BM * LDK, PB = FB::kTrans ? BK * LTB : BN * LDK;

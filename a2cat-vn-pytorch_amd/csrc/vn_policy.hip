@@ -253,36 +253,6 @@ struct DenseRows {
   VN_ROWS_LOADER
 };
 
-// Weight rows already split into three bf16 planes P[t][m][ld] (split_set_kernel: the chain
-// commit_rows_x6 applies, so the product is bit-identical to DenseRows over the fp32 matrix).
-// One slot = 8 k of one row in all three planes; K and ld are multiples of 8.
-struct SplitRows {
-  const uint16_t* P;
-  int64_t ld, plane;
-  int M;
-  static constexpr bool kTrans = false;
-  static constexpr bool kPreSplit = true;
-  template <int ROWS, int BK>
-  static constexpr int slots() { return ROWS * (BK / 8); }
-  template <int ROWS, int BK>
-  __device__ __forceinline__ void fetch(f4* r, int r0, int k0, int ke, int tid) const {
-    constexpr int Q = BK / 8, T = ROWS * Q, NS = (T + 255) / 256;
-#pragma unroll
-    for (int j = 0; j < NS; ++j) {
-      const int i = tid + j * 256;
-      const int rr = i / Q, q = i - (i / Q) * Q;
-      const int m = r0 + rr, k = k0 + 8 * q;
-      const bool ok = (T % 256 == 0 || i < T) && m < M && k < ke;
-      const uint16_t* src = P + (int64_t)(ok ? m : 0) * ld + (ok ? k : 0);
-#pragma unroll
-      for (int t = 0; t < 3; ++t) {
-        const f4 v = *reinterpret_cast<const f4*>(src + t * plane);
-        r[3 * j + t] = ok ? v : f4zero();
-      }
-    }
-  }
-};
-
 // Row-major rows [0, M) of A plus a ones row at m == M (k < kend): the transposed input
 // of a row-fill wgrad, whose ones row gives the bias gradient column.
 struct RowsOnes {
@@ -573,52 +543,6 @@ __global__ __launch_bounds__(256) void tile_transpose_kernel(const float* __rest
   }
 }
 
-// Up to 4 weight matrices [rows][cols] (fp32) split into bf16 planes [3][rows][cols] (the
-// SplitRows operand), one launch; thread = 4 consecutive elements of one matrix.
-constexpr int kSplitSet = 4;
-struct SplitSet {
-  const float* W[kSplitSet];
-  uint16_t* P[kSplitSet];
-  int64_t n4[kSplitSet + 1];  // prefix counts of float4 groups
-  int n = 0;
-  void add(const float* w, int64_t elems, uint16_t* p) {
-    if (n == 0) n4[0] = 0;
-    W[n] = w;
-    P[n] = p;
-    n4[n + 1] = n4[n] + elems / 4;
-    ++n;
-  }
-};
-
-__global__ __launch_bounds__(256) void split_set_kernel(SplitSet ss) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= ss.n4[ss.n]) return;
-  int m = 0;
-#pragma unroll
-  for (int k = 1; k < kSplitSet; ++k)
-    if (k < ss.n && i >= ss.n4[k]) m = k;
-  const int64_t g = i - ss.n4[m];
-  const int64_t elems = (ss.n4[m + 1] - ss.n4[m]) * 4;
-  const f4 v = reinterpret_cast<const f4*>(ss.W[m])[g];
-  uint32_t t0[4], t1[4], t2[4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    float r1, r2, r3;
-    t0[e] = bf16_split_bits(v[e], r1);
-    t1[e] = bf16_split_bits(r1, r2);
-    t2[e] = bf16_split_bits(r2, r3);
-  }
-  uint16_t* d = ss.P[m] + 4 * g;
-  *reinterpret_cast<uint2*>(d) = uint2{t0[0] | (t0[1] << 16), t0[2] | (t0[3] << 16)};
-  *reinterpret_cast<uint2*>(d + elems) = uint2{t1[0] | (t1[1] << 16), t1[2] | (t1[3] << 16)};
-  *reinterpret_cast<uint2*>(d + 2 * elems) = uint2{t2[0] | (t2[1] << 16), t2[2] | (t2[3] << 16)};
-}
-
-inline void launch_split_set(const SplitSet& ss, hipStream_t st) {
-  if (ss.n == 0) return;
-  hipLaunchKernelGGL(split_set_kernel, dim3((unsigned)((ss.n4[ss.n] + 255) / 256)), dim3(256), 0, st, ss);
-}
-
 inline void tile_transpose(const float* src, int rows, int cols, int64_t lds, float* dst, int64_t ldd,
                            hipStream_t st) {
   hipLaunchKernelGGL(tile_transpose_kernel, dim3((cols + 63) / 64, (rows + 63) / 64), dim3(256), 0, st, src, rows, cols,
@@ -626,8 +550,6 @@ inline void tile_transpose(const float* src, int rows, int cols, int64_t lds, fl
 }
 
 // ---- geometry & layout ------------------------------------------------------------
-constexpr int kPresplitRows = 256;  // forward batches from which the weight operands are split per call
-
 struct LayerOff {
   int64_t w, b;
   int cout, kp;
@@ -657,10 +579,6 @@ struct PolicyLayout {
   float* sk;
   int64_t sk_cap;  // floats
   int sk_dev;
-  // the forward's weight operands split once per call into bf16 planes (SplitRows; BigGoalHouseModel
-  // only): conv2 W [32][512], conv3 W [64][1024], conv_merge W [512][FCIN], each [3][rows][K]
-  uint16_t* ws;
-  int64_t ws_w2, ws_w3, ws_fc, ws_lw, ws_elems;  // ws_lw: the LSTM's W_cat [3][2048][xcat]
 };
 
 inline PolicyLayout make_layout(int H, int W, int A, int lstm = 0, int aux = 0, int arch = 0, int unreal = 0) {
@@ -751,12 +669,6 @@ inline PolicyLayout make_layout(int H, int W, int A, int lstm = 0, int aux = 0, 
   }
   L.n_params = off;
   L.wt_total = wt;
-  L.ws = nullptr;
-  L.ws_w2 = 0;
-  L.ws_w3 = L.ws_w2 + 3ll * 32 * 512;
-  L.ws_fc = L.ws_w3 + 3ll * 64 * 1024;
-  L.ws_lw = L.ws_fc + 3ll * 512 * L.FCIN;
-  L.ws_elems = arch == 1 ? 0 : L.ws_lw + (lstm ? 3ll * 2048 * L.xcat : 0);
   if (arch == 1) {  // X1 (one frame per sample), X2, X3, no X4, X5; no ReLU bitmask
     L.sz[0] = (int64_t)L.OH1 * L.OW1 * 32;
     L.sz[1] = (int64_t)L.OH2 * L.OW2 * 64;
@@ -1634,21 +1546,6 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
   const int A1 = L.A + 1;
   // goal runs: the goal frames of run starts only (checked by the caller: goal_runs_ok, u8 frames)
   const FrameList fl = gr ? FrameList{gr->goal_list, gr->goal_count, n} : FrameList{};
-  // training batches: the weight operands of the generic products (conv2, conv3, conv_merge)
-  // split once per call instead of once per tile (bit-identical; VN_NO_PRESPLIT: per tile)
-  int dev = -1;
-  const bool presplit = L.ws && n >= kPresplitRows && hipGetDevice(&dev) == hipSuccess && dev == L.sk_dev &&
-                        !getenv("VN_NO_PRESPLIT");  // read per call (A/B and parity checks)
-  if (presplit) {
-    SplitSet ss;
-    ss.add(P + L.l[1].w, 32ll * 512, L.ws + L.ws_w2);
-    ss.add(P + L.l[2].w, 64ll * 1024, L.ws + L.ws_w3);
-    ss.add(P + L.l[4].w, 512ll * G::FCIN, L.ws + L.ws_fc);
-    launch_split_set(ss, st);
-  }
-  const SplitRows w2s{L.ws + L.ws_w2, 512, 32ll * 512, 32};
-  const SplitRows w3s{L.ws + L.ws_w3, 1024, 64ll * 1024, 64};
-  const SplitRows wfs{L.ws + L.ws_fc, G::FCIN, 512ll * G::FCIN, 512};
   // conv1 (frames -> X1), 2n frames. u8 frames take the split-bf16 kernel (bands of
   // output rows staged in LDS), else the f32 LDS-frame kernel; dense float frames take the
   // generic im2col path.
@@ -1729,18 +1626,12 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
       FrameListIm2col<G::OH1, G::OW1, G::OH2, G::OW2> fa{a.X[0], 2 * n * G::OH2 * G::OW2, fl};
       DenseRows fb{P + L.l[1].w, 512, 32};
       EpiBiasActFrames<G::OH2, G::OW2> ep{a.X[1], P + L.l[1].b, fl};
-      if (presplit)
-        launch_gemm_x6<128, 32, 32, 4, 1>(fa, w2s, ep, fa.M, 32, 512, st);
-      else
-        launch_gemm_x6<128, 32, 32, 4, 1>(fa, fb, ep, fa.M, 32, 512, st);
+      launch_gemm_x6<128, 32, 32, 4, 1>(fa, fb, ep, fa.M, 32, 512, st);
     } else if (!done) {
       NhwcIm2col<32, 4, 4, 2, G::OH1, G::OW1, G::OH2, G::OW2, 1> fa{a.X[0], 2 * n * G::OH2 * G::OW2};
       DenseRows fb{P + L.l[1].w, 512, 32};
       EpiBiasAct ep{a.X[1], 32, P + L.l[1].b, 1};
-      if (presplit)
-        launch_gemm_x6_sk<128, 32, 32, 4, 1>(fa, w2s, ep, fa.M, 32, 512, st, L);
-      else
-        launch_gemm_x6_sk<128, 32, 32, 4, 1>(fa, fb, ep, fa.M, 32, 512, st, L);
+      launch_gemm_x6_sk<128, 32, 32, 4, 1>(fa, fb, ep, fa.M, 32, 512, st, L);
     }
   }
   // conv3 + conv4 of a few envs: one launch (vn_skinny.h)
@@ -1756,17 +1647,11 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
   if (!small34) {
     DenseRows fb{P + L.l[2].w, 1024, 64};
     EpiBiasAct ep{a.X[2], 64, P + L.l[2].b, 1};
-    auto conv3b = [&](auto fa, auto b) {
-      if constexpr (G::OH3 * G::OW3 >= 64)  // 174x174, 300x400: 128-row tiles (A split over more MFMAs)
-        launch_gemm_x6_sk<128, 64, 32, 2, 2>(fa, b, ep, fa.M, 64, 1024, st, L);
-      else  // 84x84: 3x3 maps, 64-row tiles keep >= 2 tiles per CU
-        launch_gemm_x6_sk<64, 64, 32, 2, 2>(fa, b, ep, fa.M, 64, 1024, st, L);
-    };
     auto conv3 = [&](auto fa) {
-      if (presplit)
-        conv3b(fa, w3s);
-      else
-        conv3b(fa, fb);
+      if constexpr (G::OH3 * G::OW3 >= 64)  // 174x174, 300x400: 128-row tiles (A split over more MFMAs)
+        launch_gemm_x6_sk<128, 64, 32, 2, 2>(fa, fb, ep, fa.M, 64, 1024, st, L);
+      else  // 84x84: 3x3 maps, 64-row tiles keep >= 2 tiles per CU
+        launch_gemm_x6_sk<64, 64, 32, 2, 2>(fa, fb, ep, fa.M, 64, 1024, st, L);
     };
     if (gr) {
       if constexpr (kGoalRunsGeo<H0, W0>)
@@ -1790,10 +1675,7 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
     } else {
       DenseRows fa{a.X[3], G::FCIN, n};
       DenseRows fb{P + L.l[4].w, G::FCIN, 512};
-      if (presplit)
-        launch_gemm_x6_sk<64, 64, 32, 2, 2>(fa, wfs, ep, n, 512, G::FCIN, st, L);
-      else
-        launch_gemm_x6_sk<64, 64, 32, 2, 2>(fa, fb, ep, n, 512, G::FCIN, st, L);
+      launch_gemm_x6_sk<64, 64, 32, 2, 2>(fa, fb, ep, n, 512, G::FCIN, st, L);
     }
   }
   // heads (X5 -> out[n][8]: logits, value); out == NULL runs the trunk only (recurrent policy)
@@ -1877,27 +1759,13 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
   {
     DenseRows fa{dz5, 512, n};
     DenseRows fb{T(4), 512, G::FCIN};  // WT [FCIN][512]
-    // training batches: WT split once (into the forward's conv_merge planes, free until the
-    // next forward re-splits them; bit-identical)
-    int dev = -1;
-    const bool presplit = L.ws && n >= kPresplitRows && hipGetDevice(&dev) == hipSuccess && dev == L.sk_dev &&
-                          !getenv("VN_NO_PRESPLIT");  // read per call (A/B and parity checks)
-    const SplitRows wts{L.ws + L.ws_fc, 512, 512ll * G::FCIN, G::FCIN};
-    if (presplit) {
-      SplitSet ss;
-      ss.add(T(4), 512ll * G::FCIN, L.ws + L.ws_fc);
-      launch_split_set(ss, st);
+    if (dx4_extra) {  // + the aux heads' gradient w.r.t. X4, under the same ReLU mask
+      EpiMaskAdd ep{w.dz4, a.X[3], G::FCIN, dx4_extra};
+      launch_gemm_x6<64, 64, 32, 2, 2>(fa, fb, ep, n, G::FCIN, 512, st);
+    } else {
+      EpiMask ep{w.dz4, a.X[3], G::FCIN};
+      launch_gemm_x6<64, 64, 32, 2, 2>(fa, fb, ep, n, G::FCIN, 512, st);
     }
-    auto dgrad = [&](auto ep) {
-      if (presplit)
-        launch_gemm_x6<64, 64, 32, 2, 2>(fa, wts, ep, n, G::FCIN, 512, st);
-      else
-        launch_gemm_x6<64, 64, 32, 2, 2>(fa, fb, ep, n, G::FCIN, 512, st);
-    };
-    if (dx4_extra)  // + the aux heads' gradient w.r.t. X4, under the same ReLU mask
-      dgrad(EpiMaskAdd{w.dz4, a.X[3], G::FCIN, dx4_extra});
-    else
-      dgrad(EpiMask{w.dz4, a.X[3], G::FCIN});
     Im2colT<DenseRows> fbw{DenseRows{a.X[3], G::FCIN, n}, G::FCIN};
     launch_wgrad6<128, 128, 2, 2>(dz5, 512, 512, fbw, G::FCIN, n, w.slab, w.slab_cap, Gr + L.l[4].w, Gr + L.l[4].b,
                                   st);
@@ -2194,18 +2062,7 @@ inline int lstm_forward_step(const PolicyLayout& L, const float* P, int E, const
     DenseRows fa{xc, L.xcat, E};
     DenseRows fb{P + L.lw, L.xcat, 2048};
     EpiBias2 ep{gates, 2048, P + L.lbih, P + L.lbhh};
-    int dev = -1;
-    const bool presplit = L.ws && E >= kPresplitRows && hipGetDevice(&dev) == hipSuccess && dev == L.sk_dev &&
-                          !getenv("VN_NO_PRESPLIT");  // read per call (A/B and parity checks)
-    if (presplit) {  // W_cat split once per step instead of once per tile (bit-identical)
-      SplitSet ss;
-      ss.add(P + L.lw, 2048ll * L.xcat, L.ws + L.ws_lw);
-      launch_split_set(ss, st);
-      launch_gemm_x6_sk<128, 128, 32, 2, 2>(fa, SplitRows{L.ws + L.ws_lw, L.xcat, 2048ll * L.xcat, 2048}, ep, E, 2048,
-                                            L.xcat, st, L);
-    } else {
-      launch_gemm_x6_sk<128, 128, 32, 2, 2>(fa, fb, ep, E, 2048, L.xcat, st, L);
-    }
+    launch_gemm_x6_sk<128, 128, 32, 2, 2>(fa, fb, ep, E, 2048, L.xcat, st, L);
   }
   const int64_t nc = (int64_t)E * 512;
   hipLaunchKernelGGL(lstm_cell_kernel, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, st, E, gates, c_prev, mask,
@@ -2302,20 +2159,6 @@ inline int lstm_backward(const PolicyLayout& L, const float* P, int T, int E, co
                        extra_envs, 512, w.dh_heads);
   }
   const unsigned cb = (unsigned)((e512 + 255) / 256);
-  // training batches: W_ih^T (x5 rows) and W_hh^T split once per update for the per-step dh
-  // products and the trunk's dz5 product (bit-identical; the forward's W_cat planes are free
-  // until the next rollout re-splits them)
-  int dev = -1;
-  const bool presplit = L.ws && E > kSkinnyRows && E >= kPresplitRows && hipGetDevice(&dev) == hipSuccess &&
-                        dev == L.sk_dev && !getenv("VN_NO_PRESPLIT");  // read per call (A/B and parity checks)
-  const int64_t pl = 512ll * 2048;
-  const SplitRows wih_s{L.ws + L.ws_lw, 2048, pl, 512}, whh_s{L.ws + L.ws_lw + 3 * pl, 2048, pl, 512};
-  if (presplit) {
-    SplitSet ss;
-    ss.add(w.wcat_t, pl, L.ws + L.ws_lw);
-    ss.add(w.wcat_t + (int64_t)L.xoff * 2048, pl, L.ws + L.ws_lw + 3 * pl);
-    launch_split_set(ss, st);
-  }
   if (E <= kSkinnyRows) {
     // a few envs: the cell backward of the last step, then per step t one launch with the
     // sequential product dh_{t-1} = m_t (dgates_t W_hh) and step t-1's cell backward
@@ -2361,10 +2204,7 @@ inline int lstm_backward(const PolicyLayout& L, const float* P, int T, int E, co
     DenseRows fa{dg, 2048, E};
     DenseRows fb{w.wcat_t + (int64_t)L.xoff * 2048, 2048, 512};
     EpiLstmDh ep{w.dh[cur], mask};
-    if (presplit)
-      launch_gemm_x6_sk<64, 64, 32, 2, 2>(fa, whh_s, ep, E, 512, 2048, st, L);
-    else
-      launch_gemm_x6_sk<64, 64, 32, 2, 2>(fa, fb, ep, E, 512, 2048, st, L);
+    launch_gemm_x6_sk<64, 64, 32, 2, 2>(fa, fb, ep, E, 512, 2048, st, L);
   }
   {  // the trunk's input gradient of all T steps in one product: dz5 = relu'(x5) (dgates x W_ih[:, :512])
     DenseRows fa{w.dgates, 2048, N};
@@ -2372,10 +2212,7 @@ inline int lstm_backward(const PolicyLayout& L, const float* P, int T, int E, co
     EpiMask ep{dz5, x5_all, 512};
     // split-K below 128 tiles: the logged run's 80 rows make 4 tiles, each walking K = 2048
     // alone (0.14 ms, 6 % of its update); bench batches have thousands of tiles and run as before
-    if (presplit)
-      launch_gemm_x6_sk<128, 128, 32, 2, 2>(fa, wih_s, ep, N, 512, 2048, st, L);
-    else
-      launch_gemm_x6_sk<128, 128, 32, 2, 2>(fa, fb, ep, N, 512, 2048, st, L);
+    launch_gemm_x6_sk<128, 128, 32, 2, 2>(fa, fb, ep, N, 512, 2048, st, L);
   }
   {  // dW_cat = dgates^T x xcat over all T*E rows (x6 core on transposed copies, k = rows
      // contiguous); b_ih and b_hh share the bias gradient
@@ -2791,19 +2628,12 @@ int vn_policy_create_ex(int frame_h, int frame_w, int num_actions, int flags, vn
     p->L.sk = nullptr;
     (void)hipGetLastError();
   }
-  // pre-split weight planes (without them the forward splits the weights per tile, as before)
-  p->L.ws = nullptr;
-  if (p->L.ws_elems > 0 && p->L.sk && hipMalloc((void**)&p->L.ws, p->L.ws_elems * 2) != hipSuccess) {
-    p->L.ws = nullptr;
-    (void)hipGetLastError();
-  }
   *out = p;
   return VN_OK;
 }
 
 int vn_policy_destroy(vn_policy* p) {
   if (p && p->L.sk) (void)hipFree(p->L.sk);
-  if (p && p->L.ws) (void)hipFree(p->L.ws);
   delete p;
   return VN_OK;
 }
