@@ -1434,9 +1434,14 @@ inline int launch_conv_wgrad_x6(const float* dz, const float* X, int n, float* s
   return VN_OK;
 }
 
-// conv3: whole 9x9 / 3x3 dZ3 maps, images packed to >= 32 reduction pixels per item
+// conv3: whole 9x9 / 3x3 dZ3 maps, images packed to >= 32 reduction pixels per item; maps
+// whose planes do not fit (300x400: 17x23 under 36x48 X2) in bands of one dZ3 row (4 X2 rows),
+// two images per item (46 reduction pixels, 114 KB of planes)
 template <int IH, int IW, int OH, int OW>
-using Conv3Wg = WgSpec<IH, IW, OH, OW, 64, 2, OH, (OH * OW >= 32 ? 1 : 32 / (OH * OW))>;
+using Conv3WgWhole = WgSpec<IH, IW, OH, OW, 64, 2, OH, (OH * OW >= 32 ? 1 : 32 / (OH * OW))>;
+template <int IH, int IW, int OH, int OW>
+using Conv3Wg = std::conditional_t<Conv3WgWhole<IH, IW, OH, OW>::fits, Conv3WgWhole<IH, IW, OH, OW>,
+                                   WgSpec<IH, IW, OH, OW, 64, 2, 1, 2>>;
 // conv2: frames (image and goal) as images; bands of 4 dZ2 rows at 174x174 (X1 rows 10 x 42),
 // whole maps at 84x84
 template <int IH, int IW, int OH, int OW>

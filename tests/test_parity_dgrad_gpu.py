@@ -32,7 +32,8 @@ def _grads(pol, img, gl, cl, cv, generic):
 
 
 @pytest.mark.parametrize("switch", ["VN_DGRAD_GENERIC", "VN_WGRAD_GENERIC"])
-@pytest.mark.parametrize("hw,N", [((84, 84), 37), ((84, 84), 1030), ((174, 174), 5), ((174, 174), 300)])
+@pytest.mark.parametrize("hw,N", [((84, 84), 37), ((84, 84), 1030), ((174, 174), 5), ((174, 174), 300),
+                                  ((300, 400), 31)])
 def test_conv3_kernels_match_generic_products(hw, N, switch):
     """VN_DGRAD_GENERIC: conv3's input gradient; VN_WGRAD_GENERIC: conv3's weight and bias
     gradient (`conv3_wgrad_x6_kernel`, per-workgroup slabs + fixed-order reduce) against the
