@@ -376,6 +376,189 @@ __global__ __launch_bounds__(kAux2Threads) void aux_deconv2_kernel(const float* 
   }
 }
 
+// The same second layer for maps whose A1 does not fit the LDS (300x400: 36x48x48 floats per
+// sample): work item = (sample, band of BYC class rows yy), staging the BYC + 1 A1 rows its taps
+// read (rows yy - 1 .. yy + BYC - 1; rows outside the map read the zero pixel). Same lane
+// tasks (four output pixels XB apart), same sums in the same order (bit-identical to the
+// whole-map form), the next item's rows prefetched into registers.
+constexpr size_t aux2b_lds(int aw, int byc) { return (size_t)((byc + 1) * aw + 1) * kAux2Pst * 4 + kAux2Wfl * 4; }
+// class rows per band: the lane tasks of a band fit one pass of a wave pair (BYC x XB <= 128)
+// and the staged rows fit the LDS; 0 = no banded form
+template <int AW, int PW>
+constexpr int aux2_byc() {
+  constexpr int XB = (PW / 2 + kAux2Px - 1) / kAux2Px;
+  int b = 128 / XB;
+  // and the prefetch registers of a band's rows stay within the whole-map kernel's (11 f4)
+  while (b > 0 && (aux2b_lds(AW, b) > 150 * 1024 || ((b + 1) * AW * 12 + kAux2Threads - 1) / kAux2Threads > 11)) --b;
+  return b;
+}
+
+template <int AH, int AW, int PH, int PW, bool LOSS, int BYC>
+__global__ __launch_bounds__(kAux2Threads) void aux_deconv2_band_kernel(const float* __restrict__ A1, int n,
+                                                                         const float* __restrict__ W2,
+                                                                         const float* __restrict__ b2,
+                                                                         float* __restrict__ pred,
+                                                                         const f4* __restrict__ table,
+                                                                         const int32_t* __restrict__ img_rows,
+                                                                         const int32_t* __restrict__ goal_rows,
+                                                                         float weight, float* __restrict__ dpred,
+                                                                         float* __restrict__ stats) {
+  constexpr int NR = BYC + 1, NPX = NR * AW;                // staged rows, pixels (+ one zero pixel)
+  constexpr int HYC = PH / 2, WXC = PW / 2;
+  constexpr int NBAND = (HYC + BYC - 1) / BYC;
+  constexpr int XB = (WXC + kAux2Px - 1) / kAux2Px, RT = BYC * XB;
+  static_assert(PH == 2 * AH + 2 && PW == 2 * AW + 2, "k4 s2 transposed conv geometry");
+  extern __shared__ __attribute__((aligned(16))) float as_auxb[];
+  float* ws_aux = as_auxb + (NPX + 1) * kAux2Pst;  // [cls][tap = 2a + b][ci][8]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int cls = __builtin_amdgcn_readfirstlane(wave >> 1), py = cls >> 1, px = cls & 1;
+  for (int i = tid; i < 48; i += kAux2Threads) as_auxb[NPX * kAux2Pst + i] = 0.0f;
+  for (int i = tid; i < kAux2Wfl; i += kAux2Threads) {
+    const int c = i & 7, ci = (i >> 3) % kAuxC1, tap = (i / (8 * kAuxC1)) & 3, cl = i / (32 * kAuxC1);
+    const int ky = (cl >> 1) + 2 * (tap >> 1), kx = (cl & 1) + 2 * (tap & 1);
+    ws_aux[i] = W2[(ci * 4 + ky) * 32 + kx * 8 + c];
+  }
+  float bias[7];
+#pragma unroll
+  for (int c = 0; c < 7; ++c) bias[c] = b2[c];
+#pragma unroll
+  for (int c = 0; c < 7; ++c) asm volatile("" ::"v"(bias[c]));
+  const float inv[3] = {2.0f * weight / ((float)n * PH * PW), 2.0f * weight / (3.0f * n * PH * PW),
+                        2.0f * weight / (3.0f * n * PH * PW)};
+  float sq[3] = {0.0f, 0.0f, 0.0f};
+  constexpr int NV = (NPX * 12 + kAux2Threads - 1) / kAux2Threads;
+  f4 pre[NV];
+  // rows y0 - 1 .. y0 + BYC - 1 of sample s; rows outside the map load row 0 and stage zeros
+  auto load_item = [&](int it) {
+    const int s = it / NBAND, y0 = (it - (it / NBAND) * NBAND) * BYC;
+    const f4* src = reinterpret_cast<const f4*>(A1 + (int64_t)s * AH * AW * kAuxC1);
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int i = min(tid + j * kAux2Threads, NPX * 12 - 1);
+      const int r = i / (AW * 12), rem = i - r * (AW * 12);
+      const int iy = y0 - 1 + r;
+      const f4 v = src[(int64_t)(iy >= 0 && iy < AH ? iy : 0) * AW * 12 + rem];
+      pre[j] = (iy >= 0 && iy < AH) ? v : f4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  const int n_items = n * NBAND;
+  if ((int)blockIdx.x < n_items) load_item(blockIdx.x);
+  for (int it = blockIdx.x; it < n_items; it += gridDim.x) {
+    const int s = it / NBAND, y0 = (it - (it / NBAND) * NBAND) * BYC;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int i = tid + j * kAux2Threads;
+      if (i < NPX * 12) {
+        const int pxl = i / 12, c4 = i - (i / 12) * 12;
+        *reinterpret_cast<f4*>(as_auxb + pxl * kAux2Pst + 4 * c4) = pre[j];
+      }
+    }
+    __syncthreads();
+    if (it + (int)gridDim.x < n_items) load_item(it + gridDim.x);
+    for (int t = (wave & 1) * 64 + lane; t < RT; t += 128) {
+      const int yl = t / XB, xb = t - (t / XB) * XB, yy = y0 + yl;
+      if (yy >= HYC) continue;  // the last band's rows past the map
+      const int npx = (WXC - xb + XB - 1) / XB;
+      f4 ti[kAux2Px], tg[kAux2Px];
+      if constexpr (LOSS) {
+        const int64_t ib = (int64_t)img_rows[s] * PH * PW, gb = (int64_t)goal_rows[s] * PH * PW;
+#pragma unroll
+        for (int i = 0; i < kAux2Px; ++i) {
+          const int pix = (2 * yy + py) * PW + 2 * min(xb + i * XB, WXC - 1) + px;
+          ti[i] = table[ib + pix];
+          tg[i] = table[gb + pix];
+        }
+      }
+      float o[kAux2Px][7];
+#pragma unroll
+      for (int i = 0; i < kAux2Px; ++i)
+#pragma unroll
+        for (int c = 0; c < 7; ++c) o[i][c] = bias[c];
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const int iy = yy - a, rl = yl + 1 - a;  // staged row of iy
+          const float* ap[kAux2Px];
+#pragma unroll
+          for (int i = 0; i < kAux2Px; ++i) {
+            const int ix = xb + i * XB - b;
+            const bool ok = iy >= 0 && iy < AH && ix >= 0 && ix < AW;
+            ap[i] = as_auxb + (ok ? rl * AW + ix : NPX) * kAux2Pst;
+          }
+          const float* wl = ws_aux + ((cls * 4 + 2 * a + b) * kAuxC1) * 8;
+#pragma unroll
+          for (int hd = 0; hd < 3; ++hd)
+#pragma unroll 2
+            for (int kq = 0; kq < 4; ++kq) {
+              const int k = 4 * hd + kq;
+              f4 av[kAux2Px];
+#pragma unroll
+              for (int i = 0; i < kAux2Px; ++i) av[i] = *reinterpret_cast<const f4*>(ap[i] + 4 * k);
+#pragma unroll
+              for (int jj = 0; jj < 4; ++jj) {
+                const int ci = 4 * k + jj;
+                const f4 wv = reinterpret_cast<const f4*>(wl + ci * 8)[hd < 2 ? 0 : 1];
+#pragma unroll
+                for (int i = 0; i < kAux2Px; ++i) {
+                  if (hd == 0) {
+                    o[i][0] = fmaf(av[i][jj], wv[0], o[i][0]);
+                  } else if (hd == 1) {
+                    o[i][1] = fmaf(av[i][jj], wv[1], o[i][1]);
+                    o[i][2] = fmaf(av[i][jj], wv[2], o[i][2]);
+                    o[i][3] = fmaf(av[i][jj], wv[3], o[i][3]);
+                  } else {
+                    o[i][4] = fmaf(av[i][jj], wv[0], o[i][4]);
+                    o[i][5] = fmaf(av[i][jj], wv[1], o[i][5]);
+                    o[i][6] = fmaf(av[i][jj], wv[2], o[i][6]);
+                  }
+                }
+              }
+            }
+        }
+#pragma unroll
+      for (int i = 0; i < kAux2Px; ++i) {
+        if (i >= npx) break;
+        const int64_t pix = (int64_t)s * PH * PW + (2 * yy + py) * PW + 2 * (xb + i * XB) + px;
+        if constexpr (!LOSS) {
+          *reinterpret_cast<f4*>(pred + pix * kAuxC2) = f4{o[i][0], o[i][1], o[i][2], o[i][3]};
+          *reinterpret_cast<f4*>(pred + pix * kAuxC2 + 4) = f4{o[i][4], o[i][5], o[i][6], 0.0f};
+        } else {
+          const float tv[7] = {ti[i][0], ti[i][1], ti[i][2], ti[i][3], tg[i][1], tg[i][2], tg[i][3]};
+          float g[8];
+#pragma unroll
+          for (int c = 0; c < 7; ++c) {
+            const float d = o[i][c] - tv[c];
+            const int h = c == 0 ? 0 : (c <= 3 ? 1 : 2);
+            sq[h] += d * d;
+            g[c] = d * inv[h];
+          }
+          g[7] = 0.0f;
+          *reinterpret_cast<f4*>(dpred + pix * kAuxC2) = f4{g[0], g[1], g[2], g[3]};
+          *reinterpret_cast<f4*>(dpred + pix * kAuxC2 + 4) = f4{g[4], g[5], g[6], g[7]};
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if constexpr (LOSS) {
+    float* red = as_auxb;
+    constexpr int NWV = kAux2Threads / 64;
+#pragma unroll
+    for (int h = 0; h < 3; ++h) {
+      float v = sq[h];
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+      if (lane == 0) red[h * NWV + wave] = v;
+    }
+    __syncthreads();
+    if (tid < 3) {
+      float v = 0.0f;
+      for (int w = 0; w < NWV; ++w) v += red[tid * NWV + w];
+      if (v != 0.0f) atomicAdd(stats + tid, v);
+    }
+  }
+}
+
 // ---- fused second-layer backward ------------------------------------------------------
 // One pass over (A1, dP) per sample replaces four launches (dW2 product, dA1 product with
 // its ReLU mask, and the two bias column sums), and keeps the block-diagonal structure the
@@ -402,6 +585,17 @@ template <int AH, int AW, int PH, int PW>
 constexpr bool auxb_fits() {
   return (AH * AW) % 16 == 0 && auxb_lds<PH, PW>() <= 80 * 1024 && auxb_lds<PH, PW>() >= 7 * 4 * 64 * 4 + 64 * 4;
 }
+// Maps whose dP does not fit (300x400: 74x98x8) run in bands of BYA A1 rows over the 2 BYA + 2
+// dP rows under them: the largest BYA whose staged rows fit 80 KB with tiles (16 A1 pixels)
+// spread evenly over the 8 waves (0 = no banded form).
+constexpr size_t auxb_band_lds(int pw, int bya) { return (size_t)(2 * bya + 2) * pw * kAuxBDs * 4; }
+template <int AH, int AW, int PH, int PW>
+constexpr int auxb_bya() {
+  for (int b = AH; b >= 1; --b)
+    if ((b * AW) % 128 == 0 && auxb_band_lds(PW, b) <= 80 * 1024 && auxb_band_lds(PW, b) >= 7 * 4 * 64 * 4 + 64 * 4)
+      return b;
+  return 0;
+}
 
 // LDS offset (pixel stride kAuxBDs) of (tap, output channel) relative to a window corner.
 template <int PW>
@@ -409,14 +603,18 @@ __device__ __forceinline__ int auxb_tap_off(int tap, int co) {
   return ((tap >> 2) * PW + (tap & 3)) * kAuxBDs + co;
 }
 
-template <int AH, int AW, int PH, int PW>
+// BYA < AH: work item = (sample, band of BYA A1 rows), staging the 2 BYA + 2 dP rows the band's
+// windows read; db2 counts each dP row in one band only (its first 2 BYA rows; the last band
+// all of its rows). BYA = AH is the whole-map form.
+template <int AH, int AW, int PH, int PW, int BYA = AH>
 __global__ __launch_bounds__(kAuxBThreads, 4) void aux_backward2_kernel(float* __restrict__ A1,
                                                                         const float* __restrict__ dP, int n,
                                                                         const float* __restrict__ W2,
                                                                         float* __restrict__ part) {
-  constexpr int NPX = AH * AW, NT = NPX / 16, NPP = PH * PW;
-  static_assert(PH == 2 * AH + 2 && PW == 2 * AW + 2 && NPX % 16 == 0, "k4 s2 transposed conv geometry");
-  extern __shared__ __attribute__((aligned(16))) float dps[];  // [NPP][kAuxBDs]
+  constexpr int NBAND = (AH + BYA - 1) / BYA;
+  static_assert(PH == 2 * AH + 2 && PW == 2 * AW + 2 && (BYA * AW) % 16 == 0 &&
+                    ((AH - (NBAND - 1) * BYA) * AW) % 16 == 0, "k4 s2 transposed conv geometry, whole tiles per band");
+  extern __shared__ __attribute__((aligned(16))) float dps[];  // [dP rows of the band][PW][kAuxBDs]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l16 = lane & 15, lq = lane >> 4;
   // dA1 operands: step u of K (4 + 12 + 12 over the heads), lane k = 4u' + lq. The LDS
@@ -450,8 +648,13 @@ __global__ __launch_bounds__(kAuxBThreads, 4) void aux_backward2_kernel(float* _
   for (int q = 0; q < 7; ++q) accw[q] = f4zero();
   float db1[3] = {0.0f, 0.0f, 0.0f};
   f4 db2 = f4zero();
-  for (int s = blockIdx.x; s < n; s += gridDim.x) {
-    const f4* src = reinterpret_cast<const f4*>(dP + (int64_t)s * NPP * kAuxC2);
+  for (int it = blockIdx.x; it < n * NBAND; it += gridDim.x) {
+    const int s = it / NBAND, y0 = (it - (it / NBAND) * NBAND) * BYA;
+    const int rows = min(BYA, AH - y0);                 // A1 rows of the band
+    const int NPX = rows * AW, NT = NPX / 16;           // its pixels, tiles
+    const int NPP = (2 * rows + 2) * PW;                // dP pixels staged (rows 2 y0 ..)
+    const int NPPC = (y0 + rows == AH ? 2 * rows + 2 : 2 * rows) * PW;  // the ones db2 counts
+    const f4* src = reinterpret_cast<const f4*>(dP + ((int64_t)s * PH + 2 * y0) * PW * kAuxC2);
     for (int i = tid; i < NPP * 2; i += kAuxBThreads) {
       const f4 v = src[i];
       float* d = dps + (i >> 1) * kAuxBDs + (i & 1) * 4;
@@ -459,10 +662,10 @@ __global__ __launch_bounds__(kAuxBThreads, 4) void aux_backward2_kernel(float* _
       d[1] = v[1];
       d[2] = v[2];
       d[3] = v[3];
-      db2 += v;
+      if ((i >> 1) < NPPC) db2 += v;
     }
     __syncthreads();
-    float* a1 = A1 + (int64_t)s * NPX * kAuxC1;
+    float* a1 = A1 + ((int64_t)s * AH + y0) * AW * kAuxC1;
     for (int t = wave; t < NT; t += kAuxBThreads / 64) {
 #pragma unroll 2
       for (int ks = 0; ks < 4; ++ks) {  // dW2 over the tile's pixels, 4 per MFMA

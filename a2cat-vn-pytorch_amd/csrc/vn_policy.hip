@@ -2318,6 +2318,21 @@ inline void launch_aux2(const float* A1, int n, const float* W2, const float* b2
                      tg ? tg->goal_rows : nullptr, weight, dpred, stats);
 }
 
+// The banded second layer (maps too large for aux_deconv2_kernel's whole-map staging).
+template <int AH, int AW, int PH, int PW, bool LOSS>
+inline void launch_aux2_band(const float* A1, int n, const float* W2, const float* b2, float* pred,
+                             const vn_aux_targets* tg, float weight, float* dpred, float* stats, hipStream_t st) {
+  constexpr int BYC = aux2_byc<AW, PW>();
+  constexpr size_t lds = aux2b_lds(AW, BYC);
+  const void* kfn = (const void*)aux_deconv2_band_kernel<AH, AW, PH, PW, LOSS, BYC>;
+  (void)ensure_dyn_lds(kfn, lds);
+  const int items = n * ((PH / 2 + BYC - 1) / BYC);
+  const int blocks = std::min(items, resident_blocks(kfn, kAux2Threads, lds));
+  hipLaunchKernelGGL((aux_deconv2_band_kernel<AH, AW, PH, PW, LOSS, BYC>), dim3(blocks), dim3(kAux2Threads), lds, st,
+                     A1, n, W2, b2, pred, tg ? reinterpret_cast<const f4*>(tg->table) : nullptr,
+                     tg ? tg->image_rows : nullptr, tg ? tg->goal_rows : nullptr, weight, dpred, stats);
+}
+
 template <int H0, int W0>
 int aux_forward_impl(const PolicyLayout& L, const float* P, const float* X4, int n, float* A1, float* Pout,
                      const AuxWork& w, hipStream_t st) {
@@ -2332,6 +2347,8 @@ int aux_forward_impl(const PolicyLayout& L, const float* P, const float* X4, int
   if (const int rc = deconv_all<32, kAuxC1, IH, IW, AH, AW>(X4, w.w1t, A1, P + L.ab1, 1, n, st); rc != VN_OK) return rc;
   if constexpr (aux2_fits<AH, AW>()) {
     launch_aux2<AH, AW, PH, PW, false>(A1, n, P + L.aw2, P + L.ab2, Pout, nullptr, 0.0f, nullptr, nullptr, st);
+  } else if constexpr (aux2_byc<AW, PW>() > 0) {
+    launch_aux2_band<AH, AW, PH, PW, false>(A1, n, P + L.aw2, P + L.ab2, Pout, nullptr, 0.0f, nullptr, nullptr, st);
   } else {
     if (const int rc = deconv_all<kAuxC1, kAuxC2, AH, AW, PH, PW>(A1, w.w2t, Pout, P + L.ab2, 0, n, st); rc != VN_OK) return rc;
   }
@@ -2348,10 +2365,13 @@ int aux_forward_loss_impl(const PolicyLayout& L, const float* P, const float* X4
                           hipStream_t st) {
   using G = Geo<H0, W0>;
   constexpr int IH = G::OH3, IW = G::OW3, AH = 2 * IH + 2, AW = 2 * IW + 2, PH = 2 * AH + 2, PW = 2 * AW + 2;
-  if constexpr (aux2_fits<AH, AW>()) {
+  if constexpr (aux2_fits<AH, AW>() || aux2_byc<AW, PW>() > 0) {
     hipLaunchKernelGGL(transpose_kernel, dim3((32 * 768 + 255) / 256), dim3(256), 0, st, P + L.aw1, 32, 768, w.w1t);
     if (const int rc = deconv_all<32, kAuxC1, IH, IW, AH, AW>(X4, w.w1t, A1, P + L.ab1, 1, n, st); rc != VN_OK) return rc;
-    launch_aux2<AH, AW, PH, PW, true>(A1, n, P + L.aw2, P + L.ab2, nullptr, tg, weight, dpred, stats, st);
+    if constexpr (aux2_fits<AH, AW>())
+      launch_aux2<AH, AW, PH, PW, true>(A1, n, P + L.aw2, P + L.ab2, nullptr, tg, weight, dpred, stats, st);
+    else
+      launch_aux2_band<AH, AW, PH, PW, true>(A1, n, P + L.aw2, P + L.ab2, nullptr, tg, weight, dpred, stats, st);
   } else {
     const int rc = aux_forward_impl<H0, W0>(L, P, X4, n, A1, pred, w, st);
     if (rc != VN_OK) return rc;
@@ -2401,6 +2421,18 @@ int aux_backward_impl(const PolicyLayout& L, const float* P, const float* X4, in
     const int blocks = std::min(n, std::min(resident_blocks(kfn, kAuxBThreads, lds), kColsumBlocks));
     hipLaunchKernelGGL((aux_backward2_kernel<AH, AW, PH, PW>), dim3(blocks), dim3(kAuxBThreads), lds, st, A1, dP, n,
                        P + L.aw2, w.slab);
+    hipLaunchKernelGGL(aux_backward2_finish_kernel, dim3((kAuxC1 * 16 * kAuxC2 + kAuxC1 + kAuxC2 + 3) / 4),
+                       dim3(256), 0, st, w.slab, blocks, Gr + L.aw2, Gr + L.ab1, Gr + L.ab2);
+  } else if constexpr (auxb_bya<AH, AW, PH, PW>() > 0) {
+    // the same pass in bands of A1 rows (300x400: 8 rows over 18 dP rows, 64 KB)
+    constexpr int BYA = auxb_bya<AH, AW, PH, PW>();
+    const void* kfn = (const void*)aux_backward2_kernel<AH, AW, PH, PW, BYA>;
+    constexpr size_t lds = auxb_band_lds(PW, BYA);
+    VN_HIP(ensure_dyn_lds(kfn, lds));
+    const int items = n * ((AH + BYA - 1) / BYA);
+    const int blocks = std::min(items, std::min(resident_blocks(kfn, kAuxBThreads, lds), kColsumBlocks));
+    hipLaunchKernelGGL((aux_backward2_kernel<AH, AW, PH, PW, BYA>), dim3(blocks), dim3(kAuxBThreads), lds, st, A1, dP,
+                       n, P + L.aw2, w.slab);
     hipLaunchKernelGGL(aux_backward2_finish_kernel, dim3((kAuxC1 * 16 * kAuxC2 + kAuxC1 + kAuxC2 + 3) / 4),
                        dim3(256), 0, st, w.slab, blocks, Gr + L.aw2, Gr + L.ab1, Gr + L.ab2);
   } else {
