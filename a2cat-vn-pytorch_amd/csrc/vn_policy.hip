@@ -2441,7 +2441,9 @@ int aux_backward_impl(const PolicyLayout& L, const float* P, const float* X4, in
   // first layer: dW1 = X4^T x im2col(dA1); dX4 = conv(dA1, W1). The weight gradient is a
   // stride-2 k4 weight gradient with X4 as the reduced map and dA1 (48 channels) under it:
   // dW1[ci][tap][co] = sum X4[iy][ix][ci] dA1[2iy + ky][2ix + kx][co] (no bias column)
-  using Wa = WgSpec<AH, AW, IH, IW, 32, 1, IH, (IH * IW >= 32 ? 1 : 32 / (IH * IW)), kAuxC1, false>;
+  using WaWhole = WgSpec<AH, AW, IH, IW, 32, 1, IH, (IH * IW >= 32 ? 1 : 32 / (IH * IW)), kAuxC1, false>;
+  // maps whose planes do not fit (300x400): bands of one X4 row (4 A1 rows), two images per item
+  using Wa = std::conditional_t<WaWhole::fits, WaWhole, WgSpec<AH, AW, IH, IW, 32, 1, 1, 2, kAuxC1, false>>;
   if (Wa::fits && !getenv("VN_WGRAD_GENERIC")) {  // read per call (A/B and parity checks)
     if constexpr (Wa::fits) {
       const int rc = launch_conv_wgrad_x6<Wa>(X4, A1, n, w.slab, slab_floats(L), Gr + L.aw1, nullptr, st);

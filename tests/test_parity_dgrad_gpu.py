@@ -64,7 +64,7 @@ def test_conv3_kernels_match_generic_products(hw, N, switch):
 
 
 @pytest.mark.parametrize("switch", ["VN_DGRAD_GENERIC", "VN_WGRAD_GENERIC"])
-@pytest.mark.parametrize("hw,N", [((84, 84), 37), ((174, 174), 300), ((300, 400), 3)])
+@pytest.mark.parametrize("hw,N", [((84, 84), 37), ((174, 174), 300), ((300, 400), 3), ((300, 400), 31)])
 def test_aux_first_layer_matches_generic_products(hw, N, switch):
     """The aux heads' predictions and every parameter gradient of their MSE, both paths:
     VN_DGRAD_GENERIC for the first transposed conv's forward (parity kernel),
