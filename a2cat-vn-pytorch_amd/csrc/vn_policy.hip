@@ -1106,6 +1106,132 @@ __global__ __launch_bounds__(S::NT, S::NT >= 512 ? 1 : 2) void parity_dgrad_x6_k
   }
 }
 
+// The same product for maps whose planes do not fit whole (300x400: the 17x23x64 dZ3 map is 169
+// KB of planes): work item = (image, band of BY class rows yy), staging the BY + 1 map rows its
+// taps read (rows yy - 1 .. yy + BY - 1; rows outside the map read the zero row). Same
+// fragments and MFMA order per output (bit-identical to the whole-map form).
+template <class S, int BY>
+constexpr size_t parity_band_lds() {
+  return (size_t)3 * ((BY + 1) * S::SW + 1) * S::PS * 2;
+}
+
+template <class S, int BY, class EP>
+__global__ __launch_bounds__(S::NT, 1) void parity_dgrad_band_x6_kernel(const float* __restrict__ map,
+                                                                       const float* __restrict__ WT, EP ep, int n) {
+  constexpr int SH = S::SH, SW = S::SW, YC = S::YC, XC = S::XC, KC = S::KC, NCOL = S::NCOL, WPC = S::WPC;
+  constexpr int PS = S::PS, NTL = S::NTL, KS = S::KS, NT = S::NT;
+  constexpr int NB = (YC + BY - 1) / BY;                       // bands per image
+  constexpr int ROWS = (BY + 1) * SW, PL = (ROWS + 1) * PS, C4 = KC / 4;
+  constexpr int TILES = (BY * XC + 15) / 16, NZ = (ROWS * C4 + NT - 1) / NT;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem_pdb[];
+  uint16_t* zs = reinterpret_cast<uint16_t*>(smem_pdb);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int cls = wave / WPC, py = cls >> 1, px = cls & 1;
+  const int col0 = (wave % WPC) * NTL * 16;
+  const int i16 = lane & 15, q = lane >> 4;
+  bf16x8_t bw[4][KS][NTL][3];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int ky = py + 2 * (t >> 1), kx = px + 2 * (t & 1);
+#pragma unroll
+    for (int h = 0; h < KS; ++h)
+#pragma unroll
+      for (int nt = 0; nt < NTL; ++nt) {
+        union { uint16_t u[8]; bf16x8_t v; } b0, b1, b2;
+        const float* w = WT + ((int64_t)(ky * 4 + kx) * NCOL + col0 + 16 * nt + i16) * KC + 32 * h + 8 * q;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) split3_bf16(w[j], b0.u[j], b1.u[j], b2.u[j]);
+        bw[t][h][nt][0] = b0.v;
+        bw[t][h][nt][1] = b1.v;
+        bw[t][h][nt][2] = b2.v;
+      }
+  }
+  for (int i = tid; i < 3 * PS / 2; i += NT) {  // zero rows
+    const int pl = i / (PS / 2), e = i - pl * (PS / 2);
+    reinterpret_cast<uint32_t*>(zs + pl * PL + ROWS * PS)[e] = 0u;
+  }
+  const int items = n * NB;
+  for (int it = blockIdx.x; it < items; it += gridDim.x) {
+    const int img = it / NB, y0 = (it - (it / NB) * NB) * BY;
+    {  // map rows y0 - 1 .. y0 + BY - 1 of the image (rows outside the map stage zeros)
+      const f4* z4 = reinterpret_cast<const f4*>(map) + (int64_t)img * SH * SW * C4;
+#pragma unroll 2
+      for (int j = 0; j < NZ; ++j) {
+        const int i = tid + j * NT;
+        if (i < ROWS * C4) {
+          const int rp = i / C4, c = i - (i / C4) * C4;
+          const int oy = y0 - 1 + rp / SW;
+          const f4 v = (oy >= 0 && oy < SH) ? z4[((int64_t)oy * SW + rp % SW) * C4 + c] : f4zero();
+          uint2 t0, t1, t2;
+          split3_pack(v, t0, t1, t2);
+          uint16_t* d = zs + rp * PS + 4 * c;
+          *reinterpret_cast<uint2*>(d) = t0;
+          *reinterpret_cast<uint2*>(d + PL) = t1;
+          *reinterpret_cast<uint2*>(d + 2 * PL) = t2;
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int tile = 0; tile < TILES; ++tile) {
+      const int pc = tile * 16 + i16;  // this lane's class pixel (MFMA column) within the band
+      const int yl = pc / XC, xx = pc - (pc / XC) * XC, yy = y0 + yl;
+      const bool live = pc < BY * XC && yy < YC;
+      int off[4];
+#pragma unroll
+      for (int tap = 0; tap < 4; ++tap) {
+        const int oy = yy - (tap >> 1), ox = xx - (tap & 1);
+        const bool ok = live && oy >= 0 && oy < SH && ox >= 0 && ox < SW;
+        off[tap] = (ok ? (oy - y0 + 1) * SW + ox : ROWS) * PS + 8 * q;
+      }
+      f4 acc[NTL];
+#pragma unroll
+      for (int nt = 0; nt < NTL; ++nt) acc[nt] = f4zero();
+#pragma unroll
+      for (int tap = 0; tap < 4; ++tap)
+#pragma unroll
+        for (int h = 0; h < KS; ++h) {
+          bf16x8_t a[3];
+#pragma unroll
+          for (int tm = 0; tm < 3; ++tm) a[tm] = *reinterpret_cast<const bf16x8_t*>(zs + tm * PL + off[tap] + 32 * h);
+#pragma unroll
+          for (int nt = 0; nt < NTL; ++nt) {  // small terms first
+            f4 c = acc[nt];
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[tap][h][nt][0], a[2], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[tap][h][nt][2], a[0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[tap][h][nt][1], a[1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[tap][h][nt][0], a[1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[tap][h][nt][1], a[0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[tap][h][nt][0], a[0], c, 0, 0, 0);
+            acc[nt] = c;
+          }
+        }
+      if (live) {
+        const int y = 2 * yy + py, x = 2 * xx + px;
+        f4 pre[NTL];
+#pragma unroll
+        for (int nt = 0; nt < NTL; ++nt) pre[nt] = ep.pre(img, y, x, col0 + 16 * nt + 4 * q);
+#pragma unroll
+        for (int nt = 0; nt < NTL; ++nt) ep.post(img, y, x, col0 + 16 * nt + 4 * q, acc[nt], pre[nt]);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// class rows per band of the banded parity product: the bands the largest that fits 150 KB
+// needs, evened out (300x400: 18 class rows -> 2 bands of 9)
+template <class S>
+constexpr int parity_band_rows() {
+  int bmax = 0;
+  for (int b = S::YC; b >= 1 && bmax == 0; --b)
+    if (parity_band_lds<S, 1>() + (size_t)3 * (b - 1) * S::SW * S::PS * 2 <= 150 * 1024) bmax = b;
+  if (bmax == 0) return 0;
+  const int nb = (S::YC + bmax - 1) / bmax;
+  return (S::YC + nb - 1) / nb;
+}
+
 // conv3's input gradient: column c is channel c % 32 of input group c / 32 (X2 layout
 // [n][2][IH][IW][32]), masked by the ReLU that produced X2 (as EpiMaskParityG).
 // mask_goal == 0 (goal-frame deduplication): group 1 is left unmasked — a sample's goal map
@@ -1471,10 +1597,22 @@ inline int dgrad_all_classes_groups(const float* dz, const float* WT, float* out
   // VN_DGRAD_GENERIC set: the four class products instead (A/B and parity checks; read per
   // call, once per backward)
   const bool generic = getenv("VN_DGRAD_GENERIC") != nullptr;
+  constexpr int BY = parity_band_rows<S>();
   if (CH % 2 == 0 && CW % 2 == 0 && S::fits && COUT == 64 && CIN == 32 && G == 2 && !generic) {
     if constexpr (CH % 2 == 0 && CW % 2 == 0 && S::fits) {
       const int rc = launch_parity_dgrad_x6<S>(dz, WT, EpiDgMaskG2<H, W>{X, out, mask_goal}, nimg, st);
       if (rc != VN_OK) return rc;
+    }
+  } else if (CH % 2 == 0 && CW % 2 == 0 && !S::fits && BY > 0 && COUT == 64 && CIN == 32 && G == 2 && !generic) {
+    if constexpr (CH % 2 == 0 && CW % 2 == 0 && !S::fits && BY > 0) {  // 300x400: bands of class rows
+      const void* kfn = (const void*)parity_dgrad_band_x6_kernel<S, BY, EpiDgMaskG2<H, W>>;
+      constexpr size_t lds = parity_band_lds<S, BY>();
+      VN_HIP(ensure_dyn_lds(kfn, lds));
+      const int items = nimg * ((S::YC + BY - 1) / BY);
+      const int blocks = std::min(items, resident_blocks(kfn, S::NT, lds));
+      if (blocks > 0)
+        hipLaunchKernelGGL((parity_dgrad_band_x6_kernel<S, BY, EpiDgMaskG2<H, W>>), dim3(blocks), dim3(S::NT), lds, st,
+                           dz, WT, EpiDgMaskG2<H, W>{X, out, mask_goal}, nimg);
     }
   } else {
     dgrad_class_groups<COUT, CIN, H, W, OH, OW, 0, 0>(dz, WT, out, X, nimg, G, st, mask_goal);

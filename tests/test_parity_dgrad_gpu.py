@@ -1,6 +1,7 @@
 """The persistent specialised kernels against the generic products they replaced (selected
 back per call by an environment switch): the parity-class kernel (`parity_dgrad_x6_kernel`,
-`VN_DGRAD_GENERIC`) for conv3's input gradient (k4 s2, 64 -> 2 x 32 channels) and the aux
+`VN_DGRAD_GENERIC`; at 300x400 its banded form `parity_dgrad_band_x6_kernel`) for conv3's
+input gradient (k4 s2, 64 -> 2 x 32 channels) and the aux
 heads' first transposed conv (32 -> 48 channels, bias + ReLU), and conv3's weight gradient
 (`conv3_wgrad_x6_kernel`, `VN_WGRAD_GENERIC`). Both compute the same exact
 split-bf16 products in another summation order, so every parameter gradient — conv3's
