@@ -105,8 +105,11 @@ def _rollout_batch(hw, T, E, seed, p_done=0.3):
     return img, gl, dones
 
 
-@pytest.mark.parametrize("hw,T,E", [((84, 84), 4, 64), ((174, 174), 3, 24), ((300, 400), 3, 20)],
-                         ids=["84x84", "174x174", "c5_300x400"])
+# the wide cases step enough envs for conv3's goal-aware product to run whole-K (>= 128 tiles,
+# the bench's form; the narrow ones take its split-K form)
+@pytest.mark.parametrize("hw,T,E", [((84, 84), 4, 64), ((174, 174), 3, 24), ((300, 400), 3, 20),
+                                    ((84, 84), 2, 928), ((174, 174), 2, 208), ((300, 400), 2, 48)],
+                         ids=["84x84", "174x174", "c5_300x400", "84x84_wide", "174x174_wide", "c5_wide"])
 def test_dedup_forward_bitwise_and_backward_vs_fp64_oracle(hw, T, E):
     from vnav import _lib
     from vnav.policy import frames_from_batch

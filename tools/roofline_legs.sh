@@ -10,8 +10,8 @@ TAG=l84$T bash tools/prof_leg.sh > /dev/null || exit 1
 TAG=l174$T LEG_ARGS="--no-train-ff --no-train-84 --no-train-ref4" UPDATES=2 PICK=2 bash tools/prof_leg.sh > /dev/null || exit 1
 TR84=$(find gpurun_out/prof_l84$T -name '*kernel_trace.csv' | sort | tail -1)
 TR174=$(find gpurun_out/prof_l174$T -name '*kernel_trace.csv' | sort | tail -1)
-python3 tools/kernel_roofline.py $TR84 3 84 > gpurun_out/kernel_roofline_84_lstm_$T.md || exit 1
-python3 tools/kernel_roofline.py $TR174 2 174 > gpurun_out/kernel_roofline_174_lstm_aux_$T.md || exit 1
+python3 tools/kernel_roofline.py $TR84 3 84 84 4096 20 0.05 0.05 > gpurun_out/kernel_roofline_84_lstm_$T.md || exit 1
+python3 tools/kernel_roofline.py $TR174 2 174 174 4096 20 0.05 0.05 > gpurun_out/kernel_roofline_174_lstm_aux_$T.md || exit 1
 bash tools/prof_ref4.sh > /dev/null || exit 1
 cp gpurun_out/breakdown_ref4.txt gpurun_out/breakdown_ref4_$T.txt
 head -3 gpurun_out/breakdown_l84$T.txt gpurun_out/breakdown_l174$T.txt gpurun_out/breakdown_ref4_$T.txt
