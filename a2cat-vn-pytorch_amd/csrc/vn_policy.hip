@@ -1755,13 +1755,16 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
     }
     if constexpr (Bd::LDS <= 160 * 1024) {
       // a few envs (174x174, 300x400): the banded kernel is one launch where the split-K
-      // product needs two; at training batches the generic product is faster (see above)
-      if (n <= kSkinnyRows) {
+      // product needs two. Training batches: at 174x174 the ring above; at 300x400 the banded
+      // kernel beats the generic product by 1.7-1.8 ms per update (profiles/r04/ab_conv2f.txt);
+      // VN_CONV2F_GENERIC keeps the product (A/B and parity checks)
+      constexpr bool ring = conv2_fwd_ring_fits<G::OH1, G::OW1, G::OH2, G::OW2>();
+      if (!done && (n <= kSkinnyRows || (!ring && !getenv("VN_CONV2F_GENERIC")))) {
         const void* kfn = (const void*)conv2_fwd_x6_kernel<G::OH1, G::OW1, G::OH2, G::OW2>;
         VN_HIP(ensure_dyn_lds(kfn, Bd::LDS));
         const int blocks = std::min(frames * Bd::NB, resident_blocks(kfn, 512, Bd::LDS));
         hipLaunchKernelGGL((conv2_fwd_x6_kernel<G::OH1, G::OW1, G::OH2, G::OW2>), dim3(blocks), dim3(512), Bd::LDS, st,
-                           a.X[0], P + L.l[1].w, P + L.l[1].b, a.X[1], frames, FrameList{});
+                           a.X[0], P + L.l[1].w, P + L.l[1].b, a.X[1], frames, gr ? fl : FrameList{});
         done = true;
       }
     }

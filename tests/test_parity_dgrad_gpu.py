@@ -107,13 +107,16 @@ def test_aux_first_layer_matches_generic_products(hw, N, switch):
     assert not bad, bad
 
 
-@pytest.mark.parametrize("N", [17, 300, 1030])
-def test_conv2_ring_forward_matches_generic_product(N):
+@pytest.mark.parametrize("hw,N", [((174, 174), 17), ((174, 174), 300), ((174, 174), 1030), ((300, 400), 17),
+                                  ((300, 400), 129)])
+def test_conv2_ring_forward_matches_generic_product(hw, N):
     """conv2's forward at 174x174 (42x42x32 -> 20x20x32) through the ring kernel
     (`conv2_fwd_ring_kernel`: frames streamed band by band, X1 rows split once into an LDS
-    ring) against the generic im2col product (`VN_CONV2F_GENERIC`): the X2 maps of every frame
-    (the kernel's whole output) to rounding, 1e-6 of scale, and the logits / value. N = 17 is
-    the smallest batch that takes it (34 frames: most workgroups idle), 300 and 1030 wrap the
+    ring) and at 300x400 (74x99x32 -> 36x48x32) through the banded kernel
+    (`conv2_fwd_x6_kernel`: bands of output rows, their X1 rows split once into LDS planes)
+    against the generic im2col product (`VN_CONV2F_GENERIC`): the X2 maps of every frame
+    (the kernel's whole output) to rounding, 2e-6 of scale, and the logits / value. N = 17 is
+    the smallest batch that takes them (34 frames: most workgroups idle), 300 and 1030 wrap the
     persistent grid (several frames per workgroup: the ring crosses frame boundaries). Every
     parameter gradient is compared at N <= 300: both paths sum the same exact split products in
     another order, and at 1030 samples (26 M X2 values) a few values within rounding of 0 take
@@ -121,7 +124,6 @@ def test_conv2_ring_forward_matches_generic_product(N):
     tests in test_prod_oracle_gpu.py run the float64 backward with the GPU's own masks)."""
     from vnav.policy import GoalNavPolicy, frames_from_batch
     torch.manual_seed(13)
-    hw = (174, 174)
     pol = GoalNavPolicy(3, 4, hw)
     net = pol.net
     with torch.no_grad():
@@ -131,7 +133,8 @@ def test_conv2_ring_forward_matches_generic_product(N):
     gl = torch.randint(0, 256, (N, 1) + hw + (3,), dtype=torch.uint8, device="cuda", generator=g)
     cl = torch.randn((N, 1, 4), device="cuda", generator=g)
     cv = torch.randn((N, 1, 1), device="cuda", generator=g)
-    m1, x1, x2 = 2 * 42 * 42, 2 * 42 * 42 * 32, 2 * 20 * 20 * 32  # per-sample act regions (vn_policy.hip:471-476)
+    (h1, w1), (h2, w2) = {174: ((42, 42), (20, 20)), 300: ((74, 99), (36, 48))}[hw[0]]
+    m1, x1, x2 = 2 * h1 * w1, 2 * h1 * w1 * 32, 2 * h2 * w2 * 32  # per-sample act regions (vn_policy.hip, acts_at)
 
     def run(generic):
         if generic:
@@ -156,7 +159,9 @@ def test_conv2_ring_forward_matches_generic_product(N):
     (xf, of, gf), (xg, og, gg) = run(False), run(True)
     assert float(xg.abs().max()) > 0
     e = float((xf - xg).abs().max()) / float(xg.abs().max())
-    assert e < 1e-6, e
+    # both sum 512 exact products per output in fp32, in another order (the banded kernel adds
+    # four kernel-row partials): ~8 ulp of the map's scale at 300x400 (1.02e-6 measured)
+    assert e < 2e-6, e
     e = float((of - og).abs().max()) / max(float(og.abs().max()), 1e-30)
     assert e < 1e-5, e
     if gg is not None:
