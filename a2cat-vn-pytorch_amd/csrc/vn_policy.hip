@@ -1569,9 +1569,13 @@ template <int IH, int IW, int OH, int OW>
 using Conv3Wg = std::conditional_t<Conv3WgWhole<IH, IW, OH, OW>::fits, Conv3WgWhole<IH, IW, OH, OW>,
                                    WgSpec<IH, IW, OH, OW, 64, 2, 1, 2>>;
 // conv2: frames (image and goal) as images; bands of 4 dZ2 rows at 174x174 (X1 rows 10 x 42),
-// whole maps at 84x84
+// whole maps at 84x84; at 300x400 bands of one dZ2 row (48 reduction pixels, the 4 X1 rows of
+// 99 under it: 109 KB of planes)
 template <int IH, int IW, int OH, int OW>
-using Conv2Wg = WgSpec<IH, IW, OH, OW, 32, 1, (OH % 4 == 0 && OH > 9 ? 4 : OH), 1>;
+using Conv2WgWide = WgSpec<IH, IW, OH, OW, 32, 1, (OH % 4 == 0 && OH > 9 ? 4 : OH), 1>;
+template <int IH, int IW, int OH, int OW>
+using Conv2Wg = std::conditional_t<Conv2WgWide<IH, IW, OH, OW>::fits, Conv2WgWide<IH, IW, OH, OW>,
+                                   WgSpec<IH, IW, OH, OW, 32, 1, 1, 1>>;
 
 template <int COUT, int CIN, int H, int W, int OH, int OW, int PY, int PX>
 inline void dgrad_class_groups(const float* dz, const float* WT, float* out, const float* X, int nimg, int G,
@@ -1963,7 +1967,9 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
     const int blocks = std::min(frames * Bd2::NB, kConv2WgradBlocks);
     constexpr size_t lds = conv2_wgrad_lds<G::OH1, G::OW1, G::OH2, G::OW2>();
     using Wg2 = Conv2Wg<G::OH1, G::OW1, G::OH2, G::OW2>;
-    if (Wg2::fits && !getenv("VN_WGRAD_GENERIC")) {  // x6 form; read per call (A/B and parity checks)
+    // x6 form; VN_WGRAD_GENERIC / VN_CONV2WG_F32 (this product only) keep the others (A/B and
+    // parity checks; read per call)
+    if (Wg2::fits && !getenv("VN_WGRAD_GENERIC") && !getenv("VN_CONV2WG_F32")) {
       if constexpr (Wg2::fits) {
         const int rc = launch_conv_wgrad_x6<Wg2>(w.dz2, a.X[0], frames, w.slab, w.slab_cap, Gr + L.l[1].w, Gr + L.l[1].b,
                                                  st, fl);
