@@ -289,14 +289,20 @@ __global__ __launch_bounds__(256) void rollout_begin_kernel(int64_t* state, floa
 // per-head MSEs summed (ai2_auxiliary/trainer.py:51-54), episode stats3].
 __global__ void metrics_kernel(const float* __restrict__ stats4, float inv_n, const float* __restrict__ scalars2,
                                const float* __restrict__ aux3, const float* __restrict__ aux_numel3,
-                               const float* __restrict__ episode3, float* __restrict__ out9) {
+                               const float* __restrict__ episode3, const float* __restrict__ unreal4,
+                               const float* __restrict__ unreal_norm3, float* __restrict__ out) {
   if (threadIdx.x != 0) return;
-  for (int i = 0; i < 4; ++i) out9[i] = stats4[i] * inv_n;
-  out9[4] = scalars2[0];
+  for (int i = 0; i < 4; ++i) out[i] = stats4[i] * inv_n;
+  out[4] = scalars2[0];
   // (h0 + h2) + h1: torch's sum of three values (two threads along the reduction, thread 0
   // takes elements 0 and 2, then one shuffle step)
-  out9[5] = aux3 ? (aux3[0] / aux_numel3[0] + aux3[2] / aux_numel3[2]) + aux3[1] / aux_numel3[1] : 0.0f;
-  for (int i = 0; i < 3; ++i) out9[6 + i] = episode3[i];
+  out[5] = aux3 ? (aux3[0] / aux_numel3[0] + aux3[2] / aux_numel3[2]) + aux3[1] / aux_numel3[1] : 0.0f;
+  for (int i = 0; i < 3; ++i) out[6 + i] = episode3[i];
+  if (unreal4) {  // [pc sum sq, rp mean CE, (rp count), vr sum sq] x [pc, rp, vr] normalisers
+    out[9] = unreal4[0] * unreal_norm3[0];
+    out[10] = unreal4[1] * unreal_norm3[1];
+    out[11] = unreal4[3] * unreal_norm3[2];
+  }
 }
 
 // ---- goal runs (vn_goal_runs, include/vnav.h) ----------------------------------------
@@ -458,14 +464,20 @@ int vn_a2c_rollout_begin(int64_t* state3, float* lr_out, double lr0, double max_
   return VN_OK;
 }
 
-int vn_a2c_metrics(const float* stats4, float inv_n, const float* scalars2, const float* aux3,
-                   const float* aux_numel3, const float* episode_stats3, float* out9, vn_stream_t stream) {
-  if (!stats4 || !scalars2 || !episode_stats3 || !out9 || (aux3 && !aux_numel3))
+int vn_a2c_metrics_ex(const float* stats4, float inv_n, const float* scalars2, const float* aux3,
+                      const float* aux_numel3, const float* episode_stats3, const float* unreal4,
+                      const float* unreal_norm3, float* out, vn_stream_t stream) {
+  if (!stats4 || !scalars2 || !episode_stats3 || !out || (aux3 && !aux_numel3) || (unreal4 && !unreal_norm3))
     return fail(VN_EINVAL, "vn_a2c_metrics: bad args");
   hipLaunchKernelGGL(metrics_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, stats4, inv_n, scalars2, aux3,
-                     aux_numel3, episode_stats3, out9);
+                     aux_numel3, episode_stats3, unreal4, unreal_norm3, out);
   VN_HIP(hipGetLastError());
   return VN_OK;
+}
+
+int vn_a2c_metrics(const float* stats4, float inv_n, const float* scalars2, const float* aux3,
+                   const float* aux_numel3, const float* episode_stats3, float* out9, vn_stream_t stream) {
+  return vn_a2c_metrics_ex(stats4, inv_n, scalars2, aux3, aux_numel3, episode_stats3, nullptr, nullptr, out9, stream);
 }
 
 int vn_policy_greedy(const float* out, int n, int num_actions, int32_t* actions, vn_stream_t stream) {

@@ -10,6 +10,9 @@
 // centre crop of 42 x 4 pixels of the image observation (_get_input_for_pixel_control,
 // thor_cached_auxiliary.py:47-48; obs scaled to [0,1] by ScaledFloatFrame), Q targets
 // R_T = max_a Q(s_T), R_t = r_t + gamma_pc (1 - done_t) R_{t+1}, loss mean (Q(s_t, a_t) - R_t)^2;
+// on a done step r_t = 0: the frame after it is the auto-reset frame of the next episode, so
+// the pixel change across the boundary is not an effect of a_t (recorded deviation: the
+// frame that ends the episode is never emitted by the batched env, DESIGN.md "Deviations");
 // reward prediction classes (r = 0, r > 0, r < 0) of the reward after frame t from frames
 // t-2, t-1, t of one episode; value replay mean (V - R)^2 against the n-step returns. The
 // oracle is oracle/unreal.py.
@@ -94,8 +97,9 @@ __global__ __launch_bounds__(256) void unreal_pc_loss_kernel(float* __restrict__
     for (int t = T - 1; t >= 0; --t) {
       const int64_t r = (int64_t)t * E + e;
       const uint8_t* f = arena + (int64_t)rows_img[r] * frame_bytes;
-      const float rew = pc_cell_change(f, fn, W, top, left, cy, cx);
-      R = rew + (dones[r] ? 0.0f : gamma * R);
+      const bool done = dones[r] != 0;
+      const float rew = done ? 0.0f : pc_cell_change(f, fn, W, top, left, cy, cx);
+      R = rew + (done ? 0.0f : gamma * R);
       const int act = actions[r];
       float* pt = p2 + ((int64_t)(t * S + e) * PP + pix) * 8;
       pc_load8(pt, v);
@@ -200,6 +204,30 @@ __global__ __launch_bounds__(256) void unreal_vr_kernel(const float* __restrict_
   if (threadIdx.x == 0 && t != 0.0f) atomicAdd(stats, t);
 }
 
+// The UNREAL losses' inputs in one launch (they were five framework copies): h_pc rows
+// t*S + e = h_all row t*E + e (t < T, e < S), rows T*S + e = boot_h row e; rp_x row
+// (t*S + e) slot k = x4 row (t+k)*E + e (t < T - 2, k < 3). One 16-B lane per 4 floats.
+__global__ __launch_bounds__(256) void unreal_gather_kernel(const float* __restrict__ h_all,
+                                                            const float* __restrict__ boot_h,
+                                                            const float* __restrict__ x4, int T, int E, int S, int F,
+                                                            float* __restrict__ h_pc, float* __restrict__ rp_x) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t n_h = (int64_t)(T + 1) * S * 128;  // 512 floats = 128 lanes per h row
+  if (i < n_h) {
+    const int j = (int)(i >> 7), q = (int)(i & 127);
+    const float* src = j < T * S ? h_all + ((int64_t)(j / S) * E + j % S) * 512 : boot_h + (int64_t)(j - T * S) * 512;
+    reinterpret_cast<f4*>(h_pc + (int64_t)j * 512)[q] = reinterpret_cast<const f4*>(src)[q];
+    return;
+  }
+  const int F4 = F / 4;
+  const int64_t r = i - n_h;
+  if (r >= (int64_t)(T - 2) * S * 3 * F4) return;
+  const int q = (int)(r % F4);
+  const int64_t js = r / F4;  // (sample, slot)
+  const int k = (int)(js % 3), j = (int)(js / 3), t = j / S, e = j - (j / S) * S;
+  reinterpret_cast<f4*>(rp_x + js * F)[q] = reinterpret_cast<const f4*>(x4 + ((int64_t)(t + k) * E + e) * F)[q];
+}
+
 }  // namespace vn
 
 using namespace vn;
@@ -240,6 +268,17 @@ int vn_unreal_rp_scatter(const float* dx, int T, int E, int S, int fcin, float* 
   const int64_t total = (int64_t)T * S * (fcin / 4);
   hipLaunchKernelGGL(unreal_rp_scatter_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                      dx, T, E, S, fcin, dx4, accumulate);
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
+
+int vn_unreal_gather(const float* h_all, const float* boot_h, const float* x4, int T, int E, int S, int fcin,
+                     float* h_pc, float* rp_x, vn_stream_t stream) {
+  if (!h_all || !boot_h || !h_pc || T <= 0 || S <= 0 || S > E || (rp_x && (!x4 || T < 3 || fcin <= 0 || fcin % 4)))
+    return fail(VN_EINVAL, "vn_unreal_gather: bad args");
+  const int64_t total = (int64_t)(T + 1) * S * 128 + (rp_x ? (int64_t)(T - 2) * S * 3 * (fcin / 4) : 0);
+  hipLaunchKernelGGL(unreal_gather_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     h_all, boot_h, x4, T, E, S, rp_x ? fcin : 0, h_pc, rp_x);
   VN_HIP(hipGetLastError());
   return VN_OK;
 }

@@ -149,6 +149,8 @@ SIGNATURES.update({
     "vn_unreal_rp_loss_grad": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p,
                                        c_void_p, c_void_p]),
     "vn_unreal_rp_scatter": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
+    "vn_unreal_gather": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                                 c_void_p]),
     "vn_unreal_vr_grad": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_void_p, c_void_p,
                                   c_void_p]),
     "vn_policy_backward_ex": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int64, c_void_p, c_void_p,
@@ -172,6 +174,8 @@ SIGNATURES.update({
                                        c_float, c_void_p]),
     "vn_a2c_schedule": (c_int, [c_void_p, c_void_p, c_double, c_double, c_int64, c_int, c_void_p]),
     "vn_a2c_metrics": (c_int, [c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "vn_a2c_metrics_ex": (c_int, [c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                  c_void_p, c_void_p]),
     "vn_a2c_rollout_begin":(c_int, [c_void_p, c_void_p, c_double, c_double, c_int64, c_int, c_void_p, c_void_p,
                                      c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
                                      c_void_p, c_void_p]),

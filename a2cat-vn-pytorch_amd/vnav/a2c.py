@@ -63,7 +63,7 @@ class A2CTrainer:
                  max_time_steps=2e6, rms_alpha=0.99, rms_epsilon=1e-5, max_gradient_norm=0.5,
                  value_coefficient=0.5, entropy_coefficient=0.01, seed=0, process_group=None, recurrent=False,
                  aux_weight=0.0, arch="goal", cuda_graph=False, aux_source="rollout", replay_size=8,
-                 capture_collectives=False, allreduce_buckets=2, time_collectives=False, dedup_goals=True,
+                 capture_collectives=False, allreduce_buckets=1, time_collectives=False, dedup_goals=None,
                  unreal=False, pc_weight=0.05, rp_weight=1.0, vr_weight=1.0, pc_gamma=0.9, unreal_envs=16):
         self.env = env
         self.lib = _lib.load()
@@ -84,7 +84,12 @@ class A2CTrainer:
             raise ValueError("allreduce_buckets must be 1 or 2")
         self.allreduce_buckets = int(allreduce_buckets)
         self.time_collectives = bool(time_collectives)
-        self.collective_events = []
+        if self.time_collectives and cuda_graph:
+            raise ValueError("time_collectives records HIP events per update, which a captured hipGraph would replay "
+                             "as fixed events: use one or the other")
+        # exposed all-reduce time: the pending update's event pair and a running (sum, count)
+        self._coll_pending = []
+        self._coll_sum_ms, self._coll_count = 0.0, 0
         self._head_work = None
         self.aux_weight = float(aux_weight)
         self.net = net if net is not None else PolicyNet(env.frame_shape[:2], env.num_actions, self.device,
@@ -200,7 +205,15 @@ class A2CTrainer:
         # after each done — and the backward sums a run's goal-map gradients before conv2 /
         # conv1 (same outputs, gradients up to summation order). Runs where the policy's
         # kernels take frame lists (84x84 / 174x174, more than 16 envs).
-        self.dedup_goals = bool(dedup_goals) and self.net.arch == "goal" and self.net.goal_runs_supported(E)
+        # dedup_goals None = on where supported. Not with companion frames (OrientedGraphEnv's
+        # third-person view, vn_env.hip goal_row = companion row + state): that second frame
+        # changes at every step, so a run start's maps are not the later steps' maps.
+        companion = any(getattr(s, "companion", None) is not None for s in getattr(env, "scenes", ()))
+        if dedup_goals and companion:
+            raise ValueError("dedup_goals=True needs a goal frame that is constant within an episode; these scenes "
+                             "emit companion frames (a per-step third-person view) as the second frame")
+        self.dedup_goals = (dedup_goals is None or bool(dedup_goals)) and not companion and \
+            self.net.arch == "goal" and self.net.goal_runs_supported(E)
         if self.dedup_goals:
             i32 = dict(dtype=torch.int32, **kw)
             self.goal_delta = torch.zeros((T, E), **i32)
@@ -296,9 +309,12 @@ class A2CTrainer:
         if self.vr_weight > 0:
             _lib.check(lib.vn_unreal_vr_grad(P(self.out), P(self.returns), T, E, S, A, ctypes.c_float(self.vr_weight),
                                              P(self.dout), P(self.unreal_stats[3:]), st), "vn_unreal_vr_grad")
-        # pixel control on h of the first S envs (+ the bootstrap's)
-        self.h_pc[:T * S].view(T, S, 512).copy_(self.h_all.view(T, E, 512)[:, :S])
-        self.h_pc[T * S:].copy_(self.boot_h[:S])
+        # pixel control on h of the first S envs (+ the bootstrap's), reward prediction on three
+        # consecutive conv_base maps of the same envs: both inputs gathered in one launch
+        F = net.fc_in
+        x4 = net.x4(self.acts, N)
+        _lib.check(lib.vn_unreal_gather(P(self.h_all), P(self.boot_h), P(x4), T, E, S, F, P(self.h_pc), P(self.rp_x),
+                                        st), "vn_unreal_gather")
         n_pc = (T + 1) * S
         net.pc_forward(self.params, self.h_pc, n_pc, self.pcb, self.pc_a1, self.pc_p2, None, self.pc_ws)
         H, W = self.env.frame_shape[:2]
@@ -311,12 +327,6 @@ class A2CTrainer:
                    "vn_unreal_pc_loss_grad")
         net.pc_backward(self.params, self.h_pc, n_pc, self.pcb, self.pc_a1, self.pc_p2, None, self.grads, self.dh_pc,
                         self.pc_ws)
-        # reward prediction on three consecutive conv_base maps of the first S envs
-        F = net.fc_in
-        x4 = net.x4(self.acts, N).view(T, E, F)
-        xv = self.rp_x.view(T - 2, S, 3, F)
-        for k in range(3):
-            xv[:, :, k].copy_(x4[k:k + T - 2, :S])
         n_rp = (T - 2) * S
         net.rp_forward(self.params, self.rp_x, n_rp, self.rp_out)
         _lib.check(lib.vn_unreal_rp_loss_grad(P(self.rp_out), P(self.rewards), P(self.dones), T, E, S,
@@ -585,6 +595,7 @@ class A2CTrainer:
             return 1.0
         ev = None
         if self.time_collectives:
+            self._collect_pending()
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
         if getattr(self, "_head_work", None) is not None:
@@ -596,17 +607,32 @@ class A2CTrainer:
             scale = vdist.allreduce_gradients_(self.grads, self.group)  # RCCL, one flat bucket
         if ev is not None:
             ev[1].record()
-            self.collective_events.append(ev)
+            self._coll_pending.append(ev)
         return scale
 
+    def _collect_pending(self, wait=False):
+        """Fold the completed event pairs into the running (sum, count): non-blocking unless
+        ``wait`` or more than 8 pairs are pending, so the record stays bounded however long
+        the run and the host does not stall behind the device."""
+        keep = []
+        for k, ev in enumerate(self._coll_pending):
+            if wait or len(self._coll_pending) - k > 8 or ev[1].query():
+                ev[1].synchronize()
+                self._coll_sum_ms += ev[0].elapsed_time(ev[1])
+                self._coll_count += 1
+            else:
+                keep.append(ev)
+        self._coll_pending = keep
+
     def collective_ms(self):
-        """Mean exposed all-reduce time per update (ms) over the recorded updates (syncs)."""
-        if not self.collective_events:
+        """Mean exposed all-reduce time per update (ms) over the updates since the last call
+        (syncs on the last update's events); None when nothing was recorded."""
+        self._collect_pending(wait=True)
+        if not self._coll_count:
             return None
-        torch.cuda.synchronize(self.device)
-        ms = [a.elapsed_time(b) for a, b in self.collective_events]
-        self.collective_events = []
-        return sum(ms) / len(ms)
+        ms = self._coll_sum_ms / self._coll_count
+        self._coll_sum_ms, self._coll_count = 0.0, 0
+        return ms
 
     def _carry_states(self):
         """(h0, c0) = (h, c) of the rollout's last step, both in one strided copy."""
@@ -629,15 +655,16 @@ class A2CTrainer:
         N = self.num_steps * self.env.num_envs
         # [stats / N, grad norm, aux loss (sum of the per-head MSEs, trainer.py:51-54),
         # episode stats] in one launch; / N is torch's tensor / scalar (times the f32 reciprocal)
-        m = torch.empty(9, dtype=torch.float32, device=self.device)
+        # with the UNREAL losses + [pc loss, rp loss, vr loss] (means: averaged over ranks too)
+        m = torch.empty(12 if self.unreal else 9, dtype=torch.float32, device=self.device)
         aux = self.aux_weight > 0
-        _lib.check(self.lib.vn_a2c_metrics(_lib.ptr(self.stats), ctypes.c_float(np.float32(1.0) / np.float32(N)),
-                                           _lib.ptr(self.scalars), _lib.ptr(self.aux_stats) if aux else None,
-                                           _lib.ptr(self._aux_numel) if aux else None, _lib.ptr(self.episode_stats),
-                                           _lib.ptr(m), self._stream()), "vn_a2c_metrics")
-        if self.unreal:  # + [pc loss, rp loss, vr loss] (means: averaged over ranks too)
-            u = torch.stack((self.unreal_stats[0], self.unreal_stats[1], self.unreal_stats[3])) * self._unreal_norm
-            m = torch.cat((m, u))
+        P = _lib.ptr
+        _lib.check(self.lib.vn_a2c_metrics_ex(P(self.stats), ctypes.c_float(np.float32(1.0) / np.float32(N)),
+                                              P(self.scalars), P(self.aux_stats) if aux else None,
+                                              P(self._aux_numel) if aux else None, P(self.episode_stats),
+                                              P(self.unreal_stats) if self.unreal else None,
+                                              P(self._unreal_norm) if self.unreal else None, P(m), self._stream()),
+                   "vn_a2c_metrics_ex")
         vdist.reduce_metrics_(m, 6, self.group)
         if self.unreal and self.world > 1:
             m[9:] /= self.world

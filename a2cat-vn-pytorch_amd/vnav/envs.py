@@ -242,9 +242,13 @@ class VectorEnv:
     def step(self, actions, out=None, gather=True):
         """actions: int32 [E] device tensor (other integer dtypes are converted).
         Returns ((image, goal), reward f32 [E], done bool [E], info dict of [E] tensors).
-        ``out`` = dict of preallocated outputs (image, goal, reward, done, state) to write
-        in place; ``gather=False`` skips the frame copy (index-only step: info img_row /
-        goal_row address the frames in the scene cache)."""
+        Without ``out`` every returned tensor is fresh, info included (a caller may keep step
+        t's results while stepping on). ``out`` = dict of preallocated outputs (image, goal,
+        reward, done, state) to write in place: the fast path, where nothing is allocated or
+        copied per step and info's tensors (ep_return, ep_length, terminal_state, truncated,
+        img_row, goal_row) are the env's own buffers, overwritten by the next step like the
+        ``out`` buffers. ``gather=False`` skips the frame copy
+        (index-only step: info img_row / goal_row address the frames in the scene cache)."""
         if type(actions) is torch.Tensor and actions.dtype == torch.int32 and actions.device == self.device \
                 and actions.shape == (self.num_envs,) and actions.is_contiguous():
             a = actions
@@ -289,7 +293,8 @@ class VectorEnv:
                                    tuple((t.data_ptr(), t.numel()) if t is not None else None for t in bufs))
         _lib.check(self.lib.vn_step(self._ctx, _lib.ptr(a), _lib.ptr(img), _lib.ptr(goal), _lib.ptr(reward),
                                     _lib.ptr(done), _lib.ptr(state), self._stream()), "vn_step")
-        info = dict(self._info)
+        # fresh info tensors unless the caller chose the in-place path (out=...)
+        info = {k: v.clone() for k, v in self._info.items()} if out is None else dict(self._info)
         info["state"] = state
         if self.aux_observations and gather:
             return (img, goal) + self._gather_aux(), reward, done, info

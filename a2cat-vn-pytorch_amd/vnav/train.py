@@ -234,6 +234,18 @@ class Experiment:
         latest = self._latest()
         return latest is not None and os.path.exists(self.rank_checkpoint_path(latest["total_steps"]))
 
+    def _resume_decision(self):
+        """Whether run(resume=True) loads: this rank's has_checkpoint(), agreed by all ranks
+        (load_checkpoint is collective). Ranks that disagree — a save_dir that is not shared,
+        one rank's file missing — raise on every rank instead of leaving some ranks in the
+        load's collectives and others in the first gradient all-reduce."""
+        have = self.has_checkpoint()
+        if self.world == 1:
+            return have
+        self._setup()
+        vdist.check_ranks_agree([int(have)], "whether a checkpoint exists to resume from (has_checkpoint)")
+        return have
+
     def load_checkpoint(self, path=None):
         """One process: checkpoint.pt (or ``path``). world > 1 (collective): this rank's file
         of the complete set named by latest.json; then the ranks check that they agree on the
@@ -271,7 +283,7 @@ class Experiment:
         """Train to max_time_steps: deep_rl's Trainer.run() (train.py:25). resume=True
         continues from save_dir's checkpoint when there is one (parameters, RMSprop state,
         per-env state and running returns, recurrent carry, update / step counters)."""
-        if resume and self.has_checkpoint():
+        if resume and self._resume_decision():
             self.load_checkpoint()
         tr = self._setup()
         window = dict(episodes=0.0, rsum=0.0, lsum=0.0)

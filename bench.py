@@ -65,8 +65,12 @@ def parse():
     p.add_argument("--no-c5", action="store_true",
                    help="skip the 300x400 + goal + aux-depth train leg (config C5, 512 envs per GPU)")
     p.add_argument("--num-steps", type=int, default=20, help="A2C rollout length (reference: 20)")
+    p.add_argument("--no-short", action="store_true",
+                   help="skip the 2-step-episode legs (goal-frame deduplication at the logged run's operating point)")
     p.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
     p.add_argument("--dist-backend", default="nccl", help="torch.distributed backend (nccl = RCCL on ROCm)")
+    p.add_argument("--allreduce-buckets", type=int, choices=(1, 2), default=1,
+                   help="gradient all-reduce buckets at world > 1 (2: heads + LSTM overlapped with the trunk backward)")
     p.add_argument("--pmc-leg", choices=sorted(LEGS), default=None,
                    help="(child of the PMC pass) run only this training leg: one warmup update, then exactly one "
                         "update between two vn_trace_marker launches; no env leg, no JSON line")
@@ -262,7 +266,7 @@ def aux_scenes(n, frame, seed=0):
 
 
 def bench_train(args, scenes, dev, world, rank, recurrent, aux_weight=0.0, envs=None, updates=None, warmup=None,
-                model=None, cuda_graph=False, marker=False, unreal=False):
+                model=None, cuda_graph=False, marker=False, unreal=False, hardness=None, max_episode_steps=900):
     """A2C training throughput: one step = rollout of num_steps on every local env (policy
     forward + sampling + env step) + backward + one RCCL all-reduce of the flat gradient +
     clip + RMSprop. recurrent: the full BigGoalHouseModel (LSTM core, BPTT over the rollout);
@@ -272,9 +276,13 @@ def bench_train(args, scenes, dev, world, rank, recurrent, aux_weight=0.0, envs=
     E, T = envs or args.envs, args.num_steps
     updates = updates or args.train_steps
     warmup = args.train_warmup if warmup is None else warmup
-    env = vnav.VectorEnv(scenes, E, seed=2000 + rank, device=dev)
+    env = vnav.VectorEnv(scenes, E, seed=2000 + rank, device=dev, max_episode_steps=max_episode_steps)
+    if hardness is not None:  # experiments/thor_cached_auxiliary.py:68-70 (before the first reset)
+        env.set_hardness(hardness)
+        env.reset()
     tr = vnav.A2CTrainer(env, num_steps=T, seed=7, max_time_steps=1e12, recurrent=recurrent, aux_weight=aux_weight,
-                         cuda_graph=cuda_graph, time_collectives=world > 1 and not cuda_graph, unreal=unreal)
+                         cuda_graph=cuda_graph, time_collectives=world > 1 and not cuda_graph, unreal=unreal,
+                         allreduce_buckets=args.allreduce_buckets)
     for _ in range(warmup):
         tr.step(sync=False)
     torch.cuda.synchronize(dev)
@@ -314,6 +322,8 @@ def bench_train(args, scenes, dev, world, rank, recurrent, aux_weight=0.0, envs=
     if model is None:
         model = "BigGoalHouseModel (LSTM core)" if recurrent else "BigGoalHouseModel trunk + heads (no LSTM)"
     res = {"model": model, "frame": [h, w, 3],
+           **({"episodes": {"hardness": hardness, "max_episode_steps": max_episode_steps}}
+              if hardness is not None or max_episode_steps != 900 else {}),
            "value": steps / el, "unit": "env-steps/s", "updates": updates, "envs_per_gpu": E,
            **({"cuda_graph": True} if cuda_graph else {}),
            "num_steps": T, "ms_per_update": el / updates * 1e3, "dtype": "f32",
@@ -367,12 +377,27 @@ LEGS = {
     "c5": dict(recurrent=True, aux_weight=AUX_WEIGHT_LOGGED, frame=(300, 400, 3), envs=512, updates=3, warmup=1,
                unreal=True, model="AuxiliaryBigGoalHouseModel (LSTM + deconv + UNREAL heads), 300x400 (config C5)"),
 }
-LEG_ORDER = ("84", "ff", "174", "ref4", "c5")
+# the logged run's operating point for goal-frame deduplication: a trained policy at hardness
+# 0.01 ends its episodes in ~2 steps (outputs/output.txt), so about half the goal frames are new
+# (the legs above, with a fresh policy, run to the 900-step TimeLimit: 5 % new). Here the
+# episodes are cut at 2 steps by the TimeLimit, which reproduces that goal-frame turnover with
+# the same kernels (the env step costs the same); the starts follow hardness 0.01.
+_SHORT = dict(hardness=0.01, max_episode_steps=2)
+LEGS["84_short"] = dict(LEGS["84"], **_SHORT, model="BigGoalHouseModel (LSTM core), episodes of <= 2 steps")
+LEGS["174_short"] = dict(LEGS["174"], **_SHORT,
+                         model="AuxiliaryBigGoalHouseModel (LSTM + deconv + UNREAL heads), 174x174, episodes of "
+                               "<= 2 steps")
+LEG_ORDER = ("84", "ff", "174", "ref4", "c5", "84_short", "174_short")
+LEG_KEYS = {"84": "train", "ff": "train_feedforward", "174": "train_174_lstm_aux", "ref4": "train_174_lstm_aux_4env",
+            "c5": "train_c5_300x400", "84_short": "train_84_short_episodes",
+            "174_short": "train_174_lstm_aux_short_episodes"}
 
 
 def leg_enabled(args, leg, world):
     return {"84": not args.no_train_84, "ff": not args.no_train_ff, "174": not args.no_train_ref and not args.no_train_174,
-            "ref4": not args.no_train_ref and not args.no_train_ref4 and world == 1, "c5": not args.no_c5}[leg]
+            "ref4": not args.no_train_ref and not args.no_train_ref4 and world == 1, "c5": not args.no_c5,
+            "84_short": not args.no_train_84 and not args.no_short,
+            "174_short": not args.no_train_ref and not args.no_train_174 and not args.no_short}[leg]
 
 
 def run_leg(leg, args, scenes, dev, world, rank, updates=None, warmup=None, marker=False):
@@ -438,12 +463,28 @@ def device_copy_rate(dev, nbytes, reps=20):
 _CPU_SHARED = {}
 
 
+def resize_standin(frame):
+    """The cost of the reference's per-frame preprocessing at equal size
+    (environments/gym_ai2thor/envs/cached.py:62-64: skimage 0.18 ``resize(image, (84, 84),
+    anti_aliasing=True)``, 99.9 % of its step time) without skimage, which the bench's python
+    lacks: float64 in [0, 1], an identity bilinear warp per channel (skimage's ``warp`` at
+    factor 1, mode 'reflect' = ndimage 'mirror'), clip. Timed in the build container: 1007 us
+    per 84x84x3 frame against 988 us for skimage's own call (DESIGN.md "Measurement")."""
+    from scipy import ndimage as ndi
+    x = frame.astype(np.float64) / 255.0
+    out = np.empty_like(x)
+    for c in range(x.shape[2]):
+        ndi.affine_transform(x[:, :, c], np.eye(2), order=1, mode="mirror", output=out[:, :, c])
+    return np.clip(out, 0.0, 1.0, out=out)
+
+
 def _cpu_worker(args):
-    n_envs, seconds, seed, frame_bytes = args
+    n_envs, seconds, seed, frame_bytes, resize = args
     from oracle.envs import VectorEnvOracle
     sd = [dict(graph=g, spd=s, rewards=(1.0, -0.0, 0.0)) for g, s in _CPU_SHARED["scenes"]]
     o = VectorEnvOracle(sd, n_envs, seed, max_steps=900)
     arena = _CPU_SHARED["arena"]  # inherited copy-on-write from the parent, read only
+    shape = _CPU_SHARED["frame_shape"]
     out_img = np.empty((n_envs, frame_bytes), dtype=np.uint8)
     out_goal = np.empty((n_envs, frame_bytes), dtype=np.uint8)
     rng = np.random.RandomState(seed)
@@ -453,6 +494,10 @@ def _cpu_worker(args):
         r = o.step(rng.randint(0, 4, size=n_envs))
         np.take(arena, r["img_row"], axis=0, out=out_img)
         np.take(arena, r["goal_row"], axis=0, out=out_goal)
+        if resize:  # the reference preprocesses the image and the goal frame of every step
+            for i in range(n_envs):
+                resize_standin(out_img[i].reshape(shape))
+                resize_standin(out_goal[i].reshape(shape))
         steps += 1
     return steps * n_envs, time.perf_counter() - t0
 
@@ -482,12 +527,12 @@ def _cpu_quota():
         return None
 
 
-def _cpu_run(workers, seconds, per, fb):
+def _cpu_run(workers, seconds, per, fb, resize=False):
     import multiprocessing as mp
     ctx = mp.get_context("fork")
     t0 = time.perf_counter()
     with ctx.Pool(workers) as pool:
-        res = pool.map(_cpu_worker, [(per, seconds, 100 + i, fb) for i in range(workers)])
+        res = pool.map(_cpu_worker, [(per, seconds, 100 + i, fb, resize) for i in range(workers)])
     wall = time.perf_counter() - t0
     return sum(r[0] / r[1] for r in res), sum(r[0] for r in res), wall
 
@@ -503,6 +548,7 @@ def cpu_baseline(scenes, seconds, sweep="1,16,all"):
     _CPU_SHARED["scenes"] = [(s.graph, s.spd) for s in scenes]
     # frame contents do not change the cost of a gather; fill (not hash) the arena
     _CPU_SHARED["arena"] = np.full((rows, fb), 7, dtype=np.uint8)
+    _CPU_SHARED["frame_shape"] = tuple(scenes[0].frame_shape)
     per = 256
     ncpu = len(os.sched_getaffinity(0))
     counts = []
@@ -515,14 +561,31 @@ def cpu_baseline(scenes, seconds, sweep="1,16,all"):
     for n in counts:
         rate, total, wall = _cpu_run(n, seconds, per, fb)
         points.append({"procs": n, "value": rate, "env_steps": total, "wall_s": wall})
+    # the reference as written: the same port plus the per-frame resize's cost (stand-in), at
+    # 1 process and at the fastest count above, 16 envs per process, half the time
+    ras = []
+    for n in sorted({1, max(points, key=lambda p: p["value"])["procs"]}):
+        rate, total, wall = _cpu_run(n, seconds / 2, 16, fb, resize=True)
+        ras.append({"procs": n, "value": rate, "env_steps": total, "wall_s": wall})
     _CPU_SHARED.clear()
     # value / cores: the fastest point (the box's cgroup quota can cap the CPUs this job gets
     # below its affinity mask: more processes than the quota only timeshare it)
     top = max(points, key=lambda p: p["value"])
     host = host_cpu_info()
     host["cgroup_cpu_quota"] = _cpu_quota()
+    ra_top = max(ras, key=lambda p: p["value"])
+    reference_as_written = {
+        "value": ra_top["value"], "unit": "env-steps/s", "cores": ra_top["procs"], "sweep": ras,
+        "sample": "the port above plus resize_standin() on both frames of every env-step (the cost of "
+                  "cached.py:62-64's skimage resize, 1.02x of it per frame in the build container), 16 envs per "
+                  "process, %.0f s" % (seconds / 2),
+        "survey_measured": {"value_1_core": 592.0, "value_8_procs": 3177.0, "unit": "env-steps/s",
+                            "source": "SURVEY.md §8d: the reference's own THORDiscreteCachedEnv (skimage resize "
+                                      "included) timed in the build container (8 Xeon cores), not on this host"}}
     return dict(value=top["value"], unit="env-steps/s", cores=top["procs"], kind="port", host=host,
-                sweep=points,
+                sweep=points, reference_as_written=reference_as_written,
+                note="value is the numpy port without the resize, a much faster CPU path than the reference as "
+                     "written; reference_as_written times the port with the resize's cost",
                 sample="oracle VectorEnvOracle (numpy), %s processes x %d envs, %.0f s each (incl. 2-frame gather "
                        "from a %d-row arena); value = the fastest point, %d processes"
                        % ("/".join(str(c) for c in counts), per, seconds, rows, top["procs"]))
@@ -627,7 +690,6 @@ def main():
                 continue
             legs[leg] = run_leg(leg, args, scenes, dev, world, rank)
             torch.cuda.empty_cache()
-    train, train_ff, train_ref, train_ref4, train_c5 = (legs.get(k) for k in ("84", "ff", "174", "ref4", "c5"))
     dist_info = None
     if world > 1:
         dist_info = ranks_seen(dev, world)
@@ -672,17 +734,22 @@ def main():
                          # torch's device copy of the same frame bytes (read + write), same process
                          "device_copy_gbs": copy_gbs, "frac_of_device_copy": achieved / copy_gbs},
             "cpu_baseline": cpu,
-            "train": train,
-            "train_feedforward": train_ff,
-            "train_174_lstm_aux": train_ref,
-            "train_174_lstm_aux_4env": train_ref4,
-            **({"train_c5_300x400": train_c5} if train_c5 else {}),
+            **{LEG_KEYS[k]: legs.get(k) for k in ("84", "ff", "174", "ref4")},
+            **{LEG_KEYS[k]: legs[k] for k in LEG_ORDER[4:] if legs.get(k)},
             **({"dist": dist_info} if dist_info else {}),
             "error_flags": flags,
         }
-        print(json.dumps(line))
+        print(json.dumps(line), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
+        # a multi-GPU line is only valid when every rank joined, each on its own GPU under RCCL
+        bad = dist_info["ranks_seen"] != world or (dist_info["backend"] == "nccl" and
+                                                   dist_info["distinct_devices"] != world)
+        if bad:
+            print("bench.py: invalid distributed run: %d of %d ranks seen, %d distinct devices (backend %s)"
+                  % (dist_info["ranks_seen"], world, dist_info["distinct_devices"], dist_info["backend"]),
+                  file=sys.stderr)
+            sys.exit(3)
 
 
 if __name__ == "__main__":

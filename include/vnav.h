@@ -365,7 +365,8 @@ int vn_rp_backward(vn_policy* p, const float* params, const float* x, int n, con
  * bootstrap observation), q = (v + a) - a formed from it; pseudo-reward r_t = mean over each
  * 4x4 cell and 3 channels of |obs_{t+1} - obs_t| / 255 on the centre 168x168 crop of the u8
  * image frames (arena rows rows_img[t*E + e], rows_last[e] for obs_T); R_T = max_a q_T,
- * R_t = r_t + gamma (1 - done_t) R_{t+1}; p2 is overwritten by dL/dp2 of weight *
+ * R_t = r_t + gamma (1 - done_t) R_{t+1} with r_t = 0 on a done step (the next frame is the
+ * auto-reset frame of the next episode: recorded deviation); p2 is overwritten by dL/dp2 of weight *
  * mean((q_t[a_t] - R_t)^2) (under the value ReLU; 0 on the bootstrap rows), ready for
  * vn_pc_backward with dq == NULL; stats[0] += sum of squared errors. */
 int vn_unreal_pc_loss_grad(float* p2, const int32_t* actions, const uint8_t* dones, const uint8_t* arena,
@@ -381,6 +382,11 @@ int vn_unreal_rp_loss_grad(const float* logits, const float* rewards, const uint
  * (stored, or added when accumulate != 0; other rows untouched). */
 int vn_unreal_rp_scatter(const float* dx, int T, int E, int S, int fcin, float* dx4, int accumulate,
                          vn_stream_t stream);
+/* The losses' inputs in one launch: h_pc [(T+1)*S][512] = h_all rows t*E + e (t < T, e < S)
+ * then boot_h rows e < S; rp_x [(T-2)*S][3][fcin] (may be NULL) slot k of sample t*S + e =
+ * x4 row (t+k)*E + e (conv_base maps of frames t..t+2). */
+int vn_unreal_gather(const float* h_all, const float* boot_h, const float* x4, int T, int E, int S, int fcin,
+                     float* h_pc, float* rp_x, vn_stream_t stream);
 /* Value replay on rows t*E + e, e < S: dout[.][A] += weight * d mean((V - R)^2) / dV;
  * stats[0] += sum of squared errors. */
 int vn_unreal_vr_grad(const float* out, const float* returns, int T, int E, int S, int num_actions, float weight,
@@ -487,6 +493,11 @@ int vn_a2c_rollout_begin(int64_t* state3, float* lr_out, double lr0, double max_
  * in one launch. */
 int vn_a2c_metrics(const float* stats4, float inv_n, const float* scalars2, const float* aux3,
                    const float* aux_numel3, const float* episode_stats3, float* out9, vn_stream_t stream);
+/* vn_a2c_metrics + the UNREAL loss means: out[9..11] = [unreal4[0] * norm3[0] (pc),
+ * unreal4[1] * norm3[1] (rp), unreal4[3] * norm3[2] (vr)] when unreal4 != NULL (out holds 12). */
+int vn_a2c_metrics_ex(const float* stats4, float inv_n, const float* scalars2, const float* aux3,
+                      const float* aux_numel3, const float* episode_stats3, const float* unreal4,
+                      const float* unreal_norm3, float* out, vn_stream_t stream);
 int vn_policy_sample_dev(const float* out, int n, int num_actions, uint64_t seed,
                          const int64_t* counter_base_dev, uint64_t counter_offset, int32_t* actions,
                          float* logp, float* entropy, float* value, vn_stream_t stream);

@@ -25,10 +25,12 @@ def pixel_change(f0, f1):
 
 def pc_loss(q, frames, actions, dones, gamma=0.9):
     """q [T+1, S, 42, 42, A] (row T: the bootstrap observation), frames u8 [T+1, S, H, W, 3],
-    actions [T, S], dones [T, S] -> (mean squared TD error, d loss / d q)."""
+    actions [T, S], dones [T, S] -> (mean squared TD error, d loss / d q). On a done step the
+    pseudo-reward is 0: the next frame is the auto-reset frame of another episode."""
     q = q.detach().double().requires_grad_()
     T = actions.shape[0]
     r = pixel_change(frames[:-1], frames[1:])  # [T, S, 42, 42]
+    r = r * (~dones.bool()).double()[:, :, None, None]
     R = q[T].detach().max(-1).values
     targets = []
     for t in range(T - 1, -1, -1):

@@ -220,6 +220,18 @@ def _ckpt_worker(rank, world, port, save_dir, q):
         out["mismatch"] = "loaded"
     except RuntimeError as e:
         out["mismatch"] = "refused" if "disagree" in str(e) else str(e)
+    # run(resume=True)'s decision is collective: agreed while both files exist, refused on
+    # every rank once rank 1's file of the set is gone (instead of a hang in the collectives)
+    out["resume_agreed"] = bad._resume_decision()
+    dist.barrier()
+    if rank == 1:
+        os.remove(bad.rank_checkpoint_path())
+    dist.barrier()
+    try:
+        bad._resume_decision()
+        out["resume_split"] = "decided"
+    except RuntimeError as e:
+        out["resume_split"] = "refused" if "disagree" in str(e) else str(e)
     q.put((rank, out))
     dist.destroy_process_group()
 
@@ -245,6 +257,7 @@ def test_gloo_world2_checkpoint_sets_are_complete_and_consistent(tmp_path):
         assert o["latest"] == {"total_steps": 200, "num_updates": 20, "world": 2}
         assert o["resumed"] == (20, 200, 200.0 + r, 20.0)   # own env state, rank 0's params
         assert o["mismatch"] == "refused"
+        assert o["resume_agreed"] is True and o["resume_split"] == "refused"
     assert res[0]["gens"] == ["ckpt-%012d" % 200]
     sd = torch.load(os.path.join(str(tmp_path), "checkpoint.pt"), weights_only=True)
     assert sd["params_only"] and sd["num_updates"] == 20 and float(sd["params"][0]) == 20.0

@@ -191,3 +191,36 @@ def test_world2_trainer_update_and_per_rank_checkpoints(tmp_path):
         assert res[r]["collective_ms"] is not None and res[r]["collective_ms"] >= 0.0
     assert res[0]["world"] == 2
     assert res[0]["same_params"] and res[0]["same_sq"], res[0]
+
+
+def test_bench_world2_line_carries_dist_record(tmp_path):
+    """bench.py at world 2 as the driver launches it (torch.distributed.run, one rank per
+    process), here with gloo and both ranks on the box's one GPU, short legs: rank 0's JSON line
+    carries the dist record (world, ranks seen) and per training leg the all-reduce bytes,
+    buckets and the exposed collective time; the run exits 0 (bench.py exits non-zero when a
+    rank is missing, or under RCCL when two ranks share a device)."""
+    import json
+    import subprocess
+    port = _free_port()
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "20",
+           "--warmup", "5", "--envs", "64", "--scenes", "2", "--train-steps", "2", "--train-warmup", "1",
+           "--no-train-ref", "--no-c5", "--dist-backend", "gloo", "--allreduce-buckets", "2"]
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-4000:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["value"] > 0
+    d = line["dist"]
+    assert d["world"] == 2 and d["ranks_seen"] == 2 and d["backend"] == "gloo", d
+    for leg in ("train", "train_feedforward"):
+        ld = line[leg]["dist"]
+        assert ld["world"] == 2 and ld["allreduce_bytes"] > 0, ld
+        assert ld["allreduce_exposed_ms_per_update"] is not None and ld["allreduce_exposed_ms_per_update"] >= 0, ld
+        assert sum(b for b, _ in ld["buckets"]) == ld["allreduce_bytes"], ld
+    assert len(line["train"]["dist"]["buckets"]) == 2           # LSTM: heads + LSTM bucket, trunk bucket
+    assert len(line["train_feedforward"]["dist"]["buckets"]) == 1

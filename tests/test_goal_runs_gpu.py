@@ -235,3 +235,36 @@ def test_goal_runs_refused_where_unsupported():
     finally:
         os.environ.pop("VN_WGRAD_GENERIC")
     assert PolicyNet((300, 400), 4).goal_runs_supported(512)
+
+
+def test_dedup_off_for_companion_frames():
+    """An oriented scene with third-person companion frames (OrientedGraphEnv's render tuple,
+    environments/gym_graph/graph.py:60-61) emits a second frame that changes every step: the
+    trainer must not reuse a run start's goal maps there. Auto mode turns the
+    deduplication off, an explicit request is refused, and the rollout outputs equal the
+    forward of the frames actually emitted."""
+    import numpy as np
+    import vnav
+    rng = np.random.default_rng(3)
+    maze = np.ones((6, 6), dtype=bool)
+    obs = rng.integers(0, 256, size=(6, 6, 4, 84, 84, 3), dtype=np.uint8)
+    tp = rng.integers(0, 256, size=(6, 6, 4, 84, 84, 3), dtype=np.uint8)
+    scene = vnav.oriented_scene(maze, obs, goals=[(5, 5, 0)], tp_observations=tp)
+    E = 32
+    env = vnav.VectorEnv([scene], E, seed=1, max_episode_steps=50)
+    with pytest.raises(ValueError, match="companion"):
+        vnav.A2CTrainer(env, num_steps=4, recurrent=False, dedup_goals=True)
+    tr = vnav.A2CTrainer(env, num_steps=4, recurrent=False)
+    assert not tr.dedup_goals and tr.net.goal_runs_supported(E)
+    tr.rollout()
+    torch.cuda.synchronize()
+    T = tr.num_steps
+    # the second frame differs between steps of one episode (so a run start's maps would be stale)
+    assert not torch.equal(tr.rows_goal[:E], tr.rows_goal[E:2 * E])
+    out = torch.zeros_like(tr.out)
+    acts = tr.net.new_acts(T * E)
+    for t in range(T):
+        sl = slice(t * E, (t + 1) * E)
+        tr.net.forward(tr.params, tr._frames(tr.rows_img[sl], tr.rows_goal[sl]), E, acts, T * E, t * E, out[sl])
+    torch.cuda.synchronize()
+    assert torch.equal(out, tr.out)

@@ -16,6 +16,7 @@ value replay) are deep_rl's and not part of the engine. What is compared is the 
 the curve: episode length from the random-walk level down to a few steps, reward -> 1.
 
     python tools/replicate_log.py [updates] [out.csv] [--entropy-coef C] [--seed S] [--aux-weight W]
+    python tools/replicate_log.py [updates] [out.csv] --experiment [--seed S]   # vnav.train's trainer
 
 The options exist for the late-entropy investigation (DESIGN.md "End-to-end check"): the same
 run with another entropy coefficient / seed / aux weight. Each 10k-step row also carries the
@@ -75,14 +76,25 @@ def main():
     ap.add_argument("--entropy-coef", type=float, default=0.01)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--aux-weight", type=float, default=0.1)
+    ap.add_argument("--experiment", action="store_true",
+                    help="the trainer of vnav.train's thor-cached-auxiliary as registered (UNREAL losses, replayed "
+                         "aux batches, its entropy cost; the other options are ignored)")
     a = ap.parse_args()
     updates, out = a.updates, a.out
     torch.cuda.set_device(0)
-    scene = make_scene()
-    env = vnav.VectorEnv([scene], 4, seed=1 + a.seed, max_episode_steps=900)
-    env.set_complexity(0.01)
-    tr = vnav.A2CTrainer(env, num_steps=20, seed=a.seed, max_time_steps=2e6, recurrent=True,
-                         aux_weight=a.aux_weight, entropy_coefficient=a.entropy_coef)
+    if a.experiment:
+        from vnav.train import make_trainer
+        exp = make_trainer("thor-cached-auxiliary", seed=a.seed, save=False, logger=None)
+        tr = exp._setup()
+        print("experiment thor-cached-auxiliary: envs %d, entropy %g, aux %g (%s), unreal %s, dedup %s"
+              % (tr.env.num_envs, tr.entropy_coefficient, tr.aux_weight, tr.aux_source, tr.unreal, tr.dedup_goals),
+              flush=True)
+    else:
+        scene = make_scene()
+        env = vnav.VectorEnv([scene], 4, seed=1 + a.seed, max_episode_steps=900)
+        env.set_complexity(0.01)
+        tr = vnav.A2CTrainer(env, num_steps=20, seed=a.seed, max_time_steps=2e6, recurrent=True,
+                             aux_weight=a.aux_weight, entropy_coefficient=a.entropy_coef)
     ref = reference_curve()
     rows = []
     t0 = time.time()
@@ -101,6 +113,9 @@ def main():
                        grad_norm=float(np.mean([x["grad_norm"] for x in window])),
                        clipped=float(np.mean([x["grad_norm"] > tr.max_gradient_norm for x in window])),
                        wall_s=time.time() - t0)
+            if tr.unreal:
+                for k in ("pc_loss", "rp_loss", "vr_loss"):
+                    row[k] = float(np.mean([x[k] for x in window]))
             rr = [r for r in ref if r[0] <= row["step"]]
             if rr:
                 row.update(ref_reward=rr[-1][1], ref_episode_length=rr[-1][2], ref_entropy=rr[-1][3],
