@@ -1849,310 +1849,6 @@ __global__ __launch_bounds__(256, 2) void conv2_fwd_ring2_kernel(const float* __
   }
 }
 
-// ---- conv1 + conv2 forward in one kernel, 174x174 frames ----------------------------------
-// The ring kernel above loads every X1 row of a frame from HBM (written there by
-// conv1_fwd_x3_kernel) and splits it into the LDS ring. Here the X1 rows are produced inside
-// the same workgroup: waves 0-3 run conv1 (the x3 product of conv1_fwd_x3_kernel — u8 image rows
-// staged as bf16, the K relayout k' = ky*24 + kr, split weights; here the 33 weight fragments
-// of a lane stay in its registers) on the image rows of the NEXT band and write its new X1 rows,
-// split, straight into the ring slots, while waves 4-7 run conv2 on the current band (the ring
-// kernel's product: role (co tile, kernel-row half), 8 taps of split weights in registers, the
-// two halves meeting through an LDS partial). X1 never makes the HBM round trip between the two
-// layers; it is still stored (with the ReLU bitmask) for conv2's weight gradient. Per band k:
-//   A: conv2 MFMAs of band k (+ partial)  |  conv1 of band k+1 -> ring slots, X1, bitmask
-//   barrier
-//   B: conv2 epilogue of band k (X2)      |  band k+2's image rows -> LDS, loads of band k+3
-//   barrier
-// Every output is the same sum in the same order as conv1_fwd_x3_kernel / conv2_fwd_ring_kernel
-// (bitwise equal; VN_CONV12_SPLIT runs those two for A/B). LDS: the 14-slot ring (three bf16
-// planes, 110 KB), one partial buffer (9 KB) and the image rows of one band as bf16 (37 KB).
-struct Conv12Ring174 {
-  using R = Conv2Ring42;
-  static constexpr int H = 174, W = 174, RB = W * 3, RS = (RB + 3) / 4 * 4;  // image row bytes / LDS stride (bf16)
-  static constexpr int NPIX1 = R::IH * R::IW;                                  // conv1 map pixels per frame
-  static constexpr int IMG_ROWS = 4 * 8 + 4;  // image rows of the largest band (8 new X1 rows, ky = 7 pad row)
-  static constexpr int ND = IMG_ROWS * RB / 4;  // dwords of the largest band
-  static constexpr int NPF = (ND + 511) / 512;  // prefetched dwords per thread if all 8 waves staged alike
-  static constexpr int TP = 64, PP = 36;
-  static constexpr size_t PLANES = (size_t)3 * R::PL * 2, PART = (size_t)TP * PP * 4;
-  static constexpr size_t IMG = (size_t)IMG_ROWS * RS * 2;
-  static constexpr size_t LDS = PLANES + PART + IMG + 32 * 4;
-  static_assert(LDS <= 160 * 1024, "fused conv1 + conv2 ring");
-  static_assert((4 * RB) % 4 == 0, "band starts on whole dwords");
-};
-
-__global__ __launch_bounds__(512, 1) void conv12_fwd_ring_kernel(FrameSrc src, int n_frames, FrameList fl,
-                                                                 const float* __restrict__ W1,
-                                                                 const float* __restrict__ b1,
-                                                                 const float* __restrict__ W2,
-                                                                 const float* __restrict__ b2, float* __restrict__ X1,
-                                                                 uint32_t* __restrict__ M1, float* __restrict__ X2) {
-  using R = Conv2Ring42;
-  using C = Conv12Ring174;
-  constexpr int IW = R::IW, OW = R::OW, NB = R::NB, WH = R::WH, PSX = R::PSX, RSP = R::RSP, PL = R::PL;
-  constexpr int PP = C::PP, NP = R::OH * R::OW, RB = C::RB, RS = C::RS, NPF = C::NPF, NS = 11;
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem_c12[];
-  uint16_t* xs = reinterpret_cast<uint16_t*>(smem_c12);
-  float* part = reinterpret_cast<float*>(smem_c12 + C::PLANES);                    // [TP][PP]
-  uint16_t* img = reinterpret_cast<uint16_t*>(smem_c12 + C::PLANES + C::PART);     // [IMG_ROWS][RS]
-  float* bsh = reinterpret_cast<float*>(smem_c12 + C::PLANES + C::PART + C::IMG);   // conv1 bias [32]
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  n_frames = fl_count(fl, n_frames);
-  const int my_frames = (int)blockIdx.x < n_frames ? (n_frames - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
-  const int n_items = my_frames * NB;
-  auto frame_of = [&](int k) { return fl_frame(fl, (int)blockIdx.x + (k / NB) * (int)gridDim.x); };
-  // image rows of item k: 4 lo .. 4 hi + 3 (the last is the zero-weighted ky = 7 row)
-  auto img_dwords = [&](int k) {
-    const int b = k % NB;
-    return (4 * (R::new_hi(b) - R::new_lo(b)) + 4) * RB / 4;
-  };
-  // dwords [0, 2048) of a band's rows are staged by the conv1 waves (8 per thread), the rest by
-  // the conv2 waves (11 per thread): the conv1 waves' registers hold the weights
-  constexpr int NJ1 = 8, NJ2 = (C::ND - NJ1 * 256 + 255) / 256;
-  static_assert(NJ2 <= NPF + 2 && NJ1 * 256 + NJ2 * 256 >= C::ND, "staging split");
-  const int i0 = wave < 4 ? tid : NJ1 * 256 + (tid - 256);
-  using I1 = std::integral_constant<int, NJ1>;
-  using I2 = std::integral_constant<int, NJ2>;
-  uint32_t pre[NJ2];
-  auto load_img = [&](auto nj, int k) {
-    constexpr int NJ = decltype(nj)::value;
-    const int b = k % NB;
-    const uint32_t* s4 =
-        reinterpret_cast<const uint32_t*>(frame_ptr(src, frame_of(k)) + (int64_t)4 * R::new_lo(b) * RB);
-    const int nd = img_dwords(k);
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) pre[j] = s4[min(i0 + j * 256, nd - 1)];  // unconditional: countable
-  };
-  auto store_img = [&](auto nj, int k) {  // u8 -> bf16 rows (RB even: byte pairs never straddle a row)
-    constexpr int NJ = decltype(nj)::value;
-    const int nd = img_dwords(k);
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int i = i0 + j * 256;
-      if (i < nd) {
-        const uint32_t v = pre[j];
-        const int e = i * 4, row = e / RB, col = e - row * RB;
-        *reinterpret_cast<uint32_t*>(img + row * RS + col) = u8x2_bf16(v);
-        const bool wrap = col + 2 == RB;
-        *reinterpret_cast<uint32_t*>(img + (row + wrap) * RS + (wrap ? 0 : col + 2)) = u8x2_bf16(v >> 16);
-      }
-    }
-  };
-  if (wave < 4) {
-    // ---------------- conv1 waves: X1 rows [new_lo(b), new_hi(b)) of band item k ----------------
-    const int h = lane >> 5, c32 = lane & 31;
-    bf16x8 wr[NS][3];  // this lane's split weight fragments (A operand: rows = channels)
-#pragma unroll
-    for (int sl = 0; sl < NS; ++sl) {
-      union { uint16_t u[8]; bf16x8 v; } t0, t1, t2;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int kp = 16 * sl + 8 * h + j, ky = kp / 24, kr = kp % 24;
-        const float w = (ky < 7 && kr < 21) ? W1[c32 * 148 + ky * 21 + kr] : 0.0f;
-        split3_bf16(w, t0.u[j], t1.u[j], t2.u[j]);
-      }
-      wr[sl][0] = t0.v;
-      wr[sl][1] = t1.v;
-      wr[sl][2] = t2.v;
-    }
-    if (tid < 32) bsh[tid] = b1[tid];  // conv1's bias in LDS (read per tile: no registers held)
-    // conv1 of item k: its new X1 rows into the ring slots (and X1 / M1 in HBM)
-    auto conv1_item = [&](int k) {
-      const int b = k % NB, lo = R::new_lo(b), npx = (R::new_hi(b) - lo) * IW;
-      const int64_t f = frame_of(k);
-      const int tiles = (npx + 31) / 32;
-      for (int t = wave; t < tiles; t += 4) {
-        const int p = min(t * 32 + c32, npx - 1);
-        const int yr = p / IW, x = p - (p / IW) * IW, y = lo + yr;
-        const uint16_t* base = img + (4 * yr) * RS + x * 12;
-        f16v acc[3];  // one chain per weight term, summed as conv1_fwd_x3_kernel does
-#pragma unroll
-        for (int q = 0; q < 3; ++q)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) acc[q][r] = 0.0f;
-#pragma unroll
-        for (int sl = 0; sl < NS; ++sl) {
-          const int k0 = 16 * sl + 8 * h, ky = k0 / 24, kr0 = k0 - (k0 / 24) * 24;
-          const uint2* qp = reinterpret_cast<const uint2*>(base + ky * RS + kr0);
-          union { uint2 u[2]; bf16x8 v; } a;
-          a.u[0] = qp[0];
-          a.u[1] = qp[1];
-#pragma unroll
-          for (int q = 0; q < 3; ++q)  // D^T = W^T A^T: rows = channels, columns = pixels
-            acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wr[sl][q], a.v, acc[q], 0, 0, 0);
-        }
-        uint32_t bits = 0;
-        f4 yv[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const f4 bj = *reinterpret_cast<const f4*>(bsh + 8 * j + 4 * h);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int i = 4 * j + r;
-            const float sum = (acc[2][i] + acc[1][i]) + acc[0][i];
-            yv[j][r] = fmaxf(sum * (1.0f / 255.0f) + bj[r], 0.0f);
-            bits |= (yv[j][r] > 0.0f ? 1u : 0u) << (8 * j + 4 * h + r);
-          }
-        }
-        bits |= (uint32_t)__shfl_xor((int)bits, 32);
-        if (t * 32 + c32 < npx) {
-          const int64_t pix = f * C::NPIX1 + y * IW + x;
-          if (X1) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) *reinterpret_cast<f4*>(X1 + pix * 32 + 8 * j + 4 * h) = yv[j];
-          }
-          if (h == 0) M1[pix] = bits;
-          uint16_t* d = xs + (y % R::SLOTS) * RSP + ((x & 1) * WH + (x >> 1)) * PSX + 4 * h;
-          const int sw = R::swz(y, x >> 1);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            uint2 t0, t1, t2;
-            split3_pack(yv[j], t0, t1, t2);
-            uint16_t* dj = d + 8 * (j ^ sw);
-            *reinterpret_cast<uint2*>(dj) = t0;
-            *reinterpret_cast<uint2*>(dj + PL) = t1;
-            *reinterpret_cast<uint2*>(dj + 2 * PL) = t2;
-          }
-        }
-      }
-    };
-    // prologue: band 0 into the ring, band 1's image rows staged, band 2's in flight
-    if (n_items > 0) {
-      load_img(I1{}, 0);
-      store_img(I1{}, 0);
-    }
-    __syncthreads();  // P1
-    if (n_items > 0) {
-      load_img(I1{}, min(1, n_items - 1));
-      conv1_item(0);
-    }
-    __syncthreads();  // P2
-    if (n_items > 1) {
-      store_img(I1{}, 1);
-      load_img(I1{}, min(2, n_items - 1));
-    }
-    __syncthreads();  // P3
-    for (int k = 0; k < n_items; ++k) {
-      if (k + 1 < n_items) conv1_item(k + 1);
-      __syncthreads();  // B1: band k+1 in the ring; the image rows read
-      if (k + 2 < n_items) {
-        store_img(I1{}, k + 2);
-        load_img(I1{}, min(k + 3, n_items - 1));
-      }
-      __syncthreads();  // B2
-    }
-  } else {
-    // ---------------- conv2 waves: the ring kernel's product on band item k ----------------
-    const int w2 = wave - 4, ct = w2 & 1, kh = w2 >> 1;
-    const int i16 = lane & 15, q = lane >> 4;
-    bf16x8_t wf[8][3];  // [tap i: ky = 2kh + (i >> 2), kx = i & 3][term]
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      union { uint16_t u[8]; bf16x8_t v; } t0, t1, t2;
-      const float* wp = W2 + (ct * 16 + i16) * 512 + ((2 * kh + (i >> 2)) * 4 + (i & 3)) * 32 + 8 * q;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) split3_bf16(wp[j], t0.u[j], t1.u[j], t2.u[j]);
-      wf[i][0] = t0.v;
-      wf[i][1] = t1.v;
-      wf[i][2] = t2.v;
-    }
-    const f4 b4 = *reinterpret_cast<const f4*>(b2 + ct * 16 + 4 * q);
-    asm volatile("" ::"v"(b4[0]), "v"(b4[1]), "v"(b4[2]), "v"(b4[3]));
-    // the image staging is shared by all 512 threads (the conv1 waves' registers hold weights)
-    if (n_items > 0) {
-      load_img(I2{}, 0);
-      store_img(I2{}, 0);
-    }
-    __syncthreads();  // P1
-    if (n_items > 0) load_img(I2{}, min(1, n_items - 1));
-    __syncthreads();  // P2
-    if (n_items > 1) {
-      store_img(I2{}, 1);
-      load_img(I2{}, min(2, n_items - 1));
-    }
-    __syncthreads();  // P3
-    f4 acc[4];
-    for (int k = 0; k < n_items; ++k) {
-      const int b = k % NB, oy0 = R::BR * b, nr = min(R::BR, R::OH - oy0);
-#pragma unroll
-      for (int pass = 0; pass < 2; ++pass) {
-        const uint16_t* xb[2][2][2];  // [tile][ky - 2kh][kx >> 1]
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int t = 2 * pass + u;
-          int r = t < 3 ? t : (i16 >> 2);
-          const int ox = t < 3 ? i16 : 16 + (i16 & 3);
-          if (r >= nr) r = 0;
-#pragma unroll
-          for (int ky = 0; ky < 2; ++ky) {
-            const int y = 2 * (oy0 + r) + 2 * kh + ky;
-#pragma unroll
-            for (int hh = 0; hh < 2; ++hh) {
-              const int xi = ox + hh;
-              xb[u][ky][hh] = xs + (y % R::SLOTS) * RSP + xi * PSX + 8 * (q ^ R::swz(y, xi));
-            }
-          }
-        }
-        auto read_b = [&](bf16x8_t (&bv)[2][3], int i) {
-          const int ky = i >> 2, kx = i & 3;
-#pragma unroll
-          for (int u = 0; u < 2; ++u) {
-            const uint16_t* xp = xb[u][ky][kx >> 1] + (kx & 1) * WH * PSX;
-#pragma unroll
-            for (int tm = 0; tm < 3; ++tm) bv[u][tm] = *reinterpret_cast<const bf16x8_t*>(xp + tm * PL);
-          }
-        };
-        f4 c2[2] = {f4zero(), f4zero()};
-        bf16x8_t bv[2][2][3];
-        read_b(bv[0], 0);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          if (i + 1 < 8) read_b(bv[(i + 1) & 1], i + 1);
-#pragma unroll
-          for (int u = 0; u < 2; ++u) {  // small terms first (conv2_fwd_ring_kernel's order)
-            const bf16x8_t* bb = bv[i & 1][u];
-            f4 c = c2[u];
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i][2], bb[0], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i][0], bb[2], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i][1], bb[1], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i][1], bb[0], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i][0], bb[1], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i][0], bb[0], c, 0, 0, 0);
-            c2[u] = c;
-          }
-        }
-        acc[2 * pass] = c2[0];
-        acc[2 * pass + 1] = c2[1];
-      }
-      if (kh == 1) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) *reinterpret_cast<f4*>(part + (t * 16 + i16) * PP + ct * 16 + 4 * q) = acc[t];
-      }
-      __syncthreads();  // B1
-      if (kh == 0) {
-        const int64_t out0 = ((int64_t)frame_of(k) * NP + oy0 * OW) * 32 + ct * 16 + 4 * q;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          int r = t < 3 ? t : (i16 >> 2);
-          const int ox = t < 3 ? i16 : 16 + (i16 & 3);
-          if (r >= nr) r = 0;  // the pixel this lane computed: the same bytes as its own lane
-          const f4 pv = *reinterpret_cast<const f4*>(part + (t * 16 + i16) * PP + ct * 16 + 4 * q);
-          f4 v = acc[t] + pv;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e] + b4[e], 0.0f);
-          *reinterpret_cast<f4*>(X2 + out0 + (int64_t)(r * OW + ox) * 32) = v;
-        }
-      }
-      if (k + 2 < n_items) {
-        store_img(I2{}, k + 2);
-        load_img(I2{}, min(k + 3, n_items - 1));
-      }
-      __syncthreads();  // B2: the partial buffer read, band k+2's image rows staged
-    }
-  }
-}
-
 // Deterministic column sums of a [rows][32] matrix: per-block partials, then one block.
 __global__ __launch_bounds__(256) void colsum32_partial_kernel(const float* __restrict__ A, int64_t rows,
                                                                float* __restrict__ partial) {

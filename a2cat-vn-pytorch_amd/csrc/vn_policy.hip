@@ -1699,23 +1699,9 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
   constexpr bool kX3 = conv1_x3_fits<H0, W0>(), kConv1Lds = kConv1LdsFrame<H0, W0>;
   const bool f32in = src.f32[0] || src.f32[1];
   const int frames = 2 * n;
-  bool conv1_done = false, conv2_done = false;
-  if constexpr (conv2_fwd_ring_fits<G::OH1, G::OW1, G::OH2, G::OW2>() && H0 == 174 && W0 == 174) {
-    // training batches at 174x174: conv1 and conv2 in one kernel, X1 rows handed over in LDS
-    // (conv12_fwd_ring_kernel); VN_CONV12_SPLIT / VN_CONV2F_RING1 / VN_CONV2F_GENERIC select the
-    // two-kernel paths (A/B and parity checks; read per call)
-    if (!f32in && n > kSkinnyRows && !getenv("VN_CONV12_SPLIT") && !getenv("VN_CONV2F_GENERIC") &&
-        !getenv("VN_CONV2F_RING1")) {
-      const void* kfn = (const void*)conv12_fwd_ring_kernel;
-      VN_HIP(ensure_dyn_lds(kfn, Conv12Ring174::LDS));
-      const int blocks = std::min(frames, resident_blocks(kfn, 512, Conv12Ring174::LDS));
-      hipLaunchKernelGGL(conv12_fwd_ring_kernel, dim3(blocks), dim3(512), Conv12Ring174::LDS, st, src, frames, fl,
-                         P + L.l[0].w, P + L.l[0].b, P + L.l[1].w, P + L.l[1].b, a.X[0], a.M1, a.X[1]);
-      conv1_done = conv2_done = true;
-    }
-  }
+  bool conv1_done = false;
   if constexpr (kX3) {
-    if (!f32in && !conv1_done) {  // bf16 MFMA on split weights (exact products)
+    if (!f32in) {  // bf16 MFMA on split weights (exact products)
       using B = Conv1X3Band<H0, W0>;
       const int blocks =
           std::min(frames * B::NB, resident_blocks((const void*)conv1_fwd_x3_kernel<H0, W0, G::OH1, G::OW1>, 256, 0));
@@ -1724,7 +1710,7 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
       conv1_done = true;
     }
   } else if constexpr (kConv1Lds) {
-    if (!f32in && !conv1_done) {
+    if (!f32in) {
       constexpr int NF = (2 * H0 * W0 * 3 <= 64 * 1024) ? 2 : 1;
       const int blocks = std::min((frames + NF - 1) / NF,
                                   resident_blocks((const void*)conv1_fwd_kernel<H0, W0, G::OH1, G::OW1, NF>, 320, 0));
@@ -1740,8 +1726,7 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
     launch_gemm_x6<128, 32, 32, 4, 1>(fa, fb, ep, fa.M, 32, 148, st);
   }
   // conv2 (X1 -> X2): X1 bands split once into LDS planes (conv2_fwd_x6_kernel)
-  if (conv2_done) {
-  } else if constexpr (conv2_fwd_x6_fits<G::OH1, G::OW1, G::OH2, G::OW2>()) {
+  if constexpr (conv2_fwd_x6_fits<G::OH1, G::OW1, G::OH2, G::OW2>()) {
     using Bd = Conv2FwdBand<G::OH1, G::OW1, G::OH2, G::OW2>;
     const void* kfn = (const void*)conv2_fwd_x6_kernel<G::OH1, G::OW1, G::OH2, G::OW2>;
     VN_HIP(ensure_dyn_lds(kfn, Bd::LDS));  // > 64 KiB dynamic LDS: opt-in

@@ -35,16 +35,19 @@ __device__ __forceinline__ float sum32(float v) {
   return v;
 }
 
-// acc[m] (m < M) += this lane's share of sum_k A[m][k] B[k] over k < K. A comes from
-// fill(m, k) -> f4 (k % 4 == 0, zeros past K), staged in As [MR][kc]; B is a 16-B aligned
-// row. Per chunk of kc <= kSkKB * 128 values the lane's B loads are issued first, then the
-// A loads of the chunk's staging, so both latencies are paid once (a chunk per memory round
-// trip, not per 128 values). All 256 threads of the workgroup call it (it synchronises).
-constexpr int kSkKB = 24;  // B f4 registers per lane: chunks of up to 3072 values
+// acc[m] (m < M) += this lane's share of sum_k A[m][k] B[k] over k < K. LPC lanes share a
+// column (lane kl takes k = 4 kl + 4 LPC i of each chunk); A comes from fill(m, k) -> f4 (k % 4
+// == 0, zeros past K), staged in As [MR][kc]; B is a 16-B aligned row. Per chunk of kc <= KB *
+// 4 LPC values the lane's B loads are issued first, then the A loads of the chunk's staging,
+// so both latencies are paid once (a chunk per memory round trip, not per 128 values). KB = the
+// B f4 registers per lane, sized by the caller to the K it runs (a lane issues exactly KB loads
+// per chunk: clamped, unconditional). All 256 threads of the workgroup call it (it
+// synchronises).
+constexpr int kSkKB = 24;  // B f4 registers per lane at most: chunks of up to 3072 values
 
-template <int MR>
-constexpr int skinny_kc() {  // chunk length: kSkKB * 128 values, as the LDS allows (<= 128 KiB)
-  return (MR * kSkKB * 128 * 4 <= 128 * 1024) ? kSkKB * 128 : (128 * 1024 / (MR * 4)) / 128 * 128;
+template <int MR, int LPC, int KB>
+constexpr int skinny_kc() {  // chunk length: KB * 4 LPC values, as the LDS allows (<= 128 KiB)
+  return (MR * KB * 4 * LPC * 4 <= 128 * 1024) ? KB * 4 * LPC : (128 * 1024 / (MR * 4)) / (4 * LPC) * (4 * LPC);
 }
 
 struct RowsFill {  // dense rows A [M][lda] (16-B aligned, lda % 4 == 0)
@@ -55,11 +58,11 @@ struct RowsFill {  // dense rows A [M][lda] (16-B aligned, lda % 4 == 0)
   }
 };
 
-template <int MR, class FILL>
+template <int MR, int LPC, int KB, class FILL>
 __device__ __forceinline__ void skinny_dot(const FILL& fill, const float* __restrict__ B, int M, int K, float* As,
                                            float (&acc)[MR]) {
-  constexpr int KC = skinny_kc<MR>(), NB = KC / 128;
-  const int tid = threadIdx.x, kl = tid & 31;
+  constexpr int KC = skinny_kc<MR, LPC, KB>(), NB = KC / (4 * LPC);
+  const int tid = threadIdx.x, kl = tid & (LPC - 1);
   // every load of a chunk (B, then all of A's staging from dense rows) is issued before the
   // first use: a staging loop that stored each value as it arrived paid one memory round trip
   // per 256 values (10 in a row for conv_merge's 4 x 2592)
@@ -69,7 +72,7 @@ __device__ __forceinline__ void skinny_dot(const FILL& fill, const float* __rest
     f4 b[NB];
 #pragma unroll
     for (int i = 0; i < NB; ++i)  // clamped (a lane past the chunk reloads its end; unused)
-      b[i] = *reinterpret_cast<const f4*>(B + k0 + min(4 * kl + 128 * i, kc - 4));
+      b[i] = *reinterpret_cast<const f4*>(B + k0 + min(4 * kl + 4 * LPC * i, kc - 4));
     const int q4 = (kc + 3) / 4, nf = M * q4;
     if constexpr (std::is_same<FILL, RowsFill>::value) {
       f4 fr[NFI];
@@ -99,7 +102,7 @@ __device__ __forceinline__ void skinny_dot(const FILL& fill, const float* __rest
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-      const int kk = 4 * kl + 128 * i;
+      const int kk = 4 * kl + 4 * LPC * i;
       if (kk < kc) {
 #pragma unroll
         for (int m = 0; m < MR; ++m) {
@@ -116,40 +119,90 @@ __device__ __forceinline__ void skinny_dot(const FILL& fill, const float* __rest
       }
     }
   }
+  // the sum over the column's lanes within a wave (LPC = 128: each wave's half, combined by the caller)
 #pragma unroll
-  for (int m = 0; m < MR; ++m) acc[m] = sum32(acc[m]);
+  for (int m = 0; m < MR; ++m) {
+    float v = acc[m];
+#pragma unroll
+    for (int o = (LPC < 64 ? LPC : 64) / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, LPC < 64 ? LPC : 64);
+    acc[m] = v;
+  }
 }
 
+// The f4 registers per lane for K at LPC lanes per column (one chunk when it fits kSkKB).
+constexpr int skinny_kb(int K, int LPC) {
+  return (K + 4 * LPC - 1) / (4 * LPC) < kSkKB ? (K + 4 * LPC - 1) / (4 * LPC) : kSkKB;
+}
 
-// C[m][col] = A[m] . B[col] for m < M <= MR, col < N; then the epilogue.
-template <int MR, class EP>
+// C[m][col] = A[m] . B[col] for m < M <= MR, col < N; then the epilogue. 256 / LPC columns per
+// workgroup: LPC = 32 (8 columns) for short rows, 128 (2 columns, two waves each, their sums
+// added in wave order through LDS) where 8 columns per workgroup would leave most CUs idle
+// (conv_merge: 512 columns -> 256 workgroups instead of 64, every weight byte streamed once).
+template <int MR, int LPC, int KB, class EP>
 __global__ __launch_bounds__(256) void skinny_kernel(const float* __restrict__ A, int64_t lda,
                                                      const float* __restrict__ B, int64_t ldb, EP ep, int M, int N,
                                                      int K) {
-  __shared__ __attribute__((aligned(16))) float As[MR * skinny_kc<MR>()];
-  const int cg = threadIdx.x >> 5, kl = threadIdx.x & 31;
-  const int col = blockIdx.x * kSkCols + cg;
+  __shared__ __attribute__((aligned(16))) float As[MR * skinny_kc<MR, LPC, KB>()];
+  const int cg = threadIdx.x / LPC, kl = threadIdx.x & (LPC - 1);
+  const int col = blockIdx.x * (256 / LPC) + cg;
   float acc[MR];
 #pragma unroll
   for (int m = 0; m < MR; ++m) acc[m] = 0.0f;
-  skinny_dot<MR>(RowsFill{A, lda}, B + (int64_t)min(col, N - 1) * ldb, M, K, As, acc);
-  if (kl == 0 && col < N) {
+  skinny_dot<MR, LPC, KB>(RowsFill{A, lda}, B + (int64_t)min(col, N - 1) * ldb, M, K, As, acc);
+  if constexpr (LPC == 128) {
+    __shared__ float red[2][MR];
+    const int wave = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0 && (wave & 1)) {
 #pragma unroll
-    for (int m = 0; m < MR; ++m)
-      if (m < M) apply_epi(ep, m, col, acc[m]);
+      for (int m = 0; m < MR; ++m) red[wave >> 1][m] = acc[m];
+    }
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0 && !(wave & 1) && col < N) {
+#pragma unroll
+      for (int m = 0; m < MR; ++m)
+        if (m < M) apply_epi(ep, m, col, acc[m] + red[wave >> 1][m]);
+    }
+  } else {
+    if (kl == 0 && col < N) {
+#pragma unroll
+      for (int m = 0; m < MR; ++m)
+        if (m < M) apply_epi(ep, m, col, acc[m]);
+    }
   }
+}
+
+template <int MR, int LPC, class EP>
+inline void launch_skinny_lpc(const float* A, int64_t lda, const float* B, int64_t ldb, EP ep, int M, int N, int K,
+                              hipStream_t st) {
+  const dim3 grid((N + 256 / LPC - 1) / (256 / LPC));
+  // K-specific register counts: a lane issues exactly the loads its chunk uses
+  if (K <= 4 * LPC * 4)
+    hipLaunchKernelGGL((skinny_kernel<MR, LPC, 4, EP>), grid, dim3(256), 0, st, A, lda, B, ldb, ep, M, N, K);
+  else if (K <= 4 * LPC * 8)
+    hipLaunchKernelGGL((skinny_kernel<MR, LPC, 8, EP>), grid, dim3(256), 0, st, A, lda, B, ldb, ep, M, N, K);
+  else
+    hipLaunchKernelGGL((skinny_kernel<MR, LPC, (LPC == 128 ? 6 : kSkKB), EP>), grid, dim3(256), 0, st, A, lda, B, ldb,
+                       ep, M, N, K);
 }
 
 template <class EP>
 inline void launch_skinny(const float* A, int64_t lda, const float* B, int64_t ldb, EP ep, int M, int N, int K,
                           hipStream_t st) {
-  const dim3 grid((N + kSkCols - 1) / kSkCols);
-  if (M <= 4)
-    hipLaunchKernelGGL((skinny_kernel<4, EP>), grid, dim3(256), 0, st, A, lda, B, ldb, ep, M, N, K);
-  else if (M <= 8)
-    hipLaunchKernelGGL((skinny_kernel<8, EP>), grid, dim3(256), 0, st, A, lda, B, ldb, ep, M, N, K);
-  else
-    hipLaunchKernelGGL((skinny_kernel<kSkinnyRows, EP>), grid, dim3(256), 0, st, A, lda, B, ldb, ep, M, N, K);
+  if (N >= 256) {  // wide products (conv_merge): two columns per workgroup
+    if (M <= 4)
+      launch_skinny_lpc<4, 128>(A, lda, B, ldb, ep, M, N, K, st);
+    else if (M <= 8)
+      launch_skinny_lpc<8, 128>(A, lda, B, ldb, ep, M, N, K, st);
+    else
+      launch_skinny_lpc<kSkinnyRows, 128>(A, lda, B, ldb, ep, M, N, K, st);
+  } else {
+    if (M <= 4)
+      launch_skinny_lpc<4, 32>(A, lda, B, ldb, ep, M, N, K, st);
+    else if (M <= 8)
+      launch_skinny_lpc<8, 32>(A, lda, B, ldb, ep, M, N, K, st);
+    else
+      launch_skinny_lpc<kSkinnyRows, 32>(A, lda, B, ldb, ep, M, N, K, st);
+  }
 }
 
 // ---- conv3 + conv4 of a few envs, one launch ------------------------------------------
@@ -265,7 +318,8 @@ __global__ __launch_bounds__(256) void lstm_step_skinny_kernel(XcatFill xf, int 
                                                                const float* __restrict__ bhh,
                                                                const float* __restrict__ c_prev, float* xc_out,
                                                                float* acts, float* c_out, float* h_out) {
-  __shared__ __attribute__((aligned(16))) float As[MR * skinny_kc<MR>()];
+  constexpr int KB = 9;  // xcat = 512 + A + 1 padded + 512 <= 1152 (A <= 7): one chunk of 9 f4 per lane
+  __shared__ __attribute__((aligned(16))) float As[MR * skinny_kc<MR, 32, KB>()];
   __shared__ float gs[MR][kSkCols];
   const int tid = threadIdx.x, cg = tid >> 5, kl = tid & 31;
   const int gate = cg >> 1, unit = 2 * blockIdx.x + (cg & 1), col = gate * 512 + unit;
@@ -280,7 +334,7 @@ __global__ __launch_bounds__(256) void lstm_step_skinny_kernel(XcatFill xf, int 
   float acc[MR];
 #pragma unroll
   for (int m = 0; m < MR; ++m) acc[m] = 0.0f;
-  skinny_dot<MR>(xf, Wcat + (int64_t)col * xcat, E, xcat, As, acc);
+  skinny_dot<MR, 32, KB>(xf, Wcat + (int64_t)col * xcat, E, xcat, As, acc);
   if (kl == 0) {
     const float b0 = bih[col], b1 = bhh[col];
 #pragma unroll
@@ -323,13 +377,14 @@ struct LstmBwdStep {
 
 template <int MR>
 __global__ __launch_bounds__(256) void lstm_bwd_skinny_kernel(LstmBwdStep p, int E) {
-  __shared__ __attribute__((aligned(16))) float As[MR * skinny_kc<MR>()];
+  constexpr int KB = 16;  // K = 2048: one chunk of 16 f4 per lane (MR = 16: two, as the LDS allows)
+  __shared__ __attribute__((aligned(16))) float As[MR * skinny_kc<MR, 32, KB>()];
   const int cg = threadIdx.x >> 5, kl = threadIdx.x & 31;
   const int j = blockIdx.x * kSkCols + cg;
   float acc[MR];
 #pragma unroll
   for (int m = 0; m < MR; ++m) acc[m] = 0.0f;
-  skinny_dot<MR>(RowsFill{p.dgates_t, 2048}, p.whh_t + (int64_t)j * 2048, E, 2048, As, acc);
+  skinny_dot<MR, 32, KB>(RowsFill{p.dgates_t, 2048}, p.whh_t + (int64_t)j * 2048, E, 2048, As, acc);
   if (kl < MR && kl < E) {  // lane m of the group: env m (lstm_cell_bwd_kernel's arithmetic)
     float v = 0.0f;
 #pragma unroll

@@ -184,48 +184,6 @@ def test_conv2_ring_forward_matches_generic_product(hw, N):
         assert not bad, bad
 
 
-@pytest.mark.parametrize("N", [17, 300, 1030])
-def test_conv12_fused_forward_matches_split_kernels(N):
-    """conv1 + conv2 forward at 174x174 in one kernel (`conv12_fwd_ring_kernel`: conv1 waves
-    write each band's X1 rows, split, into the LDS ring the conv2 waves read) against the two
-    kernels it replaces (`VN_CONV12_SPLIT`: conv1_fwd_x3_kernel, then conv2_fwd_ring2_kernel
-    reading X1 back from HBM): the same sums in the same order, so X1, the ReLU bitmask, X2
-    and the outputs are bitwise equal. N = 17: 34 frames (most workgroups idle); 300 and 1030
-    wrap the persistent grid (the ring and the image staging cross frame boundaries)."""
-    from vnav.policy import GoalNavPolicy, frames_from_batch
-    torch.manual_seed(11)
-    hw = (174, 174)
-    pol = GoalNavPolicy(3, 4, hw)
-    net = pol.net
-    with torch.no_grad():
-        pol.params.add_(torch.randn_like(pol.params) * 0.01)
-    g = torch.Generator(device="cuda").manual_seed(5)
-    img = torch.randint(0, 256, (N,) + hw + (3,), dtype=torch.uint8, device="cuda", generator=g)
-    gl = torch.randint(0, 256, (N,) + hw + (3,), dtype=torch.uint8, device="cuda", generator=g)
-    m1, x1, x2 = 2 * 42 * 42, 2 * 42 * 42 * 32, 2 * 20 * 20 * 32
-
-    def run(split):
-        if split:
-            os.environ["VN_CONV12_SPLIT"] = "1"
-        try:
-            acts = net.new_acts(N)
-            acts.fill_(float("nan"))
-            out = torch.zeros((N, 8), device="cuda")
-            net.forward(pol.params.detach(), frames_from_batch(img, gl), N, acts, N, 0, out)
-            torch.cuda.synchronize()
-            M1 = acts[:N * m1].view(torch.int32).clone()
-            X1 = acts[N * m1:N * (m1 + x1)].clone()
-            X2 = acts[N * (m1 + x1):N * (m1 + x1 + x2)].clone()
-            return M1, X1, X2, out[:, :5].clone()
-        finally:
-            os.environ.pop("VN_CONV12_SPLIT", None)
-
-    (mf, xf1, xf2, of), (ms, xs1, xs2, os_) = run(False), run(True)
-    assert not torch.isnan(xf1).any() and not torch.isnan(xf2).any(), "unwritten activations"
-    for name, a, b in (("M1", mf, ms), ("X1", xf1, xs1), ("X2", xf2, xs2), ("out", of, os_)):
-        assert torch.equal(a, b), (name, float((a.float() - b.float()).abs().max()))
-
-
 @pytest.mark.parametrize("hw,N", [((84, 84), 1), ((84, 84), 16), ((174, 174), 4), ((174, 174), 13)])
 def test_conv34_small_matches_generic_products(hw, N):
     """conv3 + conv4 of a few envs (n <= 16) in one launch (`conv34_small_kernel`: exact fp32
