@@ -1849,6 +1849,237 @@ __global__ __launch_bounds__(256, 2) void conv2_fwd_ring2_kernel(const float* __
   }
 }
 
+// ---- conv1 + conv2 forward of a few envs at 174x174: one launch ------------------------------
+// A rollout step of <= 16 envs (the logged run's 4) ran conv1_fwd_x3_kernel and then the banded
+// conv2_fwd_x6_kernel, two dependent launches of ~10 us each, both bound by their load ->
+// stage -> compute -> store chains rather than by their arithmetic. Here one workgroup takes one
+// (frame, band of 3 conv2 output rows) item: it stages the image rows under the band's 8 X1
+// rows (6 for the last band) as bf16, all 8 waves run conv1 on them (conv1_fwd_x3_kernel's
+// product: split weight fragments in LDS, three accumulation chains, the same epilogue) into the
+// ring kernel's split planes, and after one barrier the 8 waves run conv2 on the band with the
+// ring kernel's roles and sums (conv2_fwd_ring_kernel: (co tile, kernel-row half, tile pair),
+// the halves meeting through an LDS partial). The two X1 rows a band shares with the next are
+// computed by both workgroups; X1 and the ReLU bitmask of a row go to HBM from one of them.
+// X1 is bitwise conv1_fwd_x3_kernel's, X2 bitwise conv2_fwd_ring_kernel's.
+struct Conv12Small174 {
+  using R = Conv2Ring42;
+  static constexpr int RB = 174 * 3, RS = (RB + 3) / 4 * 4;  // image row bytes / LDS row stride (bf16)
+  static constexpr int ROWS = 8;                               // X1 rows of a band (6 for the last)
+  static constexpr int IMG_ROWS = 4 * ROWS + 4;                // image rows under them (+ the ky = 7 pad row)
+  static constexpr int ND = IMG_ROWS * RB / 4;                 // image dwords of a band
+  static constexpr int NJ = (ND + 511) / 512;                  // image dwords per thread
+  static constexpr int PLR = ROWS * R::RSP;                    // plane size (bf16)
+  static constexpr size_t PLANES = (size_t)3 * PLR * 2, PART = (size_t)64 * 36 * 4;
+  static constexpr size_t IMG = (size_t)IMG_ROWS * RS * 2, WFR = (size_t)kConv1X3WeightLds;
+  static constexpr size_t LDS = PLANES + PART + IMG + WFR + 32 * 4;
+  static_assert(LDS <= 160 * 1024, "conv12 small");
+};
+
+__global__ __launch_bounds__(512, 1) void conv12_small_kernel(FrameSrc src, int n_frames, const float* __restrict__ W1,
+                                                              const float* __restrict__ b1,
+                                                              const float* __restrict__ W2,
+                                                              const float* __restrict__ b2, float* __restrict__ X1,
+                                                              uint32_t* __restrict__ M1, float* __restrict__ X2) {
+  using R = Conv2Ring42;
+  using C = Conv12Small174;
+  constexpr int IW = R::IW, OW = R::OW, NB = R::NB, WH = R::WH, PSX = R::PSX, RSP = R::RSP, PL = C::PLR;
+  constexpr int NP = R::OH * R::OW, NPIX1 = R::IH * R::IW, RB = C::RB, RS = C::RS, NS = 11, PP = 36;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem_c12s[];
+  uint16_t* xs = reinterpret_cast<uint16_t*>(smem_c12s);
+  float* part = reinterpret_cast<float*>(smem_c12s + C::PLANES);                              // [64][PP]
+  uint16_t* img = reinterpret_cast<uint16_t*>(smem_c12s + C::PLANES + C::PART);               // [IMG_ROWS][RS]
+  bf16x8* bw = reinterpret_cast<bf16x8*>(smem_c12s + C::PLANES + C::PART + C::IMG);           // [NS][3][64]
+  float* bsh = reinterpret_cast<float*>(smem_c12s + C::PLANES + C::PART + C::IMG + C::WFR);  // conv1 bias
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int it = blockIdx.x;  // grid = n_frames * NB (checked by the launcher)
+  const int f = it / NB, b = it - (it / NB) * NB;
+  const int y0 = 2 * R::BR * b, ny = min(C::ROWS, R::IH - y0);  // the band's X1 rows y0 .. y0 + ny - 1
+  // image rows 4 y0 .. 4 (y0 + ny) + 3, issued first
+  const int nd = (4 * ny + 4) * RB / 4;
+  uint32_t pre[C::NJ];
+  {
+    const uint32_t* s4 = reinterpret_cast<const uint32_t*>(frame_ptr(src, f) + (int64_t)4 * y0 * RB);
+#pragma unroll
+    for (int j = 0; j < C::NJ; ++j) pre[j] = s4[min(tid + j * 512, nd - 1)];
+  }
+  // conv2's split weights for this wave's role, in registers (conv2_fwd_ring_kernel's)
+  const int ct = wave & 1, kh = (wave >> 1) & 1, tsel = wave >> 2;
+  const int i16 = lane & 15, q = lane >> 4;
+  bf16x8_t wf[8][3];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    union { uint16_t u[8]; bf16x8_t v; } t0, t1, t2;
+    const float* wp = W2 + (ct * 16 + i16) * 512 + ((2 * kh + (i >> 2)) * 4 + (i & 3)) * 32 + 8 * q;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) split3_bf16(wp[j], t0.u[j], t1.u[j], t2.u[j]);
+    wf[i][0] = t0.v;
+    wf[i][1] = t1.v;
+    wf[i][2] = t2.v;
+  }
+  const f4 b4 = *reinterpret_cast<const f4*>(b2 + ct * 16 + 4 * q);
+  // conv1's split weight fragments [slice][term][lane] (conv1_fwd_x3_kernel's) and bias in LDS
+  for (int i = tid; i < NS * 64; i += 512) {
+    const int sl = i >> 6, ln = i & 63, hh = ln >> 5, co = ln & 31;
+    union { uint16_t u[8]; bf16x8 v; } t0, t1, t2;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int kp = 16 * sl + 8 * hh + j, ky = kp / 24, kr = kp % 24;
+      const float w = (ky < 7 && kr < 21) ? W1[co * 148 + ky * 21 + kr] : 0.0f;
+      split3_bf16(w, t0.u[j], t1.u[j], t2.u[j]);
+    }
+    bw[(sl * 3 + 0) * 64 + ln] = t0.v;
+    bw[(sl * 3 + 1) * 64 + ln] = t1.v;
+    bw[(sl * 3 + 2) * 64 + ln] = t2.v;
+  }
+  if (tid < 32) bsh[tid] = b1[tid];
+#pragma unroll
+  for (int j = 0; j < C::NJ; ++j) {  // u8 -> bf16 rows (RB even: byte pairs never straddle a row)
+    const int i = tid + j * 512;
+    if (i < nd) {
+      const uint32_t v = pre[j];
+      const int e = i * 4, row = e / RB, col = e - row * RB;
+      *reinterpret_cast<uint32_t*>(img + row * RS + col) = u8x2_bf16(v);
+      const bool wrap = col + 2 == RB;
+      *reinterpret_cast<uint32_t*>(img + (row + wrap) * RS + (wrap ? 0 : col + 2)) = u8x2_bf16(v >> 16);
+    }
+  }
+  __syncthreads();
+  {  // conv1: tiles of 32 band pixels, wave w takes tiles w, w + 8
+    const int h = lane >> 5, c32 = lane & 31, npx = ny * IW;
+    const int tiles = (npx + 31) / 32;
+    for (int t = wave; t < tiles; t += 8) {
+      const int p = min(t * 32 + c32, npx - 1);
+      const int yr = p / IW, x = p - (p / IW) * IW, y = y0 + yr;
+      const uint16_t* base = img + (4 * yr) * RS + x * 12;
+      int wl = lane;
+      asm volatile("" : "+v"(wl));  // keeps the weight-fragment reads inside the tile loop
+      f16v acc[3];
+#pragma unroll
+      for (int qq = 0; qq < 3; ++qq)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[qq][r] = 0.0f;
+#pragma unroll
+      for (int sl = 0; sl < NS; ++sl) {
+        const int k0 = 16 * sl + 8 * h, ky = k0 / 24, kr0 = k0 - (k0 / 24) * 24;
+        const uint2* qp = reinterpret_cast<const uint2*>(base + ky * RS + kr0);
+        union { uint2 u[2]; bf16x8 v; } a;
+        a.u[0] = qp[0];
+        a.u[1] = qp[1];
+#pragma unroll
+        for (int qq = 0; qq < 3; ++qq)  // D^T = W^T A^T: rows = channels, columns = pixels
+          acc[qq] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bw[(sl * 3 + qq) * 64 + wl], a.v, acc[qq], 0, 0, 0);
+      }
+      uint32_t bits = 0;
+      f4 yv[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f4 bj = *reinterpret_cast<const f4*>(bsh + 8 * j + 4 * h);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = 4 * j + r;
+          const float sum = (acc[2][i] + acc[1][i]) + acc[0][i];
+          yv[j][r] = fmaxf(sum * (1.0f / 255.0f) + bj[r], 0.0f);
+          bits |= (yv[j][r] > 0.0f ? 1u : 0u) << (8 * j + 4 * h + r);
+        }
+      }
+      bits |= (uint32_t)__shfl_xor((int)bits, 32);
+      if (t * 32 + c32 < npx) {
+        // X1 / bitmask rows y0 .. y0 + 5 from this band (all of the last band's)
+        if (yr < 2 * R::BR || b == NB - 1) {
+          const int64_t pix = (int64_t)f * NPIX1 + y * IW + x;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) *reinterpret_cast<f4*>(X1 + pix * 32 + 8 * j + 4 * h) = yv[j];
+          if (h == 0) M1[pix] = bits;
+        }
+        uint16_t* d = xs + yr * RSP + ((x & 1) * WH + (x >> 1)) * PSX + 4 * h;
+        const int sw = R::swz(y, x >> 1);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          uint2 t0, t1, t2;
+          split3_pack(yv[j], t0, t1, t2);
+          uint16_t* dj = d + 8 * (j ^ sw);
+          *reinterpret_cast<uint2*>(dj) = t0;
+          *reinterpret_cast<uint2*>(dj + PL) = t1;
+          *reinterpret_cast<uint2*>(dj + 2 * PL) = t2;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // conv2 on the band (conv2_fwd_ring_kernel's product and sums): plane row = y - y0
+  const int oy0 = R::BR * b, nr = min(R::BR, R::OH - oy0);
+  f4 acc[2] = {f4zero(), f4zero()};
+  {
+    const uint16_t* xb[2][2][2];  // [tile][ky - 2kh][kx >> 1]
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int t = tsel + 2 * u;
+      int r = t < 3 ? t : (i16 >> 2);
+      const int ox = t < 3 ? i16 : 16 + (i16 & 3);
+      if (r >= nr) r = 0;
+#pragma unroll
+      for (int ky = 0; ky < 2; ++ky) {
+        const int y = 2 * (oy0 + r) + 2 * kh + ky;
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          const int xi = ox + hh;
+          xb[u][ky][hh] = xs + (y - y0) * RSP + xi * PSX + 8 * (q ^ R::swz(y, xi));
+        }
+      }
+    }
+    auto read_b = [&](bf16x8_t (&bv)[2][3], int i) {
+      const int ky = i >> 2, kx = i & 3;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const uint16_t* xp = xb[u][ky][kx >> 1] + (kx & 1) * WH * PSX;
+#pragma unroll
+        for (int tm = 0; tm < 3; ++tm) bv[u][tm] = *reinterpret_cast<const bf16x8_t*>(xp + tm * PL);
+      }
+    };
+    bf16x8_t bv[2][2][3];
+    read_b(bv[0], 0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (i + 1 < 8) read_b(bv[(i + 1) & 1], i + 1);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {  // small terms first (conv2_fwd_ring_kernel's order)
+        const bf16x8_t* bb = bv[i & 1][u];
+        f4 c = acc[u];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i][2], bb[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i][0], bb[2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i][1], bb[1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i][1], bb[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i][0], bb[1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i][0], bb[0], c, 0, 0, 0);
+        acc[u] = c;
+      }
+    }
+  }
+  if (kh == 1) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      *reinterpret_cast<f4*>(part + ((tsel + 2 * u) * 16 + i16) * PP + ct * 16 + 4 * q) = acc[u];
+  }
+  __syncthreads();
+  if (kh == 0) {
+    const int64_t out0 = ((int64_t)f * NP + oy0 * OW) * 32 + ct * 16 + 4 * q;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int t = tsel + 2 * u;
+      int r = t < 3 ? t : (i16 >> 2);
+      const int ox = t < 3 ? i16 : 16 + (i16 & 3);
+      if (r >= nr) r = 0;  // the pixel this lane computed: the same bytes as its own lane
+      const f4 pv = *reinterpret_cast<const f4*>(part + (t * 16 + i16) * PP + ct * 16 + 4 * q);
+      f4 v = acc[u] + pv;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e] + b4[e], 0.0f);
+      *reinterpret_cast<f4*>(X2 + out0 + (int64_t)(r * OW + ox) * 32) = v;
+    }
+  }
+  (void)n_frames;
+}
+
 // Deterministic column sums of a [rows][32] matrix: per-block partials, then one block.
 __global__ __launch_bounds__(256) void colsum32_partial_kernel(const float* __restrict__ A, int64_t rows,
                                                                float* __restrict__ partial) {

@@ -1699,9 +1699,20 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
   constexpr bool kX3 = conv1_x3_fits<H0, W0>(), kConv1Lds = kConv1LdsFrame<H0, W0>;
   const bool f32in = src.f32[0] || src.f32[1];
   const int frames = 2 * n;
-  bool conv1_done = false;
+  bool conv1_done = false, conv2_done = false;
+  if constexpr (H0 == 174 && W0 == 174) {
+    // a few envs (the logged run's 4): conv1 + conv2 in one launch, one workgroup per (frame,
+    // band) item (conv12_small_kernel); VN_CONV12_SMALL_OFF keeps the two launches (A/B, parity)
+    if (!f32in && n <= kSkinnyRows && !gr && !getenv("VN_CONV12_SMALL_OFF")) {
+      const void* kfn = (const void*)conv12_small_kernel;
+      VN_HIP(ensure_dyn_lds(kfn, Conv12Small174::LDS));
+      hipLaunchKernelGGL(conv12_small_kernel, dim3(frames * Conv2Ring42::NB), dim3(512), Conv12Small174::LDS, st, src,
+                         frames, P + L.l[0].w, P + L.l[0].b, P + L.l[1].w, P + L.l[1].b, a.X[0], a.M1, a.X[1]);
+      conv1_done = conv2_done = true;
+    }
+  }
   if constexpr (kX3) {
-    if (!f32in) {  // bf16 MFMA on split weights (exact products)
+    if (!f32in && !conv1_done) {  // bf16 MFMA on split weights (exact products)
       using B = Conv1X3Band<H0, W0>;
       const int blocks =
           std::min(frames * B::NB, resident_blocks((const void*)conv1_fwd_x3_kernel<H0, W0, G::OH1, G::OW1>, 256, 0));
@@ -1710,7 +1721,7 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
       conv1_done = true;
     }
   } else if constexpr (kConv1Lds) {
-    if (!f32in) {
+    if (!f32in && !conv1_done) {
       constexpr int NF = (2 * H0 * W0 * 3 <= 64 * 1024) ? 2 : 1;
       const int blocks = std::min((frames + NF - 1) / NF,
                                   resident_blocks((const void*)conv1_fwd_kernel<H0, W0, G::OH1, G::OW1, NF>, 320, 0));
@@ -1726,7 +1737,8 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
     launch_gemm_x6<128, 32, 32, 4, 1>(fa, fb, ep, fa.M, 32, 148, st);
   }
   // conv2 (X1 -> X2): X1 bands split once into LDS planes (conv2_fwd_x6_kernel)
-  if constexpr (conv2_fwd_x6_fits<G::OH1, G::OW1, G::OH2, G::OW2>()) {
+  if (conv2_done) {
+  } else if constexpr (conv2_fwd_x6_fits<G::OH1, G::OW1, G::OH2, G::OW2>()) {
     using Bd = Conv2FwdBand<G::OH1, G::OW1, G::OH2, G::OW2>;
     const void* kfn = (const void*)conv2_fwd_x6_kernel<G::OH1, G::OW1, G::OH2, G::OW2>;
     VN_HIP(ensure_dyn_lds(kfn, Bd::LDS));  // > 64 KiB dynamic LDS: opt-in

@@ -184,6 +184,65 @@ def test_conv2_ring_forward_matches_generic_product(hw, N):
         assert not bad, bad
 
 
+@pytest.mark.parametrize("N", [1, 4, 13, 16])
+def test_conv12_small_matches_two_kernels(N):
+    """conv1 + conv2 of a few envs at 174x174 in one launch (`conv12_small_kernel`: one
+    workgroup per (frame, band) item runs conv1 on the band's X1 rows into LDS planes, then
+    conv2 on them) against the two launches it replaces (`VN_CONV12_SMALL_OFF`:
+    conv1_fwd_x3_kernel, then the banded conv2_fwd_x6_kernel): X1 and the ReLU bitmask bitwise
+    (the same products in the same order, every X1 row stored by one workgroup), X2 to rounding
+    (the ring kernel's two kernel-row halves vs the banded kernel's four partials: 2e-6 of
+    scale), the logits / value to 1e-5, and every parameter gradient to 1e-5 of scale."""
+    from vnav.policy import GoalNavPolicy, frames_from_batch
+    torch.manual_seed(17)
+    hw = (174, 174)
+    pol = GoalNavPolicy(3, 4, hw)
+    net = pol.net
+    with torch.no_grad():
+        pol.params.add_(torch.randn_like(pol.params) * 0.01)
+    g = torch.Generator(device="cuda").manual_seed(7)
+    img = torch.randint(0, 256, (N, 1) + hw + (3,), dtype=torch.uint8, device="cuda", generator=g)
+    gl = torch.randint(0, 256, (N, 1) + hw + (3,), dtype=torch.uint8, device="cuda", generator=g)
+    cl = torch.randn((N, 1, 4), device="cuda", generator=g)
+    cv = torch.randn((N, 1, 1), device="cuda", generator=g)
+    m1, x1, x2 = 2 * 42 * 42, 2 * 42 * 42 * 32, 2 * 20 * 20 * 32
+
+    def run(off):
+        if off:
+            os.environ["VN_CONV12_SMALL_OFF"] = "1"
+        try:
+            acts = net.new_acts(N)
+            acts.fill_(float("nan"))
+            out = torch.zeros((N, 8), device="cuda")
+            net.forward(pol.params.detach(), frames_from_batch(img.view((N,) + hw + (3,)), gl.view((N,) + hw + (3,))),
+                        N, acts, N, 0, out)
+            M1 = acts[:N * m1].view(torch.int32).clone()
+            X1 = acts[N * m1:N * (m1 + x1)].clone()
+            X2 = acts[N * (m1 + x1):N * (m1 + x1 + x2)].clone()
+            pol.params.grad = None
+            logits, value, _ = pol(((img, gl), None), None, None)
+            ((logits * cl).sum() + (value * cv).sum()).backward()
+            torch.cuda.synchronize()
+            return M1, X1, X2, out[:, :5].clone(), net.to_reference(pol.params.grad.clone())
+        finally:
+            os.environ.pop("VN_CONV12_SMALL_OFF", None)
+
+    (mf, xf1, xf2, of, gf), (ms, xs1, xs2, os_, gs) = run(False), run(True)
+    assert not torch.isnan(xf1).any() and not torch.isnan(xf2).any(), "unwritten activations"
+    assert torch.equal(mf, ms) and torch.equal(xf1, xs1)
+    e = float((xf2 - xs2).abs().max()) / float(xs2.abs().max())
+    assert e < 2e-6, e
+    e = float((of - os_).abs().max()) / max(float(os_.abs().max()), 1e-30)
+    assert e < 1e-5, e
+    bad = {}
+    for k in gs:
+        b = gs[k].numpy().astype(np.float64)
+        e = np.abs(gf[k].numpy() - b).max() / max(np.abs(b).max(), 1e-30)
+        if e > 1e-5:
+            bad[k] = "%.3g" % e
+    assert not bad, bad
+
+
 @pytest.mark.parametrize("hw,N", [((84, 84), 1), ((84, 84), 16), ((174, 174), 4), ((174, 174), 13)])
 def test_conv34_small_matches_generic_products(hw, N):
     """conv3 + conv4 of a few envs (n <= 16) in one launch (`conv34_small_kernel`: exact fp32
