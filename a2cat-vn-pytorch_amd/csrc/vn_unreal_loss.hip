@@ -210,9 +210,9 @@ __global__ __launch_bounds__(256) void unreal_vr_kernel(const float* __restrict_
 __global__ __launch_bounds__(256) void unreal_gather_kernel(const float* __restrict__ h_all,
                                                             const float* __restrict__ boot_h,
                                                             const float* __restrict__ x4, int T, int E, int S, int F,
-                                                            float* __restrict__ h_pc, float* __restrict__ rp_x) {
+                                                            int nh, float* __restrict__ h_pc, float* __restrict__ rp_x) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t n_h = (int64_t)(T + 1) * S * 128;  // 512 floats = 128 lanes per h row
+  const int64_t n_h = (int64_t)nh * S * 128;  // 512 floats = 128 lanes per h row (nh = T + 1, or 0)
   if (i < n_h) {
     const int j = (int)(i >> 7), q = (int)(i & 127);
     const float* src = j < T * S ? h_all + ((int64_t)(j / S) * E + j % S) * 512 : boot_h + (int64_t)(j - T * S) * 512;
@@ -274,11 +274,13 @@ int vn_unreal_rp_scatter(const float* dx, int T, int E, int S, int fcin, float* 
 
 int vn_unreal_gather(const float* h_all, const float* boot_h, const float* x4, int T, int E, int S, int fcin,
                      float* h_pc, float* rp_x, vn_stream_t stream) {
-  if (!h_all || !boot_h || !h_pc || T <= 0 || S <= 0 || S > E || (rp_x && (!x4 || T < 3 || fcin <= 0 || fcin % 4)))
+  if ((h_pc && (!h_all || !boot_h)) || (!h_pc && !rp_x) || T <= 0 || S <= 0 || S > E ||
+      (rp_x && (!x4 || T < 3 || fcin <= 0 || fcin % 4)))
     return fail(VN_EINVAL, "vn_unreal_gather: bad args");
-  const int64_t total = (int64_t)(T + 1) * S * 128 + (rp_x ? (int64_t)(T - 2) * S * 3 * (fcin / 4) : 0);
+  const int nh = h_pc ? T + 1 : 0;  // h rows to copy (none when h_pc == NULL)
+  const int64_t total = (int64_t)nh * S * 128 + (rp_x ? (int64_t)(T - 2) * S * 3 * (fcin / 4) : 0);
   hipLaunchKernelGGL(unreal_gather_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                     h_all, boot_h, x4, T, E, S, rp_x ? fcin : 0, h_pc, rp_x);
+                     h_all, boot_h, x4, T, E, S, rp_x ? fcin : 0, nh, h_pc, rp_x);
   VN_HIP(hipGetLastError());
   return VN_OK;
 }

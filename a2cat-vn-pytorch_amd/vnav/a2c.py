@@ -64,7 +64,8 @@ class A2CTrainer:
                  value_coefficient=0.5, entropy_coefficient=0.01, seed=0, process_group=None, recurrent=False,
                  aux_weight=0.0, arch="goal", cuda_graph=False, aux_source="rollout", replay_size=8,
                  capture_collectives=False, allreduce_buckets=1, time_collectives=False, dedup_goals=None,
-                 unreal=False, pc_weight=0.05, rp_weight=1.0, vr_weight=1.0, pc_gamma=0.9, unreal_envs=16):
+                 unreal=False, pc_weight=0.05, rp_weight=1.0, vr_weight=1.0, pc_gamma=0.9, unreal_envs=16,
+                 unreal_source="rollout"):
         self.env = env
         self.lib = _lib.load()
         self.device = env.device
@@ -172,16 +173,24 @@ class A2CTrainer:
         # trunk forward + backward, gradients added to the on-policy ones
         if aux_source not in ("rollout", "replay"):
             raise ValueError("aux_source must be 'rollout' or 'replay'")
+        if unreal_source not in ("rollout", "replay"):
+            raise ValueError("unreal_source must be 'rollout' or 'replay'")
         self.aux_source = aux_source
-        if aux_source == "replay":
-            if self.aux_weight <= 0:
-                raise ValueError("aux_source='replay' needs aux_weight > 0")
+        self.unreal_source = unreal_source if unreal else "rollout"
+        # the replay ring of the last replay_size rollouts (deep_rl's replay buffer, absent: its
+        # capacity and sequence shape are parity unpinned); one stored rollout is drawn per update
+        self.replay = aux_source == "replay" or self.unreal_source == "replay"
+        if self.replay:
             if cuda_graph:
-                raise ValueError("aux_source='replay' draws its sequence on the host each update: use cuda_graph=False")
+                raise ValueError("a replay source draws its sequence on the host each update: use cuda_graph=False")
             self.replay_rows = torch.zeros((int(replay_size), 2, N), dtype=torch.int32, **kw)
             self.replay_filled = 0
             self.replay_pos = 0
             self._replay_rng = torch.Generator().manual_seed(vdist.rank_seed(self.seed + 17, self.rank))
+            self._replay_k = 0
+        if aux_source == "replay":
+            if self.aux_weight <= 0:
+                raise ValueError("aux_source='replay' needs aux_weight > 0")
             self.aux_rows = torch.zeros((2, N), dtype=torch.int32, **kw)
             self.aux_acts = self.net.new_acts(N)
             self.aux_out = torch.zeros((N, OUT_LD), dtype=torch.float32, **kw)
@@ -264,9 +273,11 @@ class A2CTrainer:
     def _setup_unreal(self, unreal, pc_weight, rp_weight, vr_weight, pc_gamma, unreal_envs):
         """Buffers of the UNREAL losses: the first S envs' T + 1 LSTM features (the last row
         the bootstrap's) through the pixel-control heads, their T - 2 three-frame conv_base
-        samples through reward prediction."""
+        samples through reward prediction. unreal_source 'replay': the same losses on the first
+        S envs' sequences of a stored rollout (their own trunk, LSTM and heads pass)."""
         self.unreal = bool(unreal)
         if not self.unreal:
+            self.unreal_source = "rollout"
             return
         net, E, T = self.net, self.env.num_envs, self.num_steps
         if not (net.unreal and net.recurrent and net.arch == "goal"):
@@ -297,6 +308,39 @@ class A2CTrainer:
         self.unreal_dx4 = None if self.rp_into_aux else torch.zeros((T * E, F), **kw)
         self.unreal_stats = torch.zeros(4, **kw)  # pc sum sq, rp mean CE, rp samples, vr sum sq
         self._unreal_norm = torch.tensor([1.0 / (T * S * 42 * 42), 1.0, 1.0 / (T * S)], **kw)
+        if self.unreal_source == "replay":
+            self._setup_unreal_replay()
+
+    def _setup_unreal_replay(self):
+        """The replay ring's per-rollout record of the first S envs (rows t*S + e, the
+        bootstrap observation at t = T) and the buffers of their forward / backward pass."""
+        net, E, T, S = self.net, self.env.num_envs, self.num_steps, self.unreal_S
+        R = self.replay_rows.shape[0]
+        A1 = self.A + 1
+        n = (T + 1) * S
+        f32 = dict(dtype=torch.float32, device=self.device)
+        i32 = dict(dtype=torch.int32, device=self.device)
+        self.ur = dict(rows=torch.zeros((R, 2, n), **i32), actions=torch.zeros((R, T * S), **i32),
+                       rewards=torch.zeros((R, T, S), **f32),
+                       dones=torch.zeros((R, T, S), dtype=torch.bool, device=self.device),
+                       masks=torch.zeros((R, T + 1, S), **f32), lra=torch.zeros((R, T + 1, S, A1), **f32),
+                       hc0=torch.zeros((R, 2, S, 512), **f32))
+        X = net.lstm["xcat"]
+        self.ur_acts = net.new_acts(n)
+        self.ur_xcat = torch.zeros((n, X), **f32)
+        self.ur_lacts = torch.zeros((n, 2048), **f32)
+        self.ur_hc = torch.zeros((2, n, 512), **f32)
+        self.ur_gates = torch.zeros((S, 2048), **f32)
+        self.ur_out = torch.zeros((n, OUT_LD), **f32)
+        self.ur_returns = torch.zeros(T * S, **f32)
+        self.ur_dout = torch.zeros((n, OUT_LD), **f32)
+        self.ur_dz5 = torch.zeros((n, 512), **f32)
+        self.ur_dx4 = torch.zeros((n, net.fc_in), **f32)  # the bootstrap rows stay zero
+        self.ur_grads = torch.zeros(net.n_params, **f32)
+        self.ur_ws = torch.empty(net.workspace_floats(n), **f32)
+        self.ur_lstm_ws = torch.empty(net.lstm_workspace_floats(T + 1, S), **f32)
+        # the grads of the trunk, heads and LSTM (everything before the aux / UNREAL blocks)
+        self._ur_add_end = net.lstm["bhh"] + 2048
 
     def _unreal_forward_losses(self):
         """UNREAL losses of this rollout: vr into dout, pc and rp head gradients into grads;
@@ -353,8 +397,10 @@ class A2CTrainer:
         finished-episode statistics [count, return sum, length sum] as a device tensor."""
         self.rollout()
         batch = RolloutBatch(self, self.rows_img, self.rows_goal)
-        if self.aux_source == "replay":
-            batch["auxiliary_batch"] = self._replay_push_and_sample()
+        if self.replay:
+            aux = self._replay_push_and_sample()
+            if aux is not None:
+                batch["auxiliary_batch"] = aux
         return batch, {"episode_stats": self.episode_stats}
 
     def compute_auxiliary_loss(self, model, batch, device):
@@ -375,16 +421,104 @@ class A2CTrainer:
         return self._model_view
 
     def _replay_push_and_sample(self):
-        """Store this rollout's frame rows in the replay ring; draw one stored rollout
-        (uniform over the filled slots) as the aux sequence."""
+        """Store this rollout's frame rows (and, for the UNREAL losses, the first S envs'
+        sequences) in the replay ring; draw one stored rollout (uniform over the filled slots)
+        for this update's replayed batches. Returns the aux batch (None without aux replay)."""
         R = self.replay_rows.shape[0]
-        self.replay_rows[self.replay_pos, 0].copy_(self.rows_img)
-        self.replay_rows[self.replay_pos, 1].copy_(self.rows_goal)
+        k0 = self.replay_pos
+        self.replay_rows[k0, 0].copy_(self.rows_img)
+        self.replay_rows[k0, 1].copy_(self.rows_goal)
+        if self.unreal_source == "replay":
+            self._unreal_replay_push(k0)
         self.replay_pos = (self.replay_pos + 1) % R
         self.replay_filled = min(self.replay_filled + 1, R)
         k = int(torch.randint(self.replay_filled, (1,), generator=self._replay_rng))
+        self._replay_k = k
+        if self.aux_source != "replay":
+            return None
         self.aux_rows.copy_(self.replay_rows[k])
         return RolloutBatch(self, self.aux_rows[0], self.aux_rows[1])
+
+    def _unreal_replay_push(self, k):
+        """Slot k <- the first S envs of this rollout: frame rows of steps 0..T-1 and of the
+        bootstrap observation, actions, rewards, dones, the LSTM inputs (masks, last action /
+        reward) of steps 0..T and the (h, c) the rollout started from."""
+        E, T, S = self.env.num_envs, self.num_steps, self.unreal_S
+        u, info = self.ur, self.env._info
+        for j, (rows, last) in enumerate(((self.rows_img, info["img_row"]), (self.rows_goal, info["goal_row"]))):
+            r = u["rows"][k, j].view(T + 1, S)
+            r[:T].copy_(rows.view(T, E)[:, :S])
+            r[T].copy_(last[:S])
+        u["actions"][k].view(T, S).copy_(self.actions.view(T, E)[:, :S])
+        u["rewards"][k].copy_(self.rewards[:, :S])
+        u["dones"][k].copy_(self.dones[:, :S])
+        u["masks"][k, :T].copy_(self.masks[:, :S])
+        u["masks"][k, T].copy_(self.boot_mask[:S])
+        u["lra"][k, :T].copy_(self.lra[:, :S])
+        u["lra"][k, T].copy_(self.boot_lra[:S])
+        u["hc0"][k].copy_(self._hc0[:, :S])
+
+    def _unreal_replay_losses(self):
+        """UnrealTrainer's losses on the first S envs of the stored rollout drawn this update
+        (deep_rl samples its sequences from a replay buffer, experiments/ai2_auxiliary/trainer.py
+        :21-31; its sequence shape and initial state are absent, parity unpinned): trunk forward
+        of their T + 1 observations, the LSTM over T + 1 steps from the (h, c) the rollout started
+        from, the heads; value replay against their n-step returns (bootstrapped from step T),
+        pixel control on their h, reward prediction on their conv_base maps; then the LSTM and
+        trunk backward of those losses. Adds the trunk / heads / LSTM gradients to grads (the
+        pixel-control and reward-prediction blocks are written there directly)."""
+        lib, net = self.lib, self.net
+        T, S, A = self.num_steps, self.unreal_S, self.A
+        n = (T + 1) * S
+        P, st = _lib.ptr, self._stream()
+        u, k = self.ur, self._replay_k
+        rows = u["rows"][k]
+        frames = self._frames(rows[0], rows[1])
+        net.forward(self.params, frames, n, self.ur_acts, n, 0, None)
+        x5 = net.x5(self.ur_acts, n)
+        h_r, c_r = self.ur_hc[0], self.ur_hc[1]
+        h0, c0 = u["hc0"][k, 0], u["hc0"][k, 1]
+        for t in range(T + 1):
+            sl = slice(t * S, (t + 1) * S)
+            hp = h0 if t == 0 else h_r[(t - 1) * S:t * S]
+            cp = c0 if t == 0 else c_r[(t - 1) * S:t * S]
+            net.lstm_step(self.params, S, x5[sl], u["lra"][k, t], u["masks"][k, t], hp, cp, self.ur_xcat[sl],
+                          self.ur_gates, self.ur_lacts[sl], c_r[sl], h_r[sl])
+        net.heads(self.params, h_r, n, self.ur_out)
+        self.unreal_stats.zero_()
+        self.ur_dout.zero_()
+        rew, don = u["rewards"][k], u["dones"][k]
+        _lib.check(lib.vn_a2c_returns(P(rew), P(don), P(self.ur_out[T * S:]), T, S, A, ctypes.c_float(self.gamma),
+                                      P(self.ur_returns), st), "vn_a2c_returns")
+        if self.vr_weight > 0:
+            _lib.check(lib.vn_unreal_vr_grad(P(self.ur_out), P(self.ur_returns), T, S, S, A,
+                                             ctypes.c_float(self.vr_weight), P(self.ur_dout), P(self.unreal_stats[3:]),
+                                             st), "vn_unreal_vr_grad")
+        # pixel control on the replayed h (rows t*S + e, the bootstrap at t = T)
+        net.pc_forward(self.params, h_r, n, self.pcb, self.pc_a1, self.pc_p2, None, self.pc_ws)
+        H, W = self.env.frame_shape[:2]
+        _lib.check(lib.vn_unreal_pc_loss_grad(P(self.pc_p2), P(u["actions"][k]), P(don), ctypes.c_void_p(self._arena),
+                                              ctypes.c_int64(self._fb), H, W, P(rows[0]), P(rows[0][T * S:]), T, S, S,
+                                              A, ctypes.c_float(self.pc_gamma), ctypes.c_float(self.pc_weight),
+                                              P(self.unreal_stats), st), "vn_unreal_pc_loss_grad")
+        net.pc_backward(self.params, h_r, n, self.pcb, self.pc_a1, self.pc_p2, None, self.grads, self.dh_pc, self.pc_ws)
+        # reward prediction on three consecutive conv_base maps of the replayed envs
+        F = net.fc_in
+        _lib.check(lib.vn_unreal_gather(None, None, P(net.x4(self.ur_acts, n)), T, S, S, F, None, P(self.rp_x), st),
+                   "vn_unreal_gather")
+        n_rp = (T - 2) * S
+        net.rp_forward(self.params, self.rp_x, n_rp, self.rp_out)
+        _lib.check(lib.vn_unreal_rp_loss_grad(P(self.rp_out), P(rew), P(don), T, S, S, ctypes.c_float(self.rp_weight),
+                                              P(self.rp_dout), P(self.unreal_stats[1:3]), st), "vn_unreal_rp_loss_grad")
+        net.rp_backward(self.params, self.rp_x, n_rp, self.rp_dout, self.grads, self.rp_dx, self.pc_ws)
+        _lib.check(lib.vn_unreal_rp_scatter(P(self.rp_dx), T, S, S, F, P(self.ur_dx4), 0, st), "vn_unreal_rp_scatter")
+        # BPTT over the T + 1 replayed steps (value replay's dout + pixel control's dh), the trunk
+        net.lstm_backward(self.params, T + 1, S, self.ur_dout, h_r, self.ur_xcat, self.ur_lacts, c_r, c0,
+                          u["masks"][k], x5, self.ur_dz5, self.ur_grads, self.ur_lstm_ws, dh_extra=self.dh_pc,
+                          extra_envs=S)
+        net.backward_ex(self.params, frames, n, self.ur_acts, n, None, self.ur_dz5, self.ur_dx4, self.ur_grads,
+                        self.ur_ws)
+        self.grads[:self._ur_add_end].add_(self.ur_grads[:self._ur_add_end])
 
     def _stream(self):
         return _lib.stream_ptr(self.device)
@@ -499,7 +633,8 @@ class A2CTrainer:
 
     def update(self, batch=None):
         """One A2C update on the rollout just sampled (``batch`` from sample_training_batch;
-        None = the trainer's own rollout buffers with the on-policy aux batch)."""
+        None = the trainer's own rollout buffers with the on-policy aux batch; with
+        unreal_source='replay' the rollout is then pushed into the ring and a sequence drawn)."""
         lib, net = self.lib, self.net
         E, T, A = self.env.num_envs, self.num_steps, self.A
         N = T * E
@@ -530,7 +665,7 @@ class A2CTrainer:
                                       self.aux_weight, self.dpred, self.aux_stats, self.aux_ws)
             net.aux_backward(self.params, self.acts, N, N, self.a1, self.dpred, self.grads, self.dx4, self.aux_ws)
             dx4 = self.dx4
-        if self.unreal:  # after the aux heads: reward prediction adds to their dX4
+        if self.unreal and self.unreal_source == "rollout":  # after the aux heads: rp adds to their dX4
             unreal_dh, dx4 = self._unreal_forward_losses()
         frames = self._frames(self.rows_img, self.rows_goal)
         goals = None
@@ -555,6 +690,10 @@ class A2CTrainer:
                             goals=goals)
         if aux_batch is not None:
             self._add_trunk_grads(self.aux_grads)
+        if self.unreal and self.unreal_source == "replay":
+            if batch is None:  # a bare rollout(): store it and draw this update's sequence now
+                self._replay_push_and_sample()
+            self._unreal_replay_losses()
         if self._custom_aux:
             loss, self.aux_losses = self.compute_auxiliary_loss(self.model_view(), batch, self.device)
             if loss is not None:
@@ -577,7 +716,8 @@ class A2CTrainer:
         [head.w, P) = heads + LSTM + aux heads (flat layout, include/vnav.h), [0, head.w) =
         the conv / conv_merge trunk. One bucket otherwise (feed-forward nets compute heads and
         trunk in one call; a compute_auxiliary_loss override may touch every parameter)."""
-        return self.world > 1 and self.allreduce_buckets == 2 and self.recurrent and not self._custom_aux
+        return (self.world > 1 and self.allreduce_buckets == 2 and self.recurrent and not self._custom_aux
+                and self.unreal_source != "replay")  # the replayed UNREAL pass adds to head / LSTM grads later
 
     def _allreduce_head_bucket(self):
         self._head_work = None
@@ -759,10 +899,13 @@ class A2CTrainer:
         if self.recurrent:
             for k in self._RECURRENT_STATE:
                 sd[k] = getattr(self, k).cpu()
-        if self.aux_source == "replay":  # the replay ring and its draw stream resume exactly
+        if self.replay:  # the replay ring and its draw stream resume exactly
             sd["replay_rows"] = self.replay_rows.cpu()
             sd["replay_fill_pos"] = torch.tensor([self.replay_filled, self.replay_pos], dtype=torch.int64)
             sd["replay_rng"] = self._replay_rng.get_state()
+            if self.unreal_source == "replay":
+                for key, v in self.ur.items():
+                    sd["ur_" + key] = v.cpu()
         return sd
 
     def params_state_dict(self):
@@ -808,10 +951,13 @@ class A2CTrainer:
         if self.recurrent:
             for k in self._RECURRENT_STATE:
                 getattr(self, k).copy_(sd[k].to(self.device))
-        if self.aux_source == "replay" and "replay_rows" in sd:
+        if self.replay and "replay_rows" in sd:
             self.replay_rows.copy_(sd["replay_rows"].to(self.device))
             self.replay_filled, self.replay_pos = (int(x) for x in sd["replay_fill_pos"])
             self._replay_rng.set_state(sd["replay_rng"])
+            if self.unreal_source == "replay":
+                for key, v in self.ur.items():
+                    v.copy_(sd["ur_" + key].to(self.device))
         self.env.observe(gather=False)
 
 

@@ -107,6 +107,7 @@ class Experiment:
     # UnrealTrainer's pixel-control / reward-prediction / value-replay losses (deep_rl, absent:
     # parity unpinned) on the UNREAL heads of BigGoalHouseModel (goal.py:94-137)
     unreal = False
+    unreal_source = "rollout"
     rp_weight = 1.0
     pc_weight = 0.05
     vr_weight = 1.0
@@ -144,7 +145,7 @@ class Experiment:
                           # stand-in frames train without the UNREAL losses
                           unreal=self.unreal and min(self.env.frame_shape[:2]) >= 168,
                           pc_weight=self.pc_weight, rp_weight=self.rp_weight,
-                          vr_weight=self.vr_weight,
+                          vr_weight=self.vr_weight, unreal_source=self.unreal_source,
                           # world > 1: only on explicit opt-in (the captured RCCL path is unvalidated)
                           cuda_graph=self.cuda_graph and (self.world == 1 or self.capture_collectives),
                           capture_collectives=self.capture_collectives)
@@ -367,7 +368,8 @@ class ThorCachedAuxiliary(Experiment):
     auxiliary_weight 0.1 (:42), frames 174x174 (screen_size is not forwarded).
     env_kwargs: scene (a ThorGridWorld pickle path) or grid / frame / goal of the synthetic
     stand-in. The UNREAL losses run with the weights of :39-41 (rp 1.0, pc 0.05, vr 1.0) on
-    the on-policy sequences (deep_rl samples them from its replay buffer, absent)."""
+    sequences of a stored rollout, as deep_rl's UnrealTrainer samples them from its replay buffer
+    (absent: the buffer's capacity, sequence shape and initial states are parity unpinned)."""
 
     num_processes = 4
     auxiliary_weight = 0.1
@@ -385,6 +387,9 @@ class ThorCachedAuxiliary(Experiment):
     # (its capacity and sequence shape) is absent, so the sequence shape is parity unpinned.
     aux_source = "replay"
     unreal = True
+    # UnrealTrainer draws the pixel-control / value-replay / reward-prediction sequences from
+    # its replay buffer too: the first 16 envs of the stored rollout drawn for the aux batch
+    unreal_source = "replay"
 
     def create_env(self, kwargs):
         goal = tuple(kwargs.get("goal", (10, 14, 0)))

@@ -266,7 +266,8 @@ def aux_scenes(n, frame, seed=0):
 
 
 def bench_train(args, scenes, dev, world, rank, recurrent, aux_weight=0.0, envs=None, updates=None, warmup=None,
-                model=None, cuda_graph=False, marker=False, unreal=False, hardness=None, max_episode_steps=900):
+                model=None, cuda_graph=False, marker=False, unreal=False, hardness=None, max_episode_steps=900,
+                replay_sources=False):
     """A2C training throughput: one step = rollout of num_steps on every local env (policy
     forward + sampling + env step) + backward + one RCCL all-reduce of the flat gradient +
     clip + RMSprop. recurrent: the full BigGoalHouseModel (LSTM core, BPTT over the rollout);
@@ -282,7 +283,8 @@ def bench_train(args, scenes, dev, world, rank, recurrent, aux_weight=0.0, envs=
         env.reset()
     tr = vnav.A2CTrainer(env, num_steps=T, seed=7, max_time_steps=1e12, recurrent=recurrent, aux_weight=aux_weight,
                          cuda_graph=cuda_graph, time_collectives=world > 1 and not cuda_graph, unreal=unreal,
-                         allreduce_buckets=args.allreduce_buckets)
+                         allreduce_buckets=args.allreduce_buckets,
+                         **(dict(aux_source="replay", unreal_source="replay") if replay_sources else {}))
     for _ in range(warmup):
         tr.step(sync=False)
     torch.cuda.synchronize(dev)
@@ -421,6 +423,14 @@ def run_leg(leg, args, scenes, dev, world, rank, updates=None, warmup=None, mark
                             aux_weight=AUX_WEIGHT_LOGGED, envs=4, model="eager", unreal=True)
         res["eager_value"] = eager["value"]
         res["eager_ms_per_update"] = eager["ms_per_update"]
+        # the logged experiment's loss mix as thor-cached-auxiliary runs it: the aux deconv batch
+        # and the UNREAL sequences drawn from the replay ring (their own trunk / LSTM passes;
+        # a host draw per update, so eager)
+        mix = bench_train(args, sc, dev, world, rank, updates=100, warmup=3, recurrent=True,
+                          aux_weight=AUX_WEIGHT_LOGGED, envs=4, model="replay sources", unreal=True,
+                          replay_sources=True)
+        res["replay_sources"] = {"aux_source": "replay", "unreal_source": "replay", "value": mix["value"],
+                                 "ms_per_update": mix["ms_per_update"]}
     return res
 
 

@@ -384,7 +384,8 @@ int vn_unreal_rp_scatter(const float* dx, int T, int E, int S, int fcin, float* 
                          vn_stream_t stream);
 /* The losses' inputs in one launch: h_pc [(T+1)*S][512] = h_all rows t*E + e (t < T, e < S)
  * then boot_h rows e < S; rp_x [(T-2)*S][3][fcin] (may be NULL) slot k of sample t*S + e =
- * x4 row (t+k)*E + e (conv_base maps of frames t..t+2). */
+ * x4 row (t+k)*E + e (conv_base maps of frames t..t+2). h_pc == NULL (h_all / boot_h unused) gathers
+ * only rp_x. */
 int vn_unreal_gather(const float* h_all, const float* boot_h, const float* x4, int T, int E, int S, int fcin,
                      float* h_pc, float* rp_x, vn_stream_t stream);
 /* Value replay on rows t*E + e, e < S: dout[.][A] += weight * d mean((V - R)^2) / dV;

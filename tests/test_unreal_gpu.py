@@ -279,6 +279,55 @@ def test_trainer_unreal_losses_and_graph():
         np.testing.assert_allclose(x["pc_loss"], y["pc_loss"], rtol=1e-5)
 
 
+def test_unreal_replayed_sequence_of_this_rollout_equals_on_policy_losses():
+    """unreal_source='replay' with a one-slot ring replays the rollout just collected: its own
+    trunk, LSTM (from the (h, c) the rollout started from) and heads pass over the first S envs
+    must give the on-policy path's pc / rp / vr losses and the same total gradient, up to
+    rounding (the replayed batch runs other product paths: (T + 1) S samples against E). Both
+    trainers then step on; the replayed path's checkpoint resumes bit-exactly."""
+    import vnav
+    E, T, S = 16, 5, 16
+    trs = []
+    for src in ("rollout", "replay"):
+        env = _unreal_env(E, seed=5)
+        trs.append(vnav.A2CTrainer(env, num_steps=T, seed=3, max_time_steps=1e9, recurrent=True, unreal=True,
+                                   unreal_envs=S, unreal_source=src, replay_size=1))
+    a, b = trs
+    assert b.replay and b.unreal_source == "replay" and a.unreal_source == "rollout"
+    stats = []
+    for tr in trs:
+        batch, _ = tr.sample_training_batch()
+        tr.update(batch)
+        torch.cuda.synchronize()
+        stats.append(tr.unreal_stats.clone())
+    assert torch.equal(a.actions, b.actions) and torch.equal(a.rows_img, b.rows_img)
+    sa, sb = stats
+    np.testing.assert_allclose(sb.cpu().numpy(), sa.cpu().numpy(), rtol=2e-4, atol=1e-7)
+    ga, gb = a.net.to_reference(a.grads), b.net.to_reference(b.grads)
+    bad = {}
+    for k in ga:
+        ref = ga[k].numpy().astype(np.float64)
+        sc = np.abs(ref).max()
+        if sc == 0:
+            continue
+        e = np.abs(gb[k].numpy() - ref).max() / sc
+        if e > 1e-4:
+            bad[k] = "%.3g" % e
+    assert not bad, bad
+    # resume: a checkpoint of the replay trainer reproduces its next updates exactly
+    import copy
+    sd = copy.deepcopy(b.state_dict())
+    m1 = [b.step(sync=True) for _ in range(2)]
+    env = _unreal_env(E, seed=5)
+    c = vnav.A2CTrainer(env, num_steps=T, seed=3, max_time_steps=1e9, recurrent=True, unreal=True, unreal_envs=S,
+                        unreal_source="replay", replay_size=1)
+    c.load_state_dict(sd)
+    m2 = [c.step(sync=True) for _ in range(2)]
+    assert torch.equal(b.params, c.params)
+    for x, y in zip(m1, m2):
+        assert x["rp_loss"] == y["rp_loss"] and x["vr_loss"] == y["vr_loss"]
+
+
 def test_goal_nav_policy_reward_prediction_and_pixel_control(golden):
     """GoalNavPolicy(unreal=True).reward_prediction on uint8 frames vs the REFERENCE module's
     golden (the frames regenerate from the golden's seed: gen_model_goldens.unreal_case draws
