@@ -179,8 +179,29 @@ __device__ __forceinline__ void split3_bf16(float w, uint16_t& hi, uint16_t& mid
   lo = (uint16_t)(__float_as_uint(r2) >> 16);
 }
 
-__device__ __forceinline__ uint32_t u8x2_bf16(uint32_t v) {  // two low bytes -> two bf16
-  return (__float_as_uint((float)(v & 0xffu)) >> 16) | (__float_as_uint((float)((v >> 8) & 0xffu)) & 0xffff0000u);
+// Four frame bytes -> four bf16 (exact integers): v_cvt_f32_ubyte0..3 and one v_perm_b32 per pair
+// taking the two upper halves (6 VALU; the shift + and-or form took 8)
+__device__ __forceinline__ uint2 u8x4_bf16(uint32_t v) {
+  const uint32_t f0 = __float_as_uint((float)(v & 0xffu)), f1 = __float_as_uint((float)((v >> 8) & 0xffu));
+  const uint32_t f2 = __float_as_uint((float)((v >> 16) & 0xffu)), f3 = __float_as_uint((float)(v >> 24));
+  return uint2{__builtin_amdgcn_perm(f1, f0, 0x07060302u), __builtin_amdgcn_perm(f3, f2, 0x07060302u)};
+}
+
+// Dword i of a band of frame rows (RB bytes each, contiguous) into bf16 LDS rows of RS elements:
+// byte pairs never straddle a row (RB even); the second pair of the dword that ends a row
+// (col + 2 == RB) starts the next one
+template <int RB, int RS>
+__device__ __forceinline__ void stage_u8x4_bf16(uint16_t* img, int i, uint32_t v) {
+  static_assert(RB % 2 == 0, "byte pairs within rows");
+  const uint2 p = u8x4_bf16(v);
+  const int e = i * 4, row = e / RB, col = e - row * RB;
+  uint16_t* d0 = img + row * RS + col;
+  if constexpr (RB % 4 == 0) {  // a dword never straddles a row
+    *reinterpret_cast<uint2*>(d0) = p;
+  } else {
+    *reinterpret_cast<uint32_t*>(d0) = p.x;
+    *reinterpret_cast<uint32_t*>(d0 + 2 + (col + 2 == RB ? RS - RB : 0)) = p.y;
+  }
 }
 
 template <int H, int W, int OH, int OW>
@@ -242,17 +263,7 @@ __global__ __launch_bounds__(256, 2) void conv1_fwd_x3_kernel(FrameSrc src, int 
 #pragma unroll
     for (int j = 0; j < NPF; ++j) {  // u8 -> bf16 rows
       const int i = tid + j * 256;
-      if (i < nd) {
-        const uint32_t v = pre[j];
-        const int e = i * 4, row = e / RB, col = e - row * RB;
-        if constexpr (RB % 4 == 0) {  // a dword never straddles a row
-          *reinterpret_cast<uint2*>(img + row * RS + col) = uint2{u8x2_bf16(v), u8x2_bf16(v >> 16)};
-        } else {  // byte pairs never straddle (RB even)
-          *reinterpret_cast<uint32_t*>(img + row * RS + col) = u8x2_bf16(v);
-          const bool wrap = col + 2 == RB;
-          *reinterpret_cast<uint32_t*>(img + (row + wrap) * RS + (wrap ? 0 : col + 2)) = u8x2_bf16(v >> 16);
-        }
-      }
+      if (i < nd) stage_u8x4_bf16<RB, RS>(img, i, pre[j]);
     }
     __syncthreads();
     load_item(min(it + (int)gridDim.x, n_items - 1));
@@ -1936,13 +1947,7 @@ __global__ __launch_bounds__(512, 1) void conv12_small_kernel(FrameSrc src, int 
 #pragma unroll
   for (int j = 0; j < C::NJ; ++j) {  // u8 -> bf16 rows (RB even: byte pairs never straddle a row)
     const int i = tid + j * 512;
-    if (i < nd) {
-      const uint32_t v = pre[j];
-      const int e = i * 4, row = e / RB, col = e - row * RB;
-      *reinterpret_cast<uint32_t*>(img + row * RS + col) = u8x2_bf16(v);
-      const bool wrap = col + 2 == RB;
-      *reinterpret_cast<uint32_t*>(img + (row + wrap) * RS + (wrap ? 0 : col + 2)) = u8x2_bf16(v >> 16);
-    }
+    if (i < nd) stage_u8x4_bf16<RB, RS>(img, i, pre[j]);
   }
   __syncthreads();
   {  // conv1: tiles of 32 band pixels, wave w takes tiles w, w + 8

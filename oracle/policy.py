@@ -359,3 +359,55 @@ def reward_prediction(sd, feats):
     """goal.py:121-129 after conv_base: logits [R, 3] of feats [R, 3, 32, h3, w3] (Flatten =
     view(R, -1))."""
     return F.linear(feats.reshape(feats.shape[0], -1), sd["rp.1.weight"], sd["rp.1.bias"])
+
+
+BIGHOUSE_UNREAL_PARAM_ORDER = (  # BigHouseModel.named_parameters() order of pc_base, pc_action, pc_value, rp
+    "pc_base.0.0.weight", "pc_base.0.0.bias", "pc_action.0.0.weight", "pc_action.0.0.bias",
+    "pc_value.0.0.weight", "pc_value.0.0.bias", "rp.weight", "rp.bias",
+)
+
+
+def bighouse_unreal_shapes(num_outputs=4, fcin=7 * 7 * 32):
+    """bignet.py:77-96: pc_base Linear(512, 32*9*9), pc_action ConvTranspose2d(32, 1, 4, 2),
+    pc_value ConvTranspose2d(32, A, 4, 2); rp Linear(3 * fcin, 3) (bignet.py:96 writes 9*9*32*3,
+    which fits only 100x100 frames: at 84x84 conv_base ends at 7x7, in_features derived)."""
+    return {"pc_base.0.0.weight": (32 * 9 * 9, 512), "pc_base.0.0.bias": (32 * 9 * 9,),
+            "pc_action.0.0.weight": (32, 1, 4, 4), "pc_action.0.0.bias": (1,),
+            "pc_value.0.0.weight": (32, num_outputs, 4, 4), "pc_value.0.0.bias": (num_outputs,),
+            "rp.weight": (3, 3 * fcin), "rp.bias": (3,)}
+
+
+def seeded_bighouse_unreal_state(seed, num_outputs=4):
+    """gen_model_goldens.py:seeded_weights over BigHouseModel's four UNREAL modules (PCG64)."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    shapes = bighouse_unreal_shapes(num_outputs)
+    out = {}
+    for name in BIGHOUSE_UNREAL_PARAM_ORDER:
+        shape = shapes[name]
+        if name.endswith("bias"):
+            v = rng.uniform(-0.05, 0.05, size=shape)
+        else:
+            d = 1.0 / np.sqrt(int(np.prod(shape[1:])))
+            v = rng.uniform(-d, d, size=shape)
+        out[name] = v.astype(np.float32)
+    return out
+
+
+def bighouse_pixel_control(sd, h, masks=None):
+    """bignet.py:105-111 after _forward_base: q [N, A, 20, 20] of features h [N, 512]: pc_base
+    (Linear + ReLU) viewed (32, 9, 9), one ConvTranspose2d(k4, s2) + ReLU per branch, value +
+    action - mean(action). masks (optional): the ReLU masks of a run under test ({"pc_base"
+    [N, 32, 9, 9], "pc_value" [N, A, 20, 20], "pc_action" [N, 1, 20, 20]})."""
+    def act(x, key):
+        return F.relu(x) if masks is None else x * masks[key].to(x.dtype)
+
+    f = act(F.linear(h, sd["pc_base.0.0.weight"], sd["pc_base.0.0.bias"]).view(-1, 32, 9, 9), "pc_base")
+    a = act(F.conv_transpose2d(f, sd["pc_action.0.0.weight"], sd["pc_action.0.0.bias"], stride=2), "pc_action")
+    v = act(F.conv_transpose2d(f, sd["pc_value.0.0.weight"], sd["pc_value.0.0.bias"], stride=2), "pc_value")
+    return v + a - a.mean(1, keepdim=True)
+
+
+def bighouse_reward_prediction(sd, feats):
+    """bignet.py:98-103 after conv_base: logits [R, 3] of feats [R, 3, 32, h3, w3]."""
+    return F.linear(feats.reshape(feats.shape[0], -1), sd["rp.weight"], sd["rp.bias"])

@@ -10,6 +10,7 @@ Cases
          reference's own init_weights; biases then perturbed so bias paths are exercised.
   174x174 the unmodified reference topology (Linear(2592, 512)).
   unreal174 the pixel-control and reward-prediction heads (goal.py:94-137) at 174x174.
+  bighouse_unreal84 BigHouseModel's pixel-control and reward-prediction heads (bignet.py:77-111).
 For each: weights (reference state-dict names), uint8 frame inputs, trunk features,
 logits and value from the reference modules, and the gradients of the engine's A2C
 loss (oracle/a2c.py, parity unpinned at the trainer level) through the reference
@@ -225,12 +226,60 @@ def unreal_case(B, T, R, seed):
     return out
 
 
+BIG_UNREAL = ("pc_base", "pc_action", "pc_value", "rp")
+
+
+def bighouse_unreal_case(B, T, R, seed):
+    """BigHouseModel's UNREAL heads (models/bignet.py:77-111) at 84x84: pixel control (pc_base
+    Linear(512, 32*9*9) + ReLU, pc_action / pc_value one ConvTranspose2d(32, 1 / A, 4, 2) + ReLU
+    each, value + action - mean(action)) on stored LSTM features h [B,T,512] (_forward_base
+    replaced, as in unreal_case), and reward prediction on R samples of 3 frames. bignet.py's rp is
+    Linear(9*9*32*3, 3), which fits only 100x100 inputs (conv_base ends at 9x9 there, at 7x7 for
+    84x84 frames: view(R, -1) gives 3*7*7*32 = 4704): rebuilt as Linear(4704, 3) and re-initialised
+    with the reference's own init_weights (the derived-in_features deviation of the 84x84 goal
+    net's conv_merge). Weights from the seed (PCG64) over the four modules, conv_base from seed + 1."""
+    torch.manual_seed(seed)
+    model = BigHouseModel(3, 4)
+    model.rp = nn.Linear(3 * 7 * 7 * 32, 3)
+    model.init_weights(model.rp)
+    seeded_weights(model, seed, BIG_UNREAL)
+    seeded_weights(model, seed + 1, ("conv_base",))
+    rng = np.random.RandomState(seed)
+    h = torch.as_tensor((rng.rand(B, T, 512) * 2.0 - 0.5).astype(np.float32)).requires_grad_()
+    f = model.pc_base(h).view(B, T, 32, 9, 9)
+    a = model.pc_action(f)
+    q = model.pc_value(f) + a - a.mean(2, keepdim=True)
+    model._forward_base = lambda inputs, masks, states: (h, None)
+    with torch.no_grad():
+        q_ref, _ = model.pixel_control(None, None, None)
+    assert torch.equal(q, q_ref)
+    dq = torch.as_tensor(rng.randn(*q.shape).astype(np.float32))
+    image = torch.as_tensor(rng.randint(0, 256, size=(R, 3, 84, 84, 3)).astype(np.uint8))
+    img = (image.permute(0, 1, 4, 2, 3).float() / 255.0).contiguous()  # TransposeImage's arrays
+    feats = model.conv_base(img).detach().requires_grad_()
+    logits = model.rp(feats.view(R, -1))
+    with torch.no_grad():
+        assert torch.equal(logits, model.reward_prediction((img, None)))
+    drp = torch.as_tensor(rng.randn(R, 3).astype(np.float32))
+    model.zero_grad()
+    ((q * dq).sum() + (logits * drp).sum()).backward()
+    out = {"seed": np.array([seed]), "h": h.detach().numpy(), "q": q.detach().numpy(), "dq": dq.numpy(),
+           "dh": h.grad.numpy(), "image": image.numpy(), "rp_features": feats.detach().numpy(),
+           "rp_logits": logits.detach().numpy(), "drp": drp.numpy(), "d_rp_features": feats.grad.numpy()}
+    for name, p in model.named_parameters():
+        if name.split(".")[0] in BIG_UNREAL:
+            out["g:" + name] = p.grad.numpy()
+    out["g:pc_base.0.0.weight"] = out["g:pc_base.0.0.weight"][::16].copy()  # every 16th row (size)
+    return out
+
+
 def main():
     np.savez_compressed(os.path.join(HERE, "policy84.npz"), **case(84, 3, 2, 11))
     np.savez_compressed(os.path.join(HERE, "policy174.npz"), **case(174, 2, 1, 12, store_weights=False))
     np.savez_compressed(os.path.join(HERE, "aux174.npz"), **aux_case(174, 2, 1, 13))
     np.savez_compressed(os.path.join(HERE, "bighouse84.npz"), **bighouse_case(2, 2, 14))
     np.savez_compressed(os.path.join(HERE, "unreal174.npz"), **unreal_case(2, 3, 3, 15))
+    np.savez_compressed(os.path.join(HERE, "bighouse_unreal84.npz"), **bighouse_unreal_case(2, 3, 3, 16))
     n_params = sum(p.numel() for n, p in build(84, 0).named_parameters() if n.split(".")[0] in USED)
     print("84x84 trunk+heads parameters:", n_params)
 
