@@ -654,14 +654,17 @@ inline PolicyLayout make_layout(int H, int W, int A, int lstm = 0, int aux = 0, 
     off += (int64_t)kPcBase * 512;
     L.upb = off;
     off += kPcBase;
+    // BigHouseModel (bignet.py:77-91): one transposed conv per branch, 32 -> 8 (value 0..A-1,
+    // action A, padding) in W1 / b1; no second layer (W2, b2 empty)
+    const int c1 = arch == 1 ? kPcC2 : kPcC1;
     L.uw1 = off;
-    off += 32ll * 16 * kPcC1;
+    off += 32ll * 16 * c1;
     L.ub1 = off;
-    off += kPcC1;
+    off += c1;
     L.uw2 = off;
-    off += (int64_t)kPcC1 * 16 * kPcC2;
+    if (arch != 1) off += (int64_t)kPcC1 * 16 * kPcC2;
     L.ub2 = off;
-    off += kPcC2;
+    if (arch != 1) off += kPcC2;
     L.urw = off;
     off += 3ll * 3 * L.FCIN;
     L.urb = off;
@@ -2142,7 +2145,8 @@ int forward_bignet(const PolicyLayout& L, const float* P, const FrameSrc& src, i
 
 template <int H0, int W0>
 int backward_bignet(const PolicyLayout& L, const float* P, const FrameSrc& src, int n, const Acts& a,
-                    const float* dout, const float* dz5_in, float* Gr, const BwdWork& w, hipStream_t st) {
+                    const float* dout, const float* dz5_in, const float* dx3_extra, float* Gr, const BwdWork& w,
+                    hipStream_t st) {
   constexpr int OH1 = (H0 - 8) / 4 + 1, OW1 = (W0 - 8) / 4 + 1;
   constexpr int OH2 = (OH1 - 4) / 2 + 1, OW2 = (OW1 - 4) / 2 + 1;
   constexpr int OH3 = OH2 - 2, OW3 = OW2 - 2, FCIN = 32 * OH3 * OW3;
@@ -2164,11 +2168,16 @@ int backward_bignet(const PolicyLayout& L, const float* P, const FrameSrc& src, 
   }
   float* dz3 = w.dz4;  // [n][FCIN]
   float* dz2 = w.dz2;  // [n][OH2*OW2*64]
-  {  // conv_merge: dX3 = dz5 x Wfc masked by X3 ; dWfc
+  {  // conv_merge: dX3 = dz5 x Wfc (+ reward prediction's dX3) masked by X3 ; dWfc
     DenseRows fa{dz5, 512, n};
     DenseRows fb{T(4), 512, FCIN};
-    EpiMask ep{dz3, a.X[2], FCIN};
-    launch_gemm_x6<64, 64, 32, 2, 2>(fa, fb, ep, n, FCIN, 512, st);
+    if (dx3_extra) {
+      EpiMaskAdd ep{dz3, a.X[2], FCIN, dx3_extra};
+      launch_gemm_x6<64, 64, 32, 2, 2>(fa, fb, ep, n, FCIN, 512, st);
+    } else {
+      EpiMask ep{dz3, a.X[2], FCIN};
+      launch_gemm_x6<64, 64, 32, 2, 2>(fa, fb, ep, n, FCIN, 512, st);
+    }
     Im2colT<DenseRows> fbw{DenseRows{a.X[2], FCIN, n}, FCIN};
     launch_wgrad6<128, 128, 2, 2>(dz5, 512, 512, fbw, FCIN, n, w.slab, w.slab_cap, Gr + L.l[4].w, Gr + L.l[4].b, st);
   }
@@ -2653,6 +2662,9 @@ inline PcWork pc_carve(const PolicyLayout& L, float* ws) {
 // pixel_control (goal.py:131-137) on feature rows h [n][512]: pc_base (x6 product, bias,
 // ReLU), the two first deconvs as one 32 -> 64 deconv, the two second deconvs as one
 // block-diagonal 64 -> 8 deconv (ReLU on both), then the value/action combination.
+// The pixel-control map's side: 42 (BigGoalHouseModel's two k4 s2 layers) or 20 (BigHouseModel's one).
+inline int pc_side(const PolicyLayout& L) { return L.arch == 1 ? kPcA1 : kPcP; }
+
 int pc_forward_impl(const PolicyLayout& L, const float* P, const float* h, int n, float* pcb, float* A1, float* P2,
                     float* q, const PcWork& w, hipStream_t st) {
   {
@@ -2661,18 +2673,29 @@ int pc_forward_impl(const PolicyLayout& L, const float* P, const float* h, int n
     EpiBiasAct ep{pcb, kPcBase, P + L.upb, 1};
     launch_gemm_x6_sk<64, 64, 32, 2, 2>(fa, fb, ep, n, kPcBase, 512, st, L);
   }
-  {
+  if (L.arch == 1) {  // bignet.py:105-111: pc_value / pc_action side by side as one 32 -> 8 deconv
     TransposeSet ts;
-    ts.add(P + L.uw1, 32, 16 * kPcC1, w.w1t);
-    ts.add(P + L.uw2, kPcC1, 16 * kPcC2, w.w2t);
+    ts.add(P + L.uw1, 32, 16 * kPcC2, w.w1t);
     launch_transpose_set(ts, st);
+    if (const int rc = deconv_all<32, kPcC2, kPcMap, kPcMap, kPcA1, kPcA1>(pcb, w.w1t, P2, P + L.ub1, 1, n, st);
+        rc != VN_OK)
+      return rc;
+  } else {
+    {
+      TransposeSet ts;
+      ts.add(P + L.uw1, 32, 16 * kPcC1, w.w1t);
+      ts.add(P + L.uw2, kPcC1, 16 * kPcC2, w.w2t);
+      launch_transpose_set(ts, st);
+    }
+    if (const int rc = deconv_all<32, kPcC1, kPcMap, kPcMap, kPcA1, kPcA1>(pcb, w.w1t, A1, P + L.ub1, 1, n, st);
+        rc != VN_OK)
+      return rc;
+    if (const int rc = deconv_all<kPcC1, kPcC2, kPcA1, kPcA1, kPcP, kPcP>(A1, w.w2t, P2, P + L.ub2, 1, n, st);
+        rc != VN_OK)
+      return rc;
   }
-  if (const int rc = deconv_all<32, kPcC1, kPcMap, kPcMap, kPcA1, kPcA1>(pcb, w.w1t, A1, P + L.ub1, 1, n, st); rc != VN_OK)
-    return rc;
-  if (const int rc = deconv_all<kPcC1, kPcC2, kPcA1, kPcA1, kPcP, kPcP>(A1, w.w2t, P2, P + L.ub2, 1, n, st); rc != VN_OK)
-    return rc;
   if (q) {  // the trainer's pixel-control loss forms q from P2 itself
-    const int64_t npix = (int64_t)n * kPcP * kPcP;
+    const int64_t npix = (int64_t)n * pc_side(L) * pc_side(L);
     hipLaunchKernelGGL(pc_combine_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, st, P2, npix, L.A, q);
   }
   VN_HIP(hipGetLastError());
@@ -2683,33 +2706,46 @@ int pc_forward_impl(const PolicyLayout& L, const float* P, const float* h, int n
 // accumulate) from dq [n][42][42][A]. Consumes P2 (-> dP2), A1 (-> dA1) and pcb (-> dpcb).
 int pc_backward_impl(const PolicyLayout& L, const float* P, const float* h, int n, float* pcb, float* A1, float* P2,
                      const float* dq, float* Gr, float* dh, int accumulate, const PcWork& w, hipStream_t st) {
-  const int64_t npix = (int64_t)n * kPcP * kPcP;
+  const int64_t npix = (int64_t)n * pc_side(L) * pc_side(L);
   if (dq)  // else P2 already holds dL/dP2 (vn_unreal_pc_loss_grad)
     hipLaunchKernelGGL(pc_dq_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, st, P2, dq, npix, L.A);
-  // second layer: dW2 = A1^T x im2col(dP2) (block-diagonal mask), db2, dA1 masked in place, db1
-  const int P1 = n * kPcA1 * kPcA1;
-  using Im2 = NhwcIm2col<kPcC2, 4, 4, 2, kPcP, kPcP, kPcA1, kPcA1, 1>;  // dP2 windows per A1 pixel
-  launch_wgrad6<64, 128, 2, 2>(A1, kPcC1, kPcC1, Im2colT<Im2>{Im2{P2, P1}, 16 * kPcC2}, 16 * kPcC2, P1, w.slab,
-                               slab_floats(L), Gr + L.uw2, nullptr, st);
-  hipLaunchKernelGGL(pc_blockdiag_mask_kernel, dim3((kPcC1 * 16 * kPcC2 + 255) / 256), dim3(256), 0, st, Gr + L.uw2,
-                     L.A);
-  colsum(P2, npix, kPcC2, w.colsum, Gr + L.ub2, st);
-  {
-    DenseRows fb{P + L.uw2, 16 * kPcC2, kPcC1};
-    EpiMask ep{A1, A1, kPcC1};
-    launch_gemm_x6<64, 64, 32, 2, 2>(Im2{P2, P1}, fb, ep, P1, kPcC1, 16 * kPcC2, st);
-  }
-  colsum(A1, (int64_t)P1, kPcC1, w.colsum, Gr + L.ub1, st);
-  // first layer: dW1[ci][tap][co] = sum pcb[iy][ix][ci] dA1[2iy + ky][2ix + kx][co]; dpcb =
-  // conv(dA1, W1) under pc_base's ReLU, over pcb
-  const int P0 = n * kPcMap * kPcMap;
-  using Im1 = NhwcIm2col<kPcC1, 4, 4, 2, kPcA1, kPcA1, kPcMap, kPcMap, 1>;  // dA1 windows per pcb pixel
-  launch_wgrad6<32, 128, 1, 4>(pcb, 32, 32, Im2colT<Im1>{Im1{A1, P0}, 16 * kPcC1}, 16 * kPcC1, P0, w.slab,
-                               slab_floats(L), Gr + L.uw1, nullptr, st);
-  {
-    DenseRows fb{P + L.uw1, 16 * kPcC1, 32};
+  if (L.arch == 1) {
+    // the one layer: dW1[ci][tap][co] = sum pcb[iy][ix][ci] dP2[2iy + ky][2ix + kx][co] (the
+    // action and padding columns see dP2 = 0), db1, dpcb = conv(dP2, W1) under pc_base's ReLU
+    const int P0 = n * kPcMap * kPcMap;
+    using Im1 = NhwcIm2col<kPcC2, 4, 4, 2, kPcA1, kPcA1, kPcMap, kPcMap, 1>;  // dP2 windows per pcb pixel
+    launch_wgrad6<32, 128, 1, 4>(pcb, 32, 32, Im2colT<Im1>{Im1{P2, P0}, 16 * kPcC2}, 16 * kPcC2, P0, w.slab,
+                                 slab_floats(L), Gr + L.uw1, nullptr, st);
+    colsum(P2, npix, kPcC2, w.colsum, Gr + L.ub1, st);
+    DenseRows fb{P + L.uw1, 16 * kPcC2, 32};
     EpiMask ep{pcb, pcb, 32};
-    launch_gemm_x6<128, 32, 32, 4, 1>(Im1{A1, P0}, fb, ep, P0, 32, 16 * kPcC1, st);
+    launch_gemm_x6<128, 32, 32, 4, 1>(Im1{P2, P0}, fb, ep, P0, 32, 16 * kPcC2, st);
+  } else {
+    // second layer: dW2 = A1^T x im2col(dP2) (block-diagonal mask), db2, dA1 masked in place, db1
+    const int P1 = n * kPcA1 * kPcA1;
+    using Im2 = NhwcIm2col<kPcC2, 4, 4, 2, kPcP, kPcP, kPcA1, kPcA1, 1>;  // dP2 windows per A1 pixel
+    launch_wgrad6<64, 128, 2, 2>(A1, kPcC1, kPcC1, Im2colT<Im2>{Im2{P2, P1}, 16 * kPcC2}, 16 * kPcC2, P1, w.slab,
+                                 slab_floats(L), Gr + L.uw2, nullptr, st);
+    hipLaunchKernelGGL(pc_blockdiag_mask_kernel, dim3((kPcC1 * 16 * kPcC2 + 255) / 256), dim3(256), 0, st, Gr + L.uw2,
+                       L.A);
+    colsum(P2, npix, kPcC2, w.colsum, Gr + L.ub2, st);
+    {
+      DenseRows fb{P + L.uw2, 16 * kPcC2, kPcC1};
+      EpiMask ep{A1, A1, kPcC1};
+      launch_gemm_x6<64, 64, 32, 2, 2>(Im2{P2, P1}, fb, ep, P1, kPcC1, 16 * kPcC2, st);
+    }
+    colsum(A1, (int64_t)P1, kPcC1, w.colsum, Gr + L.ub1, st);
+    // first layer: dW1[ci][tap][co] = sum pcb[iy][ix][ci] dA1[2iy + ky][2ix + kx][co]; dpcb =
+    // conv(dA1, W1) under pc_base's ReLU, over pcb
+    const int P0 = n * kPcMap * kPcMap;
+    using Im1 = NhwcIm2col<kPcC1, 4, 4, 2, kPcA1, kPcA1, kPcMap, kPcMap, 1>;  // dA1 windows per pcb pixel
+    launch_wgrad6<32, 128, 1, 4>(pcb, 32, 32, Im2colT<Im1>{Im1{A1, P0}, 16 * kPcC1}, 16 * kPcC1, P0, w.slab,
+                                 slab_floats(L), Gr + L.uw1, nullptr, st);
+    {
+      DenseRows fb{P + L.uw1, 16 * kPcC1, 32};
+      EpiMask ep{pcb, pcb, 32};
+      launch_gemm_x6<128, 32, 32, 4, 1>(Im1{A1, P0}, fb, ep, P0, 32, 16 * kPcC1, st);
+    }
   }
   // pc_base: dW = dpcb^T x h (+ bias column), dh = dpcb x W
   {
@@ -2803,8 +2839,6 @@ int vn_policy_create_ex(int frame_h, int frame_w, int num_actions, int flags, vn
   if (!out) return fail(VN_EINVAL, "vn_policy_create: out is NULL");
   if (flags & ~(VN_POLICY_LSTM | VN_POLICY_AUX | VN_POLICY_BIGHOUSE | VN_POLICY_UNREAL))
     return fail(VN_EINVAL, "vn_policy_create: unknown flags");
-  if ((flags & VN_POLICY_BIGHOUSE) && (flags & VN_POLICY_UNREAL))
-    return fail(VN_EINVAL, "vn_policy_create: the UNREAL heads are BigGoalHouseModel's (goal.py:94-133)");
   if ((flags & VN_POLICY_BIGHOUSE) && (frame_h != 84 || frame_w != 84 || (flags & VN_POLICY_AUX)))
     return fail(VN_EINVAL, "vn_policy_create: BigHouseModel takes 84x84 frames (Linear(7*7*32)) and no aux heads");
   *out = nullptr;
@@ -2924,8 +2958,8 @@ int vn_policy_backward_goals(vn_policy* p, const float* params, const vn_frames*
   hipStream_t st = (hipStream_t)stream;
   const float* d = dz5 ? nullptr : dout;
   if (p->L.arch == 1) {
-    if (dx4_extra) return fail(VN_EINVAL, "vn_policy_backward: BigHouseModel has no aux heads");
-    return backward_bignet<84, 84>(p->L, params, src, n, a, d, dz5, grads, w, st);
+    // dx4_extra: dL/d conv_base's output (X3 here: reward prediction, bignet.py:98-103)
+    return backward_bignet<84, 84>(p->L, params, src, n, a, d, dz5, dx4_extra, grads, w, st);
   }
   return dispatch_geo(p->L, [&](auto g) {
     return backward_impl<decltype(g)::H, decltype(g)::W>(p->L, params, src, n, a, d, dz5, dx4_extra, grads, w, st,
@@ -2966,14 +3000,15 @@ int vn_pc_workspace_floats(vn_policy* p, int64_t* floats) {
 
 int vn_pc_forward(vn_policy* p, const float* params, const float* h, int n, float* pcb, float* a1, float* p2, float* q,
                   float* workspace, vn_stream_t stream) {
-  if (!p || !p->L.unreal || !params || !h || !pcb || !a1 || !p2 || !workspace || n <= 0)
+  if (!p || !p->L.unreal || !params || !h || !pcb || (!a1 && p->L.arch != 1) || !p2 || !workspace || n <= 0)
     return fail(VN_EINVAL, "vn_pc_forward: bad args");
   return pc_forward_impl(p->L, params, h, n, pcb, a1, p2, q, pc_carve(p->L, workspace), (hipStream_t)stream);
 }
 
 int vn_pc_backward(vn_policy* p, const float* params, const float* h, int n, float* pcb, float* a1, float* p2,
                    const float* dq, float* grads, float* dh, int accumulate, float* workspace, vn_stream_t stream) {
-  if (!p || !p->L.unreal || !params || !h || !pcb || !a1 || !p2 || !grads || !dh || !workspace || n <= 0)
+  if (!p || !p->L.unreal || !params || !h || !pcb || (!a1 && p->L.arch != 1) || !p2 || !grads || !dh || !workspace ||
+      n <= 0)
     return fail(VN_EINVAL, "vn_pc_backward: bad args");
   return pc_backward_impl(p->L, params, h, n, pcb, a1, p2, dq, grads, dh, accumulate, pc_carve(p->L, workspace),
                           (hipStream_t)stream);

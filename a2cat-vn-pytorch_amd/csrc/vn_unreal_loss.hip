@@ -24,7 +24,8 @@ namespace vn {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
-constexpr int kPcCells = 42;  // the pixel-control map (goal.py:103-112)
+constexpr int kPcCells = 42;  // BigGoalHouseModel's pixel-control map (goal.py:103-112)
+constexpr int kPcCellsBig = 20;  // BigHouseModel's (bignet.py:77-91, one k4 s2 layer on 9x9)
 constexpr int kPcCellPx = 4;
 
 // Mean |f1 - f0| / 255 over cell (cy, cx)'s 4 x 4 pixels and 3 channels (u8 HWC frames).
@@ -72,14 +73,15 @@ __global__ __launch_bounds__(256) void unreal_pc_loss_kernel(float* __restrict__
                                                              const uint8_t* __restrict__ arena, int64_t frame_bytes,
                                                              int H, int W, const int32_t* __restrict__ rows_img,
                                                              const int32_t* __restrict__ rows_last, int T, int E, int S,
-                                                             int A, float gamma, float coef, float* __restrict__ stats) {
+                                                             int A, int cells, float gamma, float coef,
+                                                             float* __restrict__ stats) {
   __shared__ float red[4];
-  constexpr int PP = kPcCells * kPcCells;
+  const int PP = cells * cells;
   const int idx = blockIdx.x * 256 + threadIdx.x;
   float sq = 0.0f;
   if (idx < S * PP) {
-    const int e = idx / PP, pix = idx - e * PP, cy = pix / kPcCells, cx = pix - cy * kPcCells;
-    const int top = (H - kPcCells * kPcCellPx) / 2, left = (W - kPcCells * kPcCellPx) / 2;
+    const int e = idx / PP, pix = idx - e * PP, cy = pix / cells, cx = pix - cy * cells;
+    const int top = (H - cells * kPcCellPx) / 2, left = (W - cells * kPcCellPx) / 2;
     float v[8];
     float* pb = p2 + ((int64_t)(T * S + e) * PP + pix) * 8;
     pc_load8(pb, v);
@@ -234,21 +236,29 @@ using namespace vn;
 
 extern "C" {
 
+int vn_unreal_pc_loss_grad_ex(float* p2, int cells, const int32_t* actions, const uint8_t* dones,
+                              const uint8_t* arena, int64_t frame_bytes, int height, int width,
+                              const int32_t* rows_img, const int32_t* rows_last, int T, int E, int S, int num_actions,
+                              float gamma, float weight, float* stats, vn_stream_t stream) {
+  if (!p2 || !actions || !dones || !arena || !rows_img || !rows_last || !stats || T <= 0 || S <= 0 || S > E ||
+      (cells != kPcCells && cells != kPcCellsBig) || num_actions < 1 || num_actions > 7 ||
+      height < cells * kPcCellPx || width < cells * kPcCellPx || frame_bytes < (int64_t)height * width * 3)
+    return fail(VN_EINVAL, "vn_unreal_pc_loss_grad: bad args");
+  const int n = S * cells * cells;
+  const float coef = weight / ((float)T * n);
+  hipLaunchKernelGGL(unreal_pc_loss_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, p2, actions,
+                     dones, arena, frame_bytes, height, width, rows_img, rows_last, T, E, S, num_actions, cells, gamma,
+                     coef, stats);
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
+
 int vn_unreal_pc_loss_grad(float* p2, const int32_t* actions, const uint8_t* dones, const uint8_t* arena,
                            int64_t frame_bytes, int height, int width, const int32_t* rows_img,
                            const int32_t* rows_last, int T, int E, int S, int num_actions, float gamma, float weight,
                            float* stats, vn_stream_t stream) {
-  if (!p2 || !actions || !dones || !arena || !rows_img || !rows_last || !stats || T <= 0 || S <= 0 || S > E ||
-      num_actions < 1 || num_actions > 7 || height < kPcCells * kPcCellPx || width < kPcCells * kPcCellPx ||
-      frame_bytes < (int64_t)height * width * 3)
-    return fail(VN_EINVAL, "vn_unreal_pc_loss_grad: bad args");
-  const int n = S * kPcCells * kPcCells;
-  const float coef = weight / ((float)T * n);
-  hipLaunchKernelGGL(unreal_pc_loss_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, p2, actions,
-                     dones, arena, frame_bytes, height, width, rows_img, rows_last, T, E, S, num_actions, gamma, coef,
-                     stats);
-  VN_HIP(hipGetLastError());
-  return VN_OK;
+  return vn_unreal_pc_loss_grad_ex(p2, kPcCells, actions, dones, arena, frame_bytes, height, width, rows_img, rows_last,
+                                   T, E, S, num_actions, gamma, weight, stats, stream);
 }
 
 int vn_unreal_rp_loss_grad(const float* logits, const float* rewards, const uint8_t* dones, int T, int E, int S,

@@ -146,6 +146,9 @@ SIGNATURES.update({
     "vn_lstm_backward_ex": (c_int, [c_void_p, c_void_p, c_int, c_int] + [c_void_p] * 9 + [c_int] + [c_void_p] * 4),
     "vn_unreal_pc_loss_grad": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p,
                                        c_void_p, c_int, c_int, c_int, c_int, c_float, c_float, c_void_p, c_void_p]),
+    "vn_unreal_pc_loss_grad_ex": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int,
+                                          c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_float, c_void_p,
+                                          c_void_p]),
     "vn_unreal_rp_loss_grad": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p,
                                        c_void_p, c_void_p]),
     "vn_unreal_rp_scatter": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),

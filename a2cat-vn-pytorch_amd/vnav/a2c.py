@@ -280,11 +280,12 @@ class A2CTrainer:
             self.unreal_source = "rollout"
             return
         net, E, T = self.net, self.env.num_envs, self.num_steps
-        if not (net.unreal and net.recurrent and net.arch == "goal"):
-            raise ValueError("unreal=True needs a recurrent BigGoalHouseModel policy with the UNREAL heads")
+        if not (net.unreal and net.recurrent):
+            raise ValueError("unreal=True needs a recurrent policy with the UNREAL heads")
         H, W = self.env.frame_shape[:2]
-        if H < 168 or W < 168:
-            raise ValueError("pixel control crops 42 cells of 4 px (goal.py:72, 112): frames need >= 168 px")
+        C = self.pc_cells = net.pc_side  # 42 (goal.py:72, 112) or 20 (BigHouseModel, bignet.py:77-91)
+        if H < 4 * C or W < 4 * C:
+            raise ValueError("pixel control crops %d cells of 4 px: frames need >= %d px" % (C, 4 * C))
         if T < 3:
             raise ValueError("reward prediction needs num_steps >= 3")
         self.pc_weight, self.rp_weight, self.vr_weight = float(pc_weight), float(rp_weight), float(vr_weight)
@@ -307,7 +308,7 @@ class A2CTrainer:
         self.rp_into_aux = self.aux_weight > 0 and self.aux_source == "rollout"
         self.unreal_dx4 = None if self.rp_into_aux else torch.zeros((T * E, F), **kw)
         self.unreal_stats = torch.zeros(4, **kw)  # pc sum sq, rp mean CE, rp samples, vr sum sq
-        self._unreal_norm = torch.tensor([1.0 / (T * S * 42 * 42), 1.0, 1.0 / (T * S)], **kw)
+        self._unreal_norm = torch.tensor([1.0 / (T * S * C * C), 1.0, 1.0 / (T * S)], **kw)
         if self.unreal_source == "replay":
             self._setup_unreal_replay()
 
@@ -364,11 +365,11 @@ class A2CTrainer:
         H, W = self.env.frame_shape[:2]
         info = self.env._info
         # q formed from p2 in the loss kernel, which leaves dL/dp2 in p2 for the backward
-        _lib.check(lib.vn_unreal_pc_loss_grad(P(self.pc_p2), P(self.actions), P(self.dones), ctypes.c_void_p(self._arena),
-                                              ctypes.c_int64(self._fb), H, W, P(self.rows_img), P(info["img_row"]),
-                                              T, E, S, A, ctypes.c_float(self.pc_gamma),
-                                              ctypes.c_float(self.pc_weight), P(self.unreal_stats), st),
-                   "vn_unreal_pc_loss_grad")
+        _lib.check(lib.vn_unreal_pc_loss_grad_ex(P(self.pc_p2), self.pc_cells, P(self.actions), P(self.dones),
+                                                 ctypes.c_void_p(self._arena), ctypes.c_int64(self._fb), H, W,
+                                                 P(self.rows_img), P(info["img_row"]), T, E, S, A,
+                                                 ctypes.c_float(self.pc_gamma), ctypes.c_float(self.pc_weight),
+                                                 P(self.unreal_stats), st), "vn_unreal_pc_loss_grad")
         net.pc_backward(self.params, self.h_pc, n_pc, self.pcb, self.pc_a1, self.pc_p2, None, self.grads, self.dh_pc,
                         self.pc_ws)
         n_rp = (T - 2) * S
@@ -497,10 +498,11 @@ class A2CTrainer:
         # pixel control on the replayed h (rows t*S + e, the bootstrap at t = T)
         net.pc_forward(self.params, h_r, n, self.pcb, self.pc_a1, self.pc_p2, None, self.pc_ws)
         H, W = self.env.frame_shape[:2]
-        _lib.check(lib.vn_unreal_pc_loss_grad(P(self.pc_p2), P(u["actions"][k]), P(don), ctypes.c_void_p(self._arena),
-                                              ctypes.c_int64(self._fb), H, W, P(rows[0]), P(rows[0][T * S:]), T, S, S,
-                                              A, ctypes.c_float(self.pc_gamma), ctypes.c_float(self.pc_weight),
-                                              P(self.unreal_stats), st), "vn_unreal_pc_loss_grad")
+        _lib.check(lib.vn_unreal_pc_loss_grad_ex(P(self.pc_p2), self.pc_cells, P(u["actions"][k]), P(don),
+                                                 ctypes.c_void_p(self._arena), ctypes.c_int64(self._fb), H, W, P(rows[0]),
+                                                 P(rows[0][T * S:]), T, S, S, A, ctypes.c_float(self.pc_gamma),
+                                                 ctypes.c_float(self.pc_weight), P(self.unreal_stats), st),
+                   "vn_unreal_pc_loss_grad")
         net.pc_backward(self.params, h_r, n, self.pcb, self.pc_a1, self.pc_p2, None, self.grads, self.dh_pc, self.pc_ws)
         # reward prediction on three consecutive conv_base maps of the replayed envs
         F = net.fc_in

@@ -127,6 +127,9 @@ class PolicyNet:
             self.aux_layout = dict(w1=info[0], b1=info[1], w2=info[2], b2=info[3], a_hw=(info[4], info[5]),
                                    p_hw=(info[6], info[7]))
         self.unreal_layout = None
+        # pixel-control map side and first deconv width: BigGoalHouseModel's two k4 s2 layers
+        # (32 -> 64 -> 8, 42x42), BigHouseModel's one (32 -> 8, 20x20; bignet.py:77-91)
+        self.pc_side, self.pc_c1 = (PC_A1, 8) if arch == "bighouse" else (PC_P, 64)
         if self.unreal:
             info = (ctypes.c_int64 * 8)()
             _lib.check(self.lib.vn_policy_unreal_info(h, info), "vn_policy_unreal_info")
@@ -172,12 +175,13 @@ class PolicyNet:
                           flat[X["w2"]:X["w2"] + 48 * 16 * 8].view(48, 4, 4, 8), flat[X["b2"]:X["b2"] + 8])
         if self.unreal_layout:
             U = self.unreal_layout
-            k = 3 * self.fc_in
+            k, c1 = 3 * self.fc_in, self.pc_c1
             out["unreal"] = dict(
                 pc_w=flat[U["pc_w"]:U["pc_w"] + PC_BASE * 512].view(PC_BASE, 512), pc_b=flat[U["pc_b"]:U["pc_b"] + PC_BASE],
-                w1=flat[U["w1"]:U["w1"] + 32 * 16 * 64].view(32, 4, 4, 64), b1=flat[U["b1"]:U["b1"] + 64],
-                w2=flat[U["w2"]:U["w2"] + 64 * 16 * 8].view(64, 4, 4, 8), b2=flat[U["b2"]:U["b2"] + 8],
+                w1=flat[U["w1"]:U["w1"] + 32 * 16 * c1].view(32, 4, 4, c1), b1=flat[U["b1"]:U["b1"] + c1],
                 rp_w=flat[U["rp_w"]:U["rp_w"] + 3 * k].view(3, k), rp_b=flat[U["rp_b"]:U["rp_b"] + 4])
+            if self.arch == "goal":
+                out["unreal"].update(w2=flat[U["w2"]:U["w2"] + 64 * 16 * 8].view(64, 4, 4, 8), b2=flat[U["b2"]:U["b2"] + 8])
         return out
 
     def new_params(self):
@@ -210,13 +214,19 @@ class PolicyNet:
                 d1, d2 = 1.0 / math.sqrt(16 * 16), 1.0 / math.sqrt(c * 16)
                 w1[:, :, :, 16 * hd:16 * hd + 16].uniform_(-d1, d1, generator=g)
                 w2[16 * hd:16 * hd + 16, :, :, o:o + c].uniform_(-d2, d2, generator=g)
-        if self.unreal_layout:  # goal.py:26-30 on pc_base, the four ConvTranspose2d and rp
+        if self.unreal_layout:  # goal.py:26-30 (bignet.py:17-21) on pc_base, the ConvTranspose2d and rp
             u, A = v["unreal"], self.num_actions
             d = 1.0 / math.sqrt(512)
             u["pc_w"].uniform_(-d, d, generator=g)
-            u["w1"].uniform_(-d, d, generator=g)  # fan_in = 32 out channels x 16
-            u["w2"][:32, :, :, :A].uniform_(-1.0 / math.sqrt(16 * A), 1.0 / math.sqrt(16 * A), generator=g)
-            u["w2"][32:, :, :, A].uniform_(-0.25, 0.25, generator=g)
+            # ConvTranspose2d's fan_in = out_channels x 16 (torch's convention)
+            dv = 1.0 / math.sqrt(16 * A)
+            if self.arch == "bighouse":
+                u["w1"][..., :A].uniform_(-dv, dv, generator=g)
+                u["w1"][..., A].uniform_(-0.25, 0.25, generator=g)
+            else:
+                u["w1"].uniform_(-d, d, generator=g)  # 32 out channels x 16
+                u["w2"][:32, :, :, :A].uniform_(-dv, dv, generator=g)
+                u["w2"][32:, :, :, A].uniform_(-0.25, 0.25, generator=g)
             d = 1.0 / math.sqrt(u["rp_w"].shape[1])
             u["rp_w"].uniform_(-d, d, generator=g)
         return flat.to(self.device)
@@ -273,6 +283,12 @@ class PolicyNet:
             u, A, m = v["unreal"], self.num_actions, PC_MAP
             u["pc_w"][:] = t(pick("pc_base", 0, "weight")).view(32, m, m, 512).permute(1, 2, 0, 3).reshape(PC_BASE, 512)
             u["pc_b"][:] = t(pick("pc_base", 0, "bias")).view(32, m, m).permute(1, 2, 0).reshape(-1)
+        if self.unreal_layout and self.arch == "bighouse":  # bignet.py:77-96: one deconv per branch
+            u["w1"][:, :, :, :A] = t(pick("pc_value", 0, "weight")).permute(0, 2, 3, 1)
+            u["w1"][:, :, :, A:A + 1] = t(pick("pc_action", 0, "weight")).permute(0, 2, 3, 1)
+            u["b1"][:A] = t(pick("pc_value", 0, "bias"))
+            u["b1"][A] = t(pick("pc_action", 0, "bias")).view(())
+        elif self.unreal_layout:
             u["w1"][:, :, :, :32] = t(pick("pc_value", 0, "weight")).permute(0, 2, 3, 1)
             u["w1"][:, :, :, 32:] = t(pick("pc_action", 0, "weight")).permute(0, 2, 3, 1)
             u["b1"][:32] = t(pick("pc_value", 0, "bias"))
@@ -281,6 +297,7 @@ class PolicyNet:
             u["w2"][32:, :, :, A:A + 1] = t(pick("pc_action", 1, "weight")).permute(0, 2, 3, 1)
             u["b2"][:A] = t(pick("pc_value", 1, "bias"))
             u["b2"][A] = t(pick("pc_action", 1, "bias")).view(())
+        if self.unreal_layout:
             rw = t(pick("rp", 0, "weight"))
             if rw.shape[1] != u["rp_w"].shape[1]:
                 raise ValueError("rp weight takes %d inputs, this frame size gives %d" % (rw.shape[1], u["rp_w"].shape[1]))
@@ -338,6 +355,14 @@ class PolicyNet:
             u, m = v["unreal"], PC_MAP
             out["pc_base.0.0.weight"] = u["pc_w"].view(m, m, 32, 512).permute(2, 0, 1, 3).reshape(PC_BASE, 512).clone()
             out["pc_base.0.0.bias"] = u["pc_b"].view(m, m, 32).permute(2, 0, 1).reshape(-1).clone()
+        if self.unreal_layout and self.arch == "bighouse":
+            out["pc_action.0.0.weight"] = u["w1"][:, :, :, A:A + 1].permute(0, 3, 1, 2).contiguous()
+            out["pc_action.0.0.bias"] = u["b1"][A:A + 1].clone()
+            out["pc_value.0.0.weight"] = u["w1"][:, :, :, :A].permute(0, 3, 1, 2).contiguous()
+            out["pc_value.0.0.bias"] = u["b1"][:A].clone()
+            out["rp.weight"] = u["rp_w"].view(3, 3, o3[0], o3[1], 32).permute(0, 1, 4, 2, 3).reshape(3, -1).clone()
+            out["rp.bias"] = u["rp_b"][:3].clone()
+        elif self.unreal_layout:
             out["pc_value.0.0.weight"] = u["w1"][:, :, :, :32].permute(0, 3, 1, 2).contiguous()
             out["pc_value.0.0.bias"] = u["b1"][:32].clone()
             out["pc_action.0.0.weight"] = u["w1"][:, :, :, 32:].permute(0, 3, 1, 2).contiguous()
@@ -455,11 +480,13 @@ class PolicyNet:
         return f.value
 
     def pc_buffers(self, n, with_q=True):
-        """pcb [n,9,9,32], a1 [n,20,20,64], p2 [n,42,42,8], q [n,42,42,A] (None without q)."""
+        """pcb [n,9,9,32], a1 [n,20,20,64], p2 [n,42,42,8], q [n,42,42,A] (None without q);
+        BigHouseModel: a1 None, p2 [n,20,20,8], q [n,20,20,A]."""
         kw = dict(dtype=torch.float32, device=self.device)
-        return (torch.empty((n, PC_MAP, PC_MAP, 32), **kw), torch.empty((n, PC_A1, PC_A1, 64), **kw),
-                torch.empty((n, PC_P, PC_P, 8), **kw),
-                torch.empty((n, PC_P, PC_P, self.num_actions), **kw) if with_q else None)
+        s = self.pc_side
+        a1 = None if self.arch == "bighouse" else torch.empty((n, PC_A1, PC_A1, 64), **kw)
+        return (torch.empty((n, PC_MAP, PC_MAP, 32), **kw), a1, torch.empty((n, s, s, 8), **kw),
+                torch.empty((n, s, s, self.num_actions), **kw) if with_q else None)
 
     def pc_forward(self, params, h, n, pcb, a1, p2, q, workspace):
         P = _lib.ptr
@@ -743,7 +770,8 @@ class _PixelControlFunction(torch.autograd.Function):
         grads = torch.zeros_like(params)
         dh = torch.empty_like(h)
         ws = torch.empty(net.pc_workspace_floats(), dtype=torch.float32, device=params.device)
-        net.pc_backward(params, h, n, pcb.clone(), a1.clone(), p2.clone(), dq.contiguous(), grads, dh, ws)
+        net.pc_backward(params, h, n, pcb.clone(), None if a1 is None else a1.clone(), p2.clone(), dq.contiguous(), grads,
+                        dh, ws)
         return grads, dh, None
 
 
@@ -916,7 +944,7 @@ class GoalNavPolicy(torch.nn.Module):
             raise ValueError("pixel_control needs GoalNavPolicy(recurrent=True, unreal=True)")
         img, gl, lr, m, h0, c0, T, B = self._time_major_inputs(inputs, masks, states)
         h, hT, cT = _RecurrentFeaturesFunction.apply(self.params, img, gl, lr, m, h0, c0, self.net, T, B)
-        q = _PixelControlFunction.apply(self.params, h, self.net)  # [T*B, 42, 42, A]
+        q = _PixelControlFunction.apply(self.params, h, self.net)  # [T*B, 42, 42, A] (20x20: BigHouseModel)
         q = q.view(T, B, *q.shape[1:]).permute(1, 0, 4, 2, 3)
         return q, (hT.view(B, 1, 512), cT.view(B, 1, 512))
 
@@ -967,14 +995,30 @@ class BigHousePolicy(GoalNavPolicy):
 
     _ARCH = "bighouse"
 
-    def __init__(self, num_inputs=3, num_outputs=4, device=None, seed=0, recurrent=True):
-        super().__init__(num_inputs, num_outputs, (84, 84), device, seed, recurrent=recurrent)
+    def __init__(self, num_inputs=3, num_outputs=4, device=None, seed=0, recurrent=True, unreal=False):
+        super().__init__(num_inputs, num_outputs, (84, 84), device, seed, recurrent=recurrent, unreal=unreal)
 
-    def forward(self, inputs, masks=None, states=None):
+    @staticmethod
+    def _both_slots(inputs):
         observations, last_reward_action = inputs if isinstance(inputs, tuple) and len(inputs) == 2 \
             else (inputs, None)
         # the image feeds both frame slots; the BigHouse kernels read only the first
-        return super().forward(((observations, observations), last_reward_action), masks, states)
+        return (observations, observations), last_reward_action
+
+    def forward(self, inputs, masks=None, states=None):
+        return super().forward(self._both_slots(inputs), masks, states)
+
+    def pixel_control(self, inputs, masks=None, states=None):
+        """BigHouseModel.pixel_control (bignet.py:105-111): Q maps [B,T,A,20,20] = pc_value +
+        pc_action - mean(pc_action) (one ConvTranspose2d(32, ., 4, 2) + ReLU per branch on
+        pc_base's 9x9 map) over the recurrent features, and the states."""
+        return super().pixel_control(self._both_slots(inputs), masks, states)
+
+    def reward_prediction(self, inputs):
+        """BigHouseModel.reward_prediction (bignet.py:98-103): logits [B,3] of the conv_base
+        maps of each sample's 3 frames (observations [B,3,...]); rp takes 3 * 7*7*32 inputs at
+        84x84 (bignet.py:96 writes 9*9*32*3, which fits 100x100 frames only)."""
+        return super().reward_prediction(self._both_slots(inputs))
 
     def forward_deconv(self, inputs, masks=None, states=None):
         raise NotImplementedError("BigHouseModel has no deconv heads (bignet.py)")

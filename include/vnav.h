@@ -327,8 +327,9 @@ int vn_aux_forward_loss_grad(vn_policy* p, const float* params, float* acts, int
  * dx4; consumes a1. */
 int vn_aux_backward(vn_policy* p, const float* params, float* acts, int64_t act_capacity, int n, float* a1,
                     const float* dpred, float* grads, float* dx4, float* workspace, vn_stream_t stream);
-/* ---- UNREAL heads: pixel control and reward prediction (models/goal.py:94-133) ----
- * A policy created with VN_POLICY_UNREAL (BigGoalHouseModel only) appends, 16-byte aligned:
+/* ---- UNREAL heads: pixel control and reward prediction (models/goal.py:94-133,
+ * models/bignet.py:77-111) ----
+ * A policy created with VN_POLICY_UNREAL appends, 16-byte aligned (BigGoalHouseModel):
  *   pc_base W [2592][512] (rows in (y, x, c) order of the reference's (32, 9, 9) view), b [2592];
  *   pc W1 [32][4][4][64], b1 [64]: pc_value's ConvTranspose2d(32,32,4,2) -> channels 0-31,
  *     pc_action's -> 32-63;
@@ -337,6 +338,13 @@ int vn_aux_backward(vn_policy* p, const float* params, float* acts, int64_t act_
  *     rows 32-63, the rest padding;
  *   rp W [3][3 * FCIN] (FCIN = h3 * w3 * 32; the three frames' conv_base maps, NHWC each:
  *     the reference's Linear(9*9*32*3, 3) at 174x174), b [4] (3 + pad).
+ * With VN_POLICY_BIGHOUSE (BigHouseModel: one ConvTranspose2d(32, C, 4, 2) + ReLU per branch):
+ *   pc_base W, b as above; pc W1 [32][4][4][8], b1 [8]: pc_value's ConvTranspose2d(32,A,4,2)
+ *     -> channels 0..A-1, pc_action's ConvTranspose2d(32,1,4,2) -> channel A, the rest padding;
+ *   no second layer (W2, b2 empty: their offsets equal rp W's); rp W [3][3 * 1568] (the
+ *     reference's Linear(9*9*32*3, 3) fits 100x100 frames only: in_features derived), b [4].
+ *   The pixel-control map is 20x20 (p2 [n][20][20][8], q [n][20][20][A]); a1 is unused (NULL ok);
+ *   conv_base's output is X3, whose gradient vn_policy_backward_ex takes as dx4_extra.
  * info8 = (pc_base W, pc_base b, W1, b1, W2, b2, rp W, rp b offsets). */
 #define VN_POLICY_UNREAL 8
 int vn_policy_unreal_info(vn_policy* p, int64_t* info8);
@@ -373,6 +381,12 @@ int vn_unreal_pc_loss_grad(float* p2, const int32_t* actions, const uint8_t* don
                            int64_t frame_bytes, int height, int width, const int32_t* rows_img,
                            const int32_t* rows_last, int T, int E, int S, int num_actions, float gamma, float weight,
                            float* stats, vn_stream_t stream);
+/* The same on a cells x cells map: 42 (above) or 20 (BigHouseModel's p2 [(T+1)*S][20][20][8],
+ * the centre 80x80 crop of 84x84 frames). */
+int vn_unreal_pc_loss_grad_ex(float* p2, int cells, const int32_t* actions, const uint8_t* dones,
+                              const uint8_t* arena, int64_t frame_bytes, int height, int width,
+                              const int32_t* rows_img, const int32_t* rows_last, int T, int E, int S, int num_actions,
+                              float gamma, float weight, float* stats, vn_stream_t stream);
 /* Reward prediction: logits [(T-2)*S][4] of samples j = (ts-2)*S + e (frames ts-2..ts of env
  * e); class of rewards[ts][e]: 0 (r = 0), 1 (r > 0), 2 (r < 0); samples with a done at ts-2
  * or ts-1 are skipped. dlogits = weight * d mean CE / dlogits; stats2 = (mean CE, count). */

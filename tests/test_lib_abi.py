@@ -63,8 +63,9 @@ def test_recurrent_policy_layout(built_lib):
 
 def test_unreal_policy_layout(built_lib):
     """VN_POLICY_UNREAL appends, 16-byte aligned, pc_base W [2592][512], b [2592], W1 [32][4][4][64],
-    b1 [64], W2 [64][4][4][8], b2 [8], rp W [3][3 FCIN], b [4] (goal.py:94-119); refused with
-    VN_POLICY_BIGHOUSE (bignet.py's heads differ)."""
+    b1 [64], W2 [64][4][4][8], b2 [8], rp W [3][3 FCIN], b [4] (goal.py:94-119); with
+    VN_POLICY_BIGHOUSE bignet.py:77-96's one deconv per branch: W1 [32][4][4][8], b1 [8], no
+    W2 / b2, rp W [3][3 * 1568]."""
     from vnav import _lib
     lib = _lib.load()
     for hw, fcin in ((84, 288), (174, 2592)):
@@ -85,7 +86,21 @@ def test_unreal_policy_layout(built_lib):
         assert lib.vn_policy_info(h, ctypes.byref(n), None, None) == 0
         assert n.value == want[-1] + 4
         lib.vn_policy_destroy(h)
-    assert lib.vn_policy_create_ex(84, 84, 4, 4 | 8, ctypes.byref(h)) != 0
+    for flags in (4, 4 | 1):
+        assert lib.vn_policy_create_ex(84, 84, 4, flags, ctypes.byref(h)) == 0
+        assert lib.vn_policy_info(h, ctypes.byref(n), None, None) == 0
+        base = n.value
+        lib.vn_policy_destroy(h)
+        assert lib.vn_policy_create_ex(84, 84, 4, flags | 8, ctypes.byref(h)) == 0
+        assert lib.vn_policy_unreal_info(h, info) == 0
+        o = (base + 3) // 4 * 4
+        sizes = (2592 * 512, 2592, 32 * 16 * 8, 8, 0, 0, 3 * 3 * 1568, 4)
+        want = [o + sum(sizes[:i]) for i in range(8)]
+        assert list(info) == want and all(v % 4 == 0 for v in info)
+        assert lib.vn_policy_info(h, ctypes.byref(n), None, None) == 0
+        assert n.value == want[-1] + 4
+        lib.vn_policy_destroy(h)
+    assert lib.vn_policy_create_ex(84, 84, 4, 4 | 2 | 8, ctypes.byref(h)) != 0  # no aux heads on BigHouseModel
 
 
 def test_aux_policy_layout(built_lib):

@@ -129,11 +129,15 @@ def test_unreal_heads_vs_fp64_oracle(hw, n, R):
             _close(g[name].numpy(), ref[name].grad.numpy(), 1e-4, name)
 
 
-def test_unreal_flag_refused_for_bighouse():
+def test_unreal_flag_taken_for_bighouse():
+    """BigHouseModel's own heads (bignet.py:77-111; tests/test_bighouse_unreal_gpu.py); the aux
+    deconv heads stay BigGoalHouseModel's."""
     from vnav import _lib
     from vnav.policy import PolicyNet
+    net = PolicyNet((84, 84), 4, device="cuda:0", arch="bighouse", unreal=True)
+    assert net.pc_side == 20
     with pytest.raises(_lib.VnavError):
-        PolicyNet((84, 84), 4, device="cuda:0", arch="bighouse", unreal=True)
+        PolicyNet((84, 84), 4, device="cuda:0", arch="bighouse", aux=True)
 
 
 # ---- the UNREAL losses (csrc/vn_unreal_loss.hip) vs oracle/unreal.py (parity unpinned:
