@@ -278,6 +278,22 @@ __device__ __forceinline__ uint32_t bf16_split_bits(float v, float& rest) {
   return hb >> 16;
 }
 
+// Row-fill slot i -> (row rr, quad q). With 8 quads a row (BK = 32) the 16 lanes of a
+// ds_write_b64 group hold rows rr and rr + 4 of an 8-row block, not rr and rr + 1: their
+// 8-byte runs start 4 LDK / 2 = 80 dwords apart (16 mod 32, LDK = 40) instead of 20, so the
+// two rows' 16 dwords each land on disjoint banks (tools/gemm_banks.py: 1 -> 0 extra cycles
+// per group). Fetch and commit share it; global reads stay 128-B row runs.
+template <int ROWS, int Q>
+__device__ __forceinline__ void rows_slot(int i, int& rr, int& q) {
+  if constexpr (Q == 8 && ROWS % 8 == 0) {
+    rr = ((i >> 6) << 3) | (((i >> 3) & 1) << 2) | ((i >> 4) & 3);
+    q = i & 7;
+  } else {
+    rr = i / Q;
+    q = i - (i / Q) * Q;
+  }
+}
+
 template <int ROWS, int BK, int LDK>
 __device__ __forceinline__ void commit_rows_x6(const f4* r, uint16_t* s, int tid) {
   constexpr int Q = BK / 4, T = ROWS * Q, NS = (T + 255) / 256, PLANE = ROWS * LDK;
@@ -285,7 +301,8 @@ __device__ __forceinline__ void commit_rows_x6(const f4* r, uint16_t* s, int tid
   for (int j = 0; j < NS; ++j) {
     const int i = tid + j * 256;
     if (T % 256 == 0 || i < T) {
-      const int rr = i / Q, q = i - (i / Q) * Q;
+      int rr, q;
+      rows_slot<ROWS, Q>(i, rr, q);
       uint32_t t0[4], t1[4], t2[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -302,13 +319,49 @@ __device__ __forceinline__ void commit_rows_x6(const f4* r, uint16_t* s, int tid
   }
 }
 
-// Transposing source (wgrad: both operands gathered along the reduction index, fetch_trans
-// slots): the 4 rows of slot i at k = kk are split and stored k-major — planes [term][k][row]
-// with row stride trans_ld(ROWS) — as one 8-byte run per term (the former row-major image
-// took twelve 2-byte LDS stores per slot); the MFMA loop reads its fragments back with the
-// hardware transpose read (frag_tr below).
+// Transposing source (wgrad: both operands gathered along the reduction index): the 4 rows
+// of slot i at k = kk are split and stored k-major — planes [term][k][row] with row stride
+// trans_ld(ROWS) — as one 8-byte run per term (the former row-major image took twelve 2-byte
+// LDS stores per slot); the MFMA loop reads its fragments back with the hardware transpose
+// read (frag_tr below).
 constexpr int trans_ld(int rows) {  // 4 rows of a 32-lane half of ds_read_b64_tr_b16 on distinct banks
   return (rows * 2) % 128 == 0 ? rows + 32 : rows;
+}
+
+// x6 slot i -> (k = kk, row quad rq): G = min(ROWS / 4, 16) consecutive lanes take G
+// consecutive row quads of one k, so a 16-lane ds_write_b64 group writes 32 consecutive
+// dwords of one k row (the f32 path's pairs of quads over 8 k put 4 lanes on each bank
+// pair: 3 extra cycles per group, tools/gemm_banks.py); a lane group's global reads are
+// G * 16 contiguous bytes of one reduction index.
+template <int ROWS, int BK>
+__device__ __forceinline__ void trans_slot_x6(int i, int& kk, int& rq) {
+  constexpr int G = ROWS / 4 < 16 ? ROWS / 4 : 16;
+  static_assert((ROWS / 4) % G == 0, "row quads in groups");
+  kk = (i / G) % BK;
+  rq = i % G + G * (i / (G * BK));
+}
+
+template <int ROWS, int BK, class L>
+__device__ __forceinline__ void fetch_trans_x6(const L& l, f4* r, int row0, int k0, int kend, int tid) {
+  constexpr int R4 = ROWS / 4, T = R4 * BK, NS = (T + 255) / 256;
+#pragma unroll
+  for (int j = 0; j < NS; ++j) {
+    const int i = tid + j * 256;
+    if (T % 256 == 0 || i < T) {
+      int kk, rq;
+      trans_slot_x6<ROWS, BK>(i, kk, rq);
+      const int p = k0 + kk;
+      r[j] = (p < kend) ? l.load4t(p, row0 + 4 * rq) : f4zero();
+    }
+  }
+}
+
+template <int ROWS, int BK, class L>
+__device__ __forceinline__ void fetch_x6(const L& l, f4* r, int row0, int k0, int kend, int tid) {
+  if constexpr (L::kTrans)
+    fetch_trans_x6<ROWS, BK>(l, r, row0, k0, kend, tid);
+  else
+    l.template fetch<ROWS, BK>(r, row0, k0, kend, tid);
 }
 
 template <int ROWS, int BK>
@@ -318,7 +371,8 @@ __device__ __forceinline__ void commit_trans_x6(const f4* r, uint16_t* s, int ti
   for (int j = 0; j < NS; ++j) {
     const int i = tid + j * 256;
     if (T % 256 == 0 || i < T) {
-      const int kk = (i >> 1) % BK, rq = (i & 1) + 2 * (i / (2 * BK));
+      int kk, rq;
+      trans_slot_x6<ROWS, BK>(i, kk, rq);
       uint32_t t0[4], t1[4], t2[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -397,16 +451,16 @@ __global__ __launch_bounds__(256) void gemm_x6_kernel(FA fa, FB fb, EP ep, int M
   const int rb = (wn * TN * 32 + (lane & 31)) * LDK + 8 * (lane >> 5);
   f4 pa[NA], pb[NB];
   if (kb < ke) {
-    fa.template fetch<BM, BK>(pa, m0, kb, ke, tid);
-    fb.template fetch<BN, BK>(pb, n0, kb, ke, tid);
+    fetch_x6<BM, BK>(fa, pa, m0, kb, ke, tid);
+    fetch_x6<BN, BK>(fb, pb, n0, kb, ke, tid);
   }
   for (int k0 = kb; k0 < ke; k0 += BK) {
     commit_x6<BM, BK, LDK, FA>(pa, As, tid);
     commit_x6<BN, BK, LDK, FB>(pb, Bs, tid);
     __syncthreads();
     if (k0 + BK < ke) {
-      fa.template fetch<BM, BK>(pa, m0, k0 + BK, ke, tid);
-      fb.template fetch<BN, BK>(pb, n0, k0 + BK, ke, tid);
+      fetch_x6<BM, BK>(fa, pa, m0, k0 + BK, ke, tid);
+      fetch_x6<BN, BK>(fb, pb, n0, k0 + BK, ke, tid);
     }
     // the MFMA cluster at raised wave priority: the co-resident workgroup's wave on this SIMD
     // then runs its commit (VALU split, LDS writes) in this wave's MFMA gaps instead of
@@ -471,7 +525,8 @@ __device__ __forceinline__ void fetch_rows(const L& l, f4* r, int row0, int k0, 
       for (int j = 0; j < NS; ++j) {
         const int i = tid + j * 256;
         if (T % 256 == 0 || i < T) {
-          const int rr = i / Q, q = i - (i / Q) * Q;
+          int rr, q;
+          rows_slot<ROWS, Q>(i, rr, q);
           r[j] = l.load4_fast(row0 + rr, k0 + 4 * q);
         }
       }
@@ -482,7 +537,8 @@ __device__ __forceinline__ void fetch_rows(const L& l, f4* r, int row0, int k0, 
   for (int j = 0; j < NS; ++j) {
     const int i = tid + j * 256;
     if (T % 256 == 0 || i < T) {
-      const int rr = i / Q, q = i - (i / Q) * Q;
+      int rr, q;
+      rows_slot<ROWS, Q>(i, rr, q);
       r[j] = l.load4(row0 + rr, k0 + 4 * q, kend);
     }
   }
@@ -494,7 +550,8 @@ __device__ __forceinline__ void commit_rows(const f4* r, float* s, int tid) {
   for (int j = 0; j < NS; ++j) {
     const int i = tid + j * 256;
     if (T % 256 == 0 || i < T) {
-      const int rr = i / Q, q = i - (i / Q) * Q;
+      int rr, q;
+      rows_slot<ROWS, Q>(i, rr, q);
       *reinterpret_cast<f4*>(&s[rr * LD + 4 * q]) = r[j];
     }
   }

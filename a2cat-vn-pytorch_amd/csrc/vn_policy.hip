@@ -138,7 +138,9 @@ struct NhwcIm2colGoal {
     if (!ready) {
 #pragma unroll
       for (int j = 0; j < NS; ++j) {
-        const int m = row0 + (tid + j * 256) / Q;
+        int rr, q;
+        rows_slot<ROWS, Q>(tid + j * 256, rr, q);
+        const int m = row0 + rr;
         const int n = m < M ? m / (OH * OW) : 0;
         gsm[j] = n + gd[n];
       }
@@ -148,7 +150,8 @@ struct NhwcIm2colGoal {
     for (int j = 0; j < NS; ++j) {
       const int i = tid + j * 256;
       if (T % 256 == 0 || i < T) {
-        const int rr = i / Q, q = i - (i / Q) * Q;
+        int rr, q;
+        rows_slot<ROWS, Q>(i, rr, q);
         r[j] = load_at(row0 + rr, k0 + 4 * q, kend, gsm[j]);
       }
     }
