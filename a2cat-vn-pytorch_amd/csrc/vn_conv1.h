@@ -931,15 +931,37 @@ __global__ __launch_bounds__(256) void conv2_dgrad_kernel(const float* __restric
 // Wave w owns parity class (py, px) = ((w & 3) >> 1, w & 1) (with 8 waves, waves w and w + 4
 // take alternate tile pairs of the class); K step t = tap t (32 co), so an A
 // fragment (lane: class pixel i16, co 8q..8q+7 of one tap) is one 16-B read of a split dZ2
-// plane; dZ2_f is split once when it is staged (three planes, rows padded to 40 bf16 so 16
-// consecutive pixel rows fall on distinct bank quads; row NP is the zero row of
-// out-of-range taps). The split weights (4 taps x 2 ci tiles x 3 terms) stay in
-// registers; two 16-pixel tiles run together (four independent accumulators).
+// plane; dZ2_f is split once when it is staged into three planes. Plane rows: dZ2 pixel
+// (oy, ox) sits at row (oy + 1) * WXC + ox + 1 (WXC = IW / 2 = OW + 1), so tap (ty, tx) of
+// class pixel pc = yy * WXC + xx reads row pc + (1 - ty) WXC + (1 - tx): the 16 pixels of a
+// tile read 16 CONSECUTIVE rows for every tap, and out-of-range taps land on rows no pixel
+// owns (the gap column, the rows above and below), zeroed once. Rows are 32 bf16 (4 quads)
+// with the quads of row r rotated by 2 (r >> 2): the 4 lane groups of a ds_read_b128 then hit
+// 16 distinct bank quads at any tile offset (tools/dgrad_banks.py: 1.09 -> 0 extra cycles per
+// group at 174x174; the former 40-bf16 rows with a shared zero row conflicted 2-way). The
+// split weights (4 taps x 2 ci tiles x 3 terms) stay in registers; two 16-pixel tiles run
+// together (four independent accumulators).
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+
+template <int IH, int IW>
+constexpr int conv2_dgrad_x6_rows() {  // plane rows: the last tile's reads, padding included
+  return ((IH / 2) * (IW / 2) + 15) / 16 * 16 + IW / 2 + 1;
+}
 
 template <int IH, int IW, int OH, int OW>
 constexpr size_t conv2_dgrad_x6_lds() {  // three dZ2 planes + the frame's conv1 ReLU words
-  return (size_t)3 * (OH * OW + 1) * 40 * 2 + (size_t)IH * IW * 4;
+  return (size_t)3 * conv2_dgrad_x6_rows<IH, IW>() * 32 * 2 + (size_t)IH * IW * 4;
+}
+
+// bf16 offset of quad q of plane row r of NQ quads (the rotation above; rows of 8 quads, 64
+// channels, rotate by r: conflict-free for the same lane groups, tools/dgrad_banks.py)
+template <int NQ = 4>
+__device__ __forceinline__ int dg_quad_off(int r, int q) {
+  static_assert(NQ == 4 || NQ == 8, "rows of 32 or 64 bf16");
+  if constexpr (NQ == 4)
+    return r * 32 + 8 * ((q + 2 * (r >> 2)) & 3);
+  else
+    return r * 64 + 8 * ((q + r) & 7);
 }
 
 template <int IH, int IW, int OH, int OW>
@@ -978,14 +1000,15 @@ __global__ __launch_bounds__(NW * 64, 2) void conv2_dgrad_x6_kernel(const float*
   constexpr int NP = OH * OW;
   constexpr int HYC = IH / 2, WXC = IW / 2, NPC = HYC * WXC;
   constexpr int TILES = (NPC + 15) / 16;
-  constexpr int PS = 40;                 // plane row stride (bf16)
-  constexpr int PL = (NP + 1) * PS;      // plane size
+  constexpr int NR = conv2_dgrad_x6_rows<IH, IW>();
+  constexpr int PL = NR * 32;  // plane size (bf16)
   static_assert(IH % 2 == 0 && IW % 2 == 0, "even conv1 maps");
+  static_assert(WXC == OW + 1, "k4 s2: the class width is the dZ2 width + 1 (the gap column)");
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_dg[];
   uint16_t* zs = reinterpret_cast<uint16_t*>(smem_dg);
   // the frame's ReLU words, staged with dZ2: a global load in the epilogue made every tile
   // wait (vmcnt counts stores too) for its previous tile's stores
-  uint32_t* ms = reinterpret_cast<uint32_t*>(smem_dg + (size_t)3 * (NP + 1) * 40 * 2);
+  uint32_t* ms = reinterpret_cast<uint32_t*>(smem_dg + (size_t)3 * PL * 2);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   constexpr int NT = NW * 64;
   const int cls = wave & 3, py = cls >> 1, px = cls & 1;
@@ -1005,19 +1028,16 @@ __global__ __launch_bounds__(NW * 64, 2) void conv2_dgrad_x6_kernel(const float*
       bw[t][nt][2] = b2.v;
     }
   }
-  for (int i = tid; i < 3 * PS / 2; i += NT) {  // zero rows
-    const int pl = i / (PS / 2), e = i - pl * (PS / 2);
-    reinterpret_cast<uint32_t*>(zs + pl * PL + NP * PS)[e] = 0u;
-  }
+  // every plane row zero once: rows no dZ2 pixel owns stay zero (the staging writes only the
+  // pixels' rows), the barrier orders these stores before the first frame's
+  for (int i = tid; i < 3 * PL / 8; i += NT) reinterpret_cast<uint4*>(zs)[i] = uint4{0u, 0u, 0u, 0u};
+  __syncthreads();
   constexpr int NZ = (NP * 8 + NT - 1) / NT, NM = (IH * IW + NT - 1) / NT;
   f4 zr[NZ];
   uint32_t mr[NM];
-  // staging slot i -> (pixel, 4-channel chunk). With 4 waves (84x84) each half-wave takes 16
-  // consecutive pixels x 2 chunks, whose 8-B plane writes (pixel stride 20 dwords) fill the 64
-  // banks exactly once (pixel-major slots wrap every 3.2 pixels: 2-way conflicts): -12.6 %
-  // per launch; with 8 waves (174x174) the pixel-major order measured 3 % faster (coalesced
-  // 64-B runs of the dZ2 loads) and is kept.
-  auto slot_pc = [](int i) { return NW == 4 ? ((i & 15) + 16 * (i >> 7)) * 8 + ((i >> 4) & 7) : i; };
+  // staging slot i -> (pixel i >> 3, 4-channel chunk i & 7), pixel-major (coalesced 128-B
+  // dZ2 runs): two neighbouring pixels' 8-B writes fill a 16-lane group's 32 banks once
+  auto slot_pc = [](int i) { return i; };
   // dZ2 and the ReLU words of frame f, into registers; unconditional (slots past the frame
   // reload its last one, staging skips them; past the last frame the frame repeats): no branch
   // around the loads for the compiler's wait counts to get lost in
@@ -1040,7 +1060,8 @@ __global__ __launch_bounds__(NW * 64, 2) void conv2_dgrad_x6_kernel(const float*
       if (i < NP * 8) {
         uint2 t0, t1, t2;
         split3_pack(zr[j], t0, t1, t2);
-        uint16_t* d = zs + (i >> 3) * PS + 4 * (i & 7);
+        const int p = i >> 3, c = i & 7;
+        uint16_t* d = zs + dg_quad_off(p + p / OW + WXC + 1, c >> 1) + 4 * (c & 1);
         *reinterpret_cast<uint2*>(d) = t0;
         *reinterpret_cast<uint2*>(d + PL) = t1;
         *reinterpret_cast<uint2*>(d + 2 * PL) = t2;
@@ -1058,14 +1079,10 @@ __global__ __launch_bounds__(NW * 64, 2) void conv2_dgrad_x6_kernel(const float*
       int off[2][4];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        const int pc = (t0 + u) * 16 + i16;  // this lane's class pixel (A row)
-        const int yy = pc / WXC, xx = pc - (pc / WXC) * WXC;
+        const int pc = (t0 + u) * 16 + i16;  // this lane's class pixel (A row); past NPC: a row
+                                             // the last tile reads, its column never stored
 #pragma unroll
-        for (int tap = 0; tap < 4; ++tap) {
-          const int oy = yy - (tap >> 1), ox = xx - (tap & 1);
-          const bool ok = pc < NPC && oy >= 0 && oy < OH && ox >= 0 && ox < OW;
-          off[u][tap] = (ok ? (oy * OW + ox) : NP) * PS + 8 * q;
-        }
+        for (int tap = 0; tap < 4; ++tap) off[u][tap] = dg_quad_off(pc + (1 - (tap >> 1)) * WXC + (1 - (tap & 1)), q);
       }
       f4 acc[2][2];
 #pragma unroll

@@ -972,34 +972,42 @@ __global__ void zero_uncovered_kernel(float* __restrict__ out, int nimg_g, int c
 // conv2_dgrad_x6_kernel (vn_conv1.h). Wave w owns class w / WPC and the NTL 16-wide column
 // tiles of column group w % WPC; its split weights (4 taps x KC/32 k steps x NTL tiles x 3
 // terms) stay in registers for the kernel's lifetime. A work item is IMG images: their maps
-// are split once when staged (three bf16 planes, pixel rows padded to KC + 8 so the 16 rows of
-// a fragment fall on distinct bank quads; row IMG*NP is the zero row of out-of-range taps),
-// where the generic class products re-split every map value at each of its 16 uses (22 VALU
-// per MFMA). The product is transposed (rows = columns of W, MFMA columns = class pixels), so
+// are split once when staged (three bf16 planes), where the generic class products re-split
+// every map value at each of its 16 uses (22 VALU per MFMA). Plane rows as in
+// conv2_dgrad_x6_kernel: map pixel (oy, ox) of item image im at row im NPC + (oy + 1) XC +
+// ox + 1 (XC = SW + 1, YC = SH + 1: an image's rows, padding included, are exactly its NPC
+// class pixels), so every tap of a 16-pixel tile reads 16 consecutive rows; out-of-range taps
+// read rows no pixel owns (zeroed once); quads rotated per row (dg_quad_off): no bank
+// conflicts on the fragment reads (the former KC + 8 padded rows with a shared zero row
+// conflicted 2-way, 0.55 of the LDS cycles). The product is transposed (rows = columns of W, MFMA columns = class pixels), so
 // each lane hands the epilogue 4 consecutive channels of one output pixel.
 template <int SH_, int SW_, int YC_, int XC_, int KC_, int NCOL_, int WPC_>
 struct ParityDg {
   static constexpr int SH = SH_, SW = SW_, YC = YC_, XC = XC_, KC = KC_, NCOL = NCOL_, WPC = WPC_;
   static constexpr int NP = SH * SW;                     // staged map pixels per image
   static constexpr int NPC = YC * XC;                    // class pixels per image
-  static constexpr int PS = KC + 8;                      // plane row stride (bf16)
+  static constexpr int PS = KC + 8;                      // banded form's plane row stride (bf16)
+  static constexpr int rows(int img) { return (img * NPC + 15) / 16 * 16 + XC + 1; }  // + the last tile's reads
   // images per work item: >= 64 class pixels; two large maps where their planes fit (the
   // next item then loads at the item's start: prefetch registers would spill), one else
-  static constexpr int IMG = NPC >= 64 ? ((size_t)3 * (2 * NP + 1) * PS * 2 <= 160 * 1024 ? 2 : 1) : 64 / NPC;
+  static constexpr int IMG = NPC >= 64 ? ((size_t)3 * rows(2) * KC * 2 <= 160 * 1024 ? 2 : 1) : 64 / NPC;
+  static constexpr int NR = rows(IMG);
   static constexpr int NTL = NCOL / (16 * WPC);          // column tiles per wave
   static constexpr int KS = KC / 32;                     // MFMA k steps per tap
   static constexpr int NT = 256 * WPC;
-  static constexpr size_t LDS = (size_t)3 * (IMG * NP + 1) * PS * 2;
+  static constexpr size_t LDS = (size_t)3 * NR * KC * 2;
   static constexpr bool fits = LDS <= 160 * 1024;
   static_assert(KC % 32 == 0 && NCOL % (16 * WPC) == 0, "k steps of 32, whole 16-column tiles per wave");
+  static_assert(KC == 32 || KC == 64, "plane rows of 4 or 8 quads (dg_quad_off)");
+  static_assert(XC == SW + 1 && YC == SH + 1, "k4 s2 classes: the map plus one gap row and column");
 };
 
 template <class S, class EP>
 __global__ __launch_bounds__(S::NT, S::NT >= 512 ? 1 : 2) void parity_dgrad_x6_kernel(const float* __restrict__ map,
                                                                 const float* __restrict__ WT, EP ep, int n) {
-  constexpr int SH = S::SH, SW = S::SW, XC = S::XC, KC = S::KC, NCOL = S::NCOL, WPC = S::WPC;
-  constexpr int NP = S::NP, NPC = S::NPC, IMG = S::IMG, PS = S::PS, NTL = S::NTL, KS = S::KS, NT = S::NT;
-  constexpr int ROWS = IMG * NP, PL = (ROWS + 1) * PS, C4 = KC / 4;
+  constexpr int SW = S::SW, XC = S::XC, KC = S::KC, NCOL = S::NCOL, WPC = S::WPC;
+  constexpr int NP = S::NP, NPC = S::NPC, IMG = S::IMG, NTL = S::NTL, KS = S::KS, NT = S::NT;
+  constexpr int ROWS = IMG * NP, PL = S::NR * KC, C4 = KC / 4, NQ = KC / 8;
   constexpr int TILES = (IMG * NPC + 15) / 16, NZ = (ROWS * C4 + NT - 1) / NT;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_pdg[];
   uint16_t* zs = reinterpret_cast<uint16_t*>(smem_pdg);
@@ -1025,10 +1033,10 @@ __global__ __launch_bounds__(S::NT, S::NT >= 512 ? 1 : 2) void parity_dgrad_x6_k
         bw[t][h][nt][2] = b2.v;
       }
   }
-  for (int i = tid; i < 3 * PS / 2; i += NT) {  // zero rows
-    const int pl = i / (PS / 2), e = i - pl * (PS / 2);
-    reinterpret_cast<uint32_t*>(zs + pl * PL + ROWS * PS)[e] = 0u;
-  }
+  // every plane row zero once (rows no map pixel owns stay zero); the barrier orders these
+  // stores before the first item's
+  for (int i = tid; i < 3 * PL / 8; i += NT) reinterpret_cast<uint4*>(zs)[i] = uint4{0u, 0u, 0u, 0u};
+  __syncthreads();
   const int items = (n + IMG - 1) / IMG;
   f4 zr[NZ];
   auto load_z = [&](int it) {  // the item's map rows (images consecutive), zeros past n
@@ -1053,7 +1061,9 @@ __global__ __launch_bounds__(S::NT, S::NT >= 512 ? 1 : 2) void parity_dgrad_x6_k
       if (i < ROWS * C4) {
         uint2 t0, t1, t2;
         split3_pack(zr[j], t0, t1, t2);
-        uint16_t* d = zs + (i / C4) * PS + 4 * (i % C4);
+        const int pix = i / C4, c = i - (i / C4) * C4, im = pix / NP, rem = pix - (pix / NP) * NP;
+        const int row = im * NPC + (rem / SW + 1) * XC + rem % SW + 1;
+        uint16_t* d = zs + dg_quad_off<NQ>(row, c >> 1) + 4 * (c & 1);
         *reinterpret_cast<uint2*>(d) = t0;
         *reinterpret_cast<uint2*>(d + PL) = t1;
         *reinterpret_cast<uint2*>(d + 2 * PL) = t2;
@@ -1068,13 +1078,9 @@ __global__ __launch_bounds__(S::NT, S::NT >= 512 ? 1 : 2) void parity_dgrad_x6_k
       const int im = pc / NPC, r = pc - (pc / NPC) * NPC;
       const int yy = r / XC, xx = r - (r / XC) * XC;
       const bool live = pc < IMG * NPC && img0 + im < n;
-      int off[4];
+      int row[4];  // tap (ty, tx) reads row pc + (1 - ty) XC + (1 - tx)
 #pragma unroll
-      for (int tap = 0; tap < 4; ++tap) {
-        const int oy = yy - (tap >> 1), ox = xx - (tap & 1);
-        const bool ok = live && oy >= 0 && oy < SH && ox >= 0 && ox < SW;
-        off[tap] = (ok ? im * NP + oy * SW + ox : ROWS) * PS + 8 * q;
-      }
+      for (int tap = 0; tap < 4; ++tap) row[tap] = pc + (1 - (tap >> 1)) * XC + (1 - (tap & 1));
       f4 acc[NTL];
 #pragma unroll
       for (int nt = 0; nt < NTL; ++nt) acc[nt] = f4zero();
@@ -1084,7 +1090,8 @@ __global__ __launch_bounds__(S::NT, S::NT >= 512 ? 1 : 2) void parity_dgrad_x6_k
         for (int h = 0; h < KS; ++h) {
           bf16x8_t a[3];
 #pragma unroll
-          for (int tm = 0; tm < 3; ++tm) a[tm] = *reinterpret_cast<const bf16x8_t*>(zs + tm * PL + off[tap] + 32 * h);
+          for (int tm = 0; tm < 3; ++tm)
+            a[tm] = *reinterpret_cast<const bf16x8_t*>(zs + tm * PL + dg_quad_off<NQ>(row[tap], q + 4 * h));
 #pragma unroll
           for (int nt = 0; nt < NTL; ++nt) {  // small terms first
             f4 c = acc[nt];
@@ -1354,6 +1361,25 @@ __device__ __forceinline__ s16x4_ lds_tr(const uint16_t* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
 }
 
+// Staging slot i -> (row, 4-channel chunk) of a plane with Q chunks a row and a row stride of
+// RSTRIDE dwords: with Q = 8 the 16 lanes of a ds_write_b64 group take rows r and r + D, D
+// chosen so that D RSTRIDE = 16 mod 32 (their 16-dword runs on disjoint banks; rows r, r + 1
+// overlapped 2-way at strides 20 and 24), in whole blocks of 2D rows; the tail rows and other
+// widths keep the identity. Loads and stores share it (tools/wgrad_banks.py).
+template <int Q, int RSTRIDE, int ROWS>
+__device__ __forceinline__ void wg_slot(int i, int& row, int& c) {
+  constexpr int D = (Q == 8 && RSTRIDE % 32 == 20) ? 4 : (Q == 8 && RSTRIDE % 32 == 24) ? 2 : 0;
+  c = i % Q;
+  const int t = i / Q;
+  if constexpr (D > 0) {
+    constexpr int FULL = ROWS / (2 * D) * (2 * D);
+    const int m = t % (2 * D);
+    row = t < FULL ? t - m + (m >> 1) + (m & 1) * D : t;
+  } else {
+    row = t;
+  }
+}
+
 template <class S>
 // fl: the images (frames) to reduce over (conv2 with goal-frame deduplication; identity
 // else). gdelta (conv3 with deduplication): input group 1 (the goal half of X2) of sample s is
@@ -1405,21 +1431,23 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_x6_kernel(const float* __re
     }
 #pragma unroll
     for (int j = 0; j < NZ; ++j) {
-      const int i = min(tid + j * NT, KP * C4 - 1);
-      const int k = i / C4, im = k / BP;
+      int k, c;
+      wg_slot<C4, PZ / 2, KP>(min(tid + j * NT, KP * C4 - 1), k, c);
+      const int im = k / BP;
       int imc = zi[0];  // select chain over the item's images (registers, no indexed array)
 #pragma unroll
       for (int m = 1; m < IMG; ++m) imc = im == m ? zi[m] : imc;
-      zr[j] = reinterpret_cast<const f4*>(dZ)[(((int64_t)imc * OH + band * BR) * OW + (k - im * BP)) * C4 + i % C4];
+      zr[j] = reinterpret_cast<const f4*>(dZ)[(((int64_t)imc * OH + band * BR) * OW + (k - im * BP)) * C4 + c];
     }
 #pragma unroll
     for (int j = 0; j < NX; ++j) {
-      const int i = min(tid + j * NT, IMG * NPX * X4 - 1);
-      const int r = i / X4, im = r / NPX;
+      int r, c;
+      wg_slot<X4, PX / 2, IMG * NPX>(min(tid + j * NT, IMG * NPX * X4 - 1), r, c);
+      const int im = r / NPX;
       int imc = xi[0];
 #pragma unroll
       for (int m = 1; m < IMG; ++m) imc = im == m ? xi[m] : imc;
-      xr[j] = reinterpret_cast<const f4*>(X)[((((int64_t)imc * G + g) * IH + 2 * band * BR) * IW + (r - im * NPX)) * X4 + i % X4];
+      xr[j] = reinterpret_cast<const f4*>(X)[((((int64_t)imc * G + g) * IH + 2 * band * BR) * IW + (r - im * NPX)) * X4 + c];
     }
   };
   if ((int)blockIdx.x < items) load(blockIdx.x);
@@ -1429,11 +1457,13 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_x6_kernel(const float* __re
     for (int j = 0; j < NZ; ++j) {  // split into the planes
       const int i = tid + j * NT;
       if (i < KP * C4) {
-        const f4 z = img0 + (i / C4) / BP < n ? zr[j] : f4zero();
+        int k, c;
+        wg_slot<C4, PZ / 2, KP>(i, k, c);
+        const f4 z = img0 + k / BP < n ? zr[j] : f4zero();
         if (S::BIAS && g == 0) dbs += z;
         uint2 t0, t1, t2;
         split3_pack(z, t0, t1, t2);
-        uint16_t* d = zs + (i / C4) * PZ + 4 * (i % C4);
+        uint16_t* d = zs + k * PZ + 4 * c;
         *reinterpret_cast<uint2*>(d) = t0;
         *reinterpret_cast<uint2*>(d + PLZ) = t1;
         *reinterpret_cast<uint2*>(d + 2 * PLZ) = t2;
@@ -1443,10 +1473,12 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_x6_kernel(const float* __re
     for (int j = 0; j < NX; ++j) {
       const int i = tid + j * NT;
       if (i < IMG * NPX * X4) {
-        const f4 x = img0 + (i / X4) / NPX < n ? xr[j] : f4zero();
+        int r, c;
+        wg_slot<X4, PX / 2, IMG * NPX>(i, r, c);
+        const f4 x = img0 + r / NPX < n ? xr[j] : f4zero();
         uint2 t0, t1, t2;
         split3_pack(x, t0, t1, t2);
-        uint16_t* d = xs + (i / X4) * PX + 4 * (i % X4);
+        uint16_t* d = xs + r * PX + 4 * c;
         *reinterpret_cast<uint2*>(d) = t0;
         *reinterpret_cast<uint2*>(d + PLX) = t1;
         *reinterpret_cast<uint2*>(d + 2 * PLX) = t2;
