@@ -1137,13 +1137,22 @@ __global__ __launch_bounds__(NW * 64, 2) void conv2_dgrad_x6_kernel(const float*
 // ---- conv2 input gradient, banded (maps too large to stage whole: 300x400) ------------
 // The product of conv2_dgrad_x6_kernel over a band of BY rows of the conv1 map: a work item is
 // (frame, band); the dZ2 rows its pixels' taps reach (BY/2 + 1 of them) are split once into
-// three bf16 planes (pixel stride 40, a zero row for out-of-range taps), the band's conv1 ReLU
-// words staged beside them, the next item's rows prefetched into registers. Wave w owns
-// parity class (py, px) = (w >> 1, w & 1) with its split weights in registers; a class's
-// width is (IW - px + 1) / 2, so odd maps (99 columns) work. 74x99 conv1 map, BY = 8: 61 KB of
-// LDS, two workgroups per CU; dZ2 is staged 1.25x (a row shared by neighbouring bands).
-constexpr size_t conv2_dgband_lds(int IW, int OW, int BY) {  // 3 planes of BY/2 + 1 dZ2 rows + 1, ReLU words
-  return (size_t)3 * ((BY / 2 + 1) * OW + 1) * 40 * 2 + (size_t)BY * IW * 4;
+// three bf16 planes, the band's conv1 ReLU words staged beside them, the next item's rows
+// prefetched into registers. Wave w owns parity class (py, px) = (w >> 1, w & 1) with its
+// split weights in registers; a class's width is (IW - px + 1) / 2, so odd maps (99 columns)
+// work. Plane rows as in the whole-map kernel, with one row pitch WX = (IW + 1) / 2 for both
+// classes (the narrower class's last column is a dummy: computed, not stored): staged dZ2 row
+// j (oy = zlo + j) in row block j + 1, pixel ox at column ox + 1, so class pixel (yl, xx) of the
+// band reads row (yl + yy0 - zlo + 1 - ty) WX + xx + 1 - tx, consecutive along a 16-pixel tile;
+// block 0 and the gap columns are never written (zero), the blocks past a short last band's
+// rows are zeroed per item; quads rotated (dg_quad_off): conflict-free reads
+// (tools/dgrad_banks.py). 74x99 conv1 map, BY = 8: 74 KB of LDS, two workgroups per CU; dZ2 is
+// staged 1.25x (a row shared by neighbouring bands).
+constexpr int conv2_dgband_rows(int IW, int BY) {  // plane rows: BY/2 + 3 blocks of WX, + a tile's overhang
+  return (BY / 2 + 3) * ((IW + 1) / 2) + 16;
+}
+constexpr size_t conv2_dgband_lds(int IW, int OW, int BY) {  // 3 planes, ReLU words
+  return (size_t)3 * conv2_dgband_rows(IW, BY) * 32 * 2 + (size_t)BY * IW * 4 + 0 * OW;
 }
 
 template <int IH, int IW, int OH, int OW, int BY>
@@ -1151,9 +1160,11 @@ struct Conv2DgBand {
   static_assert(BY % 2 == 0, "bands of whole parity rows");
   static constexpr int NB = (IH + BY - 1) / BY;  // bands per frame
   static constexpr int ZR = BY / 2 + 1;          // staged dZ2 rows
-  static constexpr int PS = 40;                  // plane row stride (bf16)
-  static constexpr int PL = (ZR * OW + 1) * PS;  // plane size (bf16), + the zero row
+  static constexpr int WX = (IW + 1) / 2;        // row pitch of both classes
+  static constexpr int NR = conv2_dgband_rows(IW, BY);
+  static constexpr int PL = NR * 32;             // plane size (bf16)
   static constexpr size_t LDS = conv2_dgband_lds(IW, OW, BY);
+  static_assert(WX >= OW + 1, "a gap column left of every dZ2 row");
 };
 
 template <int IW, int OW>
@@ -1170,7 +1181,7 @@ __global__ __launch_bounds__(256, 2) void conv2_dgrad_band_x6_kernel(const float
                                                                      float* __restrict__ dX1, int n_frames,
                                                                      FrameList fl) {
   using B = Conv2DgBand<IH, IW, OH, OW, BY>;
-  constexpr int NB = B::NB, ZR = B::ZR, PS = B::PS, PL = B::PL, NT = 256;
+  constexpr int NB = B::NB, ZR = B::ZR, WX = B::WX, PL = B::PL, NT = 256;
   constexpr int NP = OH * OW;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_db[];
   uint16_t* zs = reinterpret_cast<uint16_t*>(smem_db);
@@ -1194,10 +1205,10 @@ __global__ __launch_bounds__(256, 2) void conv2_dgrad_band_x6_kernel(const float
       bw[t][nt][2] = b2.v;
     }
   }
-  for (int i = tid; i < 3 * PS / 2; i += NT) {  // zero rows
-    const int pl = i / (PS / 2), e = i - pl * (PS / 2);
-    reinterpret_cast<uint32_t*>(zs + pl * PL + ZR * OW * PS)[e] = 0u;
-  }
+  // every plane row zero once (block 0, the gap columns); the barrier orders these stores
+  // before the first item's
+  for (int i = tid; i < 3 * PL / 8; i += NT) reinterpret_cast<uint4*>(zs)[i] = uint4{0u, 0u, 0u, 0u};
+  __syncthreads();
   constexpr int NZ = (ZR * OW * 8 + NT - 1) / NT, NM = (BY * IW + NT - 1) / NT;
   f4 zr[NZ];
   uint32_t mr[NM];
@@ -1220,14 +1231,22 @@ __global__ __launch_bounds__(256, 2) void conv2_dgrad_band_x6_kernel(const float
   if ((int)blockIdx.x < n_items) load(blockIdx.x);
   for (int it = blockIdx.x; it < n_items; it += gridDim.x) {
     const int f = fl_frame(fl, it / NB), band = it - (it / NB) * NB;
-    const int zlo = z_lo(band), nz = z_rows(band) * OW * 8, by = b_rows(band);
+    const int zlo = z_lo(band), nzr = z_rows(band), nz = nzr * OW * 8, by = b_rows(band);
+    if (nzr < ZR && band > 0) {  // a short last band: its taps past the map read blocks nzr + 1 .. ZR
+      const int r0 = (nzr + 1) * WX, nw = (ZR - nzr) * WX * 32 / 8;  // 16-B words per plane
+      for (int i = tid; i < 3 * nw; i += NT) {
+        const int pl = i / nw;
+        reinterpret_cast<uint4*>(zs + pl * PL + r0 * 32)[i - pl * nw] = uint4{0u, 0u, 0u, 0u};
+      }
+    }
 #pragma unroll
     for (int j = 0; j < NZ; ++j) {
       const int i = tid + j * NT;
       if (i < nz) {
         uint2 t0, t1, t2;
         split3_pack(zr[j], t0, t1, t2);
-        uint16_t* d = zs + (i >> 3) * PS + 4 * (i & 7);
+        const int p = i >> 3, c = i & 7;
+        uint16_t* d = zs + dg_quad_off((p / OW + 1) * WX + p % OW + 1, c >> 1) + 4 * (c & 1);
         *reinterpret_cast<uint2*>(d) = t0;
         *reinterpret_cast<uint2*>(d + PL) = t1;
         *reinterpret_cast<uint2*>(d + 2 * PL) = t2;
@@ -1242,20 +1261,16 @@ __global__ __launch_bounds__(256, 2) void conv2_dgrad_band_x6_kernel(const float
     load(min(it + (int)gridDim.x, n_items - 1));
     const int yy0 = BY / 2 * band;             // first class row of the band (both py: y0 even)
     const int ncy = (by - py + 1) / 2;         // class rows of this class in the band
-    const int npc = ncy * xc, tiles = (npc + 15) / 16;
+    const int npc = ncy * WX, tiles = (npc + 15) / 16;
+    const int rb = (yy0 - zlo + 1) * WX + 1;   // plane row of class pixel 0 at tap (0, 0)
 #pragma unroll 1
     for (int t0 = 0; t0 < tiles; t0 += 2) {
       int off[2][4];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        const int pc = (t0 + u) * 16 + i16;  // this lane's class pixel (A row)
-        const int yl = pc / xc, xx = pc - (pc / xc) * xc;
+        const int pc = (t0 + u) * 16 + i16;  // this lane's class pixel (A row), pitch WX
 #pragma unroll
-        for (int tap = 0; tap < 4; ++tap) {
-          const int oy = yy0 + yl - (tap >> 1), ox = xx - (tap & 1);
-          const bool ok = pc < npc && oy >= 0 && oy < OH && ox >= 0 && ox < OW;
-          off[u][tap] = (ok ? (oy - zlo) * OW + ox : ZR * OW) * PS + 8 * q;
-        }
+        for (int tap = 0; tap < 4; ++tap) off[u][tap] = dg_quad_off(pc + rb - (tap >> 1) * WX - (tap & 1), q);
       }
       f4 acc[2][2];
 #pragma unroll
@@ -1286,8 +1301,8 @@ __global__ __launch_bounds__(256, 2) void conv2_dgrad_band_x6_kernel(const float
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int pc = (t0 + u) * 16 + i16;
-        if (pc < npc) {
-          const int yl = pc / xc, xx = pc - (pc / xc) * xc;
+        const int yl = pc / WX, xx = pc - (pc / WX) * WX;
+        if (pc < npc && xx < xc) {
           const int y = 2 * (yy0 + yl) + py, x = 2 * xx + px;
           const int64_t pix = ((int64_t)f * IH + y) * IW + x;
           const uint32_t mw = ms[(y - BY * band) * IW + x];

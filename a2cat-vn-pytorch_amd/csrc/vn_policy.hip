@@ -1121,20 +1121,26 @@ __global__ __launch_bounds__(S::NT, S::NT >= 512 ? 1 : 2) void parity_dgrad_x6_k
 
 // The same product for maps whose planes do not fit whole (300x400: the 17x23x64 dZ3 map is 169
 // KB of planes): work item = (image, band of BY class rows yy), staging the BY + 1 map rows its
-// taps read (rows yy - 1 .. yy + BY - 1; rows outside the map read the zero row). Same
+// taps read (rows yy - 1 .. yy + BY - 1, staged as zeros outside the map). Plane rows as in the
+// whole-map form: staged row j, pixel ox at row j XC + ox + 1, so band pixel pc = yl XC + xx
+// reads row pc + (1 - ty) XC + (1 - tx); column 0 is never written (zero); quads rotated. Same
 // fragments and MFMA order per output (bit-identical to the whole-map form).
 template <class S, int BY>
+constexpr int parity_band_nr() {  // plane rows: the last tile's reads
+  return (BY * S::XC + 15) / 16 * 16 + S::XC + 1;
+}
+template <class S, int BY>
 constexpr size_t parity_band_lds() {
-  return (size_t)3 * ((BY + 1) * S::SW + 1) * S::PS * 2;
+  return (size_t)3 * parity_band_nr<S, BY>() * S::KC * 2;
 }
 
 template <class S, int BY, class EP>
 __global__ __launch_bounds__(S::NT, 1) void parity_dgrad_band_x6_kernel(const float* __restrict__ map,
                                                                        const float* __restrict__ WT, EP ep, int n) {
   constexpr int SH = S::SH, SW = S::SW, YC = S::YC, XC = S::XC, KC = S::KC, NCOL = S::NCOL, WPC = S::WPC;
-  constexpr int PS = S::PS, NTL = S::NTL, KS = S::KS, NT = S::NT;
+  constexpr int NTL = S::NTL, KS = S::KS, NT = S::NT, NQ = KC / 8;
   constexpr int NB = (YC + BY - 1) / BY;                       // bands per image
-  constexpr int ROWS = (BY + 1) * SW, PL = (ROWS + 1) * PS, C4 = KC / 4;
+  constexpr int ROWS = (BY + 1) * SW, PL = parity_band_nr<S, BY>() * KC, C4 = KC / 4;
   constexpr int TILES = (BY * XC + 15) / 16, NZ = (ROWS * C4 + NT - 1) / NT;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_pdb[];
   uint16_t* zs = reinterpret_cast<uint16_t*>(smem_pdb);
@@ -1160,10 +1166,10 @@ __global__ __launch_bounds__(S::NT, 1) void parity_dgrad_band_x6_kernel(const fl
         bw[t][h][nt][2] = b2.v;
       }
   }
-  for (int i = tid; i < 3 * PS / 2; i += NT) {  // zero rows
-    const int pl = i / (PS / 2), e = i - pl * (PS / 2);
-    reinterpret_cast<uint32_t*>(zs + pl * PL + ROWS * PS)[e] = 0u;
-  }
+  // every plane row zero once (column 0 of the staged rows stays zero); the barrier orders
+  // these stores before the first item's
+  for (int i = tid; i < 3 * PL / 8; i += NT) reinterpret_cast<uint4*>(zs)[i] = uint4{0u, 0u, 0u, 0u};
+  __syncthreads();
   const int items = n * NB;
   for (int it = blockIdx.x; it < items; it += gridDim.x) {
     const int img = it / NB, y0 = (it - (it / NB) * NB) * BY;
@@ -1178,7 +1184,7 @@ __global__ __launch_bounds__(S::NT, 1) void parity_dgrad_band_x6_kernel(const fl
           const f4 v = (oy >= 0 && oy < SH) ? z4[((int64_t)oy * SW + rp % SW) * C4 + c] : f4zero();
           uint2 t0, t1, t2;
           split3_pack(v, t0, t1, t2);
-          uint16_t* d = zs + rp * PS + 4 * c;
+          uint16_t* d = zs + dg_quad_off<NQ>((rp / SW) * XC + rp % SW + 1, c >> 1) + 4 * (c & 1);
           *reinterpret_cast<uint2*>(d) = t0;
           *reinterpret_cast<uint2*>(d + PL) = t1;
           *reinterpret_cast<uint2*>(d + 2 * PL) = t2;
@@ -1191,13 +1197,9 @@ __global__ __launch_bounds__(S::NT, 1) void parity_dgrad_band_x6_kernel(const fl
       const int pc = tile * 16 + i16;  // this lane's class pixel (MFMA column) within the band
       const int yl = pc / XC, xx = pc - (pc / XC) * XC, yy = y0 + yl;
       const bool live = pc < BY * XC && yy < YC;
-      int off[4];
+      int row[4];  // tap (ty, tx) reads row pc + (1 - ty) XC + (1 - tx)
 #pragma unroll
-      for (int tap = 0; tap < 4; ++tap) {
-        const int oy = yy - (tap >> 1), ox = xx - (tap & 1);
-        const bool ok = live && oy >= 0 && oy < SH && ox >= 0 && ox < SW;
-        off[tap] = (ok ? (oy - y0 + 1) * SW + ox : ROWS) * PS + 8 * q;
-      }
+      for (int tap = 0; tap < 4; ++tap) row[tap] = pc + (1 - (tap >> 1)) * XC + (1 - (tap & 1));
       f4 acc[NTL];
 #pragma unroll
       for (int nt = 0; nt < NTL; ++nt) acc[nt] = f4zero();
@@ -1207,7 +1209,8 @@ __global__ __launch_bounds__(S::NT, 1) void parity_dgrad_band_x6_kernel(const fl
         for (int h = 0; h < KS; ++h) {
           bf16x8_t a[3];
 #pragma unroll
-          for (int tm = 0; tm < 3; ++tm) a[tm] = *reinterpret_cast<const bf16x8_t*>(zs + tm * PL + off[tap] + 32 * h);
+          for (int tm = 0; tm < 3; ++tm)
+            a[tm] = *reinterpret_cast<const bf16x8_t*>(zs + tm * PL + dg_quad_off<NQ>(row[tap], q + 4 * h));
 #pragma unroll
           for (int nt = 0; nt < NTL; ++nt) {  // small terms first
             f4 c = acc[nt];
@@ -1239,7 +1242,7 @@ template <class S>
 constexpr int parity_band_rows() {
   int bmax = 0;
   for (int b = S::YC; b >= 1 && bmax == 0; --b)
-    if (parity_band_lds<S, 1>() + (size_t)3 * (b - 1) * S::SW * S::PS * 2 <= 150 * 1024) bmax = b;
+    if ((size_t)3 * ((b * S::XC + 15) / 16 * 16 + S::XC + 1) * S::KC * 2 <= 150 * 1024) bmax = b;
   if (bmax == 0) return 0;
   const int nb = (S::YC + bmax - 1) / bmax;
   return (S::YC + nb - 1) / nb;
