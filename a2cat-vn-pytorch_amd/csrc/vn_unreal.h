@@ -12,6 +12,9 @@
 //                          0..A-1 from a1 channels 0-31, pc_action's one channel A from 32-63,
 //                          A+1..7 padding,
 //   q   [n][42][42][A]     (value + action) - action, in the reference's evaluation order.
+// BigHouseModel's heads (models/bignet.py:77-111) have one k4 s2 layer per branch: pcb -> p2
+// [n][20][20][8] directly (W1 [32][4][4][8] with the same channel roles), no a1; the same
+// combination and loss kernels run on the 20x20 map (pc_forward_impl / pc_backward_impl).
 #pragma once
 
 namespace vn {

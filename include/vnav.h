@@ -349,7 +349,8 @@ int vn_aux_backward(vn_policy* p, const float* params, float* acts, int64_t act_
 #define VN_POLICY_UNREAL 8
 int vn_policy_unreal_info(vn_policy* p, int64_t* info8);
 int vn_pc_workspace_floats(vn_policy* p, int64_t* floats);
-/* pixel_control (goal.py:131-137) on feature rows h [n][512] (the LSTM outputs): writes
+/* pixel_control (goal.py:131-137; bignet.py:105-111 with VN_POLICY_BIGHOUSE: a1 unused, p2
+ * [n][20][20][8], q [n][20][20][A]) on feature rows h [n][512] (the LSTM outputs): writes
  * pcb [n][9][9][32], a1 [n][20][20][64], p2 [n][42][42][8] (kept for the backward) and
  * q [n][42][42][A] = (pc_value + pc_action) - mean_c(pc_action) (q may be NULL: not formed). */
 int vn_pc_forward(vn_policy* p, const float* params, const float* h, int n, float* pcb, float* a1, float* p2,
