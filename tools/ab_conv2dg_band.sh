@@ -1,7 +1,8 @@
 #!/bin/bash
 # A/B of conv2's input gradient at 174x174: the whole-map kernel (default) against the banded
 # kernel with BY = 8 / 14 (VN_CONV2DG_BAND): parity tests under each, then the 174 leg's
-# update time, interleaved twice.
+# update time, interleaved twice. The VN_CONV2DG_BAND dispatch existed for this run only (no gain,
+# profiles/r05/ab_c2dg/; removed): the script records how it was measured.
 set -o pipefail
 ROOT=${GRAFT_REPO_ROOT:-/root/repo}
 cd $ROOT
