@@ -346,6 +346,12 @@ class A2CTrainer:
         self.ur_lstm_ws = torch.empty(net.lstm_workspace_floats(T + 1, S), **f32)
         # the grads of the trunk, heads and LSTM (everything before the aux / UNREAL blocks)
         self._ur_add_end = net.lstm["bhh"] + 2048
+        # the replayed pass runs on a side stream beside the A2C backward (update()): its own
+        # policy handle, so its small-batch split-K products have their own scratch
+        self._net_u = PolicyNet(net.frame_hw, net.num_actions, self.device, recurrent=net.recurrent, aux=net.aux,
+                                arch=net.arch, unreal=net.unreal)
+        self._side_u = torch.cuda.Stream(device=self.device)
+        self._ev_u0, self._ev_u1 = torch.cuda.Event(), torch.cuda.Event()
 
     def _unreal_forward_losses(self, scatter=True):
         """UNREAL losses of this rollout: vr into dout, pc and rp head gradients into grads;
@@ -470,7 +476,7 @@ class A2CTrainer:
         u["lra"][k, T].copy_(self.boot_lra[:S])
         u["hc0"][k].copy_(self._hc0[:, :S])
 
-    def _unreal_replay_losses(self):
+    def _unreal_replay_losses(self, add=True):
         """UnrealTrainer's losses on the first S envs of the stored rollout drawn this update
         (deep_rl samples its sequences from a replay buffer, experiments/ai2_auxiliary/trainer.py
         :21-31; its sequence shape and initial state are absent, parity unpinned): trunk forward
@@ -478,8 +484,10 @@ class A2CTrainer:
         from, the heads; value replay against their n-step returns (bootstrapped from step T),
         pixel control on their h, reward prediction on their conv_base maps; then the LSTM and
         trunk backward of those losses. Adds the trunk / heads / LSTM gradients to grads (the
-        pixel-control and reward-prediction blocks are written there directly)."""
-        lib, net = self.lib, self.net
+        pixel-control and reward-prediction blocks are written there directly); add=False leaves
+        that sum to the caller (update(): after the side stream's join). Runs on the second
+        policy handle (its own split-K scratch)."""
+        lib, net = self.lib, self._net_u
         T, S, A = self.num_steps, self.unreal_S, self.A
         n = (T + 1) * S
         P, st = _lib.ptr, self._stream()
@@ -531,7 +539,8 @@ class A2CTrainer:
                           extra_envs=S)
         net.backward_ex(self.params, frames, n, self.ur_acts, n, None, self.ur_dz5, self.ur_dx4, self.ur_grads,
                         self.ur_ws)
-        self.grads[:self._ur_add_end].add_(self.ur_grads[:self._ur_add_end])
+        if add:
+            self.grads[:self._ur_add_end].add_(self.ur_grads[:self._ur_add_end])
 
     def _stream(self):
         return _lib.stream_ptr(self.device)
@@ -653,6 +662,20 @@ class A2CTrainer:
         N = T * E
         st = self._stream()
         aux_batch = batch.get("auxiliary_batch") if batch is not None else None
+        u_side = self.unreal and self.unreal_source == "replay"
+        if u_side:
+            # the replayed UNREAL pass reads the parameters and its own ring slot and writes its
+            # own buffers and the pc / rp gradient blocks, which the A2C backward never touches:
+            # it runs on a side stream from here; its trunk / heads / LSTM gradients are added
+            # after the join below, in the unforked order
+            if batch is None:  # a bare rollout(): store it and draw this update's sequence now
+                self._replay_push_and_sample()
+            main = torch.cuda.current_stream(self.device)
+            self._ev_u0.record(main)
+            self._side_u.wait_event(self._ev_u0)
+            with torch.cuda.stream(self._side_u):
+                self._unreal_replay_losses(add=False)
+                self._ev_u1.record(self._side_u)
         _lib.check(lib.vn_a2c_returns(_lib.ptr(self.rewards), _lib.ptr(self.dones), _lib.ptr(self.boot_out), T, E, A,
                                       ctypes.c_float(self.gamma), _lib.ptr(self.returns), st), "vn_a2c_returns")
         _lib.check(lib.vn_a2c_loss_grad(_lib.ptr(self.out), _lib.ptr(self.actions), _lib.ptr(self.returns), N, A,
@@ -719,10 +742,9 @@ class A2CTrainer:
                             goals=goals)
         if aux_batch is not None:
             self._add_trunk_grads(self.aux_grads)
-        if self.unreal and self.unreal_source == "replay":
-            if batch is None:  # a bare rollout(): store it and draw this update's sequence now
-                self._replay_push_and_sample()
-            self._unreal_replay_losses()
+        if u_side:
+            torch.cuda.current_stream(self.device).wait_event(self._ev_u1)
+            self.grads[:self._ur_add_end].add_(self.ur_grads[:self._ur_add_end])
         if self._custom_aux:
             loss, self.aux_losses = self.compute_auxiliary_loss(self.model_view(), batch, self.device)
             if loss is not None:
