@@ -167,10 +167,6 @@ class A2CTrainer:
                                            self.rows_goal.data_ptr())
             ph, pw = self.net.aux_layout["p_hw"]
             self._aux_numel = torch.tensor([1.0, 3.0, 3.0], device=self.device) * (N * ph * pw)
-            # the on-policy deconv heads run on a side stream beside the UNREAL losses and the
-            # LSTM backward (update()); the events fork and join it (captured as graph branches)
-            self._side = torch.cuda.Stream(device=self.device)
-            self._ev_fork, self._ev_aux = torch.cuda.Event(), torch.cuda.Event()
         # aux batch source: "rollout" = the on-policy batch (its trunk activations are reused),
         # "replay" = a sequence from the last replay_size rollouts (AuxiliaryTrainer's
         # self.replay.sample_sequence(), experiments/ai2_auxiliary/trainer.py:29): its own
@@ -684,7 +680,6 @@ class A2CTrainer:
                                         _lib.ptr(self.stats), st), "vn_a2c_loss_grad")
         dx4 = None
         unreal_dh = None
-        aux_join = False  # the side stream's deconv heads still to be joined
         if self.aux_weight > 0 and aux_batch is not None:
             # replayed sequence: its own trunk forward, the heads' loss and backward, and the
             # trunk backward of dL/dX4 alone into aux_grads (added after the main backward)
@@ -697,24 +692,15 @@ class A2CTrainer:
             net.backward_ex(self.params, af, N, self.aux_acts, N, None, self.aux_dz5, self.dx4, self.aux_grads,
                             self.workspace)
         elif self.aux_weight > 0:  # deconv heads: forward, loss gradient, backward -> dL/dX4
-            # on the side stream: they read the rollout's conv_base maps and write only their own
-            # buffers (a1, pred / dpred, aux_stats, their gradient block, dX4), so they run beside
-            # the UNREAL losses and the LSTM backward (a few envs' update is a chain of small
-            # launches); joined before anything reads dX4
-            main = torch.cuda.current_stream(self.device)
-            self._ev_fork.record(main)
-            self._side.wait_event(self._ev_fork)
-            with torch.cuda.stream(self._side):
-                self.aux_stats.zero_()
-                net.aux_forward_loss_grad(self.params, self.acts, N, N, self.a1, self.pred, self._aux_targets,
-                                          self.aux_weight, self.dpred, self.aux_stats, self.aux_ws)
-                net.aux_backward(self.params, self.acts, N, N, self.a1, self.dpred, self.grads, self.dx4,
-                                 self.aux_ws)
-                self._ev_aux.record(self._side)
-            aux_join = True
+            # (in line: a side stream measured slower — their persistent kernels size their grids
+            # to the whole chip, so nothing runs beside them; DESIGN "Two streams in the update")
+            self.aux_stats.zero_()
+            net.aux_forward_loss_grad(self.params, self.acts, N, N, self.a1, self.pred, self._aux_targets,
+                                      self.aux_weight, self.dpred, self.aux_stats, self.aux_ws)
+            net.aux_backward(self.params, self.acts, N, N, self.a1, self.dpred, self.grads, self.dx4, self.aux_ws)
             dx4 = self.dx4
-        if self.unreal and self.unreal_source == "rollout":  # rp's dX4 is scattered after the join
-            unreal_dh, dx4 = self._unreal_forward_losses(scatter=not aux_join)
+        if self.unreal and self.unreal_source == "rollout":  # after the aux heads: rp adds to their dX4
+            unreal_dh, dx4 = self._unreal_forward_losses()
         frames = self._frames(self.rows_img, self.rows_goal)
         goals = None
         if self.dedup_goals:  # the rollout's goal runs: starts ascending, run lengths
@@ -726,8 +712,6 @@ class A2CTrainer:
             net.lstm_backward(self.params, T, E, self.dout, self.h_all, self.xcat, self.lstm_acts, self.c_all, self.c0,
                               self.masks, net.x5(self.acts, N), self.dz5, self.grads, self.lstm_ws,
                               dh_extra=unreal_dh, extra_envs=self.unreal_S if self.unreal else 0)
-            if aux_join:
-                self._join_aux()
             # the heads + LSTM (+ aux heads) gradients are final here: their all-reduce runs on
             # RCCL's stream while the trunk backward runs on this one
             self._allreduce_head_bucket()
@@ -736,8 +720,6 @@ class A2CTrainer:
             # (h, c) after the last step carry into the next rollout (one copy launch)
             self._carry_states()
         else:
-            if aux_join:
-                self._join_aux()
             net.backward_ex(self.params, frames, N, self.acts, N, self.dout, None, dx4, self.grads, self.workspace,
                             goals=goals)
         if aux_batch is not None:
@@ -761,13 +743,6 @@ class A2CTrainer:
                                            ctypes.c_float(scale), _lib.ptr(self.scalars), _lib.ptr(self.lr_dev),
                                            ctypes.c_float(self.rms_alpha), ctypes.c_float(self.rms_epsilon), st),
                    "vn_rmsprop_step_dev")
-
-    def _join_aux(self):
-        """The compute stream waits for the side stream's deconv heads; then rp adds its dX4
-        rows (the order of the unforked update: aux heads' dX4 first)."""
-        torch.cuda.current_stream(self.device).wait_event(self._ev_aux)
-        if self.unreal and self.unreal_source == "rollout":
-            self._unreal_rp_scatter()
 
     def _buckets_split(self):
         """Two gradient buckets when the head bucket is final before the trunk backward:
