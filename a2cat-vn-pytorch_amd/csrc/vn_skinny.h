@@ -214,20 +214,22 @@ inline void launch_skinny(const float* A, int64_t lda, const float* B, int64_t l
 // fixed order (+ bias, ReLU) into X3 (kept for the backward) and LDS, and the 32 conv4
 // outputs of each pixel follow from there. Replaces the split-K conv3 product, its
 // reduce/epilogue launch and the conv4 product (three launches per rollout step).
-// k = (ky*4 + kx)*64 + g*32 + c as NhwcIm2col.
-constexpr int kC34Rows = 4;
+// k = (ky*4 + kx)*64 + g*32 + c as NhwcIm2col. Two pixels per workgroup: 4 envs' 324 pixels
+// in 162 workgroups (1 / 2 / 4 / 8 pixels: 2.12 / 1.95 / 1.99 / 2.05 ms per 4-env update,
+// profiles/r05/ab_c34/; the W3 rows a thread holds are read once per workgroup either way).
+constexpr int kC34Rows = 2;
 
-template <int H, int W, int OH, int OW>
+template <int H, int W, int OH, int OW, int R = kC34Rows>
 __global__ __launch_bounds__(1024) void conv34_small_kernel(const float* __restrict__ X2, int M,
                                                             const float* __restrict__ W3, const float* __restrict__ b3,
                                                             const float* __restrict__ W4, const float* __restrict__ b4,
                                                             float* __restrict__ X3, float* __restrict__ X4) {
-  __shared__ __attribute__((aligned(16))) float A[kC34Rows][1024];
-  __shared__ float part[16][kC34Rows][64];
-  __shared__ float x3s[kC34Rows][64];
+  __shared__ __attribute__((aligned(16))) float A[R][1024];
+  __shared__ float part[16][R][64];
+  __shared__ float x3s[R][64];
   __shared__ float w4s[32][65];  // W4, row stride 65: conv4's 32 lanes read distinct banks
   __shared__ float bs[96];       // b3 | b4
-  const int tid = threadIdx.x, row0 = blockIdx.x * kC34Rows;
+  const int tid = threadIdx.x, row0 = blockIdx.x * R;
   const int co = tid & 63, kq = tid >> 6;
   f4 wv[16];  // W3[co][64 kq .. 64 kq + 63]
   {
@@ -238,8 +240,9 @@ __global__ __launch_bounds__(1024) void conv34_small_kernel(const float* __restr
   // every global read is issued here, before the first barrier: one memory round trip
   for (int i = tid; i < 32 * 64; i += 1024) w4s[i >> 6][i & 63] = W4[i];
   if (tid < 96) bs[tid] = tid < 64 ? b3[tid] : b4[tid - 64];
-  {  // gather: f4 i of the block = (row, k / 4)
-    const int r = tid >> 8, k = (tid & 255) * 4, m = min(row0 + r, M - 1);
+#pragma unroll
+  for (int i = tid; i < R * 256; i += 1024) {  // gather: f4 i of the block = (row, k / 4)
+    const int r = i >> 8, k = (i & 255) * 4, m = min(row0 + r, M - 1);
     const int n = m / (OH * OW), rr = m - n * (OH * OW), oy = rr / OW, ox = rr - (rr / OW) * OW;
     const int c = k & 31, g = (k >> 5) & 1, t = k >> 6, ky = t >> 2, kx = t & 3;
     *reinterpret_cast<f4*>(&A[r][k]) =
@@ -247,13 +250,13 @@ __global__ __launch_bounds__(1024) void conv34_small_kernel(const float* __restr
   }
   __syncthreads();
   {
-    float acc[kC34Rows];
+    float acc[R];
 #pragma unroll
-    for (int r = 0; r < kC34Rows; ++r) acc[r] = 0.0f;
+    for (int r = 0; r < R; ++r) acc[r] = 0.0f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
 #pragma unroll
-      for (int r = 0; r < kC34Rows; ++r) {
+      for (int r = 0; r < R; ++r) {
         const f4 a = *reinterpret_cast<const f4*>(&A[r][kq * 64 + 4 * i]);
         float s = acc[r];
         s = fmaf(a[0], wv[i][0], s);
@@ -264,10 +267,10 @@ __global__ __launch_bounds__(1024) void conv34_small_kernel(const float* __restr
       }
     }
 #pragma unroll
-    for (int r = 0; r < kC34Rows; ++r) part[kq][r][co] = acc[r];
+    for (int r = 0; r < R; ++r) part[kq][r][co] = acc[r];
   }
   __syncthreads();
-  if (tid < kC34Rows * 64) {  // conv3 epilogue: (row, co), the 16 partials in a fixed order
+  if (tid < R * 64) {  // conv3 epilogue: (row, co), the 16 partials in a fixed order
     const int r = tid >> 6, c = tid & 63;
     float v = 0.0f;
 #pragma unroll
@@ -277,7 +280,7 @@ __global__ __launch_bounds__(1024) void conv34_small_kernel(const float* __restr
     if (row0 + r < M) X3[(int64_t)(row0 + r) * 64 + c] = v;
   }
   __syncthreads();
-  if (tid < kC34Rows * 32) {  // conv4: (row, co4)
+  if (tid < R * 32) {  // conv4: (row, co4)
     const int r = tid >> 5, c4 = tid & 31;
     float s = 0.0f;
 #pragma unroll 8
