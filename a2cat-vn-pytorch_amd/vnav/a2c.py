@@ -349,10 +349,9 @@ class A2CTrainer:
         self._side_u = torch.cuda.Stream(device=self.device)
         self._ev_u0, self._ev_u1 = torch.cuda.Event(), torch.cuda.Event()
 
-    def _unreal_forward_losses(self, scatter=True):
+    def _unreal_forward_losses(self):
         """UNREAL losses of this rollout: vr into dout, pc and rp head gradients into grads;
-        returns (dh_extra [T, S, 512], dX4 target). Runs after vn_a2c_loss_grad. scatter=False:
-        rp's dX4 rows are added later (_unreal_rp_scatter, after the side stream's join)."""
+        returns (dh_extra [T, S, 512], dX4 target). Runs after vn_a2c_loss_grad."""
         lib, net = self.lib, self.net
         E, T, A, S = self.env.num_envs, self.num_steps, self.A, self.unreal_S
         N = T * E
@@ -385,16 +384,10 @@ class A2CTrainer:
                                               ctypes.c_float(self.rp_weight), P(self.rp_dout),
                                               P(self.unreal_stats[1:3]), st), "vn_unreal_rp_loss_grad")
         net.rp_backward(self.params, self.rp_x, n_rp, self.rp_dout, self.grads, self.rp_dx, self.pc_ws)
-        if scatter:
-            self._unreal_rp_scatter()
-        return self.dh_pc[:T * S], self.dx4 if self.rp_into_aux else self.unreal_dx4
-
-    def _unreal_rp_scatter(self):
-        """rp's input gradient onto dX4 rows t*E + e (added to the aux heads' when they run)."""
-        E, T, S, F = self.env.num_envs, self.num_steps, self.unreal_S, self.net.fc_in
         dx4 = self.dx4 if self.rp_into_aux else self.unreal_dx4
-        _lib.check(self.lib.vn_unreal_rp_scatter(_lib.ptr(self.rp_dx), T, E, S, F, _lib.ptr(dx4), int(self.rp_into_aux),
-                                                 self._stream()), "vn_unreal_rp_scatter")
+        _lib.check(lib.vn_unreal_rp_scatter(P(self.rp_dx), T, E, S, F, P(dx4), int(self.rp_into_aux), st),
+                   "vn_unreal_rp_scatter")
+        return self.dh_pc[:T * S], dx4
 
     # deep_rl hook names (experiments/thor_cached_auxiliary.py:50-56)
     def create_env(self, kwargs):
