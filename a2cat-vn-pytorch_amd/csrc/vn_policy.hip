@@ -1962,12 +1962,21 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
   {
     DenseRows fa{dz5, 512, n};
     DenseRows fb{T(4), 512, G::FCIN};  // WT [FCIN][512]
+    // 128x128 tiles for the wide maps (174x174: N = 2592, C5): half the split work per MFMA;
+    // 0.2-0.4 ms per update (profiles/r05/ab_cm/); 84x84's N = 288 keeps 64x64
+    constexpr bool big = G::FCIN >= 1024;
     if (dx4_extra) {  // + the aux heads' gradient w.r.t. X4, under the same ReLU mask
       EpiMaskAdd ep{w.dz4, a.X[3], G::FCIN, dx4_extra};
-      launch_gemm_x6<64, 64, 32, 2, 2>(fa, fb, ep, n, G::FCIN, 512, st);
+      if constexpr (big)
+        launch_gemm_x6<128, 128, 32, 2, 2>(fa, fb, ep, n, G::FCIN, 512, st);
+      else
+        launch_gemm_x6<64, 64, 32, 2, 2>(fa, fb, ep, n, G::FCIN, 512, st);
     } else {
       EpiMask ep{w.dz4, a.X[3], G::FCIN};
-      launch_gemm_x6<64, 64, 32, 2, 2>(fa, fb, ep, n, G::FCIN, 512, st);
+      if constexpr (big)
+        launch_gemm_x6<128, 128, 32, 2, 2>(fa, fb, ep, n, G::FCIN, 512, st);
+      else
+        launch_gemm_x6<64, 64, 32, 2, 2>(fa, fb, ep, n, G::FCIN, 512, st);
     }
     Im2colT<DenseRows> fbw{DenseRows{a.X[3], G::FCIN, n}, G::FCIN};
     launch_wgrad6<128, 128, 2, 2>(dz5, 512, 512, fbw, G::FCIN, n, w.slab, w.slab_cap, Gr + L.l[4].w, Gr + L.l[4].b,
