@@ -248,3 +248,27 @@ def test_bighouse_trainer_unreal():
     trr, _, msr = run(False, "replay")
     for m in msr:
         assert np.isfinite(m["pc_loss"]) and np.isfinite(m["rp_loss"])
+
+
+def test_bighouse_unreal_trainer_learns_on_small_scene():
+    """A2CTrainer(arch='bighouse', unreal=True) on the BigHouseModel learning test's task
+    (tests/test_bighouse_gpu.py): with the pixel-control / reward-prediction / value-replay losses
+    added (20-cell pixel control on 84x84 frames) the policy still learns the fixed-goal task."""
+    import vnav
+    from oracle.frames import synth_frames
+    from oracle.graph import h5_tables
+    graph, spd, _ = h5_tables(np.ones((3, 3), dtype=bool))
+    scene = vnav.scene_from_arrays(graph, spd, synth_frames(3, np.arange(len(graph)), (84, 84, 3)))
+    env = vnav.VectorEnv([scene], 256, seed=1, max_episode_steps=60, tasks=[(0, 5)])
+    tr = vnav.A2CTrainer(env, num_steps=20, seed=0, max_time_steps=1e9, recurrent=True, learning_rate=2e-3,
+                         arch="bighouse", unreal=True)
+    lengths, pc = [], []
+    for u in range(800):
+        m = tr.step(sync=(u < 20 or u >= 790))
+        if "raw" not in m:
+            lengths.append(m["episode_length"])
+            pc.append(m["pc_loss"])
+    early = np.nanmean(lengths[5:20])
+    late = np.nanmean(lengths[-10:])
+    assert np.isfinite(late) and late < 0.8 * early, (early, late)
+    assert all(np.isfinite(pc))
