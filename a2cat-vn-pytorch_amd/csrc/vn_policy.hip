@@ -826,12 +826,16 @@ inline int splitk_count(int M, int N, int K, int BM, int BN, int BK, const Polic
   return std::max(splits, 1);
 }
 
-template <int BM, int BN, int BK, int WM, int WN, class FA, class FB, class EP>
+// BKN: the K tile of the unsplit form. 64 for conv_merge's forward and the LSTM's dh product
+// (64 x 64 tiles, K 288-12512): the same MFMAs in the same k order as BK = 32 (bitwise equal
+// output), half the barriers and twice the bytes per memory round trip (tools/gemm_x6_bench.hip
+// mode 4: dh 75 -> 69 us, conv_merge at 174x174 89 -> 84 us per call); the split form keeps BK.
+template <int BM, int BN, int BK, int WM, int WN, int BKN = BK, class FA, class FB, class EP>
 inline void launch_gemm_x6_sk(FA fa, FB fb, EP ep, int M, int N, int K, hipStream_t st, const PolicyLayout& L) {
   if (M <= 0 || N <= 0) return;
   int splits = splitk_count(M, N, K, BM, BN, BK, L);
   if (splits <= 1) {
-    launch_gemm_x6<BM, BN, BK, WM, WN>(fa, fb, ep, M, N, K, st);
+    launch_gemm_x6<BM, BN, BKN, WM, WN>(fa, fb, ep, M, N, K, st);
     return;
   }
   const int kchunk = ((K + splits - 1) / splits + BK - 1) / BK * BK;
@@ -1878,7 +1882,7 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
     } else {
       DenseRows fa{a.X[3], G::FCIN, n};
       DenseRows fb{P + L.l[4].w, G::FCIN, 512};
-      launch_gemm_x6_sk<64, 64, 32, 2, 2>(fa, fb, ep, n, 512, G::FCIN, st, L);
+      launch_gemm_x6_sk<64, 64, 32, 2, 2, 64>(fa, fb, ep, n, 512, G::FCIN, st, L);
     }
   }
   // heads (X5 -> out[n][8]: logits, value); out == NULL runs the trunk only (recurrent policy)
@@ -2178,7 +2182,7 @@ int forward_bignet(const PolicyLayout& L, const float* P, const FrameSrc& src, i
     DenseRows fa{a.X[2], FCIN, n};
     DenseRows fb{P + L.l[4].w, FCIN, 512};
     EpiBiasAct ep{a.X[4], 512, P + L.l[4].b, 1};
-    launch_gemm_x6_sk<64, 64, 32, 2, 2>(fa, fb, ep, n, 512, FCIN, st, L);
+    launch_gemm_x6_sk<64, 64, 32, 2, 2, 64>(fa, fb, ep, n, 512, FCIN, st, L);
   }
   if (out) {
     DenseRows fa{a.X[4], 512, n};
@@ -2424,7 +2428,7 @@ inline int lstm_backward(const PolicyLayout& L, const float* P, int T, int E, co
     DenseRows fa{dg, 2048, E};
     DenseRows fb{w.wcat_t + (int64_t)L.xoff * 2048, 2048, 512};
     EpiLstmDh ep{w.dh[cur], mask};
-    launch_gemm_x6_sk<64, 64, 32, 2, 2>(fa, fb, ep, E, 512, 2048, st, L);
+    launch_gemm_x6_sk<64, 64, 32, 2, 2, 64>(fa, fb, ep, E, 512, 2048, st, L);
   }
   {  // the trunk's input gradient of all T steps in one product: dz5 = relu'(x5) (dgates x W_ih[:, :512])
     DenseRows fa{w.dgates, 2048, N};

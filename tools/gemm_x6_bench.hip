@@ -388,7 +388,59 @@ static void dh_shape(int M, int N, int K, const char* name) {
   hipFree(bias);
 }
 
+// Mode 4: per-step products of the BPTT / rollout at 4096 envs against BK and split-K (the
+// split form includes its slab write and splitk_epilogue_kernel launch).
+template <int BM, int BN, int BK>
+static void sk_shape(int M, int N, int K, int splits, const char* name) {
+  float* a = dalloc((int64_t)M * K, 41, -0.5f);
+  float* b = dalloc((int64_t)N * K, 42, -0.05f);
+  float* c = dalloc((int64_t)M * N, 43, 0.f);
+  float* bias = dalloc(N, 44, 0.f);
+  float* slab = dalloc((int64_t)M * N * splits, 45, 0.f);
+  DenseRows fa{a, K, M};
+  DenseRows fb{b, K, N};
+  EpiBias2 ep{c, N, bias, bias};
+  const double fl = 2.0 * M * N * K;
+  float ms;
+  if (splits == 1) {
+    ms = timeit([&] { launch_gemm_x6<BM, BN, BK, 2, 2>(fa, fb, ep, M, N, K, 0); });
+  } else {
+    const int kchunk = ((K + splits - 1) / splits + BK - 1) / BK * BK;
+    const int sp = (K + kchunk - 1) / kchunk;
+    EpiSlab es{slab, M, N};
+    ms = timeit([&] {
+      hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, BK, 2, 2, DenseRows, DenseRows, EpiSlab>), grid_for(M, N, BM, BN, sp),
+                         dim3(256), 0, 0, fa, fb, es, M, N, K, kchunk);
+      launch_splitk_epilogue(slab, sp, M, N, ep, 0);
+    });
+  }
+  printf("%-10s M %6d N %5d K %5d <%3d,%3d,%2d> split %d  %8.1f us %7.1f TF(f32-equiv)\n", name, M, N, K, BM, BN, BK,
+         splits, ms * 1e3, fl / ms / 1e9);
+  hipFree(a);
+  hipFree(b);
+  hipFree(c);
+  hipFree(bias);
+  hipFree(slab);
+}
+
 int main(int argc, char** argv) {
+  if (argc > 1 && atoi(argv[1]) == 4) {
+    for (int rep = 0; rep < 2; ++rep) {
+      sk_shape<64, 64, 32>(4096, 512, 2048, 1, "lstm dh");
+      sk_shape<64, 64, 64>(4096, 512, 2048, 1, "lstm dh");
+      sk_shape<64, 64, 32>(4096, 512, 2048, 2, "lstm dh");
+      sk_shape<64, 64, 32>(4096, 512, 2048, 4, "lstm dh");
+      sk_shape<64, 64, 64>(4096, 512, 2048, 2, "lstm dh");
+      sk_shape<128, 128, 32>(4096, 2048, 1032, 1, "gates");
+      sk_shape<128, 128, 64>(4096, 2048, 1032, 1, "gates");
+      sk_shape<128, 128, 32>(4096, 2048, 1032, 2, "gates");
+      sk_shape<64, 64, 32>(4096, 512, 2592, 1, "merge174");
+      sk_shape<64, 64, 64>(4096, 512, 2592, 1, "merge174");
+      sk_shape<64, 64, 32>(4096, 512, 2592, 2, "merge174");
+      sk_shape<64, 64, 32>(4096, 512, 2592, 4, "merge174");
+    }
+    return 0;
+  }
   if (argc > 1 && atoi(argv[1]) == 2) {
     for (int rep = 0; rep < 2; ++rep) {
       dh_shape<64, 64, 2, 2>(4096, 512, 2048, "lstm dh");
