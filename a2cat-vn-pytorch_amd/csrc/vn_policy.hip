@@ -295,6 +295,22 @@ struct DenseT {
   VN_TRANS_LOADER
 };
 
+// wgrad B operand over dense rows read transposed: X [P][ld] as rows r..r+3 (columns of X) at
+// pixel p, plus a ones row at r == ncols (that column of the product is the bias gradient).
+struct DenseTOnes {
+  const float* A;
+  int64_t ld;
+  int ncols;
+  __device__ __forceinline__ f4 load4t(int p, int r) const {
+    const float* q = A + (int64_t)p * ld + r;
+    if (r + 3 < ncols) return *reinterpret_cast<const f4*>(q);
+    f4 v = f4zero();
+    for (int j = 0; j < 4; ++j) v[j] = r + j < ncols ? q[j] : (r + j == ncols ? 1.0f : 0.0f);
+    return v;
+  }
+  VN_TRANS_LOADER
+};
+
 // wgrad B operand: an im2col loader read transposed, plus a ones column at k == KP
 // (that column of the product is the bias gradient).
 template <class L>
@@ -898,6 +914,30 @@ inline void launch_wgrad6(const float* dZ, int64_t ldz, int M, FB fb, int KP, in
   hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, BK, WM, WN, DenseT, FB, EpiSlab>), grid_for(M, N, BM, BN, splits),
                      dim3(256), 0, st, fa, fb, ep, M, N, P, kchunk);
   launch_wgrad_reduce(slab, splits, M, N, KP, dW, db, nullptr, st);
+}
+
+// Split-K wgrad on the x6 core straight from the producers' [P][*] rows: dZ [P][ldz] as the
+// transposed A (DenseT) and X [P][ldx] as the transposed B with the ones row (DenseTOnes), k =
+// the P rows. The k-major staging (trans_slot_x6, frag_tr) hands the MFMAs the fragments the
+// row-fill form reads from transposed copies, in the same k order: bitwise its output, without
+// the two tile_transpose passes.
+template <int BM, int BN, int WM, int WN>
+inline void launch_wgrad_x6t(const float* dZ, int64_t ldz, int M, const float* X, int64_t ldx, int KP, int P,
+                             float* slab, int64_t slab_cap, float* dW, float* db, hipStream_t st, float* db2 = nullptr) {
+  constexpr int BK = 32;
+  const int N = KP + (db ? 1 : 0);  // db == nullptr: no bias column
+  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  int splits = std::max(1, std::min((2048 + tiles - 1) / tiles, (P + 255) / 256));
+  while ((int64_t)splits * M * N > slab_cap && splits > 1) splits /= 2;
+  int kchunk = (P + splits - 1) / splits;
+  kchunk = (kchunk + BK - 1) / BK * BK;
+  splits = (P + kchunk - 1) / kchunk;
+  DenseT fa{dZ, ldz, M};
+  DenseTOnes fb{X, ldx, KP};
+  EpiSlab ep{slab, M, N};
+  hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, BK, WM, WN, DenseT, DenseTOnes, EpiSlab>), grid_for(M, N, BM, BN, splits),
+                     dim3(256), 0, st, fa, fb, ep, M, N, P, kchunk);
+  launch_wgrad_reduce(slab, splits, M, N, KP, dW, db, db2, st);
 }
 
 // Split-K wgrad on the x6 core from transposed operands: dZT [M][P] (rows = output
@@ -2438,13 +2478,18 @@ inline int lstm_backward(const PolicyLayout& L, const float* P, int T, int E, co
     // alone (0.14 ms, 6 % of its update); bench batches have thousands of tiles and run as before
     launch_gemm_x6_sk<128, 128, 32, 2, 2>(fa, fb, ep, N, 512, 2048, st, L);
   }
-  {  // dW_cat = dgates^T x xcat over all T*E rows (x6 core on transposed copies, k = rows
-     // contiguous); b_ih and b_hh share the bias gradient
-    const int64_t nt = ((int64_t)N + 3) / 4 * 4;
-    tile_transpose(w.dgates, N, 2048, 2048, w.dgates_t, nt, st);
-    tile_transpose(xcat_all, N, L.xcat, L.xcat, w.xcat_t, nt, st);
-    launch_wgrad_x6<128, 128, 2, 2>(w.dgates_t, 2048, w.xcat_t, L.xcat, N, nt, w.slab, slab_floats(L), Gr + L.lw,
-                                   Gr + L.lbih, st, Gr + L.lbhh);
+  {  // dW_cat = dgates^T x xcat over all T*E rows (x6 core, both operands staged k-major from
+     // their [rows][*] stores); b_ih and b_hh share the bias gradient
+    if (getenv("VN_LSTM_WG_TRANSPOSED")) {  // A/B switch: the former transposed-copy form
+      const int64_t nt = ((int64_t)N + 3) / 4 * 4;
+      tile_transpose(w.dgates, N, 2048, 2048, w.dgates_t, nt, st);
+      tile_transpose(xcat_all, N, L.xcat, L.xcat, w.xcat_t, nt, st);
+      launch_wgrad_x6<128, 128, 2, 2>(w.dgates_t, 2048, w.xcat_t, L.xcat, N, nt, w.slab, slab_floats(L), Gr + L.lw,
+                                     Gr + L.lbih, st, Gr + L.lbhh);
+    } else {
+      launch_wgrad_x6t<128, 128, 2, 2>(w.dgates, 2048, 2048, xcat_all, L.xcat, L.xcat, N, w.slab, slab_floats(L),
+                                      Gr + L.lw, Gr + L.lbih, st, Gr + L.lbhh);
+    }
   }
   VN_HIP(hipGetLastError());
   return VN_OK;

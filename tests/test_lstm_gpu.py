@@ -232,3 +232,32 @@ def test_recurrent_trainer_learns_on_small_scene():
         if np.isfinite(best) and best < 0.6 * early:
             return
     raise AssertionError(results)
+
+
+@pytest.mark.parametrize("B,T", [(5, 6), (256, 4)])
+def test_lstm_weight_gradient_k_major_equals_transposed_copies(B, T, monkeypatch):
+    """dW_cat on the k-major staged operands (DenseT x DenseTOnes, the default) is bitwise the
+    former form on tile_transpose'd copies (VN_LSTM_WG_TRANSPOSED): same fragments, same k
+    order; (256, 4) runs 4 split-K slabs."""
+    pol = _perturbed_policy(3)
+    rng = np.random.RandomState(7)
+    img = torch.as_tensor(rng.randint(0, 256, size=(B, T, 84, 84, 3)).astype(np.uint8)).cuda()
+    gl = torch.as_tensor(rng.randint(0, 256, size=(B, T, 84, 84, 3)).astype(np.uint8)).cuda()
+    lra = torch.as_tensor(rng.randn(B, T, 5).astype(np.float32)).cuda()
+    masks = torch.as_tensor((rng.rand(B, T) > 0.2).astype(np.float32)).cuda()
+    actions = torch.as_tensor(rng.randint(0, 4, size=B * T)).cuda()
+    rets = torch.as_tensor(rng.randn(B * T).astype(np.float32)).cuda()
+    grads = []
+    for transposed in (False, True):
+        if transposed:
+            monkeypatch.setenv("VN_LSTM_WG_TRANSPOSED", "1")
+        else:
+            monkeypatch.delenv("VN_LSTM_WG_TRANSPOSED", raising=False)
+        pol.params.grad = None
+        logits, value, _ = pol(((img, gl), lra), masks, pol.initial_states(B))
+        loss, _ = oa2c.loss(logits.reshape(-1, 4), value.reshape(-1), actions, rets)
+        loss.backward()
+        torch.cuda.synchronize()
+        grads.append(pol.params.grad.detach().clone())
+    assert torch.count_nonzero(grads[0]).item() > 0
+    assert torch.equal(grads[0], grads[1])
