@@ -1343,7 +1343,11 @@ struct Conv2FwdBand {
   // apart: 1/8 of the B-fragment read conflict cycles of the row-major tiles at pixel stride 40
   // and conflict-free split stores (exhaustive check: tools/conv2f84_banks.py)
   static constexpr bool kTiled = IH == 20 && IW == 20 && OH == 9 && OW == 9;
-  static constexpr int PSX = kTiled ? 32 : 40;              // pixel stride in a plane (bf16)
+  // other maps: unpadded pixels (4 quads of 8 channels), quad q of parity column xh stored at
+  // slot (q + (xh >> 1)) & 3 — the 16 pixels of a B fragment (consecutive ox) then sit on 16
+  // distinct bank quads in each ds_read_b128 lane group, where the former 5-quad pixel stride
+  // conflicted 2-way in every group (tools/conv2f_banks.py; 0.46 of the LDS cycles at 300x400)
+  static constexpr int PSX = 32;                            // pixel stride in a plane (bf16)
   static constexpr int PO = kTiled ? 352 : WH * PSX;        // odd-x plane offset (bf16)
   static constexpr int RSP = kTiled ? 680 : 2 * WH * PSX;   // plane row stride (bf16)
   static constexpr int rows_of(int br) { return 2 * br + 2 < IH ? 2 * br + 2 : IH; }
@@ -1430,12 +1434,24 @@ __global__ __launch_bounds__(512, 2) void conv2_fwd_x6_kernel(const float* __res
   // two items' X1 in flight: item it + 2 * gridDim.x is loaded into the registers item it
   // just split into LDS (one item of MFMA work was shorter than the load under full load)
   f4 pre[2][NV];
+  // staging slot -> band f4 (pixel 8 px + channel quad c4). Untiled maps: within each block of
+  // 16 pixels, 16-lane group g stores pixels p0 and p0 + 2 (p0 = 0, 1, 4, 5, ..., 13) — same
+  // parity, neighbouring columns: 32 consecutive dwords of one ds_write_b64 group (pixels px and
+  // px + 1 sit in different parity planes and overlapped 2-way; tools/conv2f_banks.py)
+  auto slot_f4 = [](int i) {
+    if constexpr (kTiled) {
+      return i;
+    } else {
+      const int r = i & 127, g = r >> 4;
+      return (i & ~127) + 8 * ((g >> 1) * 4 + (g & 1) + 2 * ((r >> 3) & 1)) + (r & 7);
+    }
+  };
   auto load_item = [&](f4 (&pr)[NV], int it) {
     const int f = fl_frame(fl, it / NB), band = it - (it / NB) * NB;
     const f4* s4 = reinterpret_cast<const f4*>(X1 + ((int64_t)f * IH + 2 * BR * band) * IW * 32);
     const int nv = band_f4(band);
 #pragma unroll
-    for (int j = 0; j < NV; ++j) pr[j] = s4[min(tid + j * 512, nv - 1)];  // unconditional: countable
+    for (int j = 0; j < NV; ++j) pr[j] = s4[min(slot_f4(tid + j * 512), nv - 1)];  // unconditional: countable
   };
   if ((int)blockIdx.x < n_items) load_item(pre[0], blockIdx.x);
   if ((int)(blockIdx.x + gridDim.x) < n_items) load_item(pre[1], blockIdx.x + gridDim.x);
@@ -1447,12 +1463,14 @@ __global__ __launch_bounds__(512, 2) void conv2_fwd_x6_kernel(const float* __res
       const int nv = band_f4(band);
 #pragma unroll
       for (int j = 0; j < NV; ++j) {
-        const int i = tid + j * 512;
+        const int i = slot_f4(tid + j * 512);  // a permutation of each 128-slot block
         if (i < nv) {
           const int c4 = i & 7, px = i >> 3, y = px / IW, x = px - (px / IW) * IW;
           uint2 t0, t1, t2;
           split3_pack(pre[S][j], t0, t1, t2);
-          uint16_t* d = xs + y * RSP + (x & 1) * PO + (x >> 1) * PSX + 4 * c4;
+          const int xh = x >> 1;
+          const int qs = kTiled ? (c4 >> 1) : (((c4 >> 1) + (xh >> 1)) & 3);  // the quad's slot
+          uint16_t* d = xs + y * RSP + (x & 1) * PO + xh * PSX + 8 * qs + 4 * (c4 & 1);
           *reinterpret_cast<uint2*>(d) = t0;
           *reinterpret_cast<uint2*>(d + PL) = t1;
           *reinterpret_cast<uint2*>(d + 2 * PL) = t2;
@@ -1472,11 +1490,13 @@ __global__ __launch_bounds__(512, 2) void conv2_fwd_x6_kernel(const float* __res
         oy = p / OW;
         ox = p - (p / OW) * OW;
       }
-      const uint16_t* xb = xs + (2 * oy + ky) * RSP + ox * PSX + 8 * q;
+      const uint16_t* xb = xs + (2 * oy + ky) * RSP;
       f4 acc[2] = {f4zero(), f4zero()};
 #pragma unroll
       for (int kx = 0; kx < 4; ++kx) {
-        const uint16_t* xp = xb + (kx & 1) * PO + (kx >> 1) * PSX;
+        const int xh = ox + (kx >> 1);  // tap kx reads x = 2 ox + kx: parity kx & 1, column xh
+        const int qs = kTiled ? q : ((q + (xh >> 1)) & 3);
+        const uint16_t* xp = xb + (kx & 1) * PO + xh * PSX + 8 * qs;
         bf16x8_t b[3];
 #pragma unroll
         for (int tm = 0; tm < 3; ++tm) b[tm] = *reinterpret_cast<const bf16x8_t*>(xp + tm * PL);
