@@ -2353,8 +2353,6 @@ struct LstmWork {
   float* head_t;   // [512][A+1]
   float* dh_heads; // [T*E][512]
   float* dgates;   // [T*E][2048]
-  float* dgates_t; // [2048][T*E]
-  float* xcat_t;   // [xcat][T*E]
   float* dh[2];    // [E][512]
   float* dc[2];    // [E][512]
   float* slab;
@@ -2362,8 +2360,7 @@ struct LstmWork {
 
 inline int64_t lstm_workspace_floats(const PolicyLayout& L, int64_t T, int64_t E) {
   const int64_t n = T * E;
-  const int64_t nt = (n + 3) / 4 * 4;  // row stride of the transposed copies
-  return 2048ll * L.xcat + 512ll * 8 + n * 512 + n * 2048 + nt * (2048 + L.xcat) + 4 * E * 512 + slab_floats(L) + 64;
+  return 2048ll * L.xcat + 512ll * 8 + n * 512 + n * 2048 + 4 * E * 512 + slab_floats(L) + 64;
 }
 
 inline LstmWork lstm_carve(const PolicyLayout& L, float* ws, int64_t T, int64_t E) {
@@ -2377,11 +2374,6 @@ inline LstmWork lstm_carve(const PolicyLayout& L, float* ws, int64_t T, int64_t 
   p += T * E * 512;
   w.dgates = p;
   p += T * E * 2048;
-  const int64_t nt = (T * E + 3) / 4 * 4;
-  w.dgates_t = p;
-  p += nt * 2048;
-  w.xcat_t = p;
-  p += nt * L.xcat;
   for (int i = 0; i < 2; ++i) {
     w.dh[i] = p;
     p += E * 512;
@@ -2480,12 +2472,19 @@ inline int lstm_backward(const PolicyLayout& L, const float* P, int T, int E, co
   }
   {  // dW_cat = dgates^T x xcat over all T*E rows (x6 core, both operands staged k-major from
      // their [rows][*] stores); b_ih and b_hh share the bias gradient
-    if (getenv("VN_LSTM_WG_TRANSPOSED")) {  // A/B switch: the former transposed-copy form
+    if (getenv("VN_LSTM_WG_TRANSPOSED")) {
+      // A/B switch: the former form on tile_transpose'd copies, in stream-ordered scratch of
+      // its own (the workspace no longer carries the 2 x T*E x (2048 + xcat) floats)
       const int64_t nt = ((int64_t)N + 3) / 4 * 4;
-      tile_transpose(w.dgates, N, 2048, 2048, w.dgates_t, nt, st);
-      tile_transpose(xcat_all, N, L.xcat, L.xcat, w.xcat_t, nt, st);
-      launch_wgrad_x6<128, 128, 2, 2>(w.dgates_t, 2048, w.xcat_t, L.xcat, N, nt, w.slab, slab_floats(L), Gr + L.lw,
-                                     Gr + L.lbih, st, Gr + L.lbhh);
+      float* tt = nullptr;
+      VN_HIP(hipMallocAsync((void**)&tt, (size_t)nt * (2048 + L.xcat) * sizeof(float), st));
+      float* dgt = tt;
+      float* xct = tt + nt * 2048;
+      tile_transpose(w.dgates, N, 2048, 2048, dgt, nt, st);
+      tile_transpose(xcat_all, N, L.xcat, L.xcat, xct, nt, st);
+      launch_wgrad_x6<128, 128, 2, 2>(dgt, 2048, xct, L.xcat, N, nt, w.slab, slab_floats(L), Gr + L.lw, Gr + L.lbih,
+                                     st, Gr + L.lbhh);
+      VN_HIP(hipFreeAsync(tt, st));
     } else {
       launch_wgrad_x6t<128, 128, 2, 2>(w.dgates, 2048, 2048, xcat_all, L.xcat, L.xcat, N, w.slab, slab_floats(L),
                                       Gr + L.lw, Gr + L.lbih, st, Gr + L.lbhh);
