@@ -2667,6 +2667,137 @@ void aux_backward_layer2_gemm(const PolicyLayout& L, const float* P, int n, floa
   colsum(A1, (int64_t)P1, kAuxC1, w.colsum, Gr + L.ab1, st);
 }
 
+// dX4 = conv(dA1, W1) (k4 s2, 48 -> 32 channels: the aux heads' first layer's input gradient)
+// as a persistent parity-class product, in place of the generic im2col product (which re-splits
+// every dA1 value at each of its 4 uses and the weights in every workgroup). A sample's dA1 map
+// is split once into three bf16 planes per parity class (py, px) = (y & 1, x & 1): class pixel
+// (cy, cx) at row cy XC + cx (XC = IW + 1, YC = IH + 1), 48 channels a row. Output pixel (oy, ox)
+// of the consecutive-row index p = oy XC + ox (ox = IW: a dummy column) sums, per class, the
+// taps (ky, kx) = (py + 2 ty, px + 2 tx), which read class rows p + ty XC + tx: 16 consecutive
+// rows per 16-pixel tile and tap. Wave w owns class w >> 1 and output channels 16 (w & 1) ..
+// +15; its split weights (4 taps x 48 channels x 16 columns x 3 terms) stay in registers. The
+// product is transposed (MFMA rows = output channels, columns = pixels, 16x16x32, six k steps
+// of 32 over the class's 4 taps x 48 channels); after each tile the four class partials meet in
+// LDS (double-buffered by tile parity) and are summed in class order by all 512 threads.
+template <int AH, int AW, int IH, int IW>
+struct AuxDx4 {
+  static constexpr int C = kAuxC1, CO = 32;
+  static constexpr int XC = IW + 1, YC = IH + 1, NPC = XC * YC;
+  static constexpr int TP = (IH * XC + 15) / 16 * 16;  // tiled output rows (dummies included)
+  static constexpr int NR = TP + XC + 1;               // plane rows: the last tile's reads
+  static constexpr int PL = NR * C;                    // one plane (bf16)
+  static constexpr int PP = 36;                        // partial row stride (floats)
+  static constexpr int TG = 2;                         // tiles per partial-sum round (one barrier)
+  static constexpr size_t LDS = (size_t)12 * PL * 2 + (size_t)2 * TG * 4 * 16 * PP * 4;
+  static constexpr int NV = (AH * AW * (C / 4) + 511) / 512;  // prefetched f4 per thread
+  static constexpr bool fits = LDS <= 160 * 1024 && AH == 2 * IH + 2 && AW == 2 * IW + 2;
+};
+
+template <int AH, int AW, int IH, int IW>
+__global__ __launch_bounds__(512, 1) void aux_dx4_x6_kernel(const float* __restrict__ dA1,
+                                                             const float* __restrict__ W1, float* __restrict__ dX4,
+                                                             int n) {
+  using S = AuxDx4<AH, AW, IH, IW>;
+  constexpr int C = S::C, XC = S::XC, NPC = S::NPC, TP = S::TP, NR = S::NR, PL = S::PL, PP = S::PP, NV = S::NV;
+  constexpr int C4 = C / 4, NPX = AH * AW, TILES = TP / 16, TG = S::TG;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem_adx[];
+  uint16_t* pl = reinterpret_cast<uint16_t*>(smem_adx);            // [term][class][NR][C]
+  float* part = reinterpret_cast<float*>(smem_adx + (size_t)12 * PL * 2);  // [2][TG][class][16][PP]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int cls = wave >> 1, ch = wave & 1, py = cls >> 1, px = cls & 1;
+  const int i16 = lane & 15, q = lane >> 4;
+  // split weights: step s, lane (co = 16 ch + i16, q) holds k' = 32 s + 8 q .. +7 of the class's
+  // local K (tap t = k' / 48 = 2 ty + tx, channel k' % 48)
+  bf16x8_t bw[6][3];
+#pragma unroll
+  for (int st = 0; st < 6; ++st) {
+    const int kl = 32 * st + 8 * q, t = kl / C, c0 = kl - (kl / C) * C;
+    const int ky = py + 2 * (t >> 1), kx = px + 2 * (t & 1);
+    const float* w = W1 + (int64_t)(16 * ch + i16) * (16 * C) + (ky * 4 + kx) * C + c0;
+    union { uint16_t u[8]; bf16x8_t v; } b0, b1, b2;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) split3_bf16(w[j], b0.u[j], b1.u[j], b2.u[j]);
+    bw[st][0] = b0.v;
+    bw[st][1] = b1.v;
+    bw[st][2] = b2.v;
+  }
+  // plane rows no class pixel owns (the last tiles' reads past row NPC) stay zero
+  for (int i = tid; i < 12 * (NR - NPC) * C4 / 2; i += 512) {
+    const int per = (NR - NPC) * C4 / 2, pln = i / per, r = i - pln * per;
+    reinterpret_cast<uint4*>(pl + (size_t)pln * PL + NPC * C)[r] = uint4{0u, 0u, 0u, 0u};
+  }
+  f4 pre[NV];
+  auto load = [&](int smp) {
+    const f4* src = reinterpret_cast<const f4*>(dA1 + (int64_t)smp * NPX * C);
+#pragma unroll
+    for (int j = 0; j < NV; ++j) pre[j] = src[min(tid + j * 512, NPX * C4 - 1)];  // unconditional
+  };
+  if ((int)blockIdx.x < n) load(blockIdx.x);
+  int par = 0;  // partial-buffer parity (tiles run so far)
+  for (int smp = blockIdx.x; smp < n; smp += gridDim.x) {
+    __syncthreads();  // the previous sample's plane reads are done
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int i = tid + j * 512;
+      if (i < NPX * C4) {
+        const int pix = i / C4, c4 = i - (i / C4) * C4, y = pix / AW, x = pix - (pix / AW) * AW;
+        uint2 t0, t1, t2;
+        split3_pack(pre[j], t0, t1, t2);
+        uint16_t* d = pl + (size_t)((y & 1) * 2 + (x & 1)) * PL + ((y >> 1) * XC + (x >> 1)) * C + 4 * c4;
+        *reinterpret_cast<uint2*>(d) = t0;
+        *reinterpret_cast<uint2*>(d + 4 * PL) = t1;
+        *reinterpret_cast<uint2*>(d + 8 * PL) = t2;
+      }
+    }
+    __syncthreads();
+    load(min(smp + (int)gridDim.x, n - 1));
+    const uint16_t* cp = pl + (size_t)cls * PL;
+#pragma unroll 1
+    for (int t0 = 0; t0 < TILES; t0 += TG) {
+      // TG tiles per round: independent accumulators, one barrier for their partials
+      f4 acc[TG];
+#pragma unroll
+      for (int u = 0; u < TG; ++u) acc[u] = f4zero();
+#pragma unroll
+      for (int st = 0; st < 6; ++st) {
+        const int kl = 32 * st + 8 * q, t = kl / C, c0 = kl - (kl / C) * C;
+#pragma unroll
+        for (int u = 0; u < TG; ++u) {
+          // a tile past the map (odd TILES) recomputes the last one; its partials are unused
+          const int row = min(t0 + u, TILES - 1) * 16 + i16 + (t >> 1) * XC + (t & 1);
+          bf16x8_t a[3];
+#pragma unroll
+          for (int tm = 0; tm < 3; ++tm)
+            a[tm] = *reinterpret_cast<const bf16x8_t*>(cp + (size_t)tm * 4 * PL + row * C + c0);
+          f4 c = acc[u];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[st][0], a[2], c, 0, 0, 0);  // small terms first
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[st][2], a[0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[st][1], a[1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[st][0], a[1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[st][1], a[0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[st][0], a[0], c, 0, 0, 0);
+          acc[u] = c;
+        }
+      }
+      // lane (pixel i16, q) holds output channels 16 ch + 4q .. +3 of its tile pixel
+      float* pb = part + (size_t)par * TG * 4 * 16 * PP;
+#pragma unroll
+      for (int u = 0; u < TG; ++u)
+        *reinterpret_cast<f4*>(pb + ((u * 4 + cls) * 16 + i16) * PP + 16 * ch + 4 * q) = acc[u];
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < TG; ++u) {  // (pixel, channel): the four class partials in class order
+        const float* pu = pb + (size_t)u * 4 * 16 * PP;
+        const int pi = tid >> 5, co = tid & 31, pp = (t0 + u) * 16 + pi, oy = pp / XC, ox = pp - (pp / XC) * XC;
+        const float v = ((pu[pi * PP + co] + pu[(16 + pi) * PP + co]) + pu[(32 + pi) * PP + co]) + pu[(48 + pi) * PP + co];
+        if (t0 + u < TILES && oy < IH && ox < IW) dX4[(((int64_t)smp * IH + oy) * IW + ox) * S::CO + co] = v;
+      }
+      par ^= 1;
+    }
+  }
+}
+
 // Gradients of the heads' parameters and dX4 [n][IH][IW][32] (unmasked) from dP; A1 is
 // overwritten by its own gradient.
 template <int H0, int W0>
@@ -2716,7 +2847,17 @@ int aux_backward_impl(const PolicyLayout& L, const float* P, const float* X4, in
     launch_wgrad6<32, 128, 1, 4>(X4, 32, 32, Im2colT<Im1>{Im1{A1, P0}, 16 * kAuxC1}, 16 * kAuxC1, P0, w.slab,
                                  slab_floats(L), Gr + L.aw1, nullptr, st);
   }
-  {
+  using Dx = AuxDx4<AH, AW, IH, IW>;
+  if (Dx::fits && !getenv("VN_AUX_DX4_GENERIC")) {  // read per call (A/B and parity checks)
+    if constexpr (Dx::fits) {
+      const void* kfn = (const void*)aux_dx4_x6_kernel<AH, AW, IH, IW>;
+      VN_HIP(ensure_dyn_lds(kfn, Dx::LDS));
+      const int blocks = std::min(n, resident_blocks(kfn, 512, Dx::LDS));
+      if (blocks > 0)
+        hipLaunchKernelGGL((aux_dx4_x6_kernel<AH, AW, IH, IW>), dim3(blocks), dim3(512), Dx::LDS, st, A1, P + L.aw1,
+                           dX4, n);
+    }
+  } else {
     DenseRows fb{P + L.aw1, 16 * kAuxC1, 32};
     EpiStore ep{dX4, 32};
     launch_gemm_x6<128, 32, 32, 4, 1>(Im1{A1, P0}, fb, ep, P0, 32, 16 * kAuxC1, st);

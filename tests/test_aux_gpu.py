@@ -321,3 +321,49 @@ def test_full_resolution_300x400_trunk_and_aux_vs_oracle():
     for k, mod in mods.items():
         _close(mine[k + ".weight"].numpy(), mod.weight.grad.numpy(), 1e-4, k + ".weight")
         _close(mine[k + ".bias"].numpy(), mod.bias.grad.numpy(), 1e-4, k + ".bias")
+
+
+@pytest.mark.parametrize("hw,B", [((174, 174), 17), ((174, 174), 300), ((84, 84), 37)])
+def test_aux_dx4_kernel_matches_generic_product(hw, B):
+    """The aux heads' first-layer input gradient dX4 = conv(dA1, W1) on the persistent parity-
+    class kernel (aux_dx4_x6_kernel: dA1 split once into class planes, per-class partials summed
+    in class order) against the generic im2col product (VN_AUX_DX4_GENERIC): every parameter
+    gradient of a heads-only loss to 1e-5 of its scale (dX4 reaches the trunk through conv4 ..
+    conv1; the two sum the same exact split products in another order). 300 samples wrap the
+    persistent grid."""
+    import os
+    from vnav.policy import GoalNavPolicy
+    torch.manual_seed(5)
+    pol = GoalNavPolicy(3, 4, hw, aux=True)
+    with torch.no_grad():
+        pol.params.add_(torch.randn_like(pol.params) * 0.01)
+    rng = np.random.RandomState(11)
+    img = torch.as_tensor(rng.randint(0, 256, size=(B, 1) + hw + (3,)).astype(np.uint8)).cuda()
+    gl = torch.as_tensor(rng.randint(0, 256, size=(B, 1) + hw + (3,)).astype(np.uint8)).cuda()
+    shapes = [p.shape[2:] for p in pol.forward_deconv(((img[:1], gl[:1]), None))[0]]
+    targets = [torch.as_tensor(rng.rand(B, 1, *sh).astype(np.float32)).cuda() for sh in shapes]
+
+    def grads(generic):
+        if generic:
+            os.environ["VN_AUX_DX4_GENERIC"] = "1"
+        try:
+            pol.params.grad = None
+            preds, _ = pol.forward_deconv(((img, gl), None))
+            loss = sum(torch.nn.functional.mse_loss(p, t) for p, t in zip(preds, targets))
+            loss.backward()
+            torch.cuda.synchronize()
+            return pol.net.to_reference(pol.params.grad.detach().clone())
+        finally:
+            os.environ.pop("VN_AUX_DX4_GENERIC", None)
+
+    mine, ref = grads(False), grads(True)
+    bad = {}
+    for k in ref:
+        b = ref[k].numpy().astype(np.float64)
+        if np.abs(b).max() == 0.0:
+            continue
+        e = np.abs(mine[k].numpy() - b).max() / np.abs(b).max()
+        if e > 1e-5:
+            bad[k] = "%.3g" % e
+    assert not bad, bad
+    assert np.abs(mine["conv_base.0.0.weight"].numpy()).max() > 0
