@@ -2008,20 +2008,19 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
     DenseRows fb{T(4), 512, G::FCIN};  // WT [FCIN][512]
     // 128x128 tiles for the wide maps (174x174: N = 2592, C5): half the split work per MFMA;
     // 0.2-0.4 ms per update (profiles/r05/ab_cm/); 84x84's N = 288 keeps 64x64
-    constexpr bool big = G::FCIN >= 1024;
-    if (dx4_extra) {  // + the aux heads' gradient w.r.t. X4, under the same ReLU mask
-      EpiMaskAdd ep{w.dz4, a.X[3], G::FCIN, dx4_extra};
-      if constexpr (big)
+    // Few rows (the logged run's 4 x 20 = 80): 64x64 tiles, split-K below 128 tiles (the
+    // 128x128 form ran 21 workgroups down K = 512 alone: 54 us of a 2 ms update)
+    const bool big = G::FCIN >= 1024 && n >= 1024;
+    auto dgrad = [&](auto ep) {
+      if (big)
         launch_gemm_x6<128, 128, 32, 2, 2>(fa, fb, ep, n, G::FCIN, 512, st);
       else
-        launch_gemm_x6<64, 64, 32, 2, 2>(fa, fb, ep, n, G::FCIN, 512, st);
-    } else {
-      EpiMask ep{w.dz4, a.X[3], G::FCIN};
-      if constexpr (big)
-        launch_gemm_x6<128, 128, 32, 2, 2>(fa, fb, ep, n, G::FCIN, 512, st);
-      else
-        launch_gemm_x6<64, 64, 32, 2, 2>(fa, fb, ep, n, G::FCIN, 512, st);
-    }
+        launch_gemm_x6_sk<64, 64, 32, 2, 2>(fa, fb, ep, n, G::FCIN, 512, st, L);
+    };
+    if (dx4_extra)  // + the aux heads' gradient w.r.t. X4, under the same ReLU mask
+      dgrad(EpiMaskAdd{w.dz4, a.X[3], G::FCIN, dx4_extra});
+    else
+      dgrad(EpiMask{w.dz4, a.X[3], G::FCIN});
     Im2colT<DenseRows> fbw{DenseRows{a.X[3], G::FCIN, n}, G::FCIN};
     launch_wgrad6<128, 128, 2, 2>(dz5, 512, 512, fbw, G::FCIN, n, w.slab, w.slab_cap, Gr + L.l[4].w, Gr + L.l[4].b,
                                   st);
@@ -2955,7 +2954,7 @@ int pc_backward_impl(const PolicyLayout& L, const float* P, const float* h, int 
     colsum(P2, npix, kPcC2, w.colsum, Gr + L.ub1, st);
     DenseRows fb{P + L.uw1, 16 * kPcC2, 32};
     EpiMask ep{pcb, pcb, 32};
-    launch_gemm_x6<128, 32, 32, 4, 1>(Im1{P2, P0}, fb, ep, P0, 32, 16 * kPcC2, st);
+    launch_gemm_x6_sk<128, 32, 32, 4, 1>(Im1{P2, P0}, fb, ep, P0, 32, 16 * kPcC2, st, L);
   } else {
     // second layer: dW2 = A1^T x im2col(dP2) (block-diagonal mask), db2, dA1 masked in place, db1
     const int P1 = n * kPcA1 * kPcA1;
@@ -2980,7 +2979,8 @@ int pc_backward_impl(const PolicyLayout& L, const float* P, const float* h, int 
     {
       DenseRows fb{P + L.uw1, 16 * kPcC1, 32};
       EpiMask ep{pcb, pcb, 32};
-      launch_gemm_x6<128, 32, 32, 4, 1>(Im1{A1, P0}, fb, ep, P0, 32, 16 * kPcC1, st);
+      // split-K below 128 tiles (the logged run's 4 envs: 54 tiles walking K = 1024: 40 us)
+      launch_gemm_x6_sk<128, 32, 32, 4, 1>(Im1{A1, P0}, fb, ep, P0, 32, 16 * kPcC1, st, L);
     }
   }
   // pc_base: dW = dpcb^T x h (+ bias column), dh = dpcb x W
