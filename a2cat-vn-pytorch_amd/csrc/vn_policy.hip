@@ -504,42 +504,56 @@ __global__ void transpose_kernel(const float* __restrict__ W, int rows, int cols
   WT[(int64_t)c * rows + r] = W[idx];
 }
 
-// Up to kTSet weight transposes (transpose_kernel's element map) in one launch: thread idx
-// of the concatenated element ranges finds its matrix by a scan of the range starts. A
-// backward transposes its weights once (5 matrices of the trunk, 2 of the LSTM core); one
-// launch each cost a dependent dispatch apiece on the few-env path.
+// Up to kTSet weight transposes WT[c][r] = W[r][c] in one launch, 64 x 64 tiles through LDS
+// (reads and writes row-contiguous): workgroup b finds its matrix by a scan of the tile-range
+// starts. A backward transposes its weights once (5 matrices of the trunk, 2 of the LSTM
+// core); one launch each cost a dependent dispatch apiece on the few-env path, and the former
+// element-wise map wrote one 4-byte value per 64-byte line (12 us per set at 4 envs).
 constexpr int kTSet = 6;
 struct TransposeSet {
   const float* W[kTSet];
   float* WT[kTSet];
   int rows[kTSet], cols[kTSet];
-  int64_t start[kTSet + 1];
+  int tstart[kTSet + 1];  // tile-range starts
   int n = 0;
   void add(const float* w, int r, int c, float* wt) {
     if ((int64_t)r * c == 0) return;
-    if (n == 0) start[0] = 0;
+    if (n == 0) tstart[0] = 0;
     W[n] = w;
     WT[n] = wt;
     rows[n] = r;
     cols[n] = c;
-    start[n + 1] = start[n] + (int64_t)r * c;
+    tstart[n + 1] = tstart[n] + ((r + 63) / 64) * ((c + 63) / 64);
     ++n;
   }
 };
 
-__global__ void transpose_set_kernel(TransposeSet s) {
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= s.start[s.n]) return;
+__global__ __launch_bounds__(256) void transpose_set_kernel(TransposeSet s) {
+  __shared__ float t[64][65];
+  const int b = blockIdx.x;
   int i = 0;
-  while (i + 1 < s.n && idx >= s.start[i + 1]) ++i;
-  const int64_t l = idx - s.start[i];
-  const int cols = s.cols[i], r = (int)(l / cols), c = (int)(l - (l / cols) * cols);
-  s.WT[i][(int64_t)c * s.rows[i] + r] = s.W[i][l];
+  while (i + 1 < s.n && b >= s.tstart[i + 1]) ++i;
+  const int rows = s.rows[i], cols = s.cols[i], tc = (cols + 63) / 64, l = b - s.tstart[i];
+  const int r0 = (l / tc) * 64, c0 = (l - (l / tc) * tc) * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const float* src = s.W[i];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int r = r0 + ty + 4 * k, c = c0 + tx;
+    if (r < rows && c < cols) t[ty + 4 * k][tx] = src[(int64_t)r * cols + c];
+  }
+  __syncthreads();
+  float* dst = s.WT[i];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int c = c0 + ty + 4 * k, r = r0 + tx;
+    if (r < rows && c < cols) dst[(int64_t)c * rows + r] = t[tx][ty + 4 * k];
+  }
 }
 
 inline void launch_transpose_set(const TransposeSet& s, hipStream_t st) {
   if (s.n == 0) return;
-  hipLaunchKernelGGL(transpose_set_kernel, dim3((unsigned)((s.start[s.n] + 255) / 256)), dim3(256), 0, st, s);
+  hipLaunchKernelGGL(transpose_set_kernel, dim3((unsigned)s.tstart[s.n]), dim3(256), 0, st, s);
 }
 
 // dst[c][r] = src[r][c] for a rows x cols block (row strides lds / ldd), 64 x 64 tiles
