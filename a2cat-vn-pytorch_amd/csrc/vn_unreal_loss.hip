@@ -27,6 +27,7 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 constexpr int kPcCells = 42;  // BigGoalHouseModel's pixel-control map (goal.py:103-112)
 constexpr int kPcCellsBig = 20;  // BigHouseModel's (bignet.py:77-91, one k4 s2 layer on 9x9)
 constexpr int kPcCellPx = 4;
+constexpr int kPcChunk = 8;  // rollout steps whose loads unreal_pc_loss_kernel issues together
 
 // Mean |f1 - f0| / 255 over cell (cy, cx)'s 4 x 4 pixels and 3 channels (u8 HWC frames).
 __device__ __forceinline__ float pc_cell_change(const uint8_t* __restrict__ f0, const uint8_t* __restrict__ f1, int W,
@@ -95,31 +96,56 @@ __global__ __launch_bounds__(256) void unreal_pc_loss_kernel(float* __restrict__
       if (c < A) R = fmaxf(R, (v[c] + a) - a);
     reinterpret_cast<f4*>(pb)[0] = f4{0.f, 0.f, 0.f, 0.f};
     reinterpret_cast<f4*>(pb)[1] = f4{0.f, 0.f, 0.f, 0.f};
-    const uint8_t* fn = arena + (int64_t)rows_last[e] * frame_bytes;
-    for (int t = T - 1; t >= 0; --t) {
-      const int64_t r = (int64_t)t * E + e;
-      const uint8_t* f = arena + (int64_t)rows_img[r] * frame_bytes;
-      const bool done = dones[r] != 0;
-      const float rew = done ? 0.0f : pc_cell_change(f, fn, W, top, left, cy, cx);
-      R = rew + (done ? 0.0f : gamma * R);
-      const int act = actions[r];
-      float* pt = p2 + ((int64_t)(t * S + e) * PP + pix) * 8;
-      pc_load8(pt, v);
-      float at = v[0], va = v[0];
+    // steps in chunks of kPcChunk, latest first: a chunk's loads (frame rows, dones, actions,
+    // the two channels of p2 it needs, the cells of both frames) are all issued before its
+    // sequential part (the target recursion and the gradient stores), so a rollout costs
+    // T / kPcChunk memory round trips instead of T (33 -> ~10 us at 4 envs)
+    const uint8_t* fn = arena + (int64_t)rows_last[e] * frame_bytes;  // the frame after step t1
+    for (int t1 = T - 1; t1 >= 0; t1 -= kPcChunk) {
+      int64_t rowi[kPcChunk];
+      int act[kPcChunk];
+      bool done[kPcChunk];
 #pragma unroll
-      for (int c = 1; c < 8; ++c) {
-        if (c == A) at = v[c];
-        if (c == act) va = v[c];
+      for (int k = 0; k < kPcChunk; ++k) {
+        const int t = max(t1 - k, 0);  // (a step past the chunk's start repeats step 0; unused)
+        const int64_t r = (int64_t)t * E + e;
+        rowi[k] = rows_img[r];
+        act[k] = actions[r];
+        done[k] = dones[r] != 0;
       }
-      const float d = ((va + at) - at) - R;
-      sq += d * d;
-      const float g = va > 0.0f ? 2.0f * coef * d : 0.0f;
-      float o[8];
+      float rew[kPcChunk], va[kPcChunk], at[kPcChunk];
 #pragma unroll
-      for (int c = 0; c < 8; ++c) o[c] = c == act ? g : 0.0f;
-      reinterpret_cast<f4*>(pt)[0] = f4{o[0], o[1], o[2], o[3]};
-      reinterpret_cast<f4*>(pt)[1] = f4{o[4], o[5], o[6], o[7]};
-      fn = f;
+      for (int k = 0; k < kPcChunk; ++k) {
+        const int t = max(t1 - k, 0);
+        const uint8_t* f = arena + rowi[k] * frame_bytes;
+        const uint8_t* fx = k == 0 ? fn : arena + rowi[k - 1] * frame_bytes;
+        rew[k] = done[k] ? 0.0f : pc_cell_change(f, fx, W, top, left, cy, cx);
+        pc_load8(p2 + ((int64_t)(t * S + e) * PP + pix) * 8, v);
+        float a8 = v[0], v8 = v[0];
+#pragma unroll
+        for (int c = 1; c < 8; ++c) {
+          if (c == A) a8 = v[c];
+          if (c == act[k]) v8 = v[c];
+        }
+        at[k] = a8;
+        va[k] = v8;
+      }
+#pragma unroll
+      for (int k = 0; k < kPcChunk; ++k) {
+        const int t = t1 - k;
+        if (t < 0) break;
+        R = rew[k] + (done[k] ? 0.0f : gamma * R);
+        const float d = ((va[k] + at[k]) - at[k]) - R;
+        sq += d * d;
+        const float g = va[k] > 0.0f ? 2.0f * coef * d : 0.0f;
+        float o[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) o[c] = c == act[k] ? g : 0.0f;
+        float* pt = p2 + ((int64_t)(t * S + e) * PP + pix) * 8;
+        reinterpret_cast<f4*>(pt)[0] = f4{o[0], o[1], o[2], o[3]};
+        reinterpret_cast<f4*>(pt)[1] = f4{o[4], o[5], o[6], o[7]};
+      }
+      fn = arena + rowi[kPcChunk - 1] * frame_bytes;
     }
   }
   const float t = block_sum<256>(sq, red);
