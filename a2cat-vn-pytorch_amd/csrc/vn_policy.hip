@@ -435,6 +435,25 @@ struct EpiSlab {
   }
 };
 
+// A one-slab wgrad's epilogue: dW [M][KP] and the bias column into db (and db2), as
+// wgrad_reduce_kernel writes them (its sum 0 + v, kept: -0 stores as +0), without the slab
+// round trip and the reduce launch (a few-row backward ran eight of them, 7 us each).
+struct EpiWgrad {
+  float* dW;
+  float* db;
+  float* db2;
+  int KP;
+  __device__ __forceinline__ void operator()(int row, int col, float v, int) const {
+    const float s = 0.0f + v;
+    if (col < KP) {
+      dW[(int64_t)row * KP + col] = s;
+    } else {
+      db[row] = s;
+      if (db2) db2[row] = s;
+    }
+  }
+};
+
 // Split-K slab [splits][M][N] -> dW [M][KP] and, when N == KP + 1, the bias column db [M]
 // (also into db2 when given: the LSTM's b_ih and b_hh share one gradient).
 __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int M, int N, int KP, float* dW,
@@ -905,6 +924,10 @@ inline void launch_wgrad(const float* dZ, int64_t ldz, int M, FB fb, int KP, int
   kchunk = (kchunk + BK - 1) / BK * BK;
   splits = (P + kchunk - 1) / kchunk;
   DenseT fa{dZ, ldz, M};
+  if (splits == 1) {
+    launch_gemm<BM, BN, BK, WM, WN>(fa, fb, EpiWgrad{dW, db, nullptr, KP}, M, N, P, st, 1, kchunk);
+    return;
+  }
   EpiSlab ep{slab, M, N};
   launch_gemm<BM, BN, BK, WM, WN>(fa, fb, ep, M, N, P, st, splits, kchunk);
   launch_wgrad_reduce(slab, splits, M, N, KP, dW, db, nullptr, st);
@@ -924,6 +947,11 @@ inline void launch_wgrad6(const float* dZ, int64_t ldz, int M, FB fb, int KP, in
   kchunk = (kchunk + BK - 1) / BK * BK;
   splits = (P + kchunk - 1) / kchunk;
   DenseT fa{dZ, ldz, M};
+  if (splits == 1) {
+    hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, BK, WM, WN, DenseT, FB, EpiWgrad>), grid_for(M, N, BM, BN, 1), dim3(256),
+                       0, st, fa, fb, EpiWgrad{dW, db, nullptr, KP}, M, N, P, kchunk);
+    return;
+  }
   EpiSlab ep{slab, M, N};
   hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, BK, WM, WN, DenseT, FB, EpiSlab>), grid_for(M, N, BM, BN, splits),
                      dim3(256), 0, st, fa, fb, ep, M, N, P, kchunk);
@@ -948,6 +976,11 @@ inline void launch_wgrad_x6t(const float* dZ, int64_t ldz, int M, const float* X
   splits = (P + kchunk - 1) / kchunk;
   DenseT fa{dZ, ldz, M};
   DenseTOnes fb{X, ldx, KP};
+  if (splits == 1) {
+    hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, BK, WM, WN, DenseT, DenseTOnes, EpiWgrad>), grid_for(M, N, BM, BN, 1),
+                       dim3(256), 0, st, fa, fb, EpiWgrad{dW, db, db2, KP}, M, N, P, kchunk);
+    return;
+  }
   EpiSlab ep{slab, M, N};
   hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, BK, WM, WN, DenseT, DenseTOnes, EpiSlab>), grid_for(M, N, BM, BN, splits),
                      dim3(256), 0, st, fa, fb, ep, M, N, P, kchunk);
