@@ -2715,9 +2715,11 @@ void aux_backward_layer2_gemm(const PolicyLayout& L, const float* P, int n, floa
 
 // dX4 = conv(dA1, W1) (k4 s2, 48 -> 32 channels: the aux heads' first layer's input gradient)
 // as a persistent parity-class product, in place of the generic im2col product (which re-splits
-// every dA1 value at each of its 4 uses and the weights in every workgroup). A sample's dA1 map
-// is split once into three bf16 planes per parity class (py, px) = (y & 1, x & 1): class pixel
-// (cy, cx) at row cy XC + cx (XC = IW + 1, YC = IH + 1), 48 channels a row. Output pixel (oy, ox)
+// every dA1 value at each of its 4 uses and the weights in every workgroup). A work item is a
+// band of BY output rows of one sample (the whole 9x9 / 3x3 map at 174x174 / 84x84; 3 rows at
+// 300x400, whose 17x23 map does not fit): its dA1 rows are split once into three bf16 planes
+// per parity class (py, px) = (y & 1, x & 1): class pixel (oy0 + cyl, cx) at row cyl XC + cx
+// (XC = IW + 1), 48 channels a row, class rows past the map stored as zeros. Output pixel (oy, ox)
 // of the consecutive-row index p = oy XC + ox (ox = IW: a dummy column) sums, per class, the
 // taps (ky, kx) = (py + 2 ty, px + 2 tx), which read class rows p + ty XC + tx: 16 consecutive
 // rows per 16-pixel tile and tap. Wave w owns class w >> 1 and output channels 16 (w & 1) ..
@@ -2728,14 +2730,23 @@ void aux_backward_layer2_gemm(const PolicyLayout& L, const float* P, int n, floa
 template <int AH, int AW, int IH, int IW>
 struct AuxDx4 {
   static constexpr int C = kAuxC1, CO = 32;
-  static constexpr int XC = IW + 1, YC = IH + 1, NPC = XC * YC;
-  static constexpr int TP = (IH * XC + 15) / 16 * 16;  // tiled output rows (dummies included)
-  static constexpr int NR = TP + XC + 1;               // plane rows: the last tile's reads
-  static constexpr int PL = NR * C;                    // one plane (bf16)
-  static constexpr int PP = 36;                        // partial row stride (floats)
-  static constexpr int TG = 2;                         // tiles per partial-sum round (one barrier)
-  static constexpr size_t LDS = (size_t)12 * PL * 2 + (size_t)2 * TG * 4 * 16 * PP * 4;
-  static constexpr int NV = (AH * AW * (C / 4) + 511) / 512;  // prefetched f4 per thread
+  static constexpr int XC = IW + 1, YC = IH + 1;
+  static constexpr int PP = 36;  // partial row stride (floats)
+  static constexpr int TG = 2;   // tiles per partial-sum round (one barrier)
+  static constexpr int tp_of(int by) { return (by * XC + 15) / 16 * 16; }  // tiled output rows
+  static constexpr int nr_of(int by) { return tp_of(by) + XC + 1; }        // plane rows: the last tile's reads
+  static constexpr size_t lds_of(int by) { return (size_t)12 * nr_of(by) * C * 2 + (size_t)2 * TG * 4 * 16 * PP * 4; }
+  static constexpr int by_max() {
+    int by = IH;
+    while (by > 1 && lds_of(by) > 160 * 1024) --by;
+    return by;
+  }
+  // a band of BY output rows stages class rows oy0 .. oy0 + BY (dA1 rows 2 oy0 .. 2 oy0 + 2 BY + 1)
+  static constexpr int BY = by_max(), NB = (IH + BY - 1) / BY, SR = BY + 1;
+  static constexpr int TP = tp_of(BY), NR = nr_of(BY), PL = NR * C;
+  static constexpr int NS = 2 * SR * AW * (C / 4);  // staged f4 per item
+  static constexpr int NV = (NS + 511) / 512;       // prefetched f4 per thread
+  static constexpr size_t LDS = lds_of(BY);
   static constexpr bool fits = LDS <= 160 * 1024 && AH == 2 * IH + 2 && AW == 2 * IW + 2;
 };
 
@@ -2744,8 +2755,9 @@ __global__ __launch_bounds__(512, 1) void aux_dx4_x6_kernel(const float* __restr
                                                              const float* __restrict__ W1, float* __restrict__ dX4,
                                                              int n) {
   using S = AuxDx4<AH, AW, IH, IW>;
-  constexpr int C = S::C, XC = S::XC, NPC = S::NPC, TP = S::TP, NR = S::NR, PL = S::PL, PP = S::PP, NV = S::NV;
-  constexpr int C4 = C / 4, NPX = AH * AW, TILES = TP / 16, TG = S::TG;
+  constexpr int C = S::C, XC = S::XC, TP = S::TP, NR = S::NR, PL = S::PL, PP = S::PP, NV = S::NV, NS = S::NS;
+  constexpr int BY = S::BY, NB = S::NB, SR = S::SR;
+  constexpr int C4 = C / 4, TILES = TP / 16, TG = S::TG;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_adx[];
   uint16_t* pl = reinterpret_cast<uint16_t*>(smem_adx);            // [term][class][NR][C]
   float* part = reinterpret_cast<float*>(smem_adx + (size_t)12 * PL * 2);  // [2][TG][class][16][PP]
@@ -2768,36 +2780,41 @@ __global__ __launch_bounds__(512, 1) void aux_dx4_x6_kernel(const float* __restr
     bw[st][1] = b1.v;
     bw[st][2] = b2.v;
   }
-  // plane rows no class pixel owns (the last tiles' reads past row NPC) stay zero
-  for (int i = tid; i < 12 * (NR - NPC) * C4 / 2; i += 512) {
-    const int per = (NR - NPC) * C4 / 2, pln = i / per, r = i - pln * per;
-    reinterpret_cast<uint4*>(pl + (size_t)pln * PL + NPC * C)[r] = uint4{0u, 0u, 0u, 0u};
+  // plane rows past the staged class rows (the last tiles' reads) stay zero; every item
+  // rewrites rows 0 .. SR XC - 1 (zeros for class rows past the map)
+  for (int i = tid; i < 12 * (NR - SR * XC) * C4 / 2; i += 512) {
+    const int per = (NR - SR * XC) * C4 / 2, pln = i / per, r = i - pln * per;
+    reinterpret_cast<uint4*>(pl + (size_t)pln * PL + SR * XC * C)[r] = uint4{0u, 0u, 0u, 0u};
   }
+  const int items = n * NB;
   f4 pre[NV];
-  auto load = [&](int smp) {
-    const f4* src = reinterpret_cast<const f4*>(dA1 + (int64_t)smp * NPX * C);
+  auto load = [&](int it) {  // dA1 rows 2 oy0 .. of item it (rows past the map: any row, stored as 0)
+    const int smp = it / NB, b = it - (it / NB) * NB;
+    const f4* src = reinterpret_cast<const f4*>(dA1 + (int64_t)smp * AH * AW * C);
+    const int f0 = 2 * BY * b * AW * C4, fend = AH * AW * C4;
 #pragma unroll
-    for (int j = 0; j < NV; ++j) pre[j] = src[min(tid + j * 512, NPX * C4 - 1)];  // unconditional
+    for (int j = 0; j < NV; ++j) pre[j] = src[min(f0 + min(tid + j * 512, NS - 1), fend - 1)];  // unconditional
   };
-  if ((int)blockIdx.x < n) load(blockIdx.x);
-  int par = 0;  // partial-buffer parity (tiles run so far)
-  for (int smp = blockIdx.x; smp < n; smp += gridDim.x) {
-    __syncthreads();  // the previous sample's plane reads are done
+  if ((int)blockIdx.x < items) load(blockIdx.x);
+  int par = 0;  // partial-buffer parity (rounds run so far)
+  for (int it = blockIdx.x; it < items; it += gridDim.x) {
+    const int smp = it / NB, b = it - (it / NB) * NB, oy0 = BY * b, nr = min(BY, IH - oy0);
+    __syncthreads();  // the previous item's plane reads are done
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
       const int i = tid + j * 512;
-      if (i < NPX * C4) {
-        const int pix = i / C4, c4 = i - (i / C4) * C4, y = pix / AW, x = pix - (pix / AW) * AW;
+      if (i < NS) {
+        const int pix = i / C4, c4 = i - (i / C4) * C4, yl = pix / AW, x = pix - (pix / AW) * AW;
         uint2 t0, t1, t2;
-        split3_pack(pre[j], t0, t1, t2);
-        uint16_t* d = pl + (size_t)((y & 1) * 2 + (x & 1)) * PL + ((y >> 1) * XC + (x >> 1)) * C + 4 * c4;
+        split3_pack(2 * oy0 + yl < AH ? pre[j] : f4zero(), t0, t1, t2);
+        uint16_t* d = pl + (size_t)((yl & 1) * 2 + (x & 1)) * PL + ((yl >> 1) * XC + (x >> 1)) * C + 4 * c4;
         *reinterpret_cast<uint2*>(d) = t0;
         *reinterpret_cast<uint2*>(d + 4 * PL) = t1;
         *reinterpret_cast<uint2*>(d + 8 * PL) = t2;
       }
     }
     __syncthreads();
-    load(min(smp + (int)gridDim.x, n - 1));
+    load(min(it + (int)gridDim.x, items - 1));
     const uint16_t* cp = pl + (size_t)cls * PL;
 #pragma unroll 1
     for (int t0 = 0; t0 < TILES; t0 += TG) {
@@ -2835,9 +2852,10 @@ __global__ __launch_bounds__(512, 1) void aux_dx4_x6_kernel(const float* __restr
 #pragma unroll
       for (int u = 0; u < TG; ++u) {  // (pixel, channel): the four class partials in class order
         const float* pu = pb + (size_t)u * 4 * 16 * PP;
-        const int pi = tid >> 5, co = tid & 31, pp = (t0 + u) * 16 + pi, oy = pp / XC, ox = pp - (pp / XC) * XC;
+        const int pi = tid >> 5, co = tid & 31, pp = (t0 + u) * 16 + pi, oyl = pp / XC, ox = pp - (pp / XC) * XC;
         const float v = ((pu[pi * PP + co] + pu[(16 + pi) * PP + co]) + pu[(32 + pi) * PP + co]) + pu[(48 + pi) * PP + co];
-        if (t0 + u < TILES && oy < IH && ox < IW) dX4[(((int64_t)smp * IH + oy) * IW + ox) * S::CO + co] = v;
+        if (t0 + u < TILES && oyl < nr && ox < IW)
+          dX4[(((int64_t)smp * IH + oy0 + oyl) * IW + ox) * S::CO + co] = v;
       }
       par ^= 1;
     }
@@ -2898,7 +2916,7 @@ int aux_backward_impl(const PolicyLayout& L, const float* P, const float* X4, in
     if constexpr (Dx::fits) {
       const void* kfn = (const void*)aux_dx4_x6_kernel<AH, AW, IH, IW>;
       VN_HIP(ensure_dyn_lds(kfn, Dx::LDS));
-      const int blocks = std::min(n, resident_blocks(kfn, 512, Dx::LDS));
+      const int blocks = std::min(n * Dx::NB, resident_blocks(kfn, 512, Dx::LDS));
       if (blocks > 0)
         hipLaunchKernelGGL((aux_dx4_x6_kernel<AH, AW, IH, IW>), dim3(blocks), dim3(512), Dx::LDS, st, A1, P + L.aw1,
                            dX4, n);

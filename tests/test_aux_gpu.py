@@ -323,14 +323,15 @@ def test_full_resolution_300x400_trunk_and_aux_vs_oracle():
         _close(mine[k + ".bias"].numpy(), mod.bias.grad.numpy(), 1e-4, k + ".bias")
 
 
-@pytest.mark.parametrize("hw,B", [((174, 174), 17), ((174, 174), 300), ((84, 84), 37)])
+@pytest.mark.parametrize("hw,B", [((174, 174), 17), ((174, 174), 300), ((84, 84), 37), ((300, 400), 5),
+                                  ((300, 400), 43)])
 def test_aux_dx4_kernel_matches_generic_product(hw, B):
     """The aux heads' first-layer input gradient dX4 = conv(dA1, W1) on the persistent parity-
     class kernel (aux_dx4_x6_kernel: dA1 split once into class planes, per-class partials summed
     in class order) against the generic im2col product (VN_AUX_DX4_GENERIC): every parameter
     gradient of a heads-only loss to 1e-5 of its scale (dX4 reaches the trunk through conv4 ..
     conv1; the two sum the same exact split products in another order). 300 samples wrap the
-    persistent grid."""
+    persistent grid; 300x400 runs bands of 3 output rows (its last band 2)."""
     import os
     from vnav.policy import GoalNavPolicy
     torch.manual_seed(5)
