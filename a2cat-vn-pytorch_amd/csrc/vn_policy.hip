@@ -2057,7 +2057,7 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
     // 0.2-0.4 ms per update (profiles/r05/ab_cm/); 84x84's N = 288 keeps 64x64
     // Few rows (the logged run's 4 x 20 = 80): 64x64 tiles, split-K below 128 tiles (the
     // 128x128 form ran 21 workgroups down K = 512 alone: 54 us of a 2 ms update)
-    const bool big = G::FCIN >= 1024 && n >= 1024;
+    const bool big = G::FCIN >= 1024 && n >= 256;
     auto dgrad = [&](auto ep) {
       if (big)
         launch_gemm_x6<128, 128, 32, 2, 2>(fa, fb, ep, n, G::FCIN, 512, st);
