@@ -9,6 +9,8 @@
 //   clip_grad_norm_(max_norm) then RMSprop(lr, alpha, eps) with torch's update rule.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "vn_common.h"
 
 namespace vn {
@@ -113,6 +115,32 @@ __global__ __launch_bounds__(256) void sumsq_partial_kernel(const float* __restr
   double s = 0.0;
   for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     const float v = g[i] * scale;
+    s += (double)v * (double)v;
+  }
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off);
+  __shared__ double red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+// sumsq_partial_kernel with up to two gradient addends joined first: g[i] += add_j[i] for i in
+// [lo_j, hi_j) (written back, each addend in its own range, the ranges disjoint or added in
+// order j = 0, 1), so the side passes' gradient sums (the replayed aux / UNREAL trunk, heads
+// and LSTM) cost no launch of their own. The same grid-stride order as sumsq_partial_kernel:
+// the partial sums, hence the norm, are bitwise those of a separate add + norm.
+__global__ __launch_bounds__(256) void sumsq_join_partial_kernel(float* __restrict__ g, int64_t n, float scale,
+                                                                 const float* __restrict__ a0, int64_t lo0, int64_t hi0,
+                                                                 const float* __restrict__ a1, int64_t lo1, int64_t hi1,
+                                                                 double* partial) {
+  double s = 0.0;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    float x = g[i];
+    const bool j0 = a0 && i >= lo0 && i < hi0, j1 = a1 && i >= lo1 && i < hi1;
+    if (j0) x = x + a0[i];
+    if (j1) x = x + a1[i];
+    if (j0 || j1) g[i] = x;
+    const float v = x * scale;
     s += (double)v * (double)v;
   }
   for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off);
@@ -374,6 +402,69 @@ __global__ __launch_bounds__(kGoalThreads) void goal_runs_rollout_kernel(const u
 
 // Trace marker: an empty kernel whose grid size (tag workgroups of 64 lanes) a kernel
 // trace records, so a rocprofv3 trace of a test run can be split per test.
+// ---- the replay ring on the device (vn_replay_push_draw) ---------------------------
+constexpr int kReplayMaxSegs = 16;
+struct ReplaySegs {
+  vn_replay_seg s[kReplayMaxSegs];
+  int n;
+};
+
+// Slot k drawn over the filled slots after this push: Philox4x32-10 (ctr_lo, ctr_hi, 0,
+// STREAM_REPLAY) under key (seed_lo, seed_hi), uniform_below(r.x, filled') (DESIGN "RNG streams").
+__device__ __forceinline__ void replay_draw(const int64_t* meta, int R, uint32_t k0, uint32_t k1, int& pos, int& filled,
+                                            int& k) {
+  pos = (int)meta[0];
+  filled = min((int)meta[1] + 1, R);
+  const uint64_t ctr = (uint64_t)meta[2];
+  const u32x4 r = philox4x32_10(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), 0u, STREAM_REPLAY}, k0, k1);
+  k = (int)(((uint64_t)r.x * (uint64_t)filled) >> 32);
+}
+
+// Every block reads meta (pos, filled, counter), copies its share of each segment's source into
+// ring slot pos and, when cur != NULL, the drawn slot k into cur: from the source itself when
+// k == pos (the slot this launch writes), else from slot k (which no block writes). meta itself
+// is advanced by replay_meta_kernel afterwards (a block here may still be reading it).
+__global__ __launch_bounds__(256) void replay_push_draw_kernel(ReplaySegs segs, const int64_t* __restrict__ meta, int R,
+                                                               uint32_t k0, uint32_t k1) {
+  int pos, filled, k;
+  replay_draw(meta, R, k0, k1, pos, filled, k);
+  const int64_t g0 = blockIdx.x * 256ll + threadIdx.x, gs = (int64_t)gridDim.x * 256;
+  for (int j = 0; j < segs.n; ++j) {
+    const vn_replay_seg& sg = segs.s[j];
+    const int64_t cnt = (int64_t)sg.rows * sg.cols;
+    if (sg.elem_bytes == 4) {
+      const uint32_t* src = (const uint32_t*)sg.src;
+      uint32_t* ring = (uint32_t*)sg.ring;
+      uint32_t* cur = (uint32_t*)sg.cur;
+      for (int64_t i = g0; i < cnt; i += gs) {
+        const int64_t r = i / sg.cols, c = i - r * sg.cols;
+        const uint32_t v = src[r * sg.src_ld + c];
+        ring[(int64_t)pos * sg.slot_elems + i] = v;
+        if (cur) cur[i] = k == pos ? v : ring[(int64_t)k * sg.slot_elems + i];
+      }
+    } else {
+      const uint8_t* src = (const uint8_t*)sg.src;
+      uint8_t* ring = (uint8_t*)sg.ring;
+      uint8_t* cur = (uint8_t*)sg.cur;
+      for (int64_t i = g0; i < cnt; i += gs) {
+        const int64_t r = i / sg.cols, c = i - r * sg.cols;
+        const uint8_t v = src[r * sg.src_ld + c];
+        ring[(int64_t)pos * sg.slot_elems + i] = v;
+        if (cur) cur[i] = k == pos ? v : ring[(int64_t)k * sg.slot_elems + i];
+      }
+    }
+  }
+}
+
+__global__ void replay_meta_kernel(int64_t* meta, int R, uint32_t k0, uint32_t k1) {
+  int pos, filled, k;
+  replay_draw(meta, R, k0, k1, pos, filled, k);
+  meta[0] = (pos + 1) % R;
+  meta[1] = filled;
+  meta[2] += 1;
+  meta[3] = k;
+}
+
 __global__ void trace_marker_kernel() {}
 
 }  // namespace vn
@@ -386,6 +477,30 @@ int vn_a2c_episode_stats(float* episode_stats_env, int E, float* stats3, vn_stre
   if (!episode_stats_env || !stats3 || E <= 0) return fail(VN_EINVAL, "vn_a2c_episode_stats: bad args");
   hipLaunchKernelGGL(episode_stats_kernel, dim3(1), dim3(kPostThreads), 0, (hipStream_t)stream, episode_stats_env, E,
                      stats3);
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
+
+int vn_replay_push_draw(const vn_replay_seg* segs, int nseg, int64_t* meta4, int capacity, uint64_t seed,
+                        vn_stream_t stream) {
+  if (!segs || nseg < 1 || nseg > kReplayMaxSegs || !meta4 || capacity < 1)
+    return fail(VN_EINVAL, "vn_replay_push_draw: bad args (1..16 segments, capacity >= 1)");
+  ReplaySegs a{};
+  int64_t most = 0;
+  for (int j = 0; j < nseg; ++j) {
+    const vn_replay_seg& g = segs[j];
+    if (!g.src || !g.ring || g.rows < 1 || g.cols < 1 || (g.elem_bytes != 1 && g.elem_bytes != 4) ||
+        g.src_ld < g.cols || g.slot_elems < (int64_t)g.rows * g.cols)
+      return fail(VN_EINVAL, "vn_replay_push_draw: bad segment");
+    a.s[j] = g;
+    most = std::max<int64_t>(most, (int64_t)g.rows * g.cols);
+  }
+  a.n = nseg;
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((most + 255) / 256, 1024));
+  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(replay_push_draw_kernel, dim3(blocks), dim3(256), 0, st, a, meta4, capacity, k0, k1);
+  hipLaunchKernelGGL(replay_meta_kernel, dim3(1), dim3(1), 0, st, meta4, capacity, k0, k1);
   VN_HIP(hipGetLastError());
   return VN_OK;
 }
@@ -516,6 +631,20 @@ int vn_grad_norm(const float* grads, int64_t n, float scale, float max_norm, dou
   if (!grads || !partial_512 || !scalars2 || n <= 0) return fail(VN_EINVAL, "vn_grad_norm: bad args");
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(sumsq_partial_kernel, dim3(kNormBlocks), dim3(256), 0, st, grads, n, scale, partial_512);
+  hipLaunchKernelGGL(norm_final_kernel, dim3(1), dim3(256), 0, st, partial_512, kNormBlocks, max_norm, scalars2);
+  VN_HIP(hipGetLastError());
+  return VN_OK;
+}
+
+int vn_grad_norm_join(float* grads, int64_t n, const float* add0, int64_t lo0, int64_t hi0, const float* add1,
+                      int64_t lo1, int64_t hi1, float scale, float max_norm, double* partial_512, float* scalars2,
+                      vn_stream_t stream) {
+  if (!grads || !partial_512 || !scalars2 || n <= 0) return fail(VN_EINVAL, "vn_grad_norm_join: bad args");
+  if ((add0 && (lo0 < 0 || hi0 > n || lo0 > hi0)) || (add1 && (lo1 < 0 || hi1 > n || lo1 > hi1)))
+    return fail(VN_EINVAL, "vn_grad_norm_join: addend range outside [0, n)");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(sumsq_join_partial_kernel, dim3(kNormBlocks), dim3(256), 0, st, grads, n, scale, add0, lo0, hi0,
+                     add1, lo1, hi1, partial_512);
   hipLaunchKernelGGL(norm_final_kernel, dim3(1), dim3(256), 0, st, partial_512, kNormBlocks, max_norm, scalars2);
   VN_HIP(hipGetLastError());
   return VN_OK;

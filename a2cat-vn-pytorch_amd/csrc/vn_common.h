@@ -31,6 +31,7 @@ enum : uint32_t {
   STREAM_START = 1,   // start-state rejection attempts of a reset
   STREAM_ACTION = 2,  // synthetic random actions
   STREAM_POLICY = 3,  // categorical sampling from the policy
+  STREAM_REPLAY = 4,  // the replay ring's slot draw (vn_replay_push_draw)
 };
 
 __host__ __device__ inline void mulhilo32(uint32_t a, uint32_t b, uint32_t& hi, uint32_t& lo) {

@@ -319,6 +319,133 @@ __global__ __launch_bounds__(256, 2) void conv1_fwd_x3_kernel(FrameSrc src, int 
   (void)TILES;
 }
 
+// conv1_fwd_x3_kernel with the split weights resident in registers (round 6). The per-tile
+// budget of the LDS-fragment form (tools/isa_budget.py, 174x174): 33 MFMAs, 44 LDS reads (33 of
+// them the weight fragments, each waited on right before its MFMA: lgkmcnt(0/1) x 33), ~150
+// VALU; per item 21 prefetch loads at ~6.5 address instructions each and a branch per staged
+// dword. Here a lane's 33 fragments (132 VGPRs) are split once per kernel, so a tile reads only
+// its 11 image fragments; the next item's band is prefetched through a buffer descriptor over
+// the band (dwords past it read as zero: one address per thread, no clamps); the ReLU bits
+// are med3(bits(y), 0, 1) << (8j + r), shifted once by 4h. Same products, same three chains and
+// the same final sum as conv1_fwd_x3_kernel: bitwise equal outputs.
+template <int H, int W, int OH, int OW>
+__global__ __launch_bounds__(256, 2) void conv1_fwd_x3r_kernel(FrameSrc src, int n_frames, FrameList fl,
+                                                            const float* __restrict__ Wt,
+                                                            const float* __restrict__ bias, float* __restrict__ Y,
+                                                            uint32_t* __restrict__ mask) {
+  using B = Conv1X3Band<H, W>;
+  // the band's bf16 rows back to back (row stride RB elements, not B::RS): staged dword i is
+  // image elements 4i .. 4i + 3, one 8-byte store at 8i with no row arithmetic; at 174x174
+  // (522 B rows) a fragment is then only 4-byte aligned and is read as four dwords
+  constexpr int RB = B::RB, RS = RB, BR = B::BR, NB = B::NB, BRI = B::BRI;
+  constexpr int NPIX = OH * OW;
+  constexpr int NS = 11;                // k' slices of 16 (k' < 176)
+  constexpr int ND = BRI * RB / 4;      // dwords of a full band
+  constexpr int NPF = (ND + 255) / 256;  // prefetched dwords per thread
+  static_assert(RB % 2 == 0 && (BRI * RB) % 4 == 0, "band rows of whole dwords");
+  __shared__ __attribute__((aligned(16))) uint16_t img[BRI * RS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, c32 = lane & 31;
+  bf16x8 bw[NS][3];  // lane (h, co = c32): k' = 16 sl + 8h + j of output channel co
+#pragma unroll
+  for (int sl = 0; sl < NS; ++sl) {
+    union { uint16_t u[8]; bf16x8 v; } t0, t1, t2;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int kp = 16 * sl + 8 * h + j, ky = kp / 24, kr = kp - (kp / 24) * 24;
+      const float w = (ky < 7 && kr < 21) ? Wt[c32 * 148 + ky * 21 + kr] : 0.0f;
+      split3_bf16(w, t0.u[j], t1.u[j], t2.u[j]);
+    }
+    bw[sl][0] = t0.v;
+    bw[sl][1] = t1.v;
+    bw[sl][2] = t2.v;
+  }
+  f4 bs[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bs[j] = *reinterpret_cast<const f4*>(bias + 8 * j + 4 * h);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(bs[j][0]), "v"(bs[j][1]), "v"(bs[j][2]), "v"(bs[j][3]));
+  const int n_items = fl_count(fl, n_frames) * NB;
+  auto band_dwords = [&](int band) { return min(BRI, H - 4 * BR * band) * RB / 4; };
+  uint32_t pre[NPF];
+  auto load_item = [&](int it) {
+    const int f = fl_frame(fl, it / NB), band = it - (it / NB) * NB;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(frame_ptr(src, f) + (int64_t)4 * BR * band * RB), 0, band_dwords(band) * 4, 0x00020000);
+#pragma unroll
+    for (int j = 0; j < NPF; ++j) {
+      pre[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, 4 * tid + 1024 * j, 0, 0);
+      // issue order = use order, so the staging below waits vmcnt(NPF - 1 - j) for dword j (the
+      // scheduler's own order made it one vmcnt(0): every tile store of the item in flight too)
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  if ((int)blockIdx.x < n_items) load_item(blockIdx.x);
+  for (int it = blockIdx.x; it < n_items; it += gridDim.x) {
+    const int f = fl_frame(fl, it / NB), band = it - (it / NB) * NB;
+    const int oy0 = BR * band, nr = min(BR, OH - oy0), npb = nr * OW;
+#pragma unroll
+    for (int j = 0; j < NPF; ++j) {  // u8 -> bf16 rows (dwords past a short band are zeros)
+      const int i = tid + j * 256;
+      if (j + 1 < NPF || i < ND) *reinterpret_cast<uint2*>(img + 4 * i) = u8x4_bf16(pre[j]);
+    }
+    __syncthreads();
+    load_item(min(it + (int)gridDim.x, n_items - 1));
+    const int tiles = (npb + 31) / 32;
+    for (int t = wave; t < tiles; t += 4) {
+      const int px = min(t * 32 + c32, npb - 1);
+      const int oy = px / OW, ox = px - (px / OW) * OW;
+      const uint16_t* base = img + (oy * 4) * RS + ox * 12;
+      f16v acc[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[p][r] = 0.0f;
+#pragma unroll
+      for (int sl = 0; sl < NS; ++sl) {
+        const int k0 = 16 * sl + 8 * h, ky = k0 / 24, kr0 = k0 - (k0 / 24) * 24;
+        union { uint2 u[2]; uint32_t d[4]; bf16x8 v; } a;
+        if constexpr (RS % 4 == 0) {
+          const uint2* q = reinterpret_cast<const uint2*>(base + ky * RS + kr0);
+          a.u[0] = q[0];
+          a.u[1] = q[1];
+        } else {
+          const uint32_t* q = reinterpret_cast<const uint32_t*>(base + ky * RS + kr0);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) a.d[e] = q[e];
+        }
+#pragma unroll
+        for (int p = 0; p < 3; ++p) acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bw[sl][p], a.v, acc[p], 0, 0, 0);
+      }
+      const int rr = t * 32 + c32;
+      const int64_t pix = (int64_t)f * NPIX + oy0 * OW + rr;
+      uint32_t bits = 0;
+      f4 y[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = 4 * j + r;
+          const float sum = (acc[2][i] + acc[1][i]) + acc[0][i];
+          y[j][r] = fmaxf(sum * (1.0f / 255.0f) + bs[j][r], 0.0f);
+          // med3(bits(y), 0, 1) as int: 1 <=> y > 0 (y = fmaxf(., 0) is never NaN; -0 reads as 0);
+          // as C the compiler makes it v_cmp + v_cndmask of a constant + s_nop for the VCC hazard
+          uint32_t one;
+          asm("v_med3_i32 %0, %1, 0, 1" : "=v"(one) : "v"(y[j][r]));
+          bits |= one << (8 * j + r);
+        }
+      bits <<= 4 * h;
+      bits |= (uint32_t)__shfl_xor((int)bits, 32);
+      if (rr < npb) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) *reinterpret_cast<f4*>(Y + pix * 32 + 8 * j + 4 * h) = y[j];
+        if (h == 0) mask[pix] = bits;
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // ---- weight gradient ----------------------------------------------------------
 // One frame per workgroup iteration, its pixels in chunks of CP: the chunk's dZ rows
 // (CP x 32 fp32, 16-B loads) and the frame bytes are staged into LDS together, then each
@@ -1763,6 +1890,11 @@ struct Conv2Ring42x2 {
   static_assert(LDS <= 80 * 1024, "two workgroups per CU");
 };
 
+// PF (round 6): band k + 2's rows are loaded right after band k + 1's split and stay in flight
+// through band k + 1's MFMAs (the PMC of the PF = false form: waves waiting 42 % of their
+// cycles, most of it the split's wait on loads issued just before it); the split now precedes
+// the epilogue, so its wait counts no X2 store. Same sums, same order: bitwise equal.
+template <bool PF>
 __global__ __launch_bounds__(256, 2) void conv2_fwd_ring2_kernel(const float* __restrict__ X1,
                                                                  const float* __restrict__ W2,
                                                                  const float* __restrict__ bias,
@@ -1827,6 +1959,7 @@ __global__ __launch_bounds__(256, 2) void conv2_fwd_ring2_kernel(const float* __
   if (n_items > 0) {
     load_item(0);
     split_item(0);
+    if constexpr (PF) load_item(min(1, n_items - 1));
   }
   __syncthreads();
   f4 acc[4];
@@ -1890,6 +2023,10 @@ __global__ __launch_bounds__(256, 2) void conv2_fwd_ring2_kernel(const float* __
       for (int t = 0; t < 4; ++t) *reinterpret_cast<f4*>(part + (t * 16 + i16) * PP + ct * 16 + 4 * q) = acc[t];
     }
     __syncthreads();  // MFMA(k) and the partials done: band k's oldest slots are free
+    if constexpr (PF) {  // past the last item the split and the loads repeat it (same bytes, same slots)
+      split_item(min(k + 1, n_items - 1));
+      load_item(min(k + 2, n_items - 1));
+    }
     if (kh == 0) {
       const int64_t out0 = ((int64_t)fk * NP + oy0 * OW) * 32 + ct * 16 + 4 * q;
 #pragma unroll
@@ -1904,9 +2041,11 @@ __global__ __launch_bounds__(256, 2) void conv2_fwd_ring2_kernel(const float* __
         *reinterpret_cast<f4*>(X2 + out0 + (int64_t)(r * OW + ox) * 32) = v;
       }
     }
-    if (k + 1 < n_items) {  // loaded here, not a band ahead: the other workgroup on the CU covers
-      load_item(k + 1);     // the latency, and the 44 VGPRs keep the B fragments double-buffered
-      split_item(k + 1);
+    if constexpr (!PF) {
+      if (k + 1 < n_items) {  // loaded here, not a band ahead: the other workgroup on the CU covers
+        load_item(k + 1);     // the latency, and the 44 VGPRs keep the B fragments double-buffered
+        split_item(k + 1);
+      }
     }
     __syncthreads();  // band k + 1's rows in the ring, the partial buffer read
   }

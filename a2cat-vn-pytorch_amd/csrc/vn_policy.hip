@@ -1846,10 +1846,17 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
   if constexpr (kX3) {
     if (!f32in && !conv1_done) {  // bf16 MFMA on split weights (exact products)
       using B = Conv1X3Band<H0, W0>;
-      const int blocks =
-          std::min(frames * B::NB, resident_blocks((const void*)conv1_fwd_x3_kernel<H0, W0, G::OH1, G::OW1>, 256, 0));
-      hipLaunchKernelGGL((conv1_fwd_x3_kernel<H0, W0, G::OH1, G::OW1>), dim3(blocks), dim3(256), 0, st, src, frames,
-                         fl, P + L.l[0].w, P + L.l[0].b, a.X[0], a.M1);
+      // weights resident in registers; VN_CONV1F_LDSW keeps the LDS-fragment kernel (A/B, parity)
+      const bool ldsw = getenv("VN_CONV1F_LDSW") != nullptr;
+      const void* kfn = ldsw ? (const void*)conv1_fwd_x3_kernel<H0, W0, G::OH1, G::OW1>
+                             : (const void*)conv1_fwd_x3r_kernel<H0, W0, G::OH1, G::OW1>;
+      const int blocks = std::min(frames * B::NB, resident_blocks(kfn, 256, 0));
+      if (ldsw)
+        hipLaunchKernelGGL((conv1_fwd_x3_kernel<H0, W0, G::OH1, G::OW1>), dim3(blocks), dim3(256), 0, st, src, frames,
+                           fl, P + L.l[0].w, P + L.l[0].b, a.X[0], a.M1);
+      else
+        hipLaunchKernelGGL((conv1_fwd_x3r_kernel<H0, W0, G::OH1, G::OW1>), dim3(blocks), dim3(256), 0, st, src,
+                           frames, fl, P + L.l[0].w, P + L.l[0].b, a.X[0], a.M1);
       conv1_done = true;
     }
   } else if constexpr (kConv1Lds) {
@@ -1892,11 +1899,18 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
           hipLaunchKernelGGL(conv2_fwd_ring_kernel, dim3(blocks), dim3(512), Conv2Ring42::LDS, st, a.X[0],
                              P + L.l[1].w, P + L.l[1].b, a.X[1], frames, fl);
         } else {
-          const void* kfn = (const void*)conv2_fwd_ring2_kernel;
+          // band k + 2 prefetched through band k + 1's MFMAs; VN_CONV2F_RING2_NOPF keeps the form
+          // that loads each band just before its split (A/B; bitwise equal)
+          const bool pf = getenv("VN_CONV2F_RING2_NOPF") == nullptr;
+          const void* kfn = pf ? (const void*)conv2_fwd_ring2_kernel<true> : (const void*)conv2_fwd_ring2_kernel<false>;
           VN_HIP(ensure_dyn_lds(kfn, Conv2Ring42x2::LDS));
           const int blocks = std::min(frames, resident_blocks(kfn, 256, Conv2Ring42x2::LDS));
-          hipLaunchKernelGGL(conv2_fwd_ring2_kernel, dim3(blocks), dim3(256), Conv2Ring42x2::LDS, st, a.X[0],
-                             P + L.l[1].w, P + L.l[1].b, a.X[1], frames, fl);
+          if (pf)
+            hipLaunchKernelGGL(conv2_fwd_ring2_kernel<true>, dim3(blocks), dim3(256), Conv2Ring42x2::LDS, st,
+                               a.X[0], P + L.l[1].w, P + L.l[1].b, a.X[1], frames, fl);
+          else
+            hipLaunchKernelGGL(conv2_fwd_ring2_kernel<false>, dim3(blocks), dim3(256), Conv2Ring42x2::LDS, st,
+                               a.X[0], P + L.l[1].w, P + L.l[1].b, a.X[1], frames, fl);
         }
         done = true;
       }

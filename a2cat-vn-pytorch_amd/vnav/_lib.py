@@ -76,6 +76,21 @@ class GoalRuns(ctypes.Structure):
     ]
 
 
+class ReplaySeg(ctypes.Structure):
+    """vn_replay_seg (include/vnav.h)."""
+    _fields_ = [
+        ("src", c_void_p),
+        ("src_ld", c_int64),
+        ("ring", c_void_p),
+        ("cur", c_void_p),
+        ("slot_elems", c_int64),
+        ("rows", c_int),
+        ("cols", c_int),
+        ("elem_bytes", c_int),
+        ("pad_", c_int),
+    ]
+
+
 # name -> (restype, argtypes). Every symbol here is declared in include/vnav.h.
 SIGNATURES = {
     "vn_version": (ctypes.c_char_p, []),
@@ -172,6 +187,9 @@ SIGNATURES.update({
                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "vn_grad_norm": (c_int, [c_void_p, c_int64, c_float, c_float, c_void_p,
                                     c_void_p, c_void_p]),
+    "vn_grad_norm_join": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int64,
+                                  c_float, c_float, c_void_p, c_void_p, c_void_p]),
+    "vn_replay_push_draw": (c_int, [P(ReplaySeg), c_int, c_void_p, c_int, c_uint64, c_void_p]),
     "vn_rmsprop_step": (c_int, [c_void_p, c_void_p, c_void_p, c_int64,
                                        c_float, c_void_p, c_float, c_float,
                                        c_float, c_void_p]),

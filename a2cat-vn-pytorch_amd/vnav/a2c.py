@@ -43,7 +43,9 @@ on-policy sequences, and the loss formulas are the published algorithm's (parity
 csrc/vn_unreal_loss.hip, oracle/unreal.py).
 """
 import ctypes
+import os
 import time
+import warnings
 
 import numpy as np
 import torch
@@ -68,6 +70,9 @@ class A2CTrainer:
                  unreal_source="rollout"):
         self.env = env
         self.lib = _lib.load()
+        # check before every replayed UNREAL pass that the side stream's buffers and gradient
+        # block are disjoint from the main stream's (_check_side_stream_disjoint)
+        self.debug_streams = bool(os.environ.get("VN_DEBUG_STREAMS"))
         self.device = env.device
         self.num_steps = int(num_steps)
         self.gamma = float(gamma)
@@ -178,16 +183,14 @@ class A2CTrainer:
         self.aux_source = aux_source
         self.unreal_source = unreal_source if unreal else "rollout"
         # the replay ring of the last replay_size rollouts (deep_rl's replay buffer, absent: its
-        # capacity and sequence shape are parity unpinned); one stored rollout is drawn per update
+        # capacity and sequence shape are parity unpinned); one stored rollout is drawn per update.
+        # Push and draw run on the device (vn_replay_push_draw: meta = [next slot, filled, draw
+        # counter, drawn slot]), so an update with replay sources is captured by cuda_graph=True.
         self.replay = aux_source == "replay" or self.unreal_source == "replay"
         if self.replay:
-            if cuda_graph:
-                raise ValueError("a replay source draws its sequence on the host each update: use cuda_graph=False")
             self.replay_rows = torch.zeros((int(replay_size), 2, N), dtype=torch.int32, **kw)
-            self.replay_filled = 0
-            self.replay_pos = 0
-            self._replay_rng = torch.Generator().manual_seed(vdist.rank_seed(self.seed + 17, self.rank))
-            self._replay_k = 0
+            self.replay_meta = torch.zeros(4, dtype=torch.int64, **kw)
+            self._replay_seed = vdist.rank_seed(self.seed + 17, self.rank) & ((1 << 64) - 1)
         if aux_source == "replay":
             if self.aux_weight <= 0:
                 raise ValueError("aux_source='replay' needs aux_weight > 0")
@@ -202,6 +205,8 @@ class A2CTrainer:
         # compute_auxiliary_loss overridden by a subclass: called every update (autograd on a
         # GoalNavPolicy view of the flat parameters), its gradient added before the all-reduce
         self._setup_unreal(unreal, pc_weight, rp_weight, vr_weight, pc_gamma, unreal_envs)
+        if self.replay:
+            self._replay_segs = self._replay_segments()
         self._custom_aux = type(self).compute_auxiliary_loss is not A2CTrainer.compute_auxiliary_loss
         if self._custom_aux and cuda_graph:
             raise ValueError("a compute_auxiliary_loss override runs torch autograd per update: use cuda_graph=False")
@@ -326,7 +331,16 @@ class A2CTrainer:
                        dones=torch.zeros((R, T, S), dtype=torch.bool, device=self.device),
                        masks=torch.zeros((R, T + 1, S), **f32), lra=torch.zeros((R, T + 1, S, A1), **f32),
                        hc0=torch.zeros((R, 2, S, 512), **f32))
+        # the slot drawn this update, copied out of the ring by vn_replay_push_draw (fixed
+        # addresses: the replayed pass's launches do not depend on which slot was drawn)
+        self.ur_cur = {key: torch.zeros_like(v[0]) for key, v in self.ur.items()}
         X = net.lstm["xcat"]
+        # Side-stream-owned (update(): the replayed pass runs on self._side_u beside the A2C
+        # backward): ur_* and ur_cur, h_pc / pcb / pc_a1 / pc_p2 / dh_pc / pc_ws, rp_x / rp_dx /
+        # rp_out / rp_dout, unreal_stats, and the pc / rp blocks of self.grads
+        # (_side_grad_ranges()). Nothing on the main stream may touch them between the fork and
+        # the join — checked by _check_side_stream_disjoint (VN_DEBUG_STREAMS=1 or
+        # A2CTrainer.debug_streams) and tests/test_unreal_gpu.py.
         self.ur_acts = net.new_acts(n)
         self.ur_xcat = torch.zeros((n, X), **f32)
         self.ur_lacts = torch.zeros((n, 2048), **f32)
@@ -427,43 +441,63 @@ class A2CTrainer:
             self._model_view = GoalNavPolicy.wrap(self.net, self.params)
         return self._model_view
 
+    def _replay_segments(self):
+        """The vn_replay_push_draw segments (include/vnav.h vn_replay_seg) of this trainer's
+        ring: the frame rows of every sample (drawn into aux_rows for a replayed aux batch) and,
+        with unreal_source='replay', the first S envs' record (frame rows of steps 0..T - 1 and
+        of the bootstrap observation, actions, rewards, dones, the LSTM inputs of steps 0..T and
+        the (h, c) the rollout started from), drawn into ur_cur."""
+        E, T, N = self.env.num_envs, self.num_steps, self.num_steps * self.env.num_envs
+        segs = []
+
+        def seg(src, ld, rows, cols, ring, slot_elems, cur):
+            eb = src.element_size()
+            assert ring.element_size() == eb and (cur is None or cur.element_size() == eb)
+            assert src.is_contiguous() and ring.is_contiguous() and (cur is None or cur.is_contiguous())
+            segs.append(_lib.ReplaySeg(src.data_ptr(), ld, ring.data_ptr(), None if cur is None else cur.data_ptr(),
+                                       slot_elems, rows, cols, eb, 0))
+
+        aux = self.aux_source == "replay"
+        for j, rows in enumerate((self.rows_img, self.rows_goal)):
+            seg(rows, N, 1, N, self.replay_rows[0, j], 2 * N, self.aux_rows[j] if aux else None)
+        if self.unreal_source == "replay":
+            S, A1 = self.unreal_S, self.A + 1
+            n = (T + 1) * S
+            u, c, info = self.ur, self.ur_cur, self.env._info
+            for j, (rows, last) in enumerate(((self.rows_img, info["img_row"]), (self.rows_goal, info["goal_row"]))):
+                seg(rows, E, T, S, u["rows"][0, j], 2 * n, c["rows"][j])
+                seg(last, S, 1, S, u["rows"][0, j, T * S:], 2 * n, c["rows"][j, T * S:])
+            seg(self.actions, E, T, S, u["actions"][0], T * S, c["actions"])
+            seg(self.rewards, E, T, S, u["rewards"][0], T * S, c["rewards"])
+            seg(self.dones, E, T, S, u["dones"][0], T * S, c["dones"])
+            seg(self.masks, E, T, S, u["masks"][0], (T + 1) * S, c["masks"])
+            seg(self.boot_mask, S, 1, S, u["masks"][0, T], (T + 1) * S, c["masks"][T])
+            seg(self.lra, E * A1, T, S * A1, u["lra"][0], (T + 1) * S * A1, c["lra"])
+            seg(self.boot_lra, S * A1, 1, S * A1, u["lra"][0, T], (T + 1) * S * A1, c["lra"][T])
+            seg(self._hc0, E * 512, 2, S * 512, u["hc0"][0], 2 * S * 512, c["hc0"])
+        return (_lib.ReplaySeg * len(segs))(*segs)
+
+    @property
+    def replay_filled(self):
+        """Filled slots of the replay ring (reads the device meta: synchronises)."""
+        return int(self.replay_meta[1])
+
+    @property
+    def replay_pos(self):
+        return int(self.replay_meta[0])
+
     def _replay_push_and_sample(self):
         """Store this rollout's frame rows (and, for the UNREAL losses, the first S envs'
-        sequences) in the replay ring; draw one stored rollout (uniform over the filled slots)
-        for this update's replayed batches. Returns the aux batch (None without aux replay)."""
+        sequences) in the replay ring and draw one stored rollout (uniform over the filled
+        slots) for this update's replayed batches, on the device in one call
+        (vn_replay_push_draw: no host value, capturable). Returns the aux batch (None without
+        aux replay)."""
         R = self.replay_rows.shape[0]
-        k0 = self.replay_pos
-        self.replay_rows[k0, 0].copy_(self.rows_img)
-        self.replay_rows[k0, 1].copy_(self.rows_goal)
-        if self.unreal_source == "replay":
-            self._unreal_replay_push(k0)
-        self.replay_pos = (self.replay_pos + 1) % R
-        self.replay_filled = min(self.replay_filled + 1, R)
-        k = int(torch.randint(self.replay_filled, (1,), generator=self._replay_rng))
-        self._replay_k = k
+        _lib.check(self.lib.vn_replay_push_draw(self._replay_segs, len(self._replay_segs), _lib.ptr(self.replay_meta),
+                                                R, self._replay_seed, self._stream()), "vn_replay_push_draw")
         if self.aux_source != "replay":
             return None
-        self.aux_rows.copy_(self.replay_rows[k])
         return RolloutBatch(self, self.aux_rows[0], self.aux_rows[1])
-
-    def _unreal_replay_push(self, k):
-        """Slot k <- the first S envs of this rollout: frame rows of steps 0..T-1 and of the
-        bootstrap observation, actions, rewards, dones, the LSTM inputs (masks, last action /
-        reward) of steps 0..T and the (h, c) the rollout started from."""
-        E, T, S = self.env.num_envs, self.num_steps, self.unreal_S
-        u, info = self.ur, self.env._info
-        for j, (rows, last) in enumerate(((self.rows_img, info["img_row"]), (self.rows_goal, info["goal_row"]))):
-            r = u["rows"][k, j].view(T + 1, S)
-            r[:T].copy_(rows.view(T, E)[:, :S])
-            r[T].copy_(last[:S])
-        u["actions"][k].view(T, S).copy_(self.actions.view(T, E)[:, :S])
-        u["rewards"][k].copy_(self.rewards[:, :S])
-        u["dones"][k].copy_(self.dones[:, :S])
-        u["masks"][k, :T].copy_(self.masks[:, :S])
-        u["masks"][k, T].copy_(self.boot_mask[:S])
-        u["lra"][k, :T].copy_(self.lra[:, :S])
-        u["lra"][k, T].copy_(self.boot_lra[:S])
-        u["hc0"][k].copy_(self._hc0[:, :S])
 
     def _unreal_replay_losses(self, add=True):
         """UnrealTrainer's losses on the first S envs of the stored rollout drawn this update
@@ -480,23 +514,23 @@ class A2CTrainer:
         T, S, A = self.num_steps, self.unreal_S, self.A
         n = (T + 1) * S
         P, st = _lib.ptr, self._stream()
-        u, k = self.ur, self._replay_k
-        rows = u["rows"][k]
+        u = self.ur_cur  # the slot vn_replay_push_draw drew this update
+        rows = u["rows"]
         frames = self._frames(rows[0], rows[1])
         net.forward(self.params, frames, n, self.ur_acts, n, 0, None)
         x5 = net.x5(self.ur_acts, n)
         h_r, c_r = self.ur_hc[0], self.ur_hc[1]
-        h0, c0 = u["hc0"][k, 0], u["hc0"][k, 1]
+        h0, c0 = u["hc0"][0], u["hc0"][1]
         for t in range(T + 1):
             sl = slice(t * S, (t + 1) * S)
             hp = h0 if t == 0 else h_r[(t - 1) * S:t * S]
             cp = c0 if t == 0 else c_r[(t - 1) * S:t * S]
-            net.lstm_step(self.params, S, x5[sl], u["lra"][k, t], u["masks"][k, t], hp, cp, self.ur_xcat[sl],
+            net.lstm_step(self.params, S, x5[sl], u["lra"][t], u["masks"][t], hp, cp, self.ur_xcat[sl],
                           self.ur_gates, self.ur_lacts[sl], c_r[sl], h_r[sl])
         net.heads(self.params, h_r, n, self.ur_out)
         self.unreal_stats.zero_()
         self.ur_dout.zero_()
-        rew, don = u["rewards"][k], u["dones"][k]
+        rew, don = u["rewards"], u["dones"]
         _lib.check(lib.vn_a2c_returns(P(rew), P(don), P(self.ur_out[T * S:]), T, S, A, ctypes.c_float(self.gamma),
                                       P(self.ur_returns), st), "vn_a2c_returns")
         if self.vr_weight > 0:
@@ -506,7 +540,7 @@ class A2CTrainer:
         # pixel control on the replayed h (rows t*S + e, the bootstrap at t = T)
         net.pc_forward(self.params, h_r, n, self.pcb, self.pc_a1, self.pc_p2, None, self.pc_ws)
         H, W = self.env.frame_shape[:2]
-        _lib.check(lib.vn_unreal_pc_loss_grad_ex(P(self.pc_p2), self.pc_cells, P(u["actions"][k]), P(don),
+        _lib.check(lib.vn_unreal_pc_loss_grad_ex(P(self.pc_p2), self.pc_cells, P(u["actions"]), P(don),
                                                  ctypes.c_void_p(self._arena), ctypes.c_int64(self._fb), H, W, P(rows[0]),
                                                  P(rows[0][T * S:]), T, S, S, A, ctypes.c_float(self.pc_gamma),
                                                  ctypes.c_float(self.pc_weight), P(self.unreal_stats), st),
@@ -524,12 +558,67 @@ class A2CTrainer:
         _lib.check(lib.vn_unreal_rp_scatter(P(self.rp_dx), T, S, S, F, P(self.ur_dx4), 0, st), "vn_unreal_rp_scatter")
         # BPTT over the T + 1 replayed steps (value replay's dout + pixel control's dh), the trunk
         net.lstm_backward(self.params, T + 1, S, self.ur_dout, h_r, self.ur_xcat, self.ur_lacts, c_r, c0,
-                          u["masks"][k], x5, self.ur_dz5, self.ur_grads, self.ur_lstm_ws, dh_extra=self.dh_pc,
+                          u["masks"], x5, self.ur_dz5, self.ur_grads, self.ur_lstm_ws, dh_extra=self.dh_pc,
                           extra_envs=S)
         net.backward_ex(self.params, frames, n, self.ur_acts, n, None, self.ur_dz5, self.ur_dx4, self.ur_grads,
                         self.ur_ws)
         if add:
             self.grads[:self._ur_add_end].add_(self.ur_grads[:self._ur_add_end])
+
+    def _side_grad_range(self):
+        """[lo, hi) of the flat gradient the replayed UNREAL pass writes on the side stream: the
+        pixel-control and reward-prediction blocks (include/vnav.h VN_POLICY_UNREAL layout)."""
+        return min(self.net.unreal_layout.values()), self.net.n_params
+
+    def _side_owned(self):
+        """(name, tensor) the side stream writes between the fork and the join."""
+        lo, hi = self._side_grad_range()
+        out = [(k, getattr(self, k)) for k in ("ur_acts", "ur_xcat", "ur_lacts", "ur_hc", "ur_gates", "ur_out",
+                                               "ur_returns", "ur_dout", "ur_dz5", "ur_dx4", "ur_grads", "ur_ws",
+                                               "ur_lstm_ws", "h_pc", "pcb", "pc_a1", "pc_p2", "dh_pc", "pc_ws",
+                                               "rp_x", "rp_dx", "rp_out", "rp_dout", "unreal_stats")]
+        out += [("ur_cur." + k, v) for k, v in self.ur_cur.items()]
+        return out + [("grads[pc/rp]", self.grads[lo:hi])]
+
+    def _main_owned(self):
+        """(name, tensor) the main stream writes while the side stream runs."""
+        lo, _ = self._side_grad_range()
+        names = ("acts", "workspace", "dout", "returns", "stats", "out", "dz5", "dx4", "lstm_ws", "xcat", "lstm_acts",
+                 "a1", "pred", "dpred", "aux_ws", "aux_stats", "aux_acts", "aux_out", "aux_dz5", "aux_grads",
+                 "unreal_dx4", "norm_partial", "scalars", "_hc0", "h_all", "c_all", "goal_list", "goal_run_length",
+                 "goal_count")
+        out = [(k, getattr(self, k)) for k in names if isinstance(getattr(self, k, None), torch.Tensor)]
+        return out + [("grads[trunk/heads/lstm/aux]", self.grads[:lo])]
+
+    def _check_side_stream_disjoint(self):
+        """The replayed UNREAL pass runs on a side stream beside the A2C backward (update()); it
+        is race-free only while (1) its gradient block [pc_w, P) lies past every block the main
+        stream writes and past the range the join adds ([0, _ur_add_end)), and (2) no buffer it
+        writes shares memory with a buffer the main stream writes. Raises RuntimeError naming
+        the first overlap (debug check: VN_DEBUG_STREAMS=1 or trainer.debug_streams = True)."""
+        lo, hi = self._side_grad_range()
+        net = self.net
+        main_end = max(b + net.shapes[k][0] for k, (_, b) in net.offsets.items() if net.shapes[k][0])
+        if net.lstm:
+            main_end = max(main_end, net.lstm["bhh"] + 2048)
+        if net.aux_layout:
+            main_end = max(main_end, net.aux_layout["b2"] + 8)
+        if main_end > lo or self._ur_add_end > lo:
+            raise RuntimeError("side-stream gradient block [%d, %d) overlaps the main stream's blocks (end %d) or the "
+                               "join range [0, %d)" % (lo, hi, main_end, self._ur_add_end))
+
+        def span(t):
+            a = t.data_ptr()
+            return a, a + t.numel() * t.element_size()
+
+        main = [(k, span(t)) for k, t in self._main_owned() if t.numel()]
+        for ks, ts in self._side_owned():
+            if not ts.numel():
+                continue
+            a0, a1 = span(ts)
+            for km, (b0, b1) in main:
+                if a0 < b1 and b0 < a1:
+                    raise RuntimeError("side-stream buffer %s overlaps main-stream buffer %s" % (ks, km))
 
     def _stream(self):
         return _lib.stream_ptr(self.device)
@@ -651,14 +740,18 @@ class A2CTrainer:
         N = T * E
         st = self._stream()
         aux_batch = batch.get("auxiliary_batch") if batch is not None else None
+        if batch is None and self.replay:
+            # a bare rollout(): store it and draw this update's sequence now (the replayed aux
+            # batch included, as sample_training_batch() would have)
+            aux_batch = self._replay_push_and_sample()
         u_side = self.unreal and self.unreal_source == "replay"
         if u_side:
             # the replayed UNREAL pass reads the parameters and its own ring slot and writes its
             # own buffers and the pc / rp gradient blocks, which the A2C backward never touches:
             # it runs on a side stream from here; its trunk / heads / LSTM gradients are added
             # after the join below, in the unforked order
-            if batch is None:  # a bare rollout(): store it and draw this update's sequence now
-                self._replay_push_and_sample()
+            if self.debug_streams:
+                self._check_side_stream_disjoint()
             main = torch.cuda.current_stream(self.device)
             self._ev_u0.record(main)
             self._side_u.wait_event(self._ev_u0)
@@ -715,11 +808,21 @@ class A2CTrainer:
         else:
             net.backward_ex(self.params, frames, N, self.acts, N, self.dout, None, dx4, self.grads, self.workspace,
                             goals=goals)
+        # the side passes' gradient sums: in the norm's first pass (vn_grad_norm_join) on one
+        # rank with no override; before the all-reduce / the override's autograd otherwise
+        joins = []
         if aux_batch is not None:
-            self._add_trunk_grads(self.aux_grads)
+            w, _ = self.net.offsets["conv1"]
+            _, b = self.net.offsets["fc"]
+            joins.append((self.aux_grads, w, b + self.net.shapes["fc"][0]))
         if u_side:
             torch.cuda.current_stream(self.device).wait_event(self._ev_u1)
-            self.grads[:self._ur_add_end].add_(self.ur_grads[:self._ur_add_end])
+            joins.append((self.ur_grads, 0, self._ur_add_end))
+        fuse_join = self.world == 1 and not self._custom_aux
+        if not fuse_join:
+            for g, lo, hi in joins:
+                self.grads[lo:hi].add_(g[lo:hi])
+            joins = []
         if self._custom_aux:
             loss, self.aux_losses = self.compute_auxiliary_loss(self.model_view(), batch, self.device)
             if loss is not None:
@@ -728,9 +831,16 @@ class A2CTrainer:
                     self.grads.add_(g)
         scale = self._allreduce_tail()
         P = net.n_params
-        _lib.check(lib.vn_grad_norm(_lib.ptr(self.grads), P, ctypes.c_float(scale),
-                                    ctypes.c_float(self.max_gradient_norm), _lib.ptr(self.norm_partial),
-                                    _lib.ptr(self.scalars), st), "vn_grad_norm")
+        if joins:
+            (a0, lo0, hi0), (a1, lo1, hi1) = (joins + [(None, 0, 0)])[:2]
+            _lib.check(lib.vn_grad_norm_join(_lib.ptr(self.grads), P, _lib.ptr(a0), lo0, hi0, _lib.ptr(a1), lo1, hi1,
+                                             ctypes.c_float(scale), ctypes.c_float(self.max_gradient_norm),
+                                             _lib.ptr(self.norm_partial), _lib.ptr(self.scalars), st),
+                       "vn_grad_norm_join")
+        else:
+            _lib.check(lib.vn_grad_norm(_lib.ptr(self.grads), P, ctypes.c_float(scale),
+                                        ctypes.c_float(self.max_gradient_norm), _lib.ptr(self.norm_partial),
+                                        _lib.ptr(self.scalars), st), "vn_grad_norm")
         # lr of this update from the device schedule (== current_lr() of the host counters)
         _lib.check(lib.vn_rmsprop_step_dev(_lib.ptr(self.params), _lib.ptr(self.grads), _lib.ptr(self.square_avg), P,
                                            ctypes.c_float(scale), _lib.ptr(self.scalars), _lib.ptr(self.lr_dev),
@@ -927,8 +1037,7 @@ class A2CTrainer:
                 sd[k] = getattr(self, k).cpu()
         if self.replay:  # the replay ring and its draw stream resume exactly
             sd["replay_rows"] = self.replay_rows.cpu()
-            sd["replay_fill_pos"] = torch.tensor([self.replay_filled, self.replay_pos], dtype=torch.int64)
-            sd["replay_rng"] = self._replay_rng.get_state()
+            sd["replay_meta"] = self.replay_meta.cpu()  # next slot, filled, draw counter, drawn slot
             if self.unreal_source == "replay":
                 for key, v in self.ur.items():
                     sd["ur_" + key] = v.cpu()
@@ -977,14 +1086,43 @@ class A2CTrainer:
         if self.recurrent:
             for k in self._RECURRENT_STATE:
                 getattr(self, k).copy_(sd[k].to(self.device))
-        if self.replay and "replay_rows" in sd:
-            self.replay_rows.copy_(sd["replay_rows"].to(self.device))
-            self.replay_filled, self.replay_pos = (int(x) for x in sd["replay_fill_pos"])
-            self._replay_rng.set_state(sd["replay_rng"])
-            if self.unreal_source == "replay":
-                for key, v in self.ur.items():
-                    v.copy_(sd["ur_" + key].to(self.device))
+        if self.replay:
+            self._load_replay_state(sd)
         self.env.observe(gather=False)
+
+    def _load_replay_state(self, sd):
+        """The replay ring of a checkpoint. The ring restarts empty (with a warning) when the
+        checkpoint has no ring, a ring of another capacity, or no UNREAL record while this
+        trainer replays the UNREAL losses (a checkpoint of aux-only replay or of
+        unreal_source='rollout'): restoring the frame rows alone would draw slots whose UNREAL
+        record is empty. Checkpoints from before the device-side ring (host draw stream,
+        'replay_fill_pos') keep their slots; the draw stream restarts at counter 0."""
+        ring = sd.get("replay_rows")
+        need_ur = self.unreal_source == "replay"
+        why = None
+        if ring is None:
+            why = "the checkpoint holds no replay ring"
+        elif tuple(ring.shape) != tuple(self.replay_rows.shape):
+            why = "the checkpoint's ring is %s, this trainer's %s" % (tuple(ring.shape), tuple(self.replay_rows.shape))
+        elif need_ur and any("ur_" + key not in sd for key in self.ur):
+            why = "the checkpoint has no UNREAL record in its ring (saved without unreal_source='replay')"
+        if why is not None:
+            warnings.warn("replay ring restarts empty: " + why)
+            self.replay_rows.zero_()
+            self.replay_meta.zero_()
+            if need_ur:
+                for v in self.ur.values():
+                    v.zero_()
+            return
+        self.replay_rows.copy_(ring.to(self.device))
+        if "replay_meta" in sd:
+            self.replay_meta.copy_(sd["replay_meta"].to(self.device))
+        else:
+            pos_filled = [int(x) for x in sd["replay_fill_pos"]]
+            self.replay_meta.copy_(torch.tensor([pos_filled[1], pos_filled[0], 0, 0], dtype=torch.int64))
+        if need_ur:
+            for key, v in self.ur.items():
+                v.copy_(sd["ur_" + key].to(self.device))
 
 
 class RolloutBatch(dict):

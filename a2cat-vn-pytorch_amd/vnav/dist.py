@@ -2,10 +2,12 @@
 
 Envs are independent, so each rank owns its own env shard and a full replica of the
 scene cache; the only data-path exchange is the all-reduce of the flat
-fp32 gradient buffer per update (0.96 MB for the 84x84 feed-forward policy, one call;
-9.4 MB with the LSTM, in two buckets: heads + LSTM + aux heads as soon as the LSTM
-backward ends, overlapped with the trunk backward, then the trunk), plus one tiny
-all-reduce of the episode/loss statistics.
+fp32 gradient buffer per update (0.96 MB for the 84x84 feed-forward policy; 9.4-19.8 MB
+with the LSTM / aux / UNREAL heads), one flat bucket by default (A2CTrainer
+allreduce_buckets=1). allreduce_buckets=2 is opt-in: heads + LSTM + aux heads as soon as the
+LSTM backward ends, overlapped with the trunk backward, then the trunk — bitwise equal to
+one bucket in the gloo world-2 test, not yet run under RCCL across distinct GPUs. Plus one
+tiny all-reduce of the episode/loss statistics.
 The reference has no distributed code at all (it runs 4 SubprocVecEnv processes on
 one GPU, experiments/thor_cached_auxiliary.py:58-71).
 """

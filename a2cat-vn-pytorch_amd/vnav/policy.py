@@ -15,6 +15,7 @@ optimizer, the gradient norm and the RCCL all-reduce each touch one contiguous t
 import ctypes
 import math
 import re
+import warnings
 
 import numpy as np
 import torch
@@ -231,9 +232,13 @@ class PolicyNet:
             u["rp_w"].uniform_(-d, d, generator=g)
         return flat.to(self.device)
 
-    def from_reference(self, sd):
-        """Reference state dict (BigGoalHouseModel names, any prefix) -> flat params."""
-        flat = torch.zeros(self.n_params, dtype=torch.float32)
+    def from_reference(self, sd, init=None):
+        """Reference state dict (BigGoalHouseModel names, any prefix) -> flat params. ``init``
+        (flat params) supplies what the state dict cannot: BigHouseModel's rp weight as the
+        reference builds it, Linear(9*9*32*3, 3) (bignet.py:94), fits only 100x100 frames; on
+        other frames it is left at ``init`` (zeros without one) with a warning."""
+        flat = torch.zeros(self.n_params, dtype=torch.float32) if init is None else \
+            init.detach().float().cpu().clone()
         v = self.views(flat)
         pick = _ReferenceNames(sd)
         t = lambda x: torch.as_tensor(np.asarray(x), dtype=torch.float32)  # noqa: E731
@@ -299,10 +304,17 @@ class PolicyNet:
             u["b2"][A] = t(pick("pc_action", 1, "bias")).view(())
         if self.unreal_layout:
             rw = t(pick("rp", 0, "weight"))
-            if rw.shape[1] != u["rp_w"].shape[1]:
+            if self.arch == "bighouse" and rw.shape[1] == 9 * 9 * 32 * 3 != u["rp_w"].shape[1]:
+                # the reference module's rp as built (bignet.py:94), never usable at 84x84: keep
+                # this policy's own rp (DESIGN row A23u), load everything else
+                warnings.warn("BigHouseModel rp.weight takes %d inputs (bignet.py:94, 100x100 frames); this "
+                              "%dx%d policy's rp takes %d: rp left at its initialisation, the rest loaded"
+                              % (rw.shape[1], self.frame_hw[0], self.frame_hw[1], u["rp_w"].shape[1]))
+            elif rw.shape[1] != u["rp_w"].shape[1]:
                 raise ValueError("rp weight takes %d inputs, this frame size gives %d" % (rw.shape[1], u["rp_w"].shape[1]))
-            u["rp_w"][:] = rw.view(3, 3, 32, o3[0], o3[1]).permute(0, 1, 3, 4, 2).reshape(3, -1)
-            u["rp_b"][:3] = t(pick("rp", 0, "bias"))
+            else:
+                u["rp_w"][:] = rw.view(3, 3, 32, o3[0], o3[1]).permute(0, 1, 3, 4, 2).reshape(3, -1)
+                u["rp_b"][:3] = t(pick("rp", 0, "bias"))
         return flat.to(self.device)
 
     def to_reference(self, flat):
@@ -852,7 +864,7 @@ class GoalNavPolicy(torch.nn.Module):
 
     def load_reference_state_dict(self, sd):
         with torch.no_grad():
-            self.params.copy_(self.net.from_reference(sd))
+            self.params.copy_(self.net.from_reference(sd, init=self.params))
         return self
 
     def reference_state_dict(self):

@@ -329,13 +329,24 @@ def bench_train(args, scenes, dev, world, rank, recurrent, aux_weight=0.0, envs=
            "value": steps / el, "unit": "env-steps/s", "updates": updates, "envs_per_gpu": E,
            **({"cuda_graph": True} if cuda_graph else {}),
            "num_steps": T, "ms_per_update": el / updates * 1e3, "dtype": "f32",
-           "roofline": {"bound": "mfma", "achieved": tflops, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                        "frac": tflops / FP32_MFMA_PEAK_TFLOPS, "flops_per_env_step": flops,
+           # peak = the ceiling of the MFMA forms the kernels issue (x3 / x6 split-bf16 products of
+           # exact fp32 values, f32 MFMA elsewhere): frac = achieved / that ceiling, comparable with
+           # the measured matrix-pipe busy fraction (mfma_busy_measured.busy_frac). The ratio to the
+           # native fp32 MFMA peak (157.3 TF) is speed_vs_native_fp32_mfma: how much faster than an
+           # exact-fp32 MFMA implementation at full rate, not a utilisation
+           "roofline": {"bound": "mfma", "achieved": tflops, "peak": ceil, "unit": "TFLOP/s",
+                        "frac": tflops / ceil, "peak_kind": "issued split-bf16 / f32 MFMA ceiling of these kernels",
+                        "speed_vs_native_fp32_mfma": tflops / FP32_MFMA_PEAK_TFLOPS,
+                        "flops_per_env_step": flops,
                         "scope": "whole update (all kernels), executed FLOPs (fp32-equivalent): the reference's "
                                  "algorithm minus the goal frames' shared_base skipped by goal-run deduplication",
                         # the reference's algorithm (shared_base on every goal frame) at the same time
                         "algorithmic_flops_per_env_step": alg, "algorithmic_tflops": E * T * updates * alg / el / 1e12,
                         "goal_frames_computed": {"rollout_forward": gf, "update_backward": gb},
+                        **({"algorithmic_note": "algorithmic_tflops counts the reference's shared_base on every goal "
+                                                "frame; goal-run deduplication ran it on the fraction "
+                                                "goal_frames_computed, so it can exceed the 157.3 TF fp32 peak"}
+                           if E * T * updates * alg / el / 1e12 > FP32_MFMA_PEAK_TFLOPS else {}),
                         # the same FLOPs against the ceiling of the MFMA forms the kernels issue
                         # (x3 / x6 split-bf16, f32): frac_issued = achieved / that ceiling
                         "issued_ceiling_tflops": ceil, "frac_issued": tflops / ceil,
@@ -344,8 +355,11 @@ def bench_train(args, scenes, dev, world, rank, recurrent, aux_weight=0.0, envs=
                                                                    goal_fwd=gf, goal_bwd=gb, unreal=un)]}}
     if tr.unreal:
         res["unreal"] = {"sequences_per_update": tr.unreal_S, "pc_weight": tr.pc_weight, "rp_weight": tr.rp_weight,
-                         "vr_weight": tr.vr_weight, "source": "the first S envs' on-policy sequences (deep_rl samples "
-                                                             "replayed ones; parity unpinned)"}
+                         "vr_weight": tr.vr_weight,
+                         "source": ("the first S envs' sequences of a rollout drawn from the device replay ring "
+                                    "(deep_rl's replay buffer; capacity and sequence shape parity unpinned)")
+                         if tr.unreal_source == "replay" else
+                         "the first S envs' on-policy sequences (deep_rl samples replayed ones; parity unpinned)"}
     if world > 1:
         P = tr.net.n_params
         hw = tr.net.offsets["head"][0]
@@ -424,13 +438,17 @@ def run_leg(leg, args, scenes, dev, world, rank, updates=None, warmup=None, mark
         res["eager_value"] = eager["value"]
         res["eager_ms_per_update"] = eager["ms_per_update"]
         # the logged experiment's loss mix as thor-cached-auxiliary runs it: the aux deconv batch
-        # and the UNREAL sequences drawn from the replay ring (their own trunk / LSTM passes;
-        # a host draw per update, so eager)
-        mix = bench_train(args, sc, dev, world, rank, updates=100, warmup=3, recurrent=True,
+        # and the UNREAL sequences drawn from the replay ring (their own trunk / LSTM passes), the
+        # ring pushed and drawn on the device (vn_replay_push_draw), so the update is one hipGraph
+        mix = bench_train(args, sc, dev, world, rank, updates=400, warmup=3, recurrent=True,
                           aux_weight=AUX_WEIGHT_LOGGED, envs=4, model="replay sources", unreal=True,
-                          replay_sources=True)
-        res["replay_sources"] = {"aux_source": "replay", "unreal_source": "replay", "value": mix["value"],
-                                 "ms_per_update": mix["ms_per_update"]}
+                          replay_sources=True, cuda_graph=True)
+        mix_e = bench_train(args, sc, dev, world, rank, updates=100, warmup=3, recurrent=True,
+                            aux_weight=AUX_WEIGHT_LOGGED, envs=4, model="replay sources, eager", unreal=True,
+                            replay_sources=True)
+        res["replay_sources"] = {"aux_source": "replay", "unreal_source": "replay", "cuda_graph": True,
+                                 "value": mix["value"], "ms_per_update": mix["ms_per_update"],
+                                 "eager_value": mix_e["value"], "eager_ms_per_update": mix_e["ms_per_update"]}
     return res
 
 

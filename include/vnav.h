@@ -483,6 +483,36 @@ int vn_grad_norm(const float* grads, int64_t n, float scale, float max_norm, dou
                  float* scalars2, vn_stream_t stream);
 int vn_rmsprop_step(float* params, const float* grads, float* square_avg, int64_t n, float scale,
                     const float* scalars2, float lr, float alpha, float eps, vn_stream_t stream);
+/* vn_grad_norm with up to two gradient addends joined first: grads[i] += add_j[i] for i in
+ * [lo_j, hi_j) (add_j NULL = none), written back to grads, then the norm of scale*grads —
+ * the side passes' sums (a replayed aux batch's trunk gradient, the replayed UNREAL pass's
+ * trunk / heads / LSTM gradient) without a launch of their own; bitwise equal to the adds
+ * followed by vn_grad_norm. */
+int vn_grad_norm_join(float* grads, int64_t n, const float* add0, int64_t lo0, int64_t hi0, const float* add1,
+                      int64_t lo1, int64_t hi1, float scale, float max_norm, double* partial_512,
+                      float* scalars2, vn_stream_t stream);
+
+/* The replay ring on the device (deep_rl's replay buffer behind AuxiliaryTrainer's
+ * self.replay.sample_sequence(), experiments/ai2_auxiliary/trainer.py:27-31; deep_rl is
+ * absent, so capacity and sequence shape are parity unpinned). One call pushes a rollout's
+ * record into slot meta4[0] and draws this update's slot among the filled ones — no host
+ * value, so an update with replay sources is captured in a hipGraph (A2CTrainer(cuda_graph=True)).
+ * meta4 = int64 [next slot, filled slots, draw counter, last drawn slot]. Segment j copies
+ * rows x cols elements of elem_bytes (1 or 4) from src (row r at src + r*src_ld elements) to
+ * ring + slot*slot_elems (packed rows) and, when cur != NULL, the drawn slot's elements to cur
+ * (packed). The draw: k = uniform_below(Philox4x32-10(ctr_lo, ctr_hi, 0, STREAM_REPLAY = 4)
+ * under key seed, min(filled + 1, capacity)); then meta4 = [(slot + 1) % capacity,
+ * min(filled + 1, capacity), ctr + 1, k]. At most 16 segments. */
+typedef struct vn_replay_seg {
+  const void* src;
+  int64_t src_ld;
+  void* ring;
+  void* cur;
+  int64_t slot_elems;
+  int32_t rows, cols, elem_bytes, pad_;
+} vn_replay_seg;
+int vn_replay_push_draw(const vn_replay_seg* segs, int nseg, int64_t* meta4, int capacity, uint64_t seed,
+                        vn_stream_t stream);
 
 /* Device-side schedule, so that one update has no per-call host arguments and can be
  * captured once in a hipGraph and replayed (A2CTrainer(cuda_graph=True)):

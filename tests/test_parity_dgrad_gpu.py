@@ -311,3 +311,80 @@ def test_conv2_band_dgrad_matches_class_products(N):
             bad[k] = "%.3g" % e
     assert not bad, bad
     assert np.abs(fast["shared_base.0.0.weight"].numpy()).max() > 0
+
+
+@pytest.mark.parametrize("hw,N", [((84, 84), 300), ((174, 174), 130), ((174, 174), 7), ((300, 400), 37)])
+def test_conv1_resident_weights_matches_lds_fragments(hw, N):
+    """conv1's forward with the split weights resident in registers (`conv1_fwd_x3r_kernel`,
+    contiguous bf16 band rows, buffer-descriptor prefetch, med3 ReLU bits) against the
+    LDS-fragment kernel it replaces (`VN_CONV1F_LDSW`): the same products in the same three
+    chains and the same final sum, so X1 and the ReLU bitmask are bitwise equal (every frame,
+    every band, the short last band of 174x174 and 300x400 included)."""
+    from vnav.policy import GoalNavPolicy, frames_from_batch
+    torch.manual_seed(23)
+    pol = GoalNavPolicy(3, 4, hw)
+    net = pol.net
+    with torch.no_grad():
+        pol.params.add_(torch.randn_like(pol.params) * 0.01)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    img = torch.randint(0, 256, (N,) + hw + (3,), dtype=torch.uint8, device="cuda", generator=g)
+    gl = torch.randint(0, 256, (N,) + hw + (3,), dtype=torch.uint8, device="cuda", generator=g)
+    oh, ow = (hw[0] - 7) // 4 + 1, (hw[1] - 7) // 4 + 1
+    m1, x1 = 2 * oh * ow, 2 * oh * ow * 32
+
+    def run(ldsw):
+        if ldsw:
+            os.environ["VN_CONV1F_LDSW"] = "1"
+        try:
+            acts = net.new_acts(N)
+            acts.fill_(float("nan"))
+            out = torch.zeros((N, 8), device="cuda")
+            net.forward(pol.params.detach(), frames_from_batch(img, gl), N, acts, N, 0, out)
+            torch.cuda.synchronize()
+            return acts[:N * m1].view(torch.int32).clone(), acts[N * m1:N * (m1 + x1)].clone(), out[:, :5].clone()
+        finally:
+            os.environ.pop("VN_CONV1F_LDSW", None)
+
+    (mr, xr, orr), (ml, xl, ol) = run(False), run(True)
+    assert not torch.isnan(xr).any(), "unwritten X1"
+    assert float(xl.abs().max()) > 0 and int((ml != 0).sum()) > 0
+    assert torch.equal(mr, ml), int((mr != ml).sum())
+    assert torch.equal(xr, xl), float((xr - xl).abs().max())
+    assert torch.equal(orr, ol)
+
+
+@pytest.mark.parametrize("N", [3, 130, 1031])
+def test_conv2_ring_prefetch_matches_load_before_split(N):
+    """conv2's forward ring kernel at 174x174 with band k + 2 prefetched through band k + 1's
+    MFMAs (the default) against the form that loads each band just before its split
+    (`VN_CONV2F_RING2_NOPF`): the same sums in the same order, X2 bitwise, including items past
+    a workgroup's last band (the prefetch repeats the last item) and persistent-grid wraps."""
+    from vnav.policy import GoalNavPolicy, frames_from_batch
+    torch.manual_seed(29)
+    hw = (174, 174)
+    pol = GoalNavPolicy(3, 4, hw)
+    net = pol.net
+    with torch.no_grad():
+        pol.params.add_(torch.randn_like(pol.params) * 0.01)
+    g = torch.Generator(device="cuda").manual_seed(9)
+    img = torch.randint(0, 256, (N,) + hw + (3,), dtype=torch.uint8, device="cuda", generator=g)
+    gl = torch.randint(0, 256, (N,) + hw + (3,), dtype=torch.uint8, device="cuda", generator=g)
+    m1, x1, x2 = 2 * 42 * 42, 2 * 42 * 42 * 32, 2 * 20 * 20 * 32
+
+    def run(nopf):
+        if nopf:
+            os.environ["VN_CONV2F_RING2_NOPF"] = "1"
+        try:
+            acts = net.new_acts(N)
+            acts.fill_(float("nan"))
+            out = torch.zeros((N, 8), device="cuda")
+            net.forward(pol.params.detach(), frames_from_batch(img, gl), N, acts, N, 0, out)
+            torch.cuda.synchronize()
+            return acts[N * (m1 + x1):N * (m1 + x1 + x2)].clone(), out[:, :5].clone()
+        finally:
+            os.environ.pop("VN_CONV2F_RING2_NOPF", None)
+
+    (xp, op), (xn, on) = run(False), run(True)
+    assert not torch.isnan(xp).any() and float(xp.abs().max()) > 0
+    assert torch.equal(xp, xn), float((xp - xn).abs().max())
+    assert torch.equal(op, on)
