@@ -380,19 +380,22 @@ __global__ __launch_bounds__(256, 2) void conv1_fwd_x3r_kernel(FrameSrc src, int
       __builtin_amdgcn_sched_barrier(0);
     }
   };
-  if ((int)blockIdx.x < n_items) load_item(blockIdx.x);
-  for (int it = blockIdx.x; it < n_items; it += gridDim.x) {
-    const int f = fl_frame(fl, it / NB), band = it - (it / NB) * NB;
-    const int oy0 = BR * band, nr = min(BR, OH - oy0), npb = nr * OW;
+  auto stage = [&]() {
 #pragma unroll
     for (int j = 0; j < NPF; ++j) {  // u8 -> bf16 rows (dwords past a short band are zeros)
       const int i = tid + j * 256;
       if (j + 1 < NPF || i < ND) *reinterpret_cast<uint2*>(img + 4 * i) = u8x4_bf16(pre[j]);
     }
+  };
+  if ((int)blockIdx.x < n_items) load_item(blockIdx.x);
+  for (int it = blockIdx.x; it < n_items; it += gridDim.x) {
+    const int f = fl_frame(fl, it / NB), band = it - (it / NB) * NB;
+    const int oy0 = BR * band, nr = min(BR, OH - oy0), npb = nr * OW;
+    stage();
     __syncthreads();
     load_item(min(it + (int)gridDim.x, n_items - 1));
     const int tiles = (npb + 31) / 32;
-    for (int t = wave; t < tiles; t += 4) {
+    auto tile = [&](int t) {
       const int px = min(t * 32 + c32, npb - 1);
       const int oy = px / OW, ox = px - (px / OW) * OW;
       const uint16_t* base = img + (oy * 4) * RS + ox * 12;
@@ -441,7 +444,8 @@ __global__ __launch_bounds__(256, 2) void conv1_fwd_x3r_kernel(FrameSrc src, int
         for (int j = 0; j < 4; ++j) *reinterpret_cast<f4*>(Y + pix * 32 + 8 * j + 4 * h) = y[j];
         if (h == 0) mask[pix] = bits;
       }
-    }
+    };
+    for (int t = wave; t < tiles; t += 4) tile(t);
     __syncthreads();
   }
 }
@@ -587,7 +591,20 @@ constexpr bool conv1_wgrad_x3_fits() {
   return (H == 84 && W == 84) || (H == 174 && W == 174) || (H == 300 && W == 400);
 }
 
-template <int H, int W, int OH, int OW>
+// dst = the lanes of mask m ? v : 0 (v_cndmask on an SGPR-pair lane mask: one VALU, no compare)
+__device__ __forceinline__ float select_lanes(float v, uint64_t m) {
+  float r;
+  asm("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(r) : "v"(v), "s"(m));
+  return r;
+}
+
+// LEAN (round 6; tools/isa_budget.py put the 174x174 step at ~103 VALU for 15 MFMAs): the dZ
+// validity of a step depends only on the lane's half (g = 2s + h), so it is two scalar pixel
+// counts and one v_cndmask per value on an SGPR lane mask (was a compare + cndmask per value);
+// the B fragments of pad slots are left as read (finite staged bytes; their accumulator slots
+// are never read: kConv1WgradCol -1) and the bias lane reads 8 bf16 ones kept in LDS past the
+// fold area instead of masking every tile-2 fragment (12 VALU per step). dW / db bitwise equal.
+template <int H, int W, int OH, int OW, bool LEAN = false>
 __global__ __launch_bounds__(256) void conv1_wgrad_x3_kernel(FrameSrc src, int n_frames, FrameList fl,
                                                              const float* __restrict__ dZ, float* __restrict__ slab) {
   using Bd = Conv1WgBand<H, W>;
@@ -608,9 +625,11 @@ __global__ __launch_bounds__(256) void conv1_wgrad_x3_kernel(FrameSrc src, int n
   uint16_t* Q = reinterpret_cast<uint16_t*>(smem_wg);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, c32 = lane & 31;
+  const uint16_t* ones = reinterpret_cast<const uint16_t*>(smem_wg + Bd::LDS);  // LEAN: 8 bf16 ones
   {  // never-written Q entries (x >> 2 >= 2 * PAIRS, row tails) are read by padding pixels: zero
     uint4* q4 = reinterpret_cast<uint4*>(Q);
     for (int i = tid; i < BRI * RSQ / 8; i += 256) q4[i] = uint4{0u, 0u, 0u, 0u};
+    if (LEAN && tid == 0) *reinterpret_cast<uint4*>(smem_wg + Bd::LDS) = uint4{0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u};
     __syncthreads();  // before any wave stages the first item over the zeroed rows
   }
   int loff[5];
@@ -623,6 +642,8 @@ __global__ __launch_bounds__(256) void conv1_wgrad_x3_kernel(FrameSrc src, int n
   const uint32_t keep2 = col2 >= 0 && col2 < 147 ? 0xffffffffu : 0u;
   const uint32_t add2 = col2 == 148 ? 0x3f803f80u : 0u;
   const uint32_t keep4 = kConv1WgradCol[QL::ID][4][c32] >= 0 ? 0xffffffffu : 0u;
+  const bool bias_lane = col2 == 148;
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
   f16v acc[5];
 #pragma unroll
   for (int nt = 0; nt < 5; ++nt)
@@ -638,7 +659,8 @@ __global__ __launch_bounds__(256) void conv1_wgrad_x3_kernel(FrameSrc src, int n
   constexpr int KW0 = (KS_MAX + 3) / 4;
   // dZ register sets: step i + D is loaded while steps i + 1 .. i + D - 1 wait; three where KW
   // allows it without an extra masked step (174x174: 6), else two (84x84: 8)
-  constexpr int D = KW0 % 3 == 0 ? 3 : 2;
+  // LEAN at 174x174 (130 VGPRs + 80 AGPRs): every step of the next item in flight (D = KW = 6)
+  constexpr int D = (LEAN && H == 174) ? KW0 : KW0 % 3 == 0 ? 3 : 2;
   constexpr int KW = (KW0 + D - 1) / D * D;
   static_assert(NT <= KW, "staging tasks are issued one per step");
   // staging task (band row y, pair m): pixels 8m .. 8m+7 of the row = 24 frame bytes (fewer
@@ -734,9 +756,20 @@ __global__ __launch_bounds__(256) void conv1_wgrad_x3_kernel(FrameSrc src, int n
       const int s = wave + 4 * i;
       float(&z)[8] = zb[i % D];
       union { uint16_t u[8]; bf16x8 v; } a0, a1, a2;
-      const int nvz = z_valid(ng, s);
+      if constexpr (LEAN) {
+        const int su = wv + 4 * i;  // the wave's step (scalar); half h takes group 2 su + h
+        auto nvs = [&](int g) { return g < ng ? min(8, OW - 8 * (g - (g / GPR) * GPR)) : 0; };
+        const int nv0 = nvs(2 * su), nv1 = nvs(2 * su + 1);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) split3_bf16(j < nvz ? z[j] : 0.0f, a0.u[j], a1.u[j], a2.u[j]);
+        for (int j = 0; j < 8; ++j) {
+          const uint64_t m = (j < nv0 ? 0xffffffffull : 0ull) | (j < nv1 ? 0xffffffff00000000ull : 0ull);
+          split3_bf16(select_lanes(z[j], m), a0.u[j], a1.u[j], a2.u[j]);
+        }
+      } else {
+        const int nvz = z_valid(ng, s);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) split3_bf16(j < nvz ? z[j] : 0.0f, a0.u[j], a1.u[j], a2.u[j]);
+      }
       if constexpr (i < NT) load_task(i, inext, fn);
       if constexpr (i + D < KW)
         load_z(z, f, oy0, ng, s + 4 * D);
@@ -748,7 +781,8 @@ __global__ __launch_bounds__(256) void conv1_wgrad_x3_kernel(FrameSrc src, int n
       union { bf16x8 v; uint4 q; uint32_t d[4]; } b[5];
       uint32_t e[2];
 #pragma unroll
-      for (int nt = 0; nt < 5; ++nt) b[nt].q = *reinterpret_cast<const uint4*>(gb + loff[nt]);
+      for (int nt = 0; nt < 5; ++nt)
+        b[nt].q = *reinterpret_cast<const uint4*>(LEAN && nt == 2 && bias_lane ? ones : gb + loff[nt]);
 #pragma unroll
       for (int nt = 3; nt < 5; ++nt) e[nt - 3] = gb[loff[nt] + 8];
 #pragma unroll
@@ -759,10 +793,12 @@ __global__ __launch_bounds__(256) void conv1_wgrad_x3_kernel(FrameSrc src, int n
         b[nt].d[2] = __builtin_amdgcn_alignbit(d3, d2, 16);
         b[nt].d[3] = __builtin_amdgcn_alignbit(e[nt - 3], d3, 16);
       }
+      if constexpr (!LEAN) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        b[2].d[q] = (b[2].d[q] & keep2) | add2;
-        b[4].d[q] &= keep4;
+        for (int q = 0; q < 4; ++q) {
+          b[2].d[q] = (b[2].d[q] & keep2) | add2;
+          b[4].d[q] &= keep4;
+        }
       }
 #pragma unroll
       for (int nt = 0; nt < 5; ++nt) acc[nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0.v, b[nt].v, acc[nt], 0, 0, 0);
@@ -1119,11 +1155,20 @@ __device__ __forceinline__ void split3_pack(const f4& v, uint2& t0, uint2& t1, u
 // stores under 4 bits of the conv1 ReLU bitmask: 4x fewer store instructions than the
 // pixel-row layout's dword stores, which left the kernel store-issue bound; staging the
 // result in LDS instead cost a resident workgroup and measured slower).
-template <int IH, int IW, int OH, int OW, int NW>
+//
+// ROT (round 6): at 174x174 one 8-wave workgroup fills a CU, and its item loop began with
+// s_waitcnt vmcnt(0) — the staging of frame i + 1 waited for frame i's 226 KB of dX1 stores to
+// be acknowledged, with no other workgroup to fill the CU meanwhile (the compiler's one wait
+// for the first iteration, which has no store in flight, and the later ones). ROT rotates the
+// loop (load next, tiles, barrier, stage next, barrier) with a fixed tile-pair count per wave
+// and unconditional stores — lanes past the class map store to `sink` — so the staging waits
+// for its own loads only (vmcnt(stores + later loads)). Same products, same order: bitwise.
+template <int IH, int IW, int OH, int OW, int NW, bool ROT = false>
 __global__ __launch_bounds__(NW * 64, 2) void conv2_dgrad_x6_kernel(const float* __restrict__ dZ2,
                                                                 const float* __restrict__ WT,
                                                                 const uint32_t* __restrict__ mask,
-                                                                float* __restrict__ dX1, int n_frames, FrameList fl) {
+                                                                float* __restrict__ dX1, int n_frames, FrameList fl,
+                                                                float* __restrict__ sink) {
   constexpr int NP = OH * OW;
   constexpr int HYC = IH / 2, WXC = IW / 2, NPC = HYC * WXC;
   constexpr int TILES = (NPC + 15) / 16;
@@ -1177,10 +1222,7 @@ __global__ __launch_bounds__(NW * 64, 2) void conv2_dgrad_x6_kernel(const float*
 #pragma unroll
     for (int j = 0; j < NM; ++j) mr[j] = mask[(int64_t)f * IH * IW + min(tid + j * NT, IH * IW - 1)];
   };
-  n_frames = fl_count(fl, n_frames);
-  if ((int)blockIdx.x < n_frames) load_z(blockIdx.x);
-  for (int fi = blockIdx.x; fi < n_frames; fi += gridDim.x) {
-    const int f = fl_frame(fl, fi);
+  auto stage = [&]() {
 #pragma unroll
     for (int j = 0; j < NZ; ++j) {
       const int i = slot_pc(tid + j * NT);
@@ -1199,10 +1241,23 @@ __global__ __launch_bounds__(NW * 64, 2) void conv2_dgrad_x6_kernel(const float*
       const int i = tid + j * NT;
       if (i < IH * IW) ms[i] = mr[j];
     }
-    __syncthreads();
+  };
+  n_frames = fl_count(fl, n_frames);
+  if ((int)blockIdx.x < n_frames) {
+    load_z(blockIdx.x);
+    if constexpr (ROT) stage();
+  }
+  if constexpr (ROT) __syncthreads();
+  // tile pairs per wave: t0 = 2 (wave >> 2) + 2 (NW / 4) k (84x84: 4, 174x174: 7)
+  constexpr int NIT = (TILES + 2 * (NW / 4) - 1) / (2 * (NW / 4));
+  for (int fi = blockIdx.x; fi < n_frames; fi += gridDim.x) {
+    const int f = fl_frame(fl, fi);
+    if constexpr (!ROT) {
+      stage();
+      __syncthreads();
+    }
     load_z(min(fi + (int)gridDim.x, n_frames - 1));
-#pragma unroll 1
-    for (int t0 = 2 * (wave >> 2); t0 < TILES; t0 += 2 * (NW / 4)) {
+    auto tile_pair = [&](int t0) {
       int off[2][4];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
@@ -1242,7 +1297,20 @@ __global__ __launch_bounds__(NW * 64, 2) void conv2_dgrad_x6_kernel(const float*
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int pr = (t0 + u) * 16 + i16;
-        if (pr < NPC) {
+        if (ROT) {  // unconditional: a lane past the class map stores to the sink
+          const int pv = min(pr, NPC - 1);
+          const int y = (pv / WXC) * 2 + py, x = (pv % WXC) * 2 + px;
+          const int64_t pix = ((int64_t)f * IH + y) * IW + x;
+          const uint32_t mw = ms[y * IW + x];
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) {
+            const uint32_t m4 = mw >> (nt * 16 + 4 * q);
+            f4 v = acc[u][nt];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = (m4 >> r) & 1u ? v[r] : 0.0f;
+            *reinterpret_cast<f4*>(pr < NPC ? dX1 + pix * 32 + nt * 16 + 4 * q : sink) = v;
+          }
+        } else if (pr < NPC) {
           const int y = (pr / WXC) * 2 + py, x = (pr % WXC) * 2 + px;
           const int64_t pix = ((int64_t)f * IH + y) * IW + x;
           const uint32_t mw = ms[y * IW + x];
@@ -1256,6 +1324,15 @@ __global__ __launch_bounds__(NW * 64, 2) void conv2_dgrad_x6_kernel(const float*
           }
         }
       }
+    };
+    if constexpr (ROT) {
+#pragma unroll 1
+      for (int k = 0; k < NIT; ++k) tile_pair(2 * (wave >> 2) + 2 * (NW / 4) * k);
+      __syncthreads();  // every wave done with this frame's planes and ReLU words
+      stage();          // the next frame's (past the last one: the last one again)
+    } else {
+#pragma unroll 1
+      for (int t0 = 2 * (wave >> 2); t0 < TILES; t0 += 2 * (NW / 4)) tile_pair(t0);
     }
     __syncthreads();
   }

@@ -2170,12 +2170,21 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
       if constexpr (conv2_dgrad_x6_fits<G::OH1, G::OW1, G::OH2, G::OW2>()) {
         if (bits) {
           constexpr int NW = conv2_dgrad_x6_waves<G::OH1, G::OW1, G::OH2, G::OW2>();
-          const void* kfn = (const void*)conv2_dgrad_x6_kernel<G::OH1, G::OW1, G::OH2, G::OW2, NW>;
+          // the rotated item loop (ROT) by default; VN_CONV2DG_NOROT keeps the original (A/B,
+          // bitwise equal). Lanes past the class map store to a 16-B sink in the slab (free
+          // here: conv2's weight gradient has been reduced, conv1's starts after this kernel)
+          const bool rot = getenv("VN_CONV2DG_NOROT") == nullptr;
+          const void* kfn = rot ? (const void*)conv2_dgrad_x6_kernel<G::OH1, G::OW1, G::OH2, G::OW2, NW, true>
+                                : (const void*)conv2_dgrad_x6_kernel<G::OH1, G::OW1, G::OH2, G::OW2, NW, false>;
           constexpr size_t lds = conv2_dgrad_x6_lds<G::OH1, G::OW1, G::OH2, G::OW2>();
           VN_HIP(ensure_dyn_lds(kfn, lds));  // > 64 KiB dynamic LDS: opt-in
           const int blocks = std::min(frames, resident_blocks(kfn, NW * 64, lds));
-          hipLaunchKernelGGL((conv2_dgrad_x6_kernel<G::OH1, G::OW1, G::OH2, G::OW2, NW>), dim3(blocks), dim3(NW * 64), lds,
-                             st, w.dz2, T(1), a.M1, a.X[0], frames, fl);
+          if (rot)
+            hipLaunchKernelGGL((conv2_dgrad_x6_kernel<G::OH1, G::OW1, G::OH2, G::OW2, NW, true>), dim3(blocks),
+                               dim3(NW * 64), lds, st, w.dz2, T(1), a.M1, a.X[0], frames, fl, w.slab);
+          else
+            hipLaunchKernelGGL((conv2_dgrad_x6_kernel<G::OH1, G::OW1, G::OH2, G::OW2, NW, false>), dim3(blocks),
+                               dim3(NW * 64), lds, st, w.dz2, T(1), a.M1, a.X[0], frames, fl, w.slab);
           done = true;
         }
       }
@@ -2216,10 +2225,20 @@ int backward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, in
     if (!f32in) {
       const int frames = 2 * n;
       using Bd = Conv1WgBand<H0, W0>;
-      const void* kfn = (const void*)conv1_wgrad_x3_kernel<H0, W0, G::OH1, G::OW1>;
-      const int blocks = std::min(frames * Bd::NB, resident_blocks(kfn, 256, Bd::LDS));
-      hipLaunchKernelGGL((conv1_wgrad_x3_kernel<H0, W0, G::OH1, G::OW1>), dim3(blocks), dim3(256), Bd::LDS, st, src,
-                         frames, fl, a.X[0], w.slab);
+      // LEAN (scalar lane masks, no per-step B masking; bitwise equal) where it keeps its SGPRs:
+      // 174x174 and 300x400 (the 84x84 instance spills 34 SGPRs); VN_CONV1WG_NOLEAN for A/B
+      constexpr bool kLean = !(H0 == 84 && W0 == 84);
+      const bool lean = kLean && getenv("VN_CONV1WG_NOLEAN") == nullptr;
+      const void* kfn = lean ? (const void*)conv1_wgrad_x3_kernel<H0, W0, G::OH1, G::OW1, kLean>
+                             : (const void*)conv1_wgrad_x3_kernel<H0, W0, G::OH1, G::OW1, false>;
+      const size_t lds = Bd::LDS + (lean ? 16 : 0);  // + the bias lane's 8 bf16 ones
+      const int blocks = std::min(frames * Bd::NB, resident_blocks(kfn, 256, lds));
+      if (lean)
+        hipLaunchKernelGGL((conv1_wgrad_x3_kernel<H0, W0, G::OH1, G::OW1, kLean>), dim3(blocks), dim3(256), lds, st,
+                           src, frames, fl, a.X[0], w.slab);
+      else
+        hipLaunchKernelGGL((conv1_wgrad_x3_kernel<H0, W0, G::OH1, G::OW1, false>), dim3(blocks), dim3(256), lds, st,
+                           src, frames, fl, a.X[0], w.slab);
       constexpr int kParts = 32;
       float* part = w.slab + (int64_t)blocks * 32 * 160;
       hipLaunchKernelGGL(slab_partial_kernel, dim3((32 * 160 + 255) / 256, kParts), dim3(256), 0, st, w.slab, blocks,

@@ -388,3 +388,73 @@ def test_conv2_ring_prefetch_matches_load_before_split(N):
     assert not torch.isnan(xp).any() and float(xp.abs().max()) > 0
     assert torch.equal(xp, xn), float((xp - xn).abs().max())
     assert torch.equal(op, on)
+
+
+@pytest.mark.parametrize("hw,N", [((174, 174), 61), ((300, 400), 9)])
+def test_conv1_wgrad_lean_matches_masked_form(hw, N):
+    """conv1's weight gradient with scalar lane masks for the dZ validity and no per-step
+    B-fragment masking (`conv1_wgrad_x3_kernel<..., LEAN = true>`: pad slots left as read, the
+    bias lane reading 8 bf16 ones) against the masked form (`VN_CONV1WG_NOLEAN`): the same
+    products into the kept slots in the same order, so every parameter gradient is bitwise equal."""
+    from vnav.policy import GoalNavPolicy
+    torch.manual_seed(31)
+    pol = GoalNavPolicy(3, 4, hw)
+    with torch.no_grad():
+        pol.params.add_(torch.randn_like(pol.params) * 0.01)
+    g = torch.Generator(device="cuda").manual_seed(11)
+    img = torch.randint(0, 256, (N, 1) + hw + (3,), dtype=torch.uint8, device="cuda", generator=g)
+    gl = torch.randint(0, 256, (N, 1) + hw + (3,), dtype=torch.uint8, device="cuda", generator=g)
+    cl = torch.randn((N, 1, 4), device="cuda", generator=g)
+    cv = torch.randn((N, 1, 1), device="cuda", generator=g)
+
+    def run(nolean):
+        if nolean:
+            os.environ["VN_CONV1WG_NOLEAN"] = "1"
+        try:
+            pol.params.grad = None
+            logits, value, _ = pol(((img, gl), None), None, None)
+            ((logits * cl).sum() + (value * cv).sum()).backward()
+            torch.cuda.synchronize()
+            return pol.params.grad.clone()
+        finally:
+            os.environ.pop("VN_CONV1WG_NOLEAN", None)
+
+    gl_, gm = run(False), run(True)
+    w, b = pol.net.offsets["conv1"]
+    assert float(gm[w:w + 32 * 148].abs().max()) > 0 and float(gm[b:b + 32].abs().max()) > 0
+    assert torch.equal(gl_, gm), float((gl_ - gm).abs().max())
+
+
+@pytest.mark.parametrize("hw,N", [((84, 84), 37), ((174, 174), 77)])
+def test_conv2_dgrad_rotated_matches_original(hw, N):
+    """conv2's input gradient with the rotated item loop (stage the next frame after this frame's
+    tiles; fixed tile-pair count, lanes past the class map storing to the slab's sink) against
+    the original loop (`VN_CONV2DG_NOROT`): the same products and order, every parameter
+    gradient bitwise equal (conv1's weight gradient reads the dX1 it writes)."""
+    from vnav.policy import GoalNavPolicy
+    torch.manual_seed(37)
+    pol = GoalNavPolicy(3, 4, hw)
+    with torch.no_grad():
+        pol.params.add_(torch.randn_like(pol.params) * 0.01)
+    g = torch.Generator(device="cuda").manual_seed(13)
+    img = torch.randint(0, 256, (N, 1) + hw + (3,), dtype=torch.uint8, device="cuda", generator=g)
+    gl = torch.randint(0, 256, (N, 1) + hw + (3,), dtype=torch.uint8, device="cuda", generator=g)
+    cl = torch.randn((N, 1, 4), device="cuda", generator=g)
+    cv = torch.randn((N, 1, 1), device="cuda", generator=g)
+
+    def run(norot):
+        if norot:
+            os.environ["VN_CONV2DG_NOROT"] = "1"
+        try:
+            pol.params.grad = None
+            logits, value, _ = pol(((img, gl), None), None, None)
+            ((logits * cl).sum() + (value * cv).sum()).backward()
+            torch.cuda.synchronize()
+            return pol.params.grad.clone()
+        finally:
+            os.environ.pop("VN_CONV2DG_NOROT", None)
+
+    gr, go = run(False), run(True)
+    w, _ = pol.net.offsets["conv1"]
+    assert float(go[w:w + 32 * 148].abs().max()) > 0
+    assert torch.equal(gr, go), float((gr - go).abs().max())

@@ -56,7 +56,7 @@ int main(int argc, char** argv) {
       if (which[0] == 'w')
         hipLaunchKernelGGL((conv1_wgrad_x3_kernel<84, 84, 20, 20>), dim3(grid), dim3(256), (Conv1WgBand<84, 84>::LDS), 0, src, frames, FrameList{}, dz, slab);
       else if (which[0] == 'd')
-        hipLaunchKernelGGL((conv2_dgrad_x6_kernel<20, 20, 9, 9, 4>), dim3(grid), dim3(256), dlds, 0, dz2, wt, msk, dx1, frames, FrameList{});
+        hipLaunchKernelGGL((conv2_dgrad_x6_kernel<20, 20, 9, 9, 4>), dim3(grid), dim3(256), dlds, 0, dz2, wt, msk, dx1, frames, FrameList{}, slab);
       else
         hipLaunchKernelGGL((conv2_dgrad_kernel<20, 20, 9, 9, true>), dim3(grid), dim3(256), 0, 0, dz2, wt, dx1, msk, dx1, frames);
     };
