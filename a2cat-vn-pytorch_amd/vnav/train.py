@@ -390,6 +390,10 @@ class ThorCachedAuxiliary(Experiment):
     # UnrealTrainer draws the pixel-control / value-replay / reward-prediction sequences from
     # its replay buffer too: the first 16 envs of the stored rollout drawn for the aux batch
     unreal_source = "replay"
+    # the replay ring is pushed and drawn on the device (vn_replay_push_draw), so the update of
+    # this 4-env batch is one captured hipGraph (bit-identical to eager, tests/test_replay_gpu.py;
+    # single process only unless capture_collectives)
+    cuda_graph = True
 
     def create_env(self, kwargs):
         goal = tuple(kwargs.get("goal", (10, 14, 0)))

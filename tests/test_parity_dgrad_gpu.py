@@ -458,3 +458,4 @@ def test_conv2_dgrad_rotated_matches_original(hw, N):
     w, _ = pol.net.offsets["conv1"]
     assert float(go[w:w + 32 * 148].abs().max()) > 0
     assert torch.equal(gr, go), float((gr - go).abs().max())
+

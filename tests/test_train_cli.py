@@ -24,6 +24,8 @@ def test_registry_and_hyperparameters():
     assert (cls.value_coefficient, cls.entropy_coefficient) == (0.5, 0.001)
     assert (cls.auxiliary_weight, cls.hardness, cls.recurrent) == (0.1, 0.01, True)
     assert (cls.unreal, cls.rp_weight, cls.pc_weight, cls.vr_weight) == (True, 1.0, 0.05, 1.0)  # :39-41
+    # replayed aux / UNREAL batches with the ring on the device: the update is a captured hipGraph
+    assert (cls.aux_source, cls.unreal_source, cls.cuda_graph) == ("replay", "replay", True)
     with pytest.raises(KeyError):
         train.make_trainer("no-such-experiment")
     with pytest.raises(TypeError):
