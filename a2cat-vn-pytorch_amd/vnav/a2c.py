@@ -205,6 +205,13 @@ class A2CTrainer:
         # compute_auxiliary_loss overridden by a subclass: called every update (autograd on a
         # GoalNavPolicy view of the flat parameters), its gradient added before the all-reduce
         self._setup_unreal(unreal, pc_weight, rp_weight, vr_weight, pc_gamma, unreal_envs)
+        # both batches replayed and the UNREAL record holds every env (S == E, the logged run's 4
+        # envs): the replayed UNREAL pass's trunk forward covers the aux batch's samples (rows
+        # t*S + e = t*E + e), so the aux heads run on it inside the side pass and their dX4 joins
+        # the UNREAL pass's trunk backward — one trunk forward + backward of the replayed
+        # rollout instead of two (VN_REPLAY_SEPARATE=1 keeps the two passes)
+        self._merged_replay = (self.aux_source == "replay" and self.unreal_source == "replay"
+                               and self.unreal_S == E and not os.environ.get("VN_REPLAY_SEPARATE"))
         if self.replay:
             self._replay_segs = self._replay_segments()
         self._custom_aux = type(self).compute_auxiliary_loss is not A2CTrainer.compute_auxiliary_loss
@@ -518,6 +525,12 @@ class A2CTrainer:
         rows = u["rows"]
         frames = self._frames(rows[0], rows[1])
         net.forward(self.params, frames, n, self.ur_acts, n, 0, None)
+        if self._merged_replay:  # the aux heads on the replayed rows t*E + e < T*E (aux_rows' frames)
+            N = T * S
+            self.aux_stats.zero_()
+            net.aux_forward_loss_grad(self.params, self.ur_acts, n, N, self.a1, self.pred, self._aux_targets_replay,
+                                      self.aux_weight, self.dpred, self.aux_stats, self.aux_ws)
+            net.aux_backward(self.params, self.ur_acts, n, N, self.a1, self.dpred, self.grads, self.ur_dx4, self.aux_ws)
         x5 = net.x5(self.ur_acts, n)
         h_r, c_r = self.ur_hc[0], self.ur_hc[1]
         h0, c0 = u["hc0"][0], u["hc0"][1]
@@ -555,7 +568,8 @@ class A2CTrainer:
         _lib.check(lib.vn_unreal_rp_loss_grad(P(self.rp_out), P(rew), P(don), T, S, S, ctypes.c_float(self.rp_weight),
                                               P(self.rp_dout), P(self.unreal_stats[1:3]), st), "vn_unreal_rp_loss_grad")
         net.rp_backward(self.params, self.rp_x, n_rp, self.rp_dout, self.grads, self.rp_dx, self.pc_ws)
-        _lib.check(lib.vn_unreal_rp_scatter(P(self.rp_dx), T, S, S, F, P(self.ur_dx4), 0, st), "vn_unreal_rp_scatter")
+        _lib.check(lib.vn_unreal_rp_scatter(P(self.rp_dx), T, S, S, F, P(self.ur_dx4), 1 if self._merged_replay else 0,
+                                            st), "vn_unreal_rp_scatter")
         # BPTT over the T + 1 replayed steps (value replay's dout + pixel control's dh), the trunk
         net.lstm_backward(self.params, T + 1, S, self.ur_dout, h_r, self.ur_xcat, self.ur_lacts, c_r, c0,
                           u["masks"], x5, self.ur_dz5, self.ur_grads, self.ur_lstm_ws, dh_extra=self.dh_pc,
@@ -567,8 +581,12 @@ class A2CTrainer:
 
     def _side_grad_range(self):
         """[lo, hi) of the flat gradient the replayed UNREAL pass writes on the side stream: the
-        pixel-control and reward-prediction blocks (include/vnav.h VN_POLICY_UNREAL layout)."""
-        return min(self.net.unreal_layout.values()), self.net.n_params
+        pixel-control and reward-prediction blocks (include/vnav.h VN_POLICY_UNREAL layout),
+        from the aux heads' block on when those run in the same pass (_merged_replay)."""
+        lo = min(self.net.unreal_layout.values())
+        if self._merged_replay:
+            lo = min(lo, self.net.aux_layout["w1"])
+        return lo, self.net.n_params
 
     def _side_owned(self):
         """(name, tensor) the side stream writes between the fork and the join."""
@@ -578,15 +596,18 @@ class A2CTrainer:
                                                "ur_lstm_ws", "h_pc", "pcb", "pc_a1", "pc_p2", "dh_pc", "pc_ws",
                                                "rp_x", "rp_dx", "rp_out", "rp_dout", "unreal_stats")]
         out += [("ur_cur." + k, v) for k, v in self.ur_cur.items()]
+        if self._merged_replay:
+            out += [(k, getattr(self, k)) for k in ("a1", "pred", "dpred", "aux_ws", "aux_stats")]
         return out + [("grads[pc/rp]", self.grads[lo:hi])]
 
     def _main_owned(self):
         """(name, tensor) the main stream writes while the side stream runs."""
         lo, _ = self._side_grad_range()
         names = ("acts", "workspace", "dout", "returns", "stats", "out", "dz5", "dx4", "lstm_ws", "xcat", "lstm_acts",
-                 "a1", "pred", "dpred", "aux_ws", "aux_stats", "aux_acts", "aux_out", "aux_dz5", "aux_grads",
-                 "unreal_dx4", "norm_partial", "scalars", "_hc0", "h_all", "c_all", "goal_list", "goal_run_length",
-                 "goal_count")
+                 "aux_acts", "aux_out", "aux_dz5", "aux_grads", "unreal_dx4", "norm_partial", "scalars", "_hc0", "h_all",
+                 "c_all", "goal_list", "goal_run_length", "goal_count")
+        if not self._merged_replay:
+            names += ("a1", "pred", "dpred", "aux_ws", "aux_stats")
         out = [(k, getattr(self, k)) for k in names if isinstance(getattr(self, k, None), torch.Tensor)]
         return out + [("grads[trunk/heads/lstm/aux]", self.grads[:lo])]
 
@@ -601,7 +622,7 @@ class A2CTrainer:
         main_end = max(b + net.shapes[k][0] for k, (_, b) in net.offsets.items() if net.shapes[k][0])
         if net.lstm:
             main_end = max(main_end, net.lstm["bhh"] + 2048)
-        if net.aux_layout:
+        if net.aux_layout and not self._merged_replay:
             main_end = max(main_end, net.aux_layout["b2"] + 8)
         if main_end > lo or self._ur_add_end > lo:
             raise RuntimeError("side-stream gradient block [%d, %d) overlaps the main stream's blocks (end %d) or the "
@@ -766,7 +787,9 @@ class A2CTrainer:
                                         _lib.ptr(self.stats), st), "vn_a2c_loss_grad")
         dx4 = None
         unreal_dh = None
-        if self.aux_weight > 0 and aux_batch is not None:
+        if self._merged_replay:
+            pass  # the aux heads run inside the replayed UNREAL pass (side stream)
+        elif self.aux_weight > 0 and aux_batch is not None:
             # replayed sequence: its own trunk forward, the heads' loss and backward, and the
             # trunk backward of dL/dX4 alone into aux_grads (added after the main backward)
             self.aux_stats.zero_()
@@ -811,7 +834,7 @@ class A2CTrainer:
         # the side passes' gradient sums: in the norm's first pass (vn_grad_norm_join) on one
         # rank with no override; before the all-reduce / the override's autograd otherwise
         joins = []
-        if aux_batch is not None:
+        if aux_batch is not None and not self._merged_replay:
             w, _ = self.net.offsets["conv1"]
             _, b = self.net.offsets["fc"]
             joins.append((self.aux_grads, w, b + self.net.shapes["fc"][0]))

@@ -616,7 +616,11 @@ class _GoalNavFunction(torch.autograd.Function):
         n = image.shape[0]
         d = torch.zeros((n, OUT_LD), dtype=torch.float32, device=params.device)
         d[:, : net.num_actions + 1] = dout
-        grads = torch.empty_like(params)
+        # zeros: the backward writes the trunk and head blocks only; an aux / UNREAL policy's
+        # other blocks take no gradient from this output (uninitialised memory there was
+        # returned as their gradient until round 6: tools/nan_stress.py found ~1/256 of them
+        # non-finite)
+        grads = torch.zeros_like(params)
         ws = torch.empty(net.workspace_floats(n), dtype=torch.float32, device=params.device)
         net.backward(params, frames_from_batch(image, goal), n, acts, n, d, grads, ws)
         return grads, None, None, None

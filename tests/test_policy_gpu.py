@@ -396,3 +396,35 @@ def test_policy_refuses_mismatched_frames_and_moves_host_frames():
         from vnav.policy import _GoalNavFunction
         x = torch.zeros((4, 84, 84, 3), dtype=torch.uint8, device="cuda")[::2]
         _GoalNavFunction.apply(pol.params, x, x, net)
+
+
+def test_feedforward_gradient_of_heads_without_output_is_zero():
+    """The feed-forward policy's backward writes the trunk and head blocks; an aux policy's deconv
+    heads take no gradient from the policy output and their block must come back exactly zero
+    (it was uninitialised memory until round 6: non-finite in ~1/256 of the entries,
+    tools/nan_stress.py), and repeated backward passes are bitwise equal."""
+    from vnav.policy import GoalNavPolicy
+    torch.manual_seed(43)
+    hw = (174, 174)
+    pol = GoalNavPolicy(3, 4, hw, recurrent=False, aux=True)
+    with torch.no_grad():
+        pol.params.add_(torch.randn_like(pol.params) * 0.01)
+    N = 77
+    g = torch.Generator(device="cuda").manual_seed(19)
+    img = torch.randint(0, 256, (N, 1) + hw + (3,), dtype=torch.uint8, device="cuda", generator=g)
+    gl = torch.randint(0, 256, (N, 1) + hw + (3,), dtype=torch.uint8, device="cuda", generator=g)
+    cl = torch.randn((N, 1, 4), device="cuda", generator=g)
+    outs = []
+    for _ in range(2):
+        junk = torch.full((pol.params.numel() * 4,), float("nan"), device="cuda")  # poison the allocator's cache
+        del junk
+        pol.params.grad = None
+        logits, value, _ = pol(((img, gl), None), None, None)
+        ((logits * cl).sum() + value.sum()).backward()
+        torch.cuda.synchronize()
+        outs.append(pol.params.grad.clone())
+    gr = outs[0]
+    assert torch.isfinite(gr).all()
+    X = pol.net.aux_layout
+    assert float(gr[X["w1"]:X["b2"] + 8].abs().max()) == 0.0
+    assert torch.equal(outs[0], outs[1])

@@ -90,12 +90,15 @@ def _ref_trainer(graph, replay_size=4, E=16, T=5, S=8, seed=3, **kw):
                            replay_size=replay_size, cuda_graph=graph, entropy_coefficient=0.001, **kw)
 
 
-def test_cuda_graph_with_replay_sources_is_bit_identical():
+@pytest.mark.parametrize("E,S", [(16, 8), (4, 4)])
+def test_cuda_graph_with_replay_sources_is_bit_identical(E, S):
     """The registered experiment's update (replayed aux batch + replayed UNREAL pass on a side
-    stream) captured once in a hipGraph and replayed: parameters, RMSprop state, ring, meta and
-    the metrics equal the eager updates bitwise (the pc statistic to rounding: atomics)."""
+    stream; at S == E the aux heads inside the UNREAL pass) captured once in a hipGraph and
+    replayed: parameters, RMSprop state, ring, meta and the metrics equal the eager updates
+    bitwise (the pc / aux statistics to rounding: atomics)."""
     def run(graph):
-        tr = _ref_trainer(graph)
+        tr = _ref_trainer(graph, E=E, S=S)
+        assert tr._merged_replay == (E == S)
         ms = [tr.step(sync=True) for _ in range(7)]
         torch.cuda.synchronize()
         return tr, ms
@@ -114,6 +117,46 @@ def test_cuda_graph_with_replay_sources_is_bit_identical():
         # the pc and aux loss statistics sum per-workgroup partials with atomics (metrics only)
         for k in ("pc_loss", "aux_loss"):
             np.testing.assert_allclose(x[k], y[k], rtol=1e-5)
+
+
+def test_merged_replay_pass_matches_two_passes():
+    """S == E (the logged run's 4 envs): the aux heads on the replayed UNREAL pass's trunk forward,
+    their dX4 joining its trunk backward (one forward + backward of the replayed rollout) against
+    the separate aux-replay pass (`VN_REPLAY_SEPARATE`): the same update to rounding (the trunk
+    gradients of the two losses summed in another order, over three updates of drift) — every
+    gradient block to 1e-4 of its scale (the suite's gradient tolerance; measured 1.3e-5), the
+    aux / UNREAL statistics to 1e-4, the ring bitwise."""
+    import os
+
+    def run(separate):
+        if separate:
+            os.environ["VN_REPLAY_SEPARATE"] = "1"
+        try:
+            tr = _ref_trainer(False, E=4, S=4)
+        finally:
+            os.environ.pop("VN_REPLAY_SEPARATE", None)
+        assert tr._merged_replay == (not separate)
+        for _ in range(3):  # fill the ring, then one compared update
+            batch, _ = tr.sample_training_batch()
+            tr.update(batch)
+        torch.cuda.synchronize()
+        return tr
+
+    a, b = run(False), run(True)
+    assert torch.equal(a.replay_meta, b.replay_meta) and torch.equal(a.replay_rows, b.replay_rows)
+    ga, gb = a.net.to_reference(a.grads), b.net.to_reference(b.grads)
+    bad = {}
+    for k in gb:
+        ref = gb[k].numpy().astype(np.float64)
+        sc = np.abs(ref).max()
+        if sc == 0:
+            continue
+        e = np.abs(ga[k].numpy() - ref).max() / sc
+        if e > 1e-4:
+            bad[k] = "%.3g" % e
+    assert not bad, bad
+    torch.testing.assert_close(a.aux_stats, b.aux_stats, rtol=1e-4, atol=0)
+    torch.testing.assert_close(a.unreal_stats, b.unreal_stats, rtol=1e-4, atol=1e-9)
 
 
 def test_grad_norm_join_equals_adds_then_norm():
@@ -144,12 +187,14 @@ def test_grad_norm_join_equals_adds_then_norm():
         _lib.check(lib_rc, "vn_grad_norm_join")
 
 
-def test_side_stream_guard_passes_and_trips_on_overlap():
+@pytest.mark.parametrize("E,S", [(16, 8), (4, 4)])
+def test_side_stream_guard_passes_and_trips_on_overlap(E, S):
     """The replayed UNREAL pass's side stream is race-free only while its buffers and gradient
     block are disjoint from the main stream's: the debug check passes on the trainer's own
-    layout (every update of a debug run) and raises on an aliased buffer and on a join range
-    reaching into the pc / rp block."""
-    tr = _ref_trainer(False, replay_size=2)
+    layout (every update of a debug run; at S == E with the aux heads' buffers and block on the
+    side stream) and raises on an aliased buffer and on a join range reaching into the pc / rp
+    block."""
+    tr = _ref_trainer(False, replay_size=2, E=E, S=S)
     tr.debug_streams = True
     for _ in range(2):
         tr.step(sync=True)

@@ -22,6 +22,7 @@ for r in csv.DictReader(open(sys.argv[1])):
     if re.search(sys.argv[2], r["Name"]):
         print("   %9.1f us x %5d  %s" % (float(r["AverageNs"]) / 1e3, int(r["Calls"]), r["Name"][:100]))
 PY
+    rm -f $d/run_kernel_trace.csv
   done
 done
 unset $FLAG

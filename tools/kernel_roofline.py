@@ -45,7 +45,7 @@ def table(h, w, E, T, gf=1.0, gb=1.0):
     x1, x2 = p1 * 32 * f4, p2 * 32 * f4
     lstm = E * 2048 * xcat * 2
     return [
-        (r"conv1_fwd_x3_kernel", Ff * c1, Ff * (fb + x1 + p1 * 4), "x3"),
+        (r"conv1_fwd_x3r?_kernel", Ff * c1, Ff * (fb + x1 + p1 * 4), "x3"),
         (r"conv2_fwd_x6_kernel|conv2_fwd_ring2?_kernel|(NhwcIm2col<32, 4, 4, 2, %d, %d, %d, %d, 1>|FrameListIm2col<%d, %d, %d, %d>), "
          r"DenseRows, (EpiBiasAct|EpiBiasActFrames)" % (a1, b1, a2, b2, a1, b1, a2, b2), Ff * c2, Ff * (x1 + x2), "x6"),
         (r"(NhwcIm2col<32, 4, 4, 2, %d, %d, %d, %d, 2>|NhwcIm2colGoal<32, 4, 4, 2, %d, %d, %d, %d>), DenseRows, "
