@@ -275,14 +275,23 @@ __global__ __launch_bounds__(kAux2Threads) void aux_deconv2_kernel(const float* 
     for (int t = (wave & 1) * 64 + lane; t < ns * RT; t += 128) {
       const int sp = t / RT, r = t - sp * RT, yy = r / XB, xb = r - (r / XB) * XB, s = s0 + sp;
       const int npx = (WXC - xb + XB - 1) / XB;  // pixels xb + i XB < WXC
-      f4 ti[kAux2Px], tg[kAux2Px];  // targets issued before the products
+      // targets issued before the products. The goal's depth (tg .x) is not a target: loading
+      // the whole f4 let the register allocator reuse that dead lane right away, which forced an
+      // s_waitcnt vmcnt(0) on all eight loads before the products (round 6); only .yzw is loaded
+      f4 ti[kAux2Px];
+      float tg[kAux2Px][4];
       if constexpr (LOSS) {
         const int64_t ib = (int64_t)img_rows[s] * PH * PW, gb = (int64_t)goal_rows[s] * PH * PW;
 #pragma unroll
         for (int i = 0; i < kAux2Px; ++i) {
           const int pix = (2 * yy + py) * PW + 2 * min(xb + i * XB, WXC - 1) + px;
           ti[i] = table[ib + pix];
-          tg[i] = table[gb + pix];
+          {
+            const float* g3 = reinterpret_cast<const float*>(table + gb + pix) + 1;
+            tg[i][1] = g3[0];
+            tg[i][2] = g3[1];
+            tg[i][3] = g3[2];
+          }
         }
       }
       float o[kAux2Px][7];
@@ -459,14 +468,20 @@ __global__ __launch_bounds__(kAux2Threads) void aux_deconv2_band_kernel(const fl
       const int yl = t / XB, xb = t - (t / XB) * XB, yy = y0 + yl;
       if (yy >= HYC) continue;  // the last band's rows past the map
       const int npx = (WXC - xb + XB - 1) / XB;
-      f4 ti[kAux2Px], tg[kAux2Px];
+      f4 ti[kAux2Px];
+      float tg[kAux2Px][4];  // .yzw only (see aux_deconv2_kernel)
       if constexpr (LOSS) {
         const int64_t ib = (int64_t)img_rows[s] * PH * PW, gb = (int64_t)goal_rows[s] * PH * PW;
 #pragma unroll
         for (int i = 0; i < kAux2Px; ++i) {
           const int pix = (2 * yy + py) * PW + 2 * min(xb + i * XB, WXC - 1) + px;
           ti[i] = table[ib + pix];
-          tg[i] = table[gb + pix];
+          {
+            const float* g3 = reinterpret_cast<const float*>(table + gb + pix) + 1;
+            tg[i][1] = g3[0];
+            tg[i][2] = g3[1];
+            tg[i][3] = g3[2];
+          }
         }
       }
       float o[kAux2Px][7];
