@@ -205,13 +205,15 @@ class A2CTrainer:
         # compute_auxiliary_loss overridden by a subclass: called every update (autograd on a
         # GoalNavPolicy view of the flat parameters), its gradient added before the all-reduce
         self._setup_unreal(unreal, pc_weight, rp_weight, vr_weight, pc_gamma, unreal_envs)
-        # both batches replayed and the UNREAL record holds every env (S == E, the logged run's 4
-        # envs): the replayed UNREAL pass's trunk forward covers the aux batch's samples (rows
-        # t*S + e = t*E + e), so the aux heads run on it inside the side pass and their dX4 joins
-        # the UNREAL pass's trunk backward — one trunk forward + backward of the replayed
-        # rollout instead of two (VN_REPLAY_SEPARATE=1 keeps the two passes)
+        # opt-in (VN_REPLAY_MERGED=1), both batches replayed and the UNREAL record holding every
+        # env (S == E, the logged run's 4 envs): the replayed UNREAL pass's trunk forward covers
+        # the aux batch's samples (rows t*S + e = t*E + e), so the aux heads can run on it inside
+        # the side pass, their dX4 joining its trunk backward — one trunk forward + backward of
+        # the replayed rollout instead of two. Measured slower (2.51 vs 2.40 ms per 4-env update,
+        # tools/ab/replay_ab.sh): the side stream becomes the critical path while the main
+        # stream idles, so the two passes stay the default.
         self._merged_replay = (self.aux_source == "replay" and self.unreal_source == "replay"
-                               and self.unreal_S == E and not os.environ.get("VN_REPLAY_SEPARATE"))
+                               and self.unreal_S == E and bool(os.environ.get("VN_REPLAY_MERGED")))
         if self.replay:
             self._replay_segs = self._replay_segments()
         self._custom_aux = type(self).compute_auxiliary_loss is not A2CTrainer.compute_auxiliary_loss

@@ -10,6 +10,7 @@ ring here is checked against its own numpy restatement (push into slot pos, unif
 the filled slots with Philox4x32-10 stream 4, oracle/philox.py)."""
 import copy
 import ctypes
+import os
 import warnings
 
 import numpy as np
@@ -90,15 +91,20 @@ def _ref_trainer(graph, replay_size=4, E=16, T=5, S=8, seed=3, **kw):
                            replay_size=replay_size, cuda_graph=graph, entropy_coefficient=0.001, **kw)
 
 
-@pytest.mark.parametrize("E,S", [(16, 8), (4, 4)])
-def test_cuda_graph_with_replay_sources_is_bit_identical(E, S):
+@pytest.mark.parametrize("E,S,merged", [(16, 8, False), (4, 4, False), (4, 4, True)])
+def test_cuda_graph_with_replay_sources_is_bit_identical(E, S, merged):
     """The registered experiment's update (replayed aux batch + replayed UNREAL pass on a side
     stream; at S == E the aux heads inside the UNREAL pass) captured once in a hipGraph and
     replayed: parameters, RMSprop state, ring, meta and the metrics equal the eager updates
     bitwise (the pc / aux statistics to rounding: atomics)."""
     def run(graph):
-        tr = _ref_trainer(graph, E=E, S=S)
-        assert tr._merged_replay == (E == S)
+        if merged:
+            os.environ["VN_REPLAY_MERGED"] = "1"
+        try:
+            tr = _ref_trainer(graph, E=E, S=S)
+        finally:
+            os.environ.pop("VN_REPLAY_MERGED", None)
+        assert tr._merged_replay == merged
         ms = [tr.step(sync=True) for _ in range(7)]
         torch.cuda.synchronize()
         return tr, ms
@@ -120,21 +126,21 @@ def test_cuda_graph_with_replay_sources_is_bit_identical(E, S):
 
 
 def test_merged_replay_pass_matches_two_passes():
-    """S == E (the logged run's 4 envs): the aux heads on the replayed UNREAL pass's trunk forward,
-    their dX4 joining its trunk backward (one forward + backward of the replayed rollout) against
-    the separate aux-replay pass (`VN_REPLAY_SEPARATE`): the same update to rounding (the trunk
+    """S == E (the logged run's 4 envs), opt-in `VN_REPLAY_MERGED`: the aux heads on the replayed
+    UNREAL pass's trunk forward, their dX4 joining its trunk backward (one forward + backward of the
+    replayed rollout) against the separate aux-replay pass (the default): the same update to rounding (the trunk
     gradients of the two losses summed in another order, over three updates of drift) — every
     gradient block to 1e-4 of its scale (the suite's gradient tolerance; measured 1.3e-5), the
     aux / UNREAL statistics to 1e-4, the ring bitwise."""
     import os
 
     def run(separate):
-        if separate:
-            os.environ["VN_REPLAY_SEPARATE"] = "1"
+        if not separate:
+            os.environ["VN_REPLAY_MERGED"] = "1"
         try:
             tr = _ref_trainer(False, E=4, S=4)
         finally:
-            os.environ.pop("VN_REPLAY_SEPARATE", None)
+            os.environ.pop("VN_REPLAY_MERGED", None)
         assert tr._merged_replay == (not separate)
         for _ in range(3):  # fill the ring, then one compared update
             batch, _ = tr.sample_training_batch()
@@ -187,14 +193,20 @@ def test_grad_norm_join_equals_adds_then_norm():
         _lib.check(lib_rc, "vn_grad_norm_join")
 
 
-@pytest.mark.parametrize("E,S", [(16, 8), (4, 4)])
-def test_side_stream_guard_passes_and_trips_on_overlap(E, S):
+@pytest.mark.parametrize("E,S,merged", [(16, 8, False), (4, 4, True)])
+def test_side_stream_guard_passes_and_trips_on_overlap(E, S, merged):
     """The replayed UNREAL pass's side stream is race-free only while its buffers and gradient
     block are disjoint from the main stream's: the debug check passes on the trainer's own
     layout (every update of a debug run; at S == E with the aux heads' buffers and block on the
     side stream) and raises on an aliased buffer and on a join range reaching into the pc / rp
     block."""
-    tr = _ref_trainer(False, replay_size=2, E=E, S=S)
+    if merged:
+        os.environ["VN_REPLAY_MERGED"] = "1"
+    try:
+        tr = _ref_trainer(False, replay_size=2, E=E, S=S)
+    finally:
+        os.environ.pop("VN_REPLAY_MERGED", None)
+    assert tr._merged_replay == merged
     tr.debug_streams = True
     for _ in range(2):
         tr.step(sync=True)
