@@ -162,6 +162,58 @@ struct NhwcIm2colGoal {
   }
 };
 
+// conv3's forward A operand (NhwcIm2colGoal's rows and values) with the gather's addressing
+// taken out of the K loop: with BK == C a K tile is one (g, ky, kx) — uniform — so each fetch
+// slot keeps the offsets of its image and goal patches (computed at the first fetch, in 16-B
+// units from X: a goal run's start can lie gigabytes back in an earlier call's samples) and a
+// K tile adds one uniform offset. Rows past M read row 0's patch: the epilogue stores no row
+// past M, so they need no zeros. The per-slot row decomposition, bounds tests and address math
+// of the generic gather (~16 vector instructions per slot and K tile) become a select and a
+// 64-bit add. gd == nullptr: each sample's own goal half (NhwcIm2col<..., G = 2>'s rows).
+// Requires BK == C and K % BK == 0 (conv3: K = 1024).
+template <int C, int KH, int KW, int S, int H, int W, int OH, int OW>
+struct NhwcIm2colGoalF {
+  static constexpr int kMaxSlots = 8;
+  const float* X;
+  int M;  // samples * OH * OW
+  const int32_t* gd;
+  mutable int oimg[kMaxSlots], ogoal[kMaxSlots];
+  mutable bool ready;
+  static constexpr bool kTrans = false;
+  template <int ROWS, int BK>
+  static constexpr int slots() { return ROWS * (BK / 4); }
+  template <int ROWS, int BK>
+  __device__ __forceinline__ void fetch(f4* r, int row0, int k0, int kend, int tid) const {
+    static_assert(BK == C && C % 4 == 0, "one (g, ky, kx) per K tile");
+    constexpr int Q = BK / 4, T = ROWS * Q, NS = (T + 255) / 256;
+    static_assert(NS <= kMaxSlots, "fetch slots");
+    (void)kend;
+    if (!ready) {
+#pragma unroll
+      for (int j = 0; j < NS; ++j) {
+        int rr, q;
+        rows_slot<ROWS, Q>(tid + j * 256, rr, q);
+        const int m = row0 + rr < M ? row0 + rr : 0;
+        const int n = m / (OH * OW);
+        const int rm = m - n * (OH * OW);
+        const int oy = rm / OW, ox = rm - (rm / OW) * OW;
+        const int base = (((oy * S) * W + ox * S) * C + 4 * q) / 4;
+        oimg[j] = (2 * n) * (H * W * C / 4) + base;
+        ogoal[j] = (2 * (n + (gd ? gd[n] : 0)) + 1) * (H * W * C / 4) + base;
+      }
+      ready = true;
+    }
+    int t = k0 / C;
+    const bool g = t & 1;
+    t >>= 1;
+    const int ky = t / KW, kx = t - (t / KW) * KW;
+    const f4* xb = reinterpret_cast<const f4*>(X) + (ky * W + kx) * (C / 4);
+#pragma unroll
+    for (int j = 0; j < NS; ++j)
+      if (T % 256 == 0 || tid + j * 256 < T) r[j] = xb[g ? ogoal[j] : oimg[j]];
+  }
+};
+
 // conv2's im2col (one 32-channel input, k4 s2) over the frames of a FrameList (goal-frame
 // deduplication on maps without a persistent conv2 kernel, 300x400): row m = (list item
 // m / (OH*OW), output pixel); rows end at the list's device-side count (row_limit).
@@ -1790,10 +1842,12 @@ struct Geo {
 struct Acts {
   float* X[5];
   uint32_t* M1;  // [frames][OH1*OW1] channel bits of X1 > 0 (written by conv1, read by conv2's dgrad)
+  int64_t off;   // samples of the buffer before X[i] (goal runs may point back to them)
 };
 
 inline Acts acts_at(const PolicyLayout& L, float* base, int64_t cap, int64_t off) {
   Acts a;
+  a.off = off;
   a.M1 = reinterpret_cast<uint32_t*>(base) + off * L.msz;
   float* p = base + cap * L.msz;
   for (int i = 0; i < 5; ++i) {
@@ -1953,17 +2007,28 @@ int forward_impl(const PolicyLayout& L, const float* P, const FrameSrc& src, int
   // conv3 over concat(image, goal) (X2 -> X3); with goal runs the goal half of a sample is
   // read from its run start
   if (!small34) {
-    DenseRows fb{P + L.l[2].w, 1024, 64};
     EpiBiasAct ep{a.X[2], 64, P + L.l[2].b, 1};
+    DenseRows fb{P + L.l[2].w, 1024, 64};
     auto conv3 = [&](auto fa) {
       if constexpr (G::OH3 * G::OW3 >= 64)  // 174x174, 300x400: 128-row tiles (A split over more MFMAs)
         launch_gemm_x6_sk<128, 64, 32, 2, 2>(fa, fb, ep, fa.M, 64, 1024, st, L);
       else  // 84x84: 3x3 maps, 64-row tiles keep >= 2 tiles per CU
         launch_gemm_x6_sk<64, 64, 32, 2, 2>(fa, fb, ep, fa.M, 64, 1024, st, L);
     };
+    // the gather with per-slot offsets (NhwcIm2colGoalF; goal half from the run start, or
+    // from the sample itself without goal runs)
+    // (16-B offsets: int32 up to 32 GB of X2 before and after X)
+    const bool fast = (a.off + n) * 2 * G::OH2 * G::OW2 * 32 / 4 < ((int64_t)1 << 31) && !getenv("VN_CONV3F_GATHER");
+    using Fast = NhwcIm2colGoalF<32, 4, 4, 2, G::OH2, G::OW2, G::OH3, G::OW3>;
     if (gr) {
-      if constexpr (kGoalRunsGeo<H0, W0>)
-        conv3(NhwcIm2colGoal<32, 4, 4, 2, G::OH2, G::OW2, G::OH3, G::OW3>{a.X[1], n * G::OH3 * G::OW3, gr->goal_delta});
+      if constexpr (kGoalRunsGeo<H0, W0>) {
+        if (fast)
+          conv3(Fast{a.X[1], n * G::OH3 * G::OW3, gr->goal_delta});
+        else
+          conv3(NhwcIm2colGoal<32, 4, 4, 2, G::OH2, G::OW2, G::OH3, G::OW3>{a.X[1], n * G::OH3 * G::OW3, gr->goal_delta});
+      }
+    } else if (fast) {
+      conv3(Fast{a.X[1], n * G::OH3 * G::OW3, nullptr});
     } else {
       conv3(NhwcIm2col<32, 4, 4, 2, G::OH2, G::OW2, G::OH3, G::OW3, 2>{a.X[1], n * G::OH3 * G::OW3});
     }

@@ -268,3 +268,48 @@ def test_dedup_off_for_companion_frames():
         tr.net.forward(tr.params, tr._frames(tr.rows_img[sl], tr.rows_goal[sl]), E, acts, T * E, t * E, out[sl])
     torch.cuda.synchronize()
     assert torch.equal(out, tr.out)
+
+
+@pytest.mark.parametrize("flag", ["VN_CONV3F_GATHER"])
+@pytest.mark.parametrize("hw,E", [((174, 174), 208), ((300, 400), 48), ((84, 84), 64)],
+                         ids=["174x174", "c5_300x400", "84x84_splitk"])
+def test_conv3_forward_forms_bitwise(flag, hw, E):
+    """conv3's forward product with goal runs reaching back into the previous step's samples
+    (whole K with a ragged last row tile; split K at 84x84): the gather with per-slot offsets
+    kept across the K loop (the default) against the generic gather (`VN_CONV3F_GATHER`): the
+    same products in the same k order, X5 and the outputs bitwise."""
+    import os
+    from vnav import _lib
+    from vnav.policy import frames_from_batch
+    lib = _lib.load()
+    pol = _noisy_policy(hw, 12)
+    net, params = pol.net, pol.params.data
+    T = 2
+    N = T * E
+    img, gl, dones = _rollout_batch(hw, T, E, 17, p_done=0.5)
+
+    def run(on):
+        if on:
+            os.environ[flag] = "1"
+        try:
+            delta = torch.zeros((T, E), dtype=torch.int32, device="cuda")
+            lst = torch.zeros((T, E), dtype=torch.int32, device="cuda")
+            cnt = torch.zeros(T + 1, dtype=torch.int32, device="cuda")
+            acts = net.new_acts(N)
+            acts.fill_(float("nan"))
+            out = torch.zeros((N, 8), device="cuda")
+            for t in range(T):
+                sl = slice(t * E, (t + 1) * E)
+                _step_runs(lib, _lib, dones, t, delta, lst, cnt)
+                gr = _lib.GoalRuns()
+                gr.goal_list, gr.goal_count, gr.goal_delta = lst[t].data_ptr(), cnt[t:t + 1].data_ptr(), delta[t].data_ptr()
+                net.forward(params, frames_from_batch(img[sl], gl[sl]), E, acts, N, t * E, out[sl], goals=gr)
+            torch.cuda.synchronize()
+            return net.x5(acts, N).clone(), out[:, :5].clone()
+        finally:
+            os.environ.pop(flag, None)
+
+    (x_def, o_def), (x_on, o_on) = run(False), run(True)
+    assert not torch.isnan(o_def).any() and float(x_def.abs().max()) > 0
+    assert torch.equal(x_def, x_on), float((x_def - x_on).abs().max())
+    assert torch.equal(o_def, o_on)
