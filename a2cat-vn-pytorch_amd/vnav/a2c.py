@@ -214,6 +214,9 @@ class A2CTrainer:
         # stream idles, so the two passes stay the default.
         self._merged_replay = (self.aux_source == "replay" and self.unreal_source == "replay"
                                and self.unreal_S == E and bool(os.environ.get("VN_REPLAY_MERGED")))
+        # VN_UNREAL_INLINE=1: the replayed UNREAL pass runs on the main stream before the A2C
+        # backward instead of beside it (the race check: both forms must give the same update)
+        self._unreal_inline = bool(os.environ.get("VN_UNREAL_INLINE"))
         if self.replay:
             self._replay_segs = self._replay_segments()
         self._custom_aux = type(self).compute_auxiliary_loss is not A2CTrainer.compute_auxiliary_loss
@@ -775,12 +778,15 @@ class A2CTrainer:
             # after the join below, in the unforked order
             if self.debug_streams:
                 self._check_side_stream_disjoint()
-            main = torch.cuda.current_stream(self.device)
-            self._ev_u0.record(main)
-            self._side_u.wait_event(self._ev_u0)
-            with torch.cuda.stream(self._side_u):
+            if self._unreal_inline:
                 self._unreal_replay_losses(add=False)
-                self._ev_u1.record(self._side_u)
+            else:
+                main = torch.cuda.current_stream(self.device)
+                self._ev_u0.record(main)
+                self._side_u.wait_event(self._ev_u0)
+                with torch.cuda.stream(self._side_u):
+                    self._unreal_replay_losses(add=False)
+                    self._ev_u1.record(self._side_u)
         _lib.check(lib.vn_a2c_returns(_lib.ptr(self.rewards), _lib.ptr(self.dones), _lib.ptr(self.boot_out), T, E, A,
                                       ctypes.c_float(self.gamma), _lib.ptr(self.returns), st), "vn_a2c_returns")
         _lib.check(lib.vn_a2c_loss_grad(_lib.ptr(self.out), _lib.ptr(self.actions), _lib.ptr(self.returns), N, A,
@@ -841,7 +847,8 @@ class A2CTrainer:
             _, b = self.net.offsets["fc"]
             joins.append((self.aux_grads, w, b + self.net.shapes["fc"][0]))
         if u_side:
-            torch.cuda.current_stream(self.device).wait_event(self._ev_u1)
+            if not self._unreal_inline:
+                torch.cuda.current_stream(self.device).wait_event(self._ev_u1)
             joins.append((self.ur_grads, 0, self._ur_add_end))
         fuse_join = self.world == 1 and not self._custom_aux
         if not fuse_join:

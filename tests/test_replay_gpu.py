@@ -165,6 +165,36 @@ def test_merged_replay_pass_matches_two_passes():
     torch.testing.assert_close(a.unreal_stats, b.unreal_stats, rtol=1e-4, atol=1e-9)
 
 
+@pytest.mark.parametrize("merged", [False, True])
+def test_side_stream_pass_equals_inline_pass(merged):
+    """The replayed UNREAL pass on its side stream (beside the A2C backward) against the same
+    pass run on the main stream before it (`VN_UNREAL_INLINE`): every buffer the two streams
+    write is disjoint, so four updates give the same parameters, RMSprop state and ring
+    bitwise — a race between the streams would show up here as a difference (the pc / aux
+    statistics to rounding: atomics). With `VN_REPLAY_MERGED` the aux heads ride in the pass."""
+    def run(inline):
+        env = {"VN_UNREAL_INLINE": "1"} if inline else {}
+        if merged:
+            env["VN_REPLAY_MERGED"] = "1"
+        os.environ.update(env)
+        try:
+            tr = _ref_trainer(False, E=4 if merged else 16, S=4 if merged else 8)
+        finally:
+            for k in env:
+                os.environ.pop(k, None)
+        assert tr._unreal_inline == inline and tr._merged_replay == merged
+        for _ in range(4):
+            tr.step(sync=True)
+        torch.cuda.synchronize()
+        return tr
+
+    a, b = run(False), run(True)
+    assert torch.equal(a.params, b.params) and torch.equal(a.square_avg, b.square_avg)
+    assert torch.equal(a.replay_meta, b.replay_meta)
+    torch.testing.assert_close(a.unreal_stats, b.unreal_stats, rtol=1e-5, atol=1e-9)
+    torch.testing.assert_close(a.aux_stats, b.aux_stats, rtol=1e-5, atol=0)
+
+
 def test_grad_norm_join_equals_adds_then_norm():
     """vn_grad_norm_join (the side passes' gradients added inside the norm's first pass) against
     the two adds followed by vn_grad_norm: the same gradient and scalars bitwise."""

@@ -29,4 +29,6 @@ echo "== 4-env leg"
 bash tools/prof_ref4_r06.sh > /dev/null || exit 1
 cp gpurun_out/breakdown_ref4.txt gpurun_out/breakdown_ref4_$T.txt
 head -4 gpurun_out/breakdown_l84$T.txt gpurun_out/breakdown_l174$T.txt gpurun_out/breakdown_c5$T.txt gpurun_out/breakdown_ref4_$T.txt
+# the traces have been reduced to the breakdowns and tables above; gpurun returns <= 64 MiB
+find gpurun_out -name '*kernel_trace.csv' -delete
 echo "== done"

@@ -48,7 +48,7 @@ def table(h, w, E, T, gf=1.0, gb=1.0):
         (r"conv1_fwd_x3r?_kernel", Ff * c1, Ff * (fb + x1 + p1 * 4), "x3"),
         (r"conv2_fwd_x6_kernel|conv2_fwd_ring2?_kernel|(NhwcIm2col<32, 4, 4, 2, %d, %d, %d, %d, 1>|FrameListIm2col<%d, %d, %d, %d>), "
          r"DenseRows, (EpiBiasAct|EpiBiasActFrames)" % (a1, b1, a2, b2, a1, b1, a2, b2), Ff * c2, Ff * (x1 + x2), "x6"),
-        (r"(NhwcIm2col<32, 4, 4, 2, %d, %d, %d, %d, 2>|NhwcIm2colGoal<32, 4, 4, 2, %d, %d, %d, %d>), DenseRows, "
+        (r"(NhwcIm2col<32, 4, 4, 2, %d, %d, %d, %d, 2>|NhwcIm2colGoalF?<32, 4, 4, 2, %d, %d, %d, %d>), DenseRows, "
          r"EpiBiasAct" % (a2, b2, a3, b3, a2, b2, a3, b3), (N + E) * c3, (N + E) * (2 * x2 + p3 * 64 * f4), "x6"),
         (r"EpiBias2", (T + 1) * lstm, (T + 1) * (E * xcat + 2048 * xcat + E * 2048) * f4, "x6"),
         (r"conv1_wgrad_x3_kernel<", Fb * c1, Fb * (fb + x1), "x3"),
