@@ -22,8 +22,11 @@ if [ "${TRACE:-1}" = "1" ]; then
   rc=$?; tail -5 $OUT/pytest_gpu_traced_$TAG.log
   f=$(find /tmp/trace_$TAG -name "*kernel_trace.csv" | head -1)
   if [ -n "$f" ]; then
-    python3 tools/test_kernel_map.py "$f" $OUT/tests_$TAG.tsv --top ${TOP:-profiles/r02/train_kernel_stats_v12.csv} --k 20 \
-      --oracle-tests ${ORACLE_TESTS:-test_prod_oracle_gpu} --md $OUT/test_kernels_$TAG.md; echo "map rc=$?"
+    # (profiles/ does not travel to the box: without a TOP file the map lists kernels per test only;
+    # the top-kernel coverage table is built here from the returned trace)
+    TOPARG=""; [ -n "${TOP:-}" ] && [ -f "$TOP" ] && TOPARG="--top $TOP"
+    python3 tools/test_kernel_map.py "$f" $OUT/tests_$TAG.tsv $TOPARG --k 20 \
+      --oracle-tests ${ORACLE_TESTS:-test_prod_oracle_gpu vs_fp64_oracle vs_oracle} --md $OUT/test_kernels_$TAG.md; echo "map rc=$?"
     gzip -c "$f" > $OUT/kernel_trace_tests_$TAG.csv.gz
   fi
   [ $rc -eq 0 ] || exit $rc
