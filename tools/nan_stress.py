@@ -3,7 +3,7 @@ the kernel switches of the pass (debug aid for an intermittent non-finite gradie
 import os, sys, torch
 sys.path.insert(0, "a2cat-vn-pytorch_amd"); sys.path.insert(0, ".")
 from vnav.policy import GoalNavPolicy
-passes = [[], ["VN_CONV1F_LDSW", "VN_CONV1WG_NOLEAN", "VN_CONV2DG_NOROT", "VN_CONV2F_RING2_NOPF"]] * 3
+passes = [[], ["VN_CONV1F_LDSW", "VN_CONV1WG_NOLEAN", "VN_CONV2DG_NOROT", "VN_CONV2F_RING2_NOPF", "VN_CONV3F_GATHER"]] * 3
 seq = [(False, 1), (False, 77), (False, 1031), (True, 1), (True, 77), (True, 1031)]
 bad_total = 0
 for pi, flags in enumerate(passes):
