@@ -313,3 +313,42 @@ def test_conv3_forward_forms_bitwise(flag, hw, E):
     assert not torch.isnan(o_def).any() and float(x_def.abs().max()) > 0
     assert torch.equal(x_def, x_on), float((x_def - x_on).abs().max())
     assert torch.equal(o_def, o_on)
+
+
+@pytest.mark.parametrize("hw,E,back", [((84, 84), 32, 110000), ((174, 174), 24, 22000)],
+                         ids=["84x84", "174x174"])
+def test_goal_runs_reaching_back_past_2GB(hw, E, back):
+    """Goal runs whose starts lie more than 2 GB of conv2 maps behind this call's samples (the
+    bench's 20 x 4096 rollouts reach ~8 GB back at 174x174): a call at activation offset `back`
+    with every goal half read from the samples a first call wrote at offset 0 (goal_count 0: no
+    goal frame of its own) against a plain forward of the same frames — outputs and X5 bitwise.
+    conv3's gather keeps those offsets in 16-byte units (NhwcIm2colGoalF); a byte offset, or a
+    buffer descriptor based at this call's samples, would miss them."""
+    from vnav import _lib
+    from vnav.policy import frames_from_batch
+    pol = _noisy_policy(hw, 13)
+    net, params = pol.net, pol.params.data
+    assert net.goal_runs_supported(E)
+    g = torch.Generator(device="cuda").manual_seed(23)
+    img0 = torch.randint(0, 256, (E,) + hw + (3,), dtype=torch.uint8, device="cuda", generator=g)
+    img1 = torch.randint(0, 256, (E,) + hw + (3,), dtype=torch.uint8, device="cuda", generator=g)
+    gl = torch.randint(0, 256, (E,) + hw + (3,), dtype=torch.uint8, device="cuda", generator=g)
+    cap = back + E
+    acts = net.new_acts(cap)
+    out0 = torch.zeros((E, 8), device="cuda")
+    net.forward(params, frames_from_batch(img0, gl), E, acts, cap, 0, out0)  # the goal halves at samples 0..E-1
+    delta = torch.full((E,), -back, dtype=torch.int32, device="cuda")
+    lst = torch.zeros(E, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+    gr = _lib.GoalRuns()
+    gr.goal_list, gr.goal_count, gr.goal_delta = lst.data_ptr(), cnt.data_ptr(), delta.data_ptr()
+    out_far = torch.zeros((E, 8), device="cuda")
+    net.forward(params, frames_from_batch(img1, gl), E, acts, cap, back, out_far, goals=gr)
+    ref_acts = net.new_acts(E)
+    out_ref = torch.zeros((E, 8), device="cuda")
+    net.forward(params, frames_from_batch(img1, gl), E, ref_acts, E, 0, out_ref)
+    torch.cuda.synchronize()
+    assert torch.isfinite(out_ref).all()
+    assert torch.equal(out_far, out_ref), float((out_far - out_ref).abs().max())
+    assert torch.equal(net.x5(acts, cap)[back:], net.x5(ref_acts, E))
+    del acts
